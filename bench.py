@@ -1,0 +1,273 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident per-chunk reduction (fp32 sum), Gloo hot path.
+
+BASELINE.json metric "device-resident chunk-reduce GiB/s (fp32 sum) + % HBM
+roofline, 1/2/4/8 GPU" on config 2: one 64 MiB fp32 chunk reduced in place
+(dst += src, the form every schedule calls through ReductionFunction::call,
+gloo/algorithm.h:75-77) by the HIP kernel behind include/gloo_amd.h.
+
+One step = one kernel over one 64 MiB chunk.  Inputs are resident in HBM
+before the timed region.  Six (dst, src) pairs are rotated (768 MiB footprint,
+3x the 256 MiB Infinity Cache) so every step streams from HBM.
+
+Multi-GPU: one process per GPU (torch.distributed.run), each GPU reduces its
+own chunks — the reduction partitions into independent units, so there is no
+data-path collective ("scaling": "weak"); torch.distributed's gloo backend is
+used only for the harness barrier and the max-over-ranks time.
+
+Also reported (rank 0, N=1 only): the reference's own gloo::sum<float>
+(oracle/_ref, built from /root/reference as it ships) timed on the host cores
+(`cpu_baseline`), and the host-staged rate of a chunk that starts and ends in
+pinned host memory (H2D + kernel + D2H).
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "device-resident chunk-reduce GiB/s (fp32 sum) + % HBM roofline, 1/2/4/8 GPU"
+WORKLOAD = ("single-GPU device-resident fp32 sum-reduce kernel, 64 MiB chunk "
+            "(allreduce_local path, no transport)")
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+GIB = float(1 << 30)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--chunk-mib", type=int, default=64)
+    p.add_argument("--pairs", type=int, default=6, help="rotated (dst, src) pairs")
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="bounded CPU-baseline sample (seconds of CPU work)")
+    p.add_argument("--cpu-threads", type=int, default=16,
+                   help="threads for the all-cores CPU figure (the box's CPU share)")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-host-staged", action="store_true")
+    p.add_argument("--variant", type=int, default=0, help="kernel variant (tuning)")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return p.parse_args()
+
+
+def relaunch_distributed(args):
+    """`python bench.py --gpus N` outside torch.distributed.run: start the
+    launcher as a child process (no exec) before anything touches the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(29500 + os.getpid() % 1000), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def cpu_baseline(args, n):
+    """The reference's gloo::sum<float> on host memory, same in-place form and
+    rotation as the GPU leg; bounded to ~args.cpu_seconds of CPU work."""
+    import numpy as np
+    import oracle
+    if oracle.ref_available():
+        fn = oracle.ref_baseline().ref_base_sum_f32
+        kind = "reference"
+    else:
+        fn = oracle.lib().oracle_sum_f32_mt
+        kind = "port"
+    pairs = max(2, args.pairs // 2)
+    rng = np.random.default_rng(1)
+    bufs = [(rng.uniform(-1, 1, n).astype(np.float32), rng.uniform(-1, 1, n).astype(np.float32))
+            for _ in range(pairs)]
+
+    def timed(threads, budget):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            d, s = bufs[done % pairs]
+            fn(d.ctypes.data, d.ctypes.data, s.ctypes.data, n, threads)
+            done += 1
+            el = time.perf_counter() - t0
+            if el >= budget and done >= 3:
+                return done, el
+
+    d, s = bufs[0]
+    fn(d.ctypes.data, d.ctypes.data, s.ctypes.data, n, 1)  # page in
+    calls1, t1 = timed(1, args.cpu_seconds)
+    nt = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    callsn, tn = timed(nt, max(1.0, args.cpu_seconds / 4))
+    alg = 3.0 * n * 4
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
+    except OSError:
+        pass
+    return {
+        "value": round(alg * calls1 / t1 / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
+        "sample": (f"{calls1} calls of gloo::sum<float>(a,a,b,n) in place, n={n} "
+                   f"(64 MiB), {pairs} rotated pairs, {t1:.1f} s, 1 thread as Gloo calls it; "
+                   f"algorithmic bytes 3*n*4"),
+        "all_cores": {"value": round(alg * callsn / tn / GIB, 3), "threads": nt,
+                      "sample": f"{callsn} calls, range split over {nt} std::threads, {tn:.1f} s"},
+        "cpu_model": model, "host_cpus_visible": os.cpu_count(),
+    }
+
+
+def host_staged(torch, hip, n, dev, iters=20):
+    """Chunk starting and ending in pinned host memory (a transport recv
+    buffer): H2D(src) + H2D(dst) + kernel + D2H(dst), all on one stream."""
+    h_dst = torch.empty(n, dtype=torch.float32, pin_memory=True).uniform_(-1, 1)
+    h_src = torch.empty(n, dtype=torch.float32, pin_memory=True).uniform_(-1, 1)
+    d_dst = torch.empty(n, dtype=torch.float32, device=dev)
+    d_src = torch.empty(n, dtype=torch.float32, device=dev)
+    s = torch.cuda.current_stream(dev)
+
+    def once():
+        d_dst.copy_(h_dst, non_blocking=True)
+        d_src.copy_(h_src, non_blocking=True)
+        hip.reduce_ptr("sum", "f32", d_dst.data_ptr(), d_src.data_ptr(), n, s.cuda_stream)
+        h_dst.copy_(d_dst, non_blocking=True)
+
+    for _ in range(3):
+        once()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        once()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / iters
+    return {"gib_s_alg": round(3.0 * n * 4 / dt / GIB, 2), "ms_per_chunk": round(dt * 1e3, 3),
+            "payload_gib_s": round(n * 4 / dt / GIB, 2),
+            "note": "H2D dst + H2D src + kernel + D2H dst per 64 MiB chunk, pinned host memory"}
+
+
+def copy_ceiling(torch, dev, nbytes=1 << 30, iters=10):
+    """Device-to-device copy of 1 GiB (torch) as a measured HBM ceiling."""
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    t = e0.elapsed_time(e1) / 1e3 / iters
+    return round(2.0 * nbytes / t / 1e9, 1)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world == 1:
+        sys.exit(relaunch_distributed(args))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+    import gloo_amd as hip
+
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device(f"cuda:{local_rank}")
+    torch.cuda.set_device(dev)
+    hip.set_variant(args.variant)
+
+    n = args.chunk_mib * (1 << 20) // 4
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    pairs = [(torch.rand(n, device=dev, generator=g) * 2 - 1,
+              torch.rand(n, device=dev, generator=g) * 2 - 1) for _ in range(args.pairs)]
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step(i):
+        d, s = pairs[i % len(pairs)]
+        hip.reduce_ptr("sum", "f32", d.data_ptr(), s.data_ptr(), n, sh)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+
+    # Timed region: barrier + sync on both sides, exactly K steps.  One event
+    # pair per launch gives the kernel's own average duration (roofline).
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step(i)
+        evs[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    region_ms = evs[0][0].elapsed_time(evs[-1][1])
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+
+    t_local = torch.tensor([wall], dtype=torch.float64)
+    k_all = torch.tensor([kern_ms], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t_local, op=dist.ReduceOp.MAX)
+        k_list = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(k_list, k_all)
+        per_rank_kernel_ms = [float(x) for x in k_list]
+    else:
+        per_rank_kernel_ms = [kern_ms]
+    tmax = float(t_local[0])
+
+    alg_bytes = 3.0 * n * 4                       # 2 reads + 1 write per element
+    value = world * args.steps * alg_bytes / tmax / GIB
+    achieved_gbs = alg_bytes / (kern_ms / 1e3) / 1e9
+
+    if rank == 0:
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                if tj.get("elements") == n:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(tmax * 1e3 / args.steps, 5), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": WORKLOAD, "chunk_bytes": n * 4, "elements": n,
+                       "op": "sum", "form": "in-place dst += src (ReductionFunction::call)",
+                       "rotated_pairs": args.pairs, "footprint_mib": 2 * args.pairs * args.chunk_mib,
+                       "parallelism": f"{world} independent GPU(s), no data-path collective",
+                       "kernel_variant": args.variant},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "algorithmic_bytes_per_launch": int(alg_bytes),
+                         "kernel_avg_us": round(kern_ms * 1e3, 3),
+                         "per_rank_kernel_avg_us": [round(x * 1e3, 3) for x in per_rank_kernel_ms],
+                         "event_region_ms": round(region_ms, 4)},
+            "per_gpu_gib_s": round(value / world, 2),
+            "kernel_gib_s": round(alg_bytes / (kern_ms / 1e3) / GIB, 2),
+        }
+        if world == 1:
+            try:
+                out["hbm_copy_ceiling_gbs"] = copy_ceiling(torch, dev)
+            except RuntimeError as e:  # pragma: no cover
+                out["hbm_copy_ceiling_gbs"] = f"unavailable: {e}"
+            if not args.no_host_staged:
+                out["host_staged"] = host_staged(torch, hip, n, dev)
+            if not args.no_cpu:
+                out["cpu_baseline"] = cpu_baseline(args, n)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,192 @@
+"""gloo_amd — MI355X-native per-chunk reduction for Gloo (Python binding).
+
+The product is the HIP library gloo_amd/libgloo_amd.so (C-ABI declared in
+include/gloo_amd.h, kernels in gloo_amd/csrc/reduce.hip) and the C++ host
+headers under gloo_amd/include/gloo_amd/.  This module is a thin ctypes
+binding of that C-ABI for tests, smoke and the benchmark.  There is no CPU
+fallback: if the library is missing, importing this package raises.
+
+Mirrors the reference's reduction-function surface:
+  ReductionType            gloo/algorithm.h:49-57
+  ReductionFunction.call   gloo/algorithm.h:75-77  (dst = dst op src)
+  CudaReductionFunction    gloo/cuda.h:286-358      (device overload, async)
+"""
+import ctypes
+import enum
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgloo_amd.so")
+
+
+class ReductionType(enum.IntEnum):
+    """gloo::ReductionType (gloo/algorithm.h:49-57)."""
+    SUM = 1
+    PRODUCT = 2
+    MAX = 3
+    MIN = 4
+
+
+class DType(enum.IntEnum):
+    I8 = 0
+    U8 = 1
+    I32 = 2
+    U32 = 3
+    I64 = 4
+    U64 = 5
+    F16 = 6
+    BF16 = 7
+    F32 = 8
+    F64 = 9
+
+
+DTYPE_NAMES = {"i8": DType.I8, "u8": DType.U8, "i32": DType.I32, "u32": DType.U32,
+               "i64": DType.I64, "u64": DType.U64, "f16": DType.F16, "bf16": DType.BF16,
+               "f32": DType.F32, "f64": DType.F64}
+OP_NAMES = {"sum": ReductionType.SUM, "product": ReductionType.PRODUCT,
+            "max": ReductionType.MAX, "min": ReductionType.MIN}
+
+EXPORTED = ("gloo_hip_reduce", "gloo_hip_reduce3", "gloo_hip_reduce_multi",
+            "gloo_hip_dtype_size", "gloo_hip_last_error", "gloo_hip_version",
+            "gloo_hip_set_variant")
+
+
+class GlooHipError(RuntimeError):
+    """Raised when a gloo_hip_* call returns a non-zero status
+    (the Python face of GLOO_ENFORCE / EnforceNotMet, gloo/common/logging.h:32-59)."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"gloo_hip error {code}: {msg}")
+        self.code = code
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (there is deliberately no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.gloo_hip_reduce.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, vp]
+    L.gloo_hip_reduce3.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, sz, vp]
+    L.gloo_hip_reduce_multi.argtypes = [ctypes.c_int, ctypes.c_int, vp,
+                                        ctypes.POINTER(vp), ctypes.c_int, sz, vp]
+    L.gloo_hip_dtype_size.argtypes = [ctypes.c_int]
+    L.gloo_hip_dtype_size.restype = sz
+    L.gloo_hip_last_error.restype = ctypes.c_char_p
+    L.gloo_hip_version.restype = ctypes.c_char_p
+    L.gloo_hip_set_variant.argtypes = [ctypes.c_int]
+    return L
+
+
+lib = _load()
+
+
+def _check(rc):
+    if rc != 0:
+        raise GlooHipError(rc, lib.gloo_hip_last_error().decode(errors="replace"))
+
+
+def _as_op(op):
+    return int(OP_NAMES[op]) if isinstance(op, str) else int(op)
+
+
+def _as_dtype(dtype):
+    return int(DTYPE_NAMES[dtype]) if isinstance(dtype, str) else int(dtype)
+
+
+def dtype_size(dtype):
+    return lib.gloo_hip_dtype_size(_as_dtype(dtype))
+
+
+def version():
+    return lib.gloo_hip_version().decode()
+
+
+# ---- raw-pointer API (device pointers as ints, stream as int handle) -------
+
+def reduce_ptr(op, dtype, dst, src, n, stream=0):
+    """dst[i] = dst[i] op src[i] on device pointers (async on `stream`)."""
+    _check(lib.gloo_hip_reduce(_as_op(op), _as_dtype(dtype), dst, src, n, stream or None))
+
+
+def reduce3_ptr(op, dtype, c, a, b, n, stream=0):
+    """c[i] = a[i] op b[i] on device pointers (async on `stream`)."""
+    _check(lib.gloo_hip_reduce3(_as_op(op), _as_dtype(dtype), c, a, b, n, stream or None))
+
+
+def reduce_multi_ptr(op, dtype, dst, srcs, n, stream=0):
+    arr = (ctypes.c_void_p * len(srcs))(*srcs)
+    _check(lib.gloo_hip_reduce_multi(_as_op(op), _as_dtype(dtype), dst, arr, len(srcs), n,
+                                     stream or None))
+
+
+def set_variant(v):
+    """Measurement knob: fp32 SUM kernel variant (0 = tuned default)."""
+    return lib.gloo_hip_set_variant(int(v))
+
+
+# ---- torch-tensor convenience (device memory / streams come from torch) -----
+
+def _torch_dtype_code(t):
+    import torch
+    m = {torch.int8: DType.I8, torch.uint8: DType.U8, torch.int32: DType.I32,
+         torch.int64: DType.I64, torch.float16: DType.F16, torch.bfloat16: DType.BF16,
+         torch.float32: DType.F32, torch.float64: DType.F64}
+    if hasattr(torch, "uint32"):
+        m[torch.uint32] = DType.U32
+    if hasattr(torch, "uint64"):
+        m[torch.uint64] = DType.U64
+    if t.dtype not in m:
+        raise TypeError(f"unsupported dtype {t.dtype}")
+    return m[t.dtype]
+
+
+def _stream_handle(t, stream):
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream(t.device)
+    return stream.cuda_stream
+
+
+def reduce(op, dst, src, stream=None):
+    """In-place dst op= src for contiguous same-dtype device tensors —
+    CudaReductionFunction<T>::call(dst, src, n, stream) (gloo/cuda.h:326-333)."""
+    if dst.dtype != src.dtype or dst.numel() != src.numel():
+        raise ValueError("dst/src must have equal dtype and numel")
+    if not (dst.is_cuda and src.is_cuda and dst.is_contiguous() and src.is_contiguous()):
+        raise ValueError("dst/src must be contiguous device tensors")
+    reduce_ptr(op, _torch_dtype_code(dst), dst.data_ptr(), src.data_ptr(), dst.numel(),
+               _stream_handle(dst, stream))
+    return dst
+
+
+def reduce3(op, c, a, b, stream=None):
+    """c = a op b for contiguous device tensors (gloo::sum<T>(c, a, b, n) shape)."""
+    if not (c.dtype == a.dtype == b.dtype) or not (c.numel() == a.numel() == b.numel()):
+        raise ValueError("c/a/b must have equal dtype and numel")
+    reduce3_ptr(op, _torch_dtype_code(c), c.data_ptr(), a.data_ptr(), b.data_ptr(), c.numel(),
+                _stream_handle(c, stream))
+    return c
+
+
+class ReductionFunction:
+    """Python face of HipReductionFunction<T> (C++: gloo_amd/include/gloo_amd/hip.h),
+    itself the MI355X twin of CudaReductionFunction<T> (gloo/cuda.h:286-358)."""
+
+    def __init__(self, rtype):
+        self.rtype = ReductionType(rtype)
+
+    def type(self):
+        return self.rtype
+
+    def call(self, dst, src, n=None, stream=None):
+        if n is None:
+            return reduce(self.rtype, dst, src, stream)
+        return reduce(self.rtype, dst[:n], src[:n], stream)
+
+
+ReductionFunction.sum = ReductionFunction(ReductionType.SUM)
+ReductionFunction.product = ReductionFunction(ReductionType.PRODUCT)
+ReductionFunction.max = ReductionFunction(ReductionType.MAX)
+ReductionFunction.min = ReductionFunction(ReductionType.MIN)

@@ -1,0 +1,551 @@
+// reduce.hip — CDNA4 (gfx950) element-wise chunk reduction for Gloo.
+//
+// Replaces the reference's per-chunk reduction (gloo/math.h:15-73 on the host,
+// the grid-stride CUDA kernels gloo/cuda.cu:274-401 on the device).  The op is
+// one instruction per element against 2 loads + 1 store, i.e. purely
+// HBM-bound, so the kernel is built around the memory system, not arithmetic:
+//
+//  * every lane moves 16 B per access (global_load_dwordx4 / store_dwordx4),
+//    64 lanes -> 1 KiB contiguous per wave-instruction, fully coalesced;
+//  * UNROLL independent 16-B packets per operand per lane are in flight
+//    before the first use (memory-level parallelism instead of occupancy);
+//  * the aligned body is a flat tile grid (one tile = 256 lanes x UNROLL
+//    packets), tiles dealt round-robin over the 8 XCDs by the dispatcher;
+//  * a chunk may start at any element offset (Gloo chunk offsets are
+//    arbitrary element counts, gloo/allreduce_ring_chunked.h:128): the first
+//    `head` elements up to the 16-B boundary of the destination and the
+//    ragged tail are done element-wise by block 0 inside the same launch;
+//  * operands whose misalignment differs (relative offset not a multiple of
+//    16 B) take an element-wise coalesced path with the same tile shape;
+//  * 64-bit indices throughout (the reference uses `int`, Appendix A.4).
+//
+// Arithmetic is bit-exact with gloo/math.h evaluated in the same order: see
+// include/gloo_amd.h for the contract and the NaN / signed-zero rules.
+
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <type_traits>
+
+#include "gloo_amd.h"
+
+namespace gloo_amd {
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves of 64 lanes
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// Element traits.  S = storage type.  Integers compute in the unsigned type of
+// the same width so overflow wraps (gloo/math.h relies on the platform's
+// modular conversion: c[i] = a[i] + b[i] for int8 promotes to int and
+// truncates, which is the same low bits).
+// ---------------------------------------------------------------------------
+template <typename S, typename U>
+struct IntTraits {
+  using Storage = S;
+  __device__ static __forceinline__ S sum(S a, S b) { return (S)(U)((U)a + (U)b); }
+  __device__ static __forceinline__ S product(S a, S b) {
+    return (S)(U)((U)a * (U)b);
+  }
+  __device__ static __forceinline__ S max(S a, S b) { return (a < b) ? b : a; }
+  __device__ static __forceinline__ S min(S a, S b) { return (b < a) ? b : a; }
+};
+
+// uint8 * uint8 promotes to int in C++; 255*255 fits, truncation gives the
+// same low byte.  For the 32/64-bit unsigned types the product is already
+// unsigned and wraps.
+using TrI8 = IntTraits<int8_t, uint32_t>;
+using TrU8 = IntTraits<uint8_t, uint32_t>;
+using TrI32 = IntTraits<int32_t, uint32_t>;
+using TrU32 = IntTraits<uint32_t, uint32_t>;
+using TrI64 = IntTraits<int64_t, uint64_t>;
+using TrU64 = IntTraits<uint64_t, uint64_t>;
+
+template <typename S>
+struct FloatTraits {
+  using Storage = S;
+  __device__ static __forceinline__ S sum(S a, S b) { return a + b; }
+  __device__ static __forceinline__ S product(S a, S b) { return a * b; }
+  // std::max(a, b) == (a < b) ? b : a ; std::min(a, b) == (b < a) ? b : a.
+  // Written as compare + select so NaN and -0/+0 follow the reference (the
+  // IEEE v_max_f32 would return the non-NaN operand instead).
+  __device__ static __forceinline__ S max(S a, S b) { return (a < b) ? b : a; }
+  __device__ static __forceinline__ S min(S a, S b) { return (b < a) ? b : a; }
+};
+using TrF32 = FloatTraits<float>;
+using TrF64 = FloatTraits<double>;
+
+// IEEE binary16 held as raw bits.  Op in f32, round-to-nearest-even back
+// (v_cvt_f16_f32 honours the default RNE mode).  A single f32 rounding
+// followed by the f16 rounding equals one correctly rounded f16 result for
+// + and * because 24 >= 2*11+2, so this matches F16C (gloo/math.cc:17-97)
+// and CUDA __float2half(__half2float(a) op __half2float(b)) (cuda.cu:301-318).
+struct TrF16 {
+  using Storage = uint16_t;
+  __device__ static __forceinline__ float widen(uint16_t x) {
+    return (float)__builtin_bit_cast(_Float16, x);
+  }
+  __device__ static __forceinline__ uint16_t narrow(float f) {
+    return __builtin_bit_cast(uint16_t, (_Float16)f);
+  }
+  __device__ static __forceinline__ uint16_t sum(uint16_t a, uint16_t b) {
+    return narrow(widen(a) + widen(b));
+  }
+  __device__ static __forceinline__ uint16_t product(uint16_t a, uint16_t b) {
+    return narrow(widen(a) * widen(b));
+  }
+  __device__ static __forceinline__ uint16_t max(uint16_t a, uint16_t b) {
+    return (widen(a) < widen(b)) ? b : a;
+  }
+  __device__ static __forceinline__ uint16_t min(uint16_t a, uint16_t b) {
+    return (widen(b) < widen(a)) ? b : a;
+  }
+};
+
+// bfloat16 held as raw bits (c10::BFloat16 semantics: widen by <<16, op in
+// f32, round-to-nearest-even back; v_cvt_pk_bf16_f32 on gfx950).
+struct TrBF16 {
+  using Storage = uint16_t;
+  __device__ static __forceinline__ float widen(uint16_t x) {
+    return __builtin_bit_cast(float, (uint32_t)x << 16);
+  }
+  __device__ static __forceinline__ uint16_t narrow(float f) {
+    return __builtin_bit_cast(uint16_t, (__bf16)f);
+  }
+  __device__ static __forceinline__ uint16_t sum(uint16_t a, uint16_t b) {
+    return narrow(widen(a) + widen(b));
+  }
+  __device__ static __forceinline__ uint16_t product(uint16_t a, uint16_t b) {
+    return narrow(widen(a) * widen(b));
+  }
+  __device__ static __forceinline__ uint16_t max(uint16_t a, uint16_t b) {
+    return (widen(a) < widen(b)) ? b : a;
+  }
+  __device__ static __forceinline__ uint16_t min(uint16_t a, uint16_t b) {
+    return (widen(b) < widen(a)) ? b : a;
+  }
+};
+
+template <class Tr, int OP>
+__device__ __forceinline__ typename Tr::Storage apply(typename Tr::Storage a,
+                                                      typename Tr::Storage b) {
+  if constexpr (OP == GLOO_HIP_SUM) return Tr::sum(a, b);
+  else if constexpr (OP == GLOO_HIP_PRODUCT) return Tr::product(a, b);
+  else if constexpr (OP == GLOO_HIP_MAX) return Tr::max(a, b);
+  else return Tr::min(a, b);
+}
+
+// Apply the op lane-wise to one 16-byte packet.
+template <class Tr, int OP>
+__device__ __forceinline__ u32x4 apply_packet(u32x4 a, u32x4 b) {
+  using S = typename Tr::Storage;
+  constexpr int kV = 16 / sizeof(S);
+  union P {
+    u32x4 v;
+    S e[kV];
+  };
+  P pa, pb, pc;
+  pa.v = a;
+  pb.v = b;
+#pragma unroll
+  for (int i = 0; i < kV; i++) pc.e[i] = apply<Tr, OP>(pa.e[i], pb.e[i]);
+  return pc.v;
+}
+
+// Byte-lane SWAR specialisations: 16 int8/uint8 adds in 4 dword ops each
+// instead of 16 extract/insert sequences.  Wrap semantics are identical.
+__device__ __forceinline__ uint32_t swar_add8(uint32_t a, uint32_t b) {
+  return ((a & 0x7f7f7f7fu) + (b & 0x7f7f7f7fu)) ^ ((a ^ b) & 0x80808080u);
+}
+template <>
+__device__ __forceinline__ u32x4 apply_packet<TrI8, GLOO_HIP_SUM>(u32x4 a, u32x4 b) {
+  return u32x4{swar_add8(a.x, b.x), swar_add8(a.y, b.y), swar_add8(a.z, b.z),
+               swar_add8(a.w, b.w)};
+}
+template <>
+__device__ __forceinline__ u32x4 apply_packet<TrU8, GLOO_HIP_SUM>(u32x4 a, u32x4 b) {
+  return u32x4{swar_add8(a.x, b.x), swar_add8(a.y, b.y), swar_add8(a.z, b.z),
+               swar_add8(a.w, b.w)};
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// Element-wise head / tail: elements [0, head) and [tail0, n) of the chunk,
+// done by the first block's lanes.  Disjoint from the vector body, so safe
+// under c == a aliasing.
+template <class Tr, int OP>
+__device__ __forceinline__ void edges(typename Tr::Storage* c,
+                                      const typename Tr::Storage* a,
+                                      const typename Tr::Storage* b,
+                                      size_t head, size_t tail0, size_t n) {
+  const size_t t = threadIdx.x;
+  if (t < head) c[t] = apply<Tr, OP>(a[t], b[t]);
+  const size_t j = tail0 + t;
+  if (j < n) c[j] = apply<Tr, OP>(a[j], b[j]);
+}
+
+// Aligned body.  c, a, b are congruent modulo 16 B; `head` elements bring
+// them to a 16-B boundary.  Tile = kBlock lanes x UNROLL packets; within a
+// tile packet u of lane t is at t + u*kBlock (each wave-instruction covers
+// 1 KiB contiguous).  PERSIST: grid-stride over tiles with a capped grid.
+template <class Tr, int OP, int UNROLL, bool NTL, bool NTS, bool PERSIST>
+__global__ __launch_bounds__(kBlock) void reduce_vec_kernel(
+    typename Tr::Storage* c, const typename Tr::Storage* a,
+    const typename Tr::Storage* b, size_t n, size_t head) {
+  using S = typename Tr::Storage;
+  constexpr int kV = 16 / sizeof(S);
+  constexpr size_t kTile = (size_t)kBlock * UNROLL;
+  const size_t nvec = (n - head) / kV;
+  u32x4* cv = reinterpret_cast<u32x4*>(c + head);
+  const u32x4* av = reinterpret_cast<const u32x4*>(a + head);
+  const u32x4* bv = reinterpret_cast<const u32x4*>(b + head);
+
+  if (blockIdx.x == 0) edges<Tr, OP>(c, a, b, head, head + nvec * kV, n);
+
+  const size_t ntiles_full = nvec / kTile;
+  size_t tile = blockIdx.x;
+  const size_t step = PERSIST ? gridDim.x : ntiles_full + 1;
+  for (; tile < ntiles_full; tile += step) {
+    const size_t base = tile * kTile + threadIdx.x;
+    u32x4 ra[UNROLL], rb[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) ra[u] = ld16<NTL>(av + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) rb[u] = ld16<NTL>(bv + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++)
+      st16<NTS>(cv + base + u * kBlock, apply_packet<Tr, OP>(ra[u], rb[u]));
+    if constexpr (!PERSIST) return;
+  }
+  // Ragged last tile (at most one): guarded packets.
+  if (tile == ntiles_full) {
+    const size_t base = tile * kTile + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      const size_t i = base + u * kBlock;
+      if (i < nvec) st16<NTS>(cv + i, apply_packet<Tr, OP>(ld16<NTL>(av + i), ld16<NTL>(bv + i)));
+    }
+  }
+}
+
+// Operands with different misalignment: element-wise, coalesced (lane t of
+// a wave touches element t), UNROLL elements per lane in flight.
+template <class Tr, int OP, int UNROLL>
+__global__ __launch_bounds__(kBlock) void reduce_elem_kernel(
+    typename Tr::Storage* c, const typename Tr::Storage* a,
+    const typename Tr::Storage* b, size_t n) {
+  using S = typename Tr::Storage;
+  const size_t base = (size_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
+  S ra[UNROLL], rb[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; u++) {
+    const size_t i = base + (size_t)u * kBlock;
+    if (i < n) {
+      ra[u] = a[i];
+      rb[u] = b[i];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; u++) {
+    const size_t i = base + (size_t)u * kBlock;
+    if (i < n) c[i] = apply<Tr, OP>(ra[u], rb[u]);
+  }
+}
+
+// Multi-source left fold dst = ((s0 op s1) op s2) ... in one pass.
+struct SrcList {
+  const void* p[GLOO_HIP_MAX_SRCS];
+};
+
+template <class Tr, int OP, int UNROLL>
+__global__ __launch_bounds__(kBlock) void reduce_multi_vec_kernel(
+    typename Tr::Storage* dst, SrcList srcs, int k, size_t n, size_t head) {
+  using S = typename Tr::Storage;
+  constexpr int kV = 16 / sizeof(S);
+  constexpr size_t kTile = (size_t)kBlock * UNROLL;
+  const size_t nvec = (n - head) / kV;
+  const size_t tail0 = head + nvec * kV;
+  if (blockIdx.x == 0) {
+    const size_t t = threadIdx.x;
+    for (int pass = 0; pass < 2; pass++) {
+      const size_t i = pass == 0 ? t : tail0 + t;
+      if ((pass == 0 && t < head) || (pass == 1 && i < n)) {
+        S acc = static_cast<const S*>(srcs.p[0])[i];
+        for (int j = 1; j < k; j++) acc = apply<Tr, OP>(acc, static_cast<const S*>(srcs.p[j])[i]);
+        dst[i] = acc;
+      }
+    }
+  }
+  const size_t base = (size_t)blockIdx.x * kTile + threadIdx.x;
+  u32x4 acc[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; u++) {
+    const size_t i = base + u * kBlock;
+    if (i < nvec) acc[u] = reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[0]) + head)[i];
+  }
+  for (int j = 1; j < k; j++) {
+    const u32x4* sv = reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[j]) + head);
+    u32x4 r[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      const size_t i = base + u * kBlock;
+      if (i < nvec) r[u] = sv[i];
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) acc[u] = apply_packet<Tr, OP>(acc[u], r[u]);
+  }
+  u32x4* dv = reinterpret_cast<u32x4*>(dst + head);
+#pragma unroll
+  for (int u = 0; u < UNROLL; u++) {
+    const size_t i = base + u * kBlock;
+    if (i < nvec) dv[i] = acc[u];
+  }
+}
+
+template <class Tr, int OP, int UNROLL>
+__global__ __launch_bounds__(kBlock) void reduce_multi_elem_kernel(
+    typename Tr::Storage* dst, SrcList srcs, int k, size_t n) {
+  using S = typename Tr::Storage;
+  const size_t base = (size_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < UNROLL; u++) {
+    const size_t i = base + (size_t)u * kBlock;
+    if (i < n) {
+      S acc = static_cast<const S*>(srcs.p[0])[i];
+      for (int j = 1; j < k; j++) acc = apply<Tr, OP>(acc, static_cast<const S*>(srcs.p[j])[i]);
+      dst[i] = acc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side dispatch.
+// ---------------------------------------------------------------------------
+thread_local char g_last_error[512] = "";
+int g_variant = 0;  // fp32 SUM kernel variant (measurement knob)
+
+int set_error(int code, const char* what) {
+  snprintf(g_last_error, sizeof(g_last_error), "%s", what);
+  return code;
+}
+
+int check_launch(const char* name) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_last_error, sizeof(g_last_error), "%s: %s", name, hipGetErrorString(e));
+    return (int)e;
+  }
+  return GLOO_HIP_OK;
+}
+
+constexpr int kDefaultUnroll = 4;
+constexpr int kElemUnroll = 4;
+constexpr int kMultiUnroll = 2;
+
+inline size_t ceil_div(size_t a, size_t b) { return (a + b - 1) / b; }
+
+template <class Tr, int OP, int UNROLL, bool NTL, bool NTS, bool PERSIST>
+int launch_vec(void* c, const void* a, const void* b, size_t n, size_t head,
+               hipStream_t s) {
+  using S = typename Tr::Storage;
+  constexpr int kV = 16 / sizeof(S);
+  const size_t nvec = (n - head) / kV;
+  size_t grid = ceil_div(nvec, (size_t)kBlock * UNROLL);
+  if (grid == 0) grid = 1;
+  if (PERSIST) {
+    const size_t cap = 256 * 8;  // 8 blocks per CU on 256 CUs
+    if (grid > cap) grid = cap;
+  }
+  reduce_vec_kernel<Tr, OP, UNROLL, NTL, NTS, PERSIST><<<dim3((unsigned)grid), dim3(kBlock), 0, s>>>(
+      static_cast<S*>(c), static_cast<const S*>(a), static_cast<const S*>(b), n, head);
+  return check_launch("reduce_vec_kernel");
+}
+
+template <class Tr, int OP>
+int launch3(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
+  using S = typename Tr::Storage;
+  constexpr size_t kV = 16 / sizeof(S);
+  if (n == 0) return GLOO_HIP_OK;
+  const uintptr_t pc = (uintptr_t)c, pa = (uintptr_t)a, pb = (uintptr_t)b;
+  if ((pc % sizeof(S)) || (pa % sizeof(S)) || (pb % sizeof(S)))
+    return set_error(GLOO_HIP_EINVAL_PTR, "pointer not aligned to the element size");
+  if (((pc ^ pa) & 15) == 0 && ((pc ^ pb) & 15) == 0) {
+    size_t head = ((16 - (pc & 15)) & 15) / sizeof(S);
+    if (head > n) head = n;
+    (void)kV;
+    if constexpr (std::is_same<Tr, TrF32>::value && OP == GLOO_HIP_SUM) {
+      switch (g_variant) {
+        case 1: return launch_vec<Tr, OP, 1, false, false, false>(c, a, b, n, head, s);
+        case 2: return launch_vec<Tr, OP, 2, false, false, false>(c, a, b, n, head, s);
+        case 3: return launch_vec<Tr, OP, 4, false, false, false>(c, a, b, n, head, s);
+        case 4: return launch_vec<Tr, OP, 8, false, false, false>(c, a, b, n, head, s);
+        case 5: return launch_vec<Tr, OP, 4, true, false, false>(c, a, b, n, head, s);
+        case 6: return launch_vec<Tr, OP, 4, false, true, false>(c, a, b, n, head, s);
+        case 7: return launch_vec<Tr, OP, 4, true, true, false>(c, a, b, n, head, s);
+        case 8: return launch_vec<Tr, OP, 4, false, false, true>(c, a, b, n, head, s);
+        case 9: return launch_vec<Tr, OP, 8, false, true, false>(c, a, b, n, head, s);
+        case 10: return launch_vec<Tr, OP, 2, false, true, false>(c, a, b, n, head, s);
+        case 11: return launch_vec<Tr, OP, 8, true, true, true>(c, a, b, n, head, s);
+        default: break;
+      }
+    }
+    return launch_vec<Tr, OP, kDefaultUnroll, false, false, false>(c, a, b, n, head, s);
+  }
+  const size_t grid = ceil_div(n, (size_t)kBlock * kElemUnroll);
+  reduce_elem_kernel<Tr, OP, kElemUnroll><<<dim3((unsigned)grid), dim3(kBlock), 0, s>>>(
+      static_cast<S*>(c), static_cast<const S*>(a), static_cast<const S*>(b), n);
+  return check_launch("reduce_elem_kernel");
+}
+
+template <class Tr, int OP>
+int launch_multi(void* dst, const void* const* srcs, int k, size_t n, hipStream_t s) {
+  using S = typename Tr::Storage;
+  if (n == 0) return GLOO_HIP_OK;
+  SrcList list;
+  memset(&list, 0, sizeof(list));
+  const uintptr_t pd = (uintptr_t)dst;
+  if (pd % sizeof(S)) return set_error(GLOO_HIP_EINVAL_PTR, "dst not aligned to the element size");
+  bool congruent = true;
+  for (int j = 0; j < k; j++) {
+    if (srcs[j] == nullptr) return set_error(GLOO_HIP_EINVAL_PTR, "null source pointer");
+    const uintptr_t p = (uintptr_t)srcs[j];
+    if (p % sizeof(S)) return set_error(GLOO_HIP_EINVAL_PTR, "source not aligned to the element size");
+    if ((p ^ pd) & 15) congruent = false;
+    list.p[j] = srcs[j];
+  }
+  if (congruent) {
+    size_t head = ((16 - (pd & 15)) & 15) / sizeof(S);
+    if (head > n) head = n;
+    constexpr int kV = 16 / sizeof(S);
+    const size_t nvec = (n - head) / kV;
+    size_t grid = ceil_div(nvec, (size_t)kBlock * kMultiUnroll);
+    if (grid == 0) grid = 1;
+    reduce_multi_vec_kernel<Tr, OP, kMultiUnroll><<<dim3((unsigned)grid), dim3(kBlock), 0, s>>>(
+        static_cast<S*>(dst), list, k, n, head);
+    return check_launch("reduce_multi_vec_kernel");
+  }
+  const size_t grid = ceil_div(n, (size_t)kBlock * kElemUnroll);
+  reduce_multi_elem_kernel<Tr, OP, kElemUnroll><<<dim3((unsigned)grid), dim3(kBlock), 0, s>>>(
+      static_cast<S*>(dst), list, k, n);
+  return check_launch("reduce_multi_elem_kernel");
+}
+
+template <class Tr>
+int by_op3(int op, void* c, const void* a, const void* b, size_t n, hipStream_t s) {
+  switch (op) {
+    case GLOO_HIP_SUM: return launch3<Tr, GLOO_HIP_SUM>(c, a, b, n, s);
+    case GLOO_HIP_PRODUCT: return launch3<Tr, GLOO_HIP_PRODUCT>(c, a, b, n, s);
+    case GLOO_HIP_MAX: return launch3<Tr, GLOO_HIP_MAX>(c, a, b, n, s);
+    case GLOO_HIP_MIN: return launch3<Tr, GLOO_HIP_MIN>(c, a, b, n, s);
+    default: return set_error(GLOO_HIP_EINVAL_OP, "unknown reduction op");
+  }
+}
+
+template <class Tr>
+int by_op_multi(int op, void* d, const void* const* srcs, int k, size_t n, hipStream_t s) {
+  switch (op) {
+    case GLOO_HIP_SUM: return launch_multi<Tr, GLOO_HIP_SUM>(d, srcs, k, n, s);
+    case GLOO_HIP_PRODUCT: return launch_multi<Tr, GLOO_HIP_PRODUCT>(d, srcs, k, n, s);
+    case GLOO_HIP_MAX: return launch_multi<Tr, GLOO_HIP_MAX>(d, srcs, k, n, s);
+    case GLOO_HIP_MIN: return launch_multi<Tr, GLOO_HIP_MIN>(d, srcs, k, n, s);
+    default: return set_error(GLOO_HIP_EINVAL_OP, "unknown reduction op");
+  }
+}
+
+int dispatch3(int op, int dtype, void* c, const void* a, const void* b, size_t n,
+              hipStream_t s) {
+  switch (dtype) {
+    case GLOO_HIP_I8: return by_op3<TrI8>(op, c, a, b, n, s);
+    case GLOO_HIP_U8: return by_op3<TrU8>(op, c, a, b, n, s);
+    case GLOO_HIP_I32: return by_op3<TrI32>(op, c, a, b, n, s);
+    case GLOO_HIP_U32: return by_op3<TrU32>(op, c, a, b, n, s);
+    case GLOO_HIP_I64: return by_op3<TrI64>(op, c, a, b, n, s);
+    case GLOO_HIP_U64: return by_op3<TrU64>(op, c, a, b, n, s);
+    case GLOO_HIP_F16: return by_op3<TrF16>(op, c, a, b, n, s);
+    case GLOO_HIP_BF16: return by_op3<TrBF16>(op, c, a, b, n, s);
+    case GLOO_HIP_F32: return by_op3<TrF32>(op, c, a, b, n, s);
+    case GLOO_HIP_F64: return by_op3<TrF64>(op, c, a, b, n, s);
+    default: return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
+  }
+}
+
+int dispatch_multi(int op, int dtype, void* d, const void* const* srcs, int k, size_t n,
+                   hipStream_t s) {
+  switch (dtype) {
+    case GLOO_HIP_I8: return by_op_multi<TrI8>(op, d, srcs, k, n, s);
+    case GLOO_HIP_U8: return by_op_multi<TrU8>(op, d, srcs, k, n, s);
+    case GLOO_HIP_I32: return by_op_multi<TrI32>(op, d, srcs, k, n, s);
+    case GLOO_HIP_U32: return by_op_multi<TrU32>(op, d, srcs, k, n, s);
+    case GLOO_HIP_I64: return by_op_multi<TrI64>(op, d, srcs, k, n, s);
+    case GLOO_HIP_U64: return by_op_multi<TrU64>(op, d, srcs, k, n, s);
+    case GLOO_HIP_F16: return by_op_multi<TrF16>(op, d, srcs, k, n, s);
+    case GLOO_HIP_BF16: return by_op_multi<TrBF16>(op, d, srcs, k, n, s);
+    case GLOO_HIP_F32: return by_op_multi<TrF32>(op, d, srcs, k, n, s);
+    case GLOO_HIP_F64: return by_op_multi<TrF64>(op, d, srcs, k, n, s);
+    default: return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
+  }
+}
+
+}  // namespace
+}  // namespace gloo_amd
+
+using namespace gloo_amd;
+
+extern "C" {
+
+int gloo_hip_reduce3(int op, int dtype, void* c, const void* a, const void* b, size_t n,
+                     gloo_hip_stream_t stream) {
+  if (n == 0) {
+    if (op < GLOO_HIP_SUM || op > GLOO_HIP_MIN) return set_error(GLOO_HIP_EINVAL_OP, "unknown reduction op");
+    if (dtype < 0 || dtype >= GLOO_HIP_NUM_DTYPES) return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
+    return GLOO_HIP_OK;
+  }
+  if (!c || !a || !b) return set_error(GLOO_HIP_EINVAL_PTR, "null buffer pointer");
+  return dispatch3(op, dtype, c, a, b, n, static_cast<hipStream_t>(stream));
+}
+
+int gloo_hip_reduce(int op, int dtype, void* dst, const void* src, size_t n,
+                    gloo_hip_stream_t stream) {
+  return gloo_hip_reduce3(op, dtype, dst, dst, src, n, stream);
+}
+
+int gloo_hip_reduce_multi(int op, int dtype, void* dst, const void* const* srcs, int k,
+                          size_t n, gloo_hip_stream_t stream) {
+  if (k < 1 || k > GLOO_HIP_MAX_SRCS) return set_error(GLOO_HIP_EINVAL_ARG, "source count out of range");
+  if (op < GLOO_HIP_SUM || op > GLOO_HIP_MIN) return set_error(GLOO_HIP_EINVAL_OP, "unknown reduction op");
+  if (dtype < 0 || dtype >= GLOO_HIP_NUM_DTYPES) return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
+  if (n == 0) return GLOO_HIP_OK;
+  if (!dst || !srcs) return set_error(GLOO_HIP_EINVAL_PTR, "null buffer pointer");
+  return dispatch_multi(op, dtype, dst, srcs, k, n, static_cast<hipStream_t>(stream));
+}
+
+size_t gloo_hip_dtype_size(int dtype) {
+  static const size_t kSizes[GLOO_HIP_NUM_DTYPES] = {1, 1, 4, 4, 8, 8, 2, 2, 4, 8};
+  if (dtype < 0 || dtype >= GLOO_HIP_NUM_DTYPES) return 0;
+  return kSizes[dtype];
+}
+
+const char* gloo_hip_last_error(void) { return g_last_error; }
+
+const char* gloo_hip_version(void) { return "0.1.0"; }
+
+int gloo_hip_set_variant(int variant) {
+  const int prev = g_variant;
+  g_variant = variant;
+  return prev;
+}
+
+}  // extern "C"

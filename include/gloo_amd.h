@@ -1,0 +1,123 @@
+/*
+ * gloo_amd.h — C-ABI of the MI355X-native Gloo per-chunk reduction.
+ *
+ * This is the drop-in boundary for Gloo's hot path: the element-wise
+ * sum / product / max / min that every allreduce / reduce-scatter schedule
+ * applies to each arriving chunk.  Plain pointers, sizes and integer enums
+ * only; no HIP, torch or C++ types cross this boundary, and no C++ exception
+ * ever escapes it (every entry point returns a status code).
+ *
+ * Reference interfaces replaced (paths relative to facebookincubator/gloo):
+ *   gloo_hip_reduce   <- gloo::cudaSum/cudaProduct/cudaMax/cudaMin<T>
+ *                        (gloo/cuda.h:274-284, kernels gloo/cuda.cu:283-401),
+ *                        i.e. the device overload of
+ *                        CudaReductionFunction<T>::call (gloo/cuda.h:326-333):
+ *                        dst[i] = dst[i] (op) src[i], async on `stream`.
+ *   gloo_hip_reduce3  <- the 3-operand host form gloo::sum/product/max/min<T>
+ *                        (void* c, const void* a, const void* b, size_t n)
+ *                        (gloo/math.h:15-73), which is also the new-style
+ *                        reduce `Func` signature (gloo/allreduce.h:36).
+ *   gloo_hip_op_t     <- gloo::ReductionType (gloo/algorithm.h:49-57).
+ *   gloo_hip_dtype_t  <- the union of the instantiation lists of
+ *                        gloo/cuda.cu:265-272,394-401 and
+ *                        gloo/test/math_test.cc:23-32.
+ *
+ * Semantics (bit-exact with gloo/math.h evaluated in the listed order):
+ *   SUM      c = a + b      (integers wrap modulo 2^bits)
+ *   PRODUCT  c = a * b      (integers wrap modulo 2^bits)
+ *   MAX      c = (a < b) ? b : a      == std::max(a, b)  (gloo/math.h:51)
+ *   MIN      c = (b < a) ? b : a      == std::min(a, b)  (gloo/math.h:66)
+ *   For the in-place form a := dst, b := src, so a NaN already in dst is kept
+ *   and a NaN arriving in src is ignored by MAX/MIN, exactly as
+ *   `if (src op dst) dst = src` in gloo/cuda.cu:337-355.
+ *   f16 / bf16: both operands widened to f32, op in f32, rounded back to
+ *   nearest-even (gloo/math.cc:17-97 F16C path; c10::BFloat16 for bf16);
+ *   MAX/MIN compare in f32 and copy the raw 16-bit operand.
+ *
+ * Buffers may start at any element-aligned address and `c` may alias `a`
+ * (the in-place call).  n may be 0.  The functions never allocate, free or
+ * synchronise: they enqueue one kernel on `stream` and return.
+ */
+#ifndef GLOO_AMD_H_
+#define GLOO_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Mirrors gloo::ReductionType (gloo/algorithm.h:49-57). */
+typedef enum {
+  GLOO_HIP_SUM = 1,
+  GLOO_HIP_PRODUCT = 2,
+  GLOO_HIP_MAX = 3,
+  GLOO_HIP_MIN = 4,
+} gloo_hip_op_t;
+
+typedef enum {
+  GLOO_HIP_I8 = 0,
+  GLOO_HIP_U8 = 1,
+  GLOO_HIP_I32 = 2,
+  GLOO_HIP_U32 = 3,
+  GLOO_HIP_I64 = 4,
+  GLOO_HIP_U64 = 5,
+  GLOO_HIP_F16 = 6,
+  GLOO_HIP_BF16 = 7,
+  GLOO_HIP_F32 = 8,
+  GLOO_HIP_F64 = 9,
+  GLOO_HIP_NUM_DTYPES = 10,
+} gloo_hip_dtype_t;
+
+/* Status codes: 0 = success, > 0 = a hipError_t, < 0 = argument error. */
+#define GLOO_HIP_OK 0
+#define GLOO_HIP_EINVAL_OP (-1)
+#define GLOO_HIP_EINVAL_DTYPE (-2)
+#define GLOO_HIP_EINVAL_PTR (-3)
+#define GLOO_HIP_EINVAL_ARG (-4)
+
+/* A hipStream_t passed as an opaque pointer (NULL = the default stream). */
+typedef void* gloo_hip_stream_t;
+
+/* In-place per-chunk reduction: dst[i] = dst[i] (op) src[i], i < n.
+ * Replaces cudaSum/cudaProduct/cudaMax/cudaMin<T> (gloo/cuda.cu:283-401). */
+int gloo_hip_reduce(int op, int dtype, void* dst, const void* src, size_t n,
+                    gloo_hip_stream_t stream);
+
+/* Three-operand form: c[i] = a[i] (op) b[i]; c may alias a or b.
+ * Replaces gloo::sum/product/max/min<T>(c, a, b, n) (gloo/math.h:15-73). */
+int gloo_hip_reduce3(int op, int dtype, void* c, const void* a, const void* b,
+                     size_t n, gloo_hip_stream_t stream);
+
+/* Multi-source local reduction: dst[i] = (((srcs[0][i] op srcs[1][i]) op
+ * srcs[2][i]) ... op srcs[k-1][i]), left to right, in ONE pass over HBM.
+ * dst may alias srcs[0].  This is the fused form of the reference's local
+ * multi-pointer loop `for i in 1..k: fn(ptrs[0], ptrs[i], count)`
+ * (gloo/allreduce_local.cc:28-33, gloo/allreduce_ring_chunked.h:89-91),
+ * bit-identical to it because the association order is the same.
+ * k must be in [1, GLOO_HIP_MAX_SRCS]; srcs is a HOST array of k device
+ * pointers. */
+#define GLOO_HIP_MAX_SRCS 8
+int gloo_hip_reduce_multi(int op, int dtype, void* dst,
+                          const void* const* srcs, int k, size_t n,
+                          gloo_hip_stream_t stream);
+
+/* Size in bytes of one element of `dtype`, or 0 when dtype is unknown. */
+size_t gloo_hip_dtype_size(int dtype);
+
+/* Human-readable text of the last error raised on the calling thread. */
+const char* gloo_hip_last_error(void);
+
+/* Library version, "MAJOR.MINOR.PATCH". */
+const char* gloo_hip_version(void);
+
+/* Tuning knob for the measurement harness: select the kernel variant used by
+ * the fp32 SUM path.  0 = default (tuned).  Returns the previous value. */
+int gloo_hip_set_variant(int variant);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* GLOO_AMD_H_ */

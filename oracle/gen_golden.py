@@ -1,0 +1,184 @@
+"""Generate tests/golden/*.npz from the REFERENCE itself.  TEST INFRASTRUCTURE.
+
+Runs only where /root/reference exists (this build container): it calls
+oracle/_ref/libgloo_ref.so, which oracle/Makefile compiles from the unmodified
+reference sources, and records inputs + reference outputs as data fixtures.
+The fixtures (not the reference) travel to the GPU box.
+
+  math_golden.npz      gloo::sum/product/max/min<T>(c, a, b, n), gloo/math.h:15-73,
+                       every dtype of include/gloo_amd.h, n = 4099, inputs with
+                       zeros / infs / NaNs / denormals sprinkled in.  fp16 via the
+                       F16C body (gloo/math.cc:17-97); bf16 via c10::BFloat16.
+  sched_golden.npz     AllreduceRingChunked / AllreduceHalvingDoubling /
+                       AllreduceRing / ReduceScatterHalvingDoubling outputs at
+                       P ranks (threads over the reference's TCP transport).
+
+Usage:  make -C oracle ref && python oracle/gen_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import oracle  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+SEED = 20240601
+
+ALGOS = {"ring_chunked": 0, "halving_doubling": 1, "ring": 2, "local": 3}
+
+
+def special_floats(npt):
+    f = np.finfo(npt)
+    return np.array([0.0, -0.0, np.inf, -np.inf, np.nan, f.tiny / 4, -f.tiny / 8, f.max,
+                     -f.max, 1.0, -1.0], dtype=npt)
+
+
+def make_inputs(dtype, n, rng):
+    code, npt = oracle.DTYPES[dtype]
+    if dtype in ("f32", "f64"):
+        x = (rng.standard_normal(n) * np.where(rng.random(n) < 0.5, 1.0, 1e-3)).astype(npt)
+        sp = special_floats(npt)
+        idx = rng.integers(0, n, n // 40)
+        x[idx] = sp[rng.integers(0, len(sp), len(idx))]
+        return x
+    if dtype in ("f16", "bf16"):
+        # random finite values of a sane range plus special encodings
+        f = (rng.standard_normal(n) * 4).astype(np.float32)
+        conv = oracle.lib().oracle_f32_to_f16 if dtype == "f16" else oracle.lib().oracle_f32_to_bf16
+        x = np.array([conv(float(v)) for v in f], dtype=np.uint16)
+        if dtype == "f16":
+            sp = np.array([0x0000, 0x8000, 0x7C00, 0xFC00, 0x7E00, 0x0001, 0x83FF, 0x7BFF, 0xFBFF,
+                           0x3C00, 0xBC00], dtype=np.uint16)
+        else:
+            sp = np.array([0x0000, 0x8000, 0x7F80, 0xFF80, 0x7FC0, 0x0001, 0x807F, 0x7F7F, 0xFF7F,
+                           0x3F80, 0xBF80], dtype=np.uint16)
+        idx = rng.integers(0, n, n // 40)
+        x[idx] = sp[rng.integers(0, len(sp), len(idx))]
+        return x
+    return rng.integers(0, 256, n * np.dtype(npt).itemsize, dtype=np.uint8).view(npt)
+
+
+def gen_math():
+    rng = np.random.default_rng(SEED)
+    n = 4099
+    out = {}
+    for dtype in oracle.DTYPES:
+        a = make_inputs(dtype, n, rng)
+        b = make_inputs(dtype, n, rng)
+        out[f"{dtype}/a"] = a
+        out[f"{dtype}/b"] = b
+        for op in oracle.OPS:
+            out[f"{dtype}/{op}"] = oracle.ref_reduce3(op, dtype, a, b)
+    # App. A.1: the scalar float16 path as shipped without GLOO_USE_AVX.
+    a = np.array([0x5359], dtype=np.uint16)
+    b = np.array([0x7532], dtype=np.uint16)
+    c = np.empty_like(a)
+    oracle.ref().ref_reduce3_f16_scalar(1, c.ctypes.data, a.ctypes.data, b.ctypes.data, 1)
+    out["f16_scalar_defect/a"], out["f16_scalar_defect/b"], out["f16_scalar_defect/sum"] = a, b, c
+    np.savez_compressed(os.path.join(OUT, "math_golden.npz"), **out)
+    print("math_golden.npz:", len(out), "arrays")
+
+
+def ref_allreduce(algo, op, dtype, inputs):
+    code, npt = oracle.DTYPES[dtype]
+    P, k, n = inputs.shape
+    out = np.empty_like(inputs)
+    rc = oracle.ref().ref_allreduce(ALGOS[algo], oracle.OPS[op], code, P, k, n,
+                                    inputs.ctypes.data, out.ctypes.data)
+    if rc:
+        raise RuntimeError(f"ref_allreduce({algo},{P},{n}) = {rc}: {oracle.ref().ref_last_error()}")
+    return out
+
+
+def ref_reduce_scatter(op, dtype, inputs, recv):
+    code, npt = oracle.DTYPES[dtype]
+    P, n = inputs.shape
+    out = np.empty_like(inputs)
+    recv = np.ascontiguousarray(recv, dtype=np.int32)
+    rc = oracle.ref().ref_reduce_scatter(oracle.OPS[op], code, P, n, recv.ctypes.data,
+                                         inputs.ctypes.data, out.ctypes.data)
+    if rc:
+        raise RuntimeError(f"ref_reduce_scatter({P},{n}) = {rc}: {oracle.ref().ref_last_error()}")
+    return out
+
+
+def even_recv(P, n):
+    """recvElems exactly as gloo/test/reduce_scatter_test.cc:86-92 builds them."""
+    out, rem, chunk = [], n, (n + P - 1) // P
+    for _ in range(P):
+        out.append(min(chunk, rem))
+        rem = rem - chunk if rem > chunk else 0
+    return np.array(out, dtype=np.int32)
+
+
+def sched_inputs(dtype, op, shape, rng):
+    code, npt = oracle.DTYPES[dtype]
+    if op == "product":
+        f = rng.uniform(0.5, 2.0, shape).astype(np.float32)
+    else:
+        f = rng.standard_normal(shape).astype(np.float32)
+    if dtype == "f32":
+        return f
+    if dtype == "f64":
+        return f.astype(np.float64)
+    conv = oracle.lib().oracle_f32_to_f16 if dtype == "f16" else oracle.lib().oracle_f32_to_bf16
+    return np.vectorize(lambda v: conv(float(v)), otypes=[np.uint16])(f)
+
+
+def gen_sched():
+    rng = np.random.default_rng(SEED + 1)
+    out = {}
+    cases = []
+    for P in (1, 2, 3, 5, 8):
+        for n in (1, 1000) + ((10007,) if P in (3, 8) else ()):
+            cases.append(("ring_chunked", "sum", "f32", P, 1, n))
+    cases += [("ring_chunked", "sum", "f32", 3, 2, 1000), ("ring_chunked", "max", "f32", 5, 1, 999),
+              ("ring_chunked", "sum", "f64", 4, 1, 4099), ("ring_chunked", "product", "f32", 3, 1, 777)]
+    for P in (1, 2, 3, 5, 6, 8):
+        for n in (1, 64, 1000) + ((10007,) if P in (5, 8) else ()):
+            cases.append(("halving_doubling", "sum", "f32", P, 1, n))
+    cases += [("halving_doubling", "min", "f32", 5, 1, 1000), ("halving_doubling", "sum", "f32", 3, 3, 500),
+              ("halving_doubling", "sum", "f64", 7, 1, 3001)]
+    cases += [("ring", "sum", "f32", 3, 1, 1000), ("ring", "sum", "f32", 8, 1, 4096),
+              ("local", "sum", "f32", 1, 4, 1000)]
+    for algo, op, dtype, P, k, n in cases:
+        x = sched_inputs(dtype, op, (P, k, n), rng)
+        y = ref_allreduce(algo, op, dtype, x)
+        key = f"{algo}/{op}/{dtype}/P{P}/k{k}/n{n}"
+        out[key + "/in"] = x
+        if algo == "ring":
+            # AllreduceRing folds in a rank-dependent order
+            # (gloo/allreduce_ring.h:80-90): ranks differ in the last bits.
+            out[key + "/out"] = y[:, 0].copy()
+        else:
+            # every rank and pointer ends with the same bytes; keep one copy
+            assert all((y[r, j].view(np.uint8) == y[0, 0].view(np.uint8)).all()
+                       for r in range(P) for j in range(k)), key
+            out[key + "/out"] = y[0, 0].copy()
+    rs_cases = []
+    for P in (1, 2, 3, 5, 8):
+        for n in (100,) + ((10007,) if P in (3, 8) else ()):
+            rs_cases.append(("sum", "f32", P, n))
+    for dtype in ("f16", "bf16"):
+        for op in ("sum", "product", "max", "min"):
+            rs_cases.append((op, dtype, 8, 4096))
+    rs_cases.append(("sum", "f16", 4, 1024))  # gloo/test/reduce_scatter_test.cc HalfPrecisionTest shape
+    for op, dtype, P, n in rs_cases:
+        x = sched_inputs(dtype, op, (P, n), rng)
+        recv = even_recv(P, n)
+        y = ref_reduce_scatter(op, dtype, x, recv)
+        key = f"reduce_scatter/{op}/{dtype}/P{P}/n{n}"
+        out[key + "/in"] = x
+        out[key + "/recv"] = recv
+        # only rank r's reduced block out[r, :recv[r]] is defined; concatenate
+        out[key + "/out"] = np.concatenate([y[r, :recv[r]] for r in range(P)])
+    np.savez_compressed(os.path.join(OUT, "sched_golden.npz"), **out)
+    print("sched_golden.npz:", len(out), "arrays")
+
+
+if __name__ == "__main__":
+    os.makedirs(OUT, exist_ok=True)
+    gen_math()
+    gen_sched()

@@ -1,0 +1,59 @@
+"""CPU: the C-ABI library loads, exports every symbol include/gloo_amd.h
+declares, and rejects bad arguments without touching the GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    text = open(os.path.join(ROOT, "include", "gloo_amd.h")).read()
+    return sorted(set(re.findall(r"^\s*[\w\s\*]+?\b(gloo_hip_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    import gloo_amd
+    assert set(declared_functions()) == set(gloo_amd.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(os.path.join(ROOT, "gloo_amd", "libgloo_amd.so"))
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+
+
+def test_zero_length_and_argument_errors():
+    import gloo_amd
+    # n == 0 is a no-op that never reaches HIP (gloo allows count == 0)
+    assert gloo_amd.lib.gloo_hip_reduce(1, 8, None, None, 0, None) == 0
+    assert gloo_amd.lib.gloo_hip_reduce3(3, 6, None, None, None, 0, None) == 0
+    assert gloo_amd.lib.gloo_hip_reduce(7, 8, None, None, 0, None) == -1
+    assert b"op" in gloo_amd.lib.gloo_hip_last_error()
+    assert gloo_amd.lib.gloo_hip_reduce(1, 42, None, None, 0, None) == -2
+    assert gloo_amd.lib.gloo_hip_reduce(1, 8, None, None, 5, None) == -3
+    arr = (ctypes.c_void_p * 1)(None)
+    assert gloo_amd.lib.gloo_hip_reduce_multi(1, 8, None, arr, 0, 5, None) == -4
+    assert gloo_amd.lib.gloo_hip_reduce_multi(1, 8, None, arr, 9, 5, None) == -4
+    with pytest.raises(gloo_amd.GlooHipError):
+        gloo_amd.reduce_ptr("sum", "f32", 0, 0, 5)
+
+
+def test_dtype_sizes():
+    import gloo_amd
+    want = {"i8": 1, "u8": 1, "i32": 4, "u32": 4, "i64": 8, "u64": 8, "f16": 2, "bf16": 2,
+            "f32": 4, "f64": 8}
+    for k, v in want.items():
+        assert gloo_amd.dtype_size(k) == v
+    assert gloo_amd.dtype_size(99) == 0
+
+
+def test_op_and_dtype_codes_mirror_reference():
+    """gloo::ReductionType values (gloo/algorithm.h:49-57)."""
+    import gloo_amd
+    import oracle
+    assert [int(gloo_amd.ReductionType[x]) for x in ("SUM", "PRODUCT", "MAX", "MIN")] == [1, 2, 3, 4]
+    for name, (code, _) in oracle.DTYPES.items():
+        assert int(gloo_amd.DTYPE_NAMES[name]) == code

@@ -1,0 +1,246 @@
+"""GPU parity: the HIP kernels behind the C-ABI vs the reference's results.
+
+Every comparison is bit-exact (integers, bytes and IEEE floats alike: the op
+is one IEEE operation per element, no contraction, denormals preserved), with
+one documented exception class: NaN outputs of 16-bit float SUM/PRODUCT are
+compared as "is NaN" (the reference's F16C / c10 paths and gfx950's cvt
+differ only in the NaN payload they emit).
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = list(oracle.DTYPES)
+OPS = list(oracle.OPS)
+
+
+@pytest.fixture(scope="module")
+def hip():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import gloo_amd
+    return gloo_amd
+
+
+def to_dev(arr, byte_offset=0, pad=64):
+    """Copy a numpy array into fresh device memory at `byte_offset` from a
+    256-B aligned allocation; returns (tensor, device pointer)."""
+    import torch
+    raw = np.frombuffer(np.ascontiguousarray(arr).tobytes(), dtype=np.uint8)
+    t = torch.zeros(raw.size + byte_offset + pad, dtype=torch.uint8, device="cuda")
+    if raw.size:
+        t[byte_offset:byte_offset + raw.size].copy_(torch.from_numpy(raw.copy()))
+    return t, t.data_ptr() + byte_offset
+
+
+def from_dev(t, byte_offset, nbytes, npt):
+    import torch
+    torch.cuda.synchronize()
+    return t[byte_offset:byte_offset + nbytes].cpu().numpy().view(npt).copy()
+
+
+def nan_mask(dtype, x):
+    if dtype == "f16":
+        return ((x & 0x7C00) == 0x7C00) & ((x & 0x3FF) != 0)
+    if dtype == "bf16":
+        return ((x & 0x7F80) == 0x7F80) & ((x & 0x7F) != 0)
+    if dtype in ("f32", "f64"):
+        return np.isnan(x)
+    return np.zeros(x.shape, bool)
+
+
+def assert_same(dtype, op, got, want):
+    n = len(want)
+    g = got.view(np.uint8).reshape(n, -1)
+    w = want.view(np.uint8).reshape(n, -1)
+    eq = (g == w).all(1)
+    if dtype in ("f16", "bf16") and op in ("sum", "product"):
+        both_nan = nan_mask(dtype, got) & nan_mask(dtype, want)
+        eq |= both_nan
+    bad = np.where(~eq)[0]
+    assert bad.size == 0, f"{dtype}/{op}: {bad.size} mismatches, first {bad[:5]}: got {got[bad[:5]]} want {want[bad[:5]]}"
+
+
+def run3(hip, op, dtype, a, b, offs=(0, 0, 0), inplace=False):
+    code, npt = oracle.DTYPES[dtype]
+    n = len(a)
+    nbytes = a.nbytes
+    ta, pa = to_dev(a, offs[1])
+    tb, pb = to_dev(b, offs[2])
+    if inplace:
+        hip.reduce_ptr(op, dtype, pa, pb, n)
+        return from_dev(ta, offs[1], nbytes, npt)
+    tc, pc = to_dev(np.zeros_like(a), offs[0])
+    hip.reduce3_ptr(op, dtype, pc, pa, pb, n)
+    return from_dev(tc, offs[0], nbytes, npt)
+
+
+def expected(golden, dtype, op, a, b):
+    """Reference golden except where the reference's F16C host specialisation
+    and its CUDA kernel disagree (fp16 max/min with a NaN or two zeros): there
+    the CUDA-kernel rule restated by the oracle."""
+    want = golden[f"{dtype}/{op}"].copy()
+    if dtype == "f16" and op in ("max", "min"):
+        o = oracle.reduce3(op, dtype, a, b)
+        fn = lambda x: ((x & 0x7C00) == 0x7C00) & ((x & 0x3FF) != 0)  # noqa: E731
+        z = lambda x: (x & 0x7FFF) == 0  # noqa: E731
+        m = fn(a) | fn(b) | (z(a) & z(b))
+        want[m] = o[m]
+    return want
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("op", OPS)
+def test_golden_reduce3(hip, golden_math, dtype, op):
+    a, b = golden_math[f"{dtype}/a"], golden_math[f"{dtype}/b"]
+    got = run3(hip, op, dtype, a, b)
+    assert_same(dtype, op, got, expected(golden_math, dtype, op, a, b))
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("op", OPS)
+def test_golden_inplace(hip, golden_math, dtype, op):
+    """The form every schedule calls: fn_->call(dst, src, n) = dst op= src."""
+    a, b = golden_math[f"{dtype}/a"], golden_math[f"{dtype}/b"]
+    got = run3(hip, op, dtype, a, b, inplace=True)
+    assert_same(dtype, op, got, expected(golden_math, dtype, op, a, b))
+
+
+def rand_inputs(dtype, n, rng):
+    code, npt = oracle.DTYPES[dtype]
+    if dtype in ("f32", "f64"):
+        return rng.standard_normal(n).astype(npt)
+    if dtype in ("f16", "bf16"):
+        f = rng.standard_normal(n).astype(np.float32)
+        if dtype == "f16":
+            return f.astype(np.float16).view(np.uint16)
+        return (f.view(np.uint32) >> 16).astype(np.uint16)
+    return rng.integers(0, 256, n * np.dtype(npt).itemsize, dtype=np.uint8).view(npt)
+
+
+@pytest.mark.parametrize("dtype", ["i8", "f16", "f32", "f64"])
+def test_misaligned_offsets(hip, dtype):
+    """Chunks start at arbitrary element offsets (gloo/allreduce_ring_chunked.h:128):
+    every combination of destination / source misalignment inside 16 B."""
+    rng = np.random.default_rng(11)
+    code, npt = oracle.DTYPES[dtype]
+    es = np.dtype(npt).itemsize
+    for n in (1, 5, 33, 1000, 4099):
+        a, b = rand_inputs(dtype, n, rng), rand_inputs(dtype, n, rng)
+        want = oracle.reduce3("sum", dtype, a, b)
+        for oc in range(0, 16, es):
+            for ob in range(0, 16, es):
+                oa = oc  # in-place: dst is a
+                got = run3(hip, "sum", dtype, a, b, offs=(oc, oa, ob), inplace=True)
+                assert_same(dtype, "sum", got, want)
+        got = run3(hip, "max", dtype, a, b, offs=(4 % 16 // es * es, 0, 2 * es % 16))
+        assert_same(dtype, "max", got, oracle.reduce3("max", dtype, a, b))
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 4, 7, 255, 256, 257, 1023, 1024, 1025, 4095, 65537,
+                               (1 << 20) + 13])
+def test_sizes_f32_sum(hip, n):
+    rng = np.random.default_rng(n)
+    a, b = rand_inputs("f32", n, rng), rand_inputs("f32", n, rng)
+    if n == 0:
+        hip.reduce_ptr("sum", "f32", 0, 0, 0)
+        return
+    got = run3(hip, "sum", "f32", a, b, inplace=True)
+    assert_same("f32", "sum", got, oracle.reduce3("sum", "f32", a, b))
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_all_ops_ragged_sizes(hip, dtype):
+    rng = np.random.default_rng(21)
+    for n in (2, 17, 300, 5003):
+        a, b = rand_inputs(dtype, n, rng), rand_inputs(dtype, n, rng)
+        for op in OPS:
+            got = run3(hip, op, dtype, a, b, offs=(0, 0, 0), inplace=True)
+            assert_same(dtype, op, got, oracle.reduce3(op, dtype, a, b))
+
+
+def test_nan_and_signed_zero_rules(hip):
+    """max/min keep a NaN already in dst, ignore a NaN arriving in src, and keep
+    dst on ties (-0 vs +0): `if (src op dst) dst = src` (gloo/cuda.cu:337-355)."""
+    nan, inf = np.float32(np.nan), np.float32(np.inf)
+    a = np.array([nan, 1.0, nan, -0.0, 0.0, -inf, 2.0], dtype=np.float32)
+    b = np.array([1.0, nan, nan, 0.0, -0.0, inf, 2.0], dtype=np.float32)
+    for op in ("max", "min"):
+        got = run3(hip, op, "f32", a, b, inplace=True)
+        want = oracle.reduce3(op, "f32", a, b)
+        assert_same("f32", op, got, want)
+        assert np.isnan(got[0]) and got[1] == 1.0 and np.signbit(got[3]) and not np.signbit(got[4])
+
+
+def test_f32_denormals_preserved(hip):
+    t = np.float32(1.17549435e-38)
+    a = np.array([t / 4, -t / 8, t / 2, 1e-45], dtype=np.float32)
+    b = np.array([t / 4, t / 16, -t / 4, 1e-45], dtype=np.float32)
+    for op in ("sum", "product"):
+        got = run3(hip, op, "f32", a, b)
+        assert_same("f32", op, got, oracle.reduce3(op, "f32", a, b))
+
+
+def test_integer_wrap(hip):
+    a = np.array([127, -128, 100, -1], dtype=np.int8)
+    b = np.array([1, -1, 100, -1], dtype=np.int8)
+    for op in OPS:
+        assert_same("i8", op, run3(hip, op, "i8", a, b), oracle.reduce3(op, "i8", a, b))
+    a = np.array([2**63 - 1, -2**63, 3037000500], dtype=np.int64)
+    b = np.array([1, -1, 3037000500], dtype=np.int64)
+    for op in OPS:
+        assert_same("i64", op, run3(hip, op, "i64", a, b), oracle.reduce3(op, "i64", a, b))
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "i32"])
+def test_reduce_multi(hip, k, dtype):
+    """Fused local multi-pointer fold (gloo/allreduce_local.cc:28-33)."""
+    rng = np.random.default_rng(k)
+    code, npt = oracle.DTYPES[dtype]
+    n = 10007
+    srcs = [rand_inputs(dtype, n, rng) for _ in range(k)]
+    for off in (0, 4):
+        bufs = [to_dev(s, off if j % 2 else 0) for j, s in enumerate(srcs)]
+        tdst, pdst = to_dev(np.zeros_like(srcs[0]), 0)
+        for op in OPS:
+            hip.reduce_multi_ptr(op, dtype, pdst, [p for _, p in bufs], n)
+            got = from_dev(tdst, 0, srcs[0].nbytes, npt)
+            assert_same(dtype, op, got, oracle.reduce_multi(op, dtype, srcs))
+
+
+def test_full_size_64mib_f32_sum_properties(hip):
+    """BASELINE config 2 size (64 MiB fp32): bit-exact vs numpy's IEEE f32 add
+    (== the oracle), and a + b - b round trip checked through the kernel."""
+    import torch
+    n = 16 * 1024 * 1024
+    g = torch.Generator(device="cuda").manual_seed(1)
+    a = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    b = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    ref = (a.cpu().numpy() + b.cpu().numpy())  # IEEE f32 add, element-wise
+    c = torch.empty_like(a)
+    hip.reduce3("sum", c, a, b)
+    assert (c.cpu().numpy().view(np.uint32) == ref.view(np.uint32)).all()
+    hip.reduce("sum", a, b)                     # in place, the schedules' form
+    assert torch.equal(a, c)
+    m = torch.empty_like(a)
+    hip.reduce3("max", m, a, a)                 # idempotence
+    assert torch.equal(m, a)
+
+
+def test_stream_ordering(hip):
+    """Launches are async on the caller's stream (gloo/cuda.h:326-333)."""
+    import torch
+    s = torch.cuda.Stream()
+    n = 1 << 22
+    a = torch.ones(n, device="cuda")
+    b = torch.ones(n, device="cuda")
+    with torch.cuda.stream(s):
+        for _ in range(10):
+            hip.reduce("sum", a, b)             # uses the current (side) stream
+    s.synchronize()
+    assert float(a[0]) == 11.0 and float(a[-1]) == 11.0

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Tuning sweep (GPU): fp32 SUM kernel variants at 64 MiB, and the chunk-size
+regime 1 KiB .. 1 GiB for the default kernel (latency vs bandwidth, the sizes
+halving-doubling steps produce, BASELINE config 4).  Prints one JSON line per
+measurement.  Not part of the graded bench; its outputs go to profiles/."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import gloo_amd as hip  # noqa: E402
+
+VARIANTS = {0: "default (unroll4)", 1: "unroll1", 2: "unroll2", 3: "unroll4", 4: "unroll8",
+            5: "unroll4 nt-load", 6: "unroll4 nt-store", 7: "unroll4 nt-load+store",
+            8: "unroll4 persistent", 9: "unroll8 nt-store", 10: "unroll2 nt-store",
+            11: "unroll8 nt-load+store persistent"}
+
+
+def bench(n, steps, pairs, variant=0):
+    dev = torch.device("cuda:0")
+    hip.set_variant(variant)
+    bufs = [(torch.rand(n, device=dev), torch.rand(n, device=dev)) for _ in range(pairs)]
+    s = torch.cuda.current_stream().cuda_stream
+    for i in range(10):
+        d, x = bufs[i % pairs]
+        hip.reduce_ptr("sum", "f32", d.data_ptr(), x.data_ptr(), n, s)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for i in range(steps):
+        d, x = bufs[i % pairs]
+        evs[i][0].record()
+        hip.reduce_ptr("sum", "f32", d.data_ptr(), x.data_ptr(), n, s)
+        evs[i][1].record()
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) for a, b in evs)
+    mean = sum(ts) / len(ts)
+    med = ts[len(ts) // 2]
+    hip.set_variant(0)
+    del bufs
+    torch.cuda.empty_cache()
+    return mean, med
+
+
+def main():
+    n = 16 << 20
+    for v in VARIANTS:
+        mean, med = bench(n, 300, 6, v)
+        print(json.dumps({"sweep": "variant", "variant": v, "name": VARIANTS[v],
+                          "us_mean": round(mean * 1e3, 2), "us_median": round(med * 1e3, 2),
+                          "GBs_mean": round(3 * n * 4 / (mean / 1e3) / 1e9, 1)}), flush=True)
+    for lg in range(8, 29, 2):  # 1 KiB .. 1 GiB of fp32 per operand
+        n = 1 << lg
+        pairs = max(2, min(64, (768 << 20) // (8 * n)))
+        steps = 200 if n < (1 << 26) else 30
+        mean, med = bench(n, steps, pairs)
+        print(json.dumps({"sweep": "size", "bytes": 4 * n, "us_mean": round(mean * 1e3, 2),
+                          "us_median": round(med * 1e3, 2),
+                          "GBs_median": round(3 * n * 4 / (med / 1e3) / 1e9, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
