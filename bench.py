@@ -191,24 +191,27 @@ def main():
         step(i)
     torch.cuda.synchronize(dev)
 
-    # Timed region: barrier + sync on both sides, exactly K steps.  One event
-    # pair per launch gives the kernel's own average duration (roofline).
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    # Timed region: barrier + sync on both sides, exactly K back-to-back
+    # launches bracketed by two HIP events on the launch stream.  The event
+    # average (region / K) is the kernel's launch-to-launch duration; it
+    # includes the ~1-2 us dispatch boundary that rocprofv3's per-kernel
+    # duration excludes (profiles/ keeps both for comparison).
+    e_start = torch.cuda.Event(enable_timing=True)
+    e_end = torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    e_start.record(stream)
     for i in range(args.steps):
-        evs[i][0].record(stream)
         step(i)
-        evs[i][1].record(stream)
+    e_end.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    region_ms = evs[0][0].elapsed_time(evs[-1][1])
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    region_ms = e_start.elapsed_time(e_end)
+    kern_ms = region_ms / args.steps
 
     t_local = torch.tensor([wall], dtype=torch.float64)
     k_all = torch.tensor([kern_ms], dtype=torch.float64)

@@ -1,0 +1,559 @@
+// plan.cc — per-rank schedules of Gloo's reducing algorithms.
+//
+// Each planner restates one reference algorithm (constructor + run()) as the
+// ordered list of steps that rank `rank` performs: one-sided sends into a
+// peer's registered inbox region, waits for arrivals, the per-chunk
+// reductions, copies and the notification handshakes that guard inbox reuse.
+// Offsets, lengths, peers and ORDER are the reference's, so executing a plan
+// reproduces the reference's association order bit for bit.  Nothing here
+// touches HIP: the same plans drive the device executor (executor.hip) and
+// the CPU simulation in tests/.
+//
+// Inbox regions live in a per-rank "arena" laid out exactly like the
+// reference's receive buffers (inbox_[2], recvBuf_, recvBufDist_, outbox_).
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "gloo_amd.h"
+#include "gloo_amd/plan.h"
+
+namespace gloo_amd {
+
+namespace {
+
+Step mk(int kind, int peer = -1, int slot = 0, int flags = 0, uint64_t dst = 0, uint64_t src = 0,
+        uint64_t len = 0) {
+  Step s;
+  s.kind = kind;
+  s.peer = peer;
+  s.slot = slot;
+  s.flags = flags;
+  s.dst_off = dst;
+  s.src_off = src;
+  s.length = len;
+  return s;
+}
+
+// floor(log2(x)) as the reference computes it through <cmath> log2 + an
+// integer conversion (gloo/allreduce_halving_doubling.h:76 `steps_(log2(P))`).
+uint32_t ilog2(uint64_t x) { return static_cast<uint32_t>(std::log2(static_cast<double>(x))); }
+
+// gloo/allreduce_halving_doubling.h:23-33 and gloo/reduce_scatter.h:50-62.
+uint32_t reverseLastNBits(uint32_t ctr, uint32_t n) {
+  uint32_t bitMask = 1, reversed = 0;
+  while (bitMask < (static_cast<uint32_t>(1) << n)) {
+    reversed <<= 1;
+    if (ctr & bitMask) reversed |= 1;
+    bitMask <<= 1;
+  }
+  return reversed;
+}
+
+// Binary-block decomposition for non-power-of-two P
+// (gloo/allreduce_halving_doubling.h:39-64, gloo/reduce_scatter.h:21-48).
+struct Blocks {
+  uint32_t offsetToMyBinaryBlock = 0, myBinaryBlockSize = 0, stepsWithinBlock = 0;
+  uint32_t rankInBinaryBlock = 0, nextSmallerBlockSize = 0, nextLargerBlockSize = 0;
+};
+
+Blocks binaryBlocks(int rank, int size) {
+  Blocks b;
+  uint32_t offset = size, blockSize = 1, currentBlockSize = 0, prevBlockSize = 0;
+  do {
+    if (size & blockSize) {
+      prevBlockSize = currentBlockSize;
+      currentBlockSize = blockSize;
+      offset -= blockSize;
+      if (b.myBinaryBlockSize != 0) {
+        b.nextLargerBlockSize = currentBlockSize;
+        break;
+      }
+      if (offset <= (uint32_t)rank) {
+        b.offsetToMyBinaryBlock = offset;
+        b.myBinaryBlockSize = currentBlockSize;
+        b.nextSmallerBlockSize = prevBlockSize;
+      }
+    }
+    blockSize <<= 1;
+  } while (offset != 0);
+  b.stepsWithinBlock = ilog2(b.myBinaryBlockSize);
+  b.rankInBinaryBlock = rank % b.myBinaryBlockSize;
+  return b;
+}
+
+// The in-block recursive-halving geometry shared by allreduce HD and
+// reduce-scatter HD (gloo/allreduce_halving_doubling.h:107-157,
+// gloo/reduce_scatter.h:155-203).
+struct HDGeometry {
+  uint64_t steps = 0, chunkSize = 0;
+  std::vector<int> dest;
+  std::vector<uint64_t> sendOffsets, recvOffsets, sendCounts, recvCounts, regionOff;
+  uint64_t bufferOffset = 0;    // arena offset after the in-block regions
+  uint64_t stepChunkSize = 0;   // value after the loop
+};
+
+HDGeometry hdGeometry(int rank, int size, uint64_t count, const Blocks& bl) {
+  HDGeometry g;
+  g.steps = ilog2(size);
+  const uint64_t chunks = 1ull << g.steps;
+  g.chunkSize = (count + chunks - 1) / chunks;
+  uint64_t bitmask = 1;
+  uint64_t stepChunkSize = g.chunkSize << (g.steps - 1);
+  uint64_t sendOffset = 0, recvOffset = 0, bufferOffset = 0;
+  for (uint32_t i = 0; i < bl.stepsWithinBlock; i++) {
+    const int destRank = rank ^ (int)bitmask;
+    g.dest.push_back(destRank);
+    const uint64_t so = sendOffset + ((destRank & bitmask) ? stepChunkSize : 0);
+    const uint64_t ro = recvOffset + ((rank & bitmask) ? stepChunkSize : 0);
+    g.sendOffsets.push_back(so);
+    g.recvOffsets.push_back(ro);
+    g.sendCounts.push_back(so < count ? std::min(stepChunkSize, count - so) : 0);
+    g.recvCounts.push_back(ro < count ? std::min(stepChunkSize, count - ro) : 0);
+    g.regionOff.push_back(bufferOffset);
+    bufferOffset += stepChunkSize;
+    if (rank & bitmask) {
+      sendOffset += stepChunkSize;
+      recvOffset += stepChunkSize;
+    }
+    bitmask <<= 1;
+    stepChunkSize >>= 1;
+  }
+  g.bufferOffset = bufferOffset;
+  g.stepChunkSize = stepChunkSize;
+  return g;
+}
+
+// ---------------------------------------------------------------------------
+// AllreduceRingChunked (gloo/allreduce_ring_chunked.h:22-236), GPU twin
+// gloo/cuda_allreduce_ring_chunked.cc:130-273.
+// ---------------------------------------------------------------------------
+Plan planRingChunked(int rank, int size, uint64_t count, int nptrs) {
+  Plan p;
+  if (count == 0) return p;                                   // run() :84-86
+  const uint64_t chunks = 2ull * size;                        // ctor :32
+  const uint64_t chunkSize = std::max<uint64_t>(256, (count + chunks - 1) / chunks);  // :37
+  const int left = (size + rank - 1) % size, right = (rank + 1) % size;
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, 0, 0, 0, count));  // :89-91
+  if (size == 1) {                                            // :93-99
+    if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count));
+    return p;
+  }
+  p.arena = 2 * chunkSize;  // inbox_[0], inbox_[1] registered with chunkBytes_ (:58-59)
+  for (int i = 0; i < 2; i++)
+    p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, left, i, 0, i * chunkSize, 0, chunkSize));
+
+  auto span = [&](uint64_t chunkOffset, uint64_t& offset, uint64_t& length) {
+    offset = chunkOffset * chunkSize;
+    length = chunkSize;
+    if (offset + length <= count) {
+    } else if (offset < count) {
+      length = count - offset;
+    } else {
+      length = 0;
+    }
+  };
+  auto copyChunkAtOffset = [&](uint64_t chunkOffset) {     // :215-236
+    uint64_t offset = (chunkOffset % chunks) * chunkSize, length = chunkSize;
+    if (offset + length <= count) {
+    } else if (offset < count) {
+      length = count - offset;
+    } else {
+      offset = 0;  // out-of-range chunk still puts 1 element on the wire
+      length = 1;
+    }
+    p.steps.push_back(mk(GLOO_HIP_STEP_SEND, right, (int)(chunkOffset & 1), 0, 0, offset, length));
+  };
+  auto chunkAt = [&](uint64_t round) {                      // :124-126
+    return (uint64_t)((2 * (uint64_t)rank) - (round & ~1ull) + (round & 1ull) + chunks) % chunks;
+  };
+
+  copyChunkAtOffset(2 * rank);                              // :102-103
+  copyChunkAtOffset(2 * rank + 1);
+  for (uint64_t round = 2; round < chunks; round++) {       // :106-158
+    const uint64_t co = chunkAt(round);
+    uint64_t offset, length;
+    span(co, offset, length);
+    p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, left, (int)(co & 1)));
+    if (length > 0)
+      p.steps.push_back(mk(GLOO_HIP_STEP_REDUCE, -1, 0, GLOO_HIP_SRC_ARENA, offset,
+                           (co & 1) * chunkSize, length));
+    p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, left, GLOO_HIP_SLOT_NOTIFY));
+    p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, right, GLOO_HIP_SLOT_NOTIFY));
+    copyChunkAtOffset(co);
+  }
+  for (uint64_t round = 0; round < chunks - 2; round++) {   // :163-200
+    const uint64_t co = chunkAt(round);
+    uint64_t offset, length;
+    span(co, offset, length);
+    p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, left, (int)(co & 1)));
+    if (length > 0)
+      p.steps.push_back(mk(GLOO_HIP_STEP_COPY, -1, 0, GLOO_HIP_SRC_ARENA, offset,
+                           (co & 1) * chunkSize, length));
+    if (round < chunks - 4) {
+      p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, left, GLOO_HIP_SLOT_NOTIFY));
+      p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, right, GLOO_HIP_SLOT_NOTIFY));
+      copyChunkAtOffset(co);
+    }
+  }
+  p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, left, GLOO_HIP_SLOT_NOTIFY));      // :205-206
+  p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, right, GLOO_HIP_SLOT_NOTIFY));
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count));
+  return p;
+}
+
+// ---------------------------------------------------------------------------
+// AllreduceHalvingDoubling (gloo/allreduce_halving_doubling.h:67-362), GPU
+// twin gloo/cuda_allreduce_halving_doubling.cc:246-410.
+// ---------------------------------------------------------------------------
+Plan planHalvingDoubling(int rank, int size, uint64_t count, int nptrs) {
+  Plan p;
+  if (count == 0) return p;                                             // run() :226-228
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, 0, 0, 0, count));
+  if (size == 1) {
+    if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count));
+    return p;
+  }
+  const Blocks bl = binaryBlocks(rank, size);                           // :102
+  HDGeometry g = hdGeometry(rank, size, count, bl);                     // :107-157
+  const uint32_t swb = bl.stepsWithinBlock;
+  p.arena = g.chunkSize << g.steps;                                     // recvBuf_ (:80)
+  for (uint32_t i = 0; i < swb; i++)
+    p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, g.dest[i], GLOO_HIP_SLOT_DATA0, 0, g.regionOff[i],
+                         0, g.chunkSize << (g.steps - 1) >> i));
+  uint64_t ctorBufferOffset = g.bufferOffset;
+  int smallDest = -1;
+  bool smallRecv = false;
+  if (bl.nextSmallerBlockSize != 0) {                                   // :159-175
+    const uint32_t offsetToSmallerBlock = bl.offsetToMyBinaryBlock + bl.myBinaryBlockSize;
+    smallDest = offsetToSmallerBlock + bl.rankInBinaryBlock % bl.nextSmallerBlockSize;
+    const uint64_t itemCount = g.recvCounts[swb - 1];
+    if (itemCount > 0) {
+      smallRecv = true;
+      p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, smallDest, GLOO_HIP_SLOT_DATA0, 0,
+                           ctorBufferOffset, 0, itemCount));
+    }
+  }
+  std::vector<int> largeDest;
+  uint64_t sendCountToLargerBlock = 0;
+  const uint64_t totalItemsToSend = swb > 0 ? g.recvCounts[swb - 1] : count;
+  if (bl.nextLargerBlockSize != 0) {                                    // :176-222
+    const uint32_t offsetToLargerBlock = bl.offsetToMyBinaryBlock - bl.nextLargerBlockSize;
+    const uint32_t numSR = bl.nextLargerBlockSize / bl.myBinaryBlockSize;
+    sendCountToLargerBlock = g.stepChunkSize >> (static_cast<uint64_t>(ilog2(numSR)) - 1);
+    const uint32_t srcOrdinal = reverseLastNBits(bl.rankInBinaryBlock, ilog2(bl.myBinaryBlockSize));
+    uint32_t destOrdinal = srcOrdinal * numSR;
+    for (uint32_t i = 0; i < numSR; i++) {
+      const int d = offsetToLargerBlock + reverseLastNBits(destOrdinal, ilog2(bl.nextLargerBlockSize));
+      largeDest.push_back(d);
+      if (sendCountToLargerBlock * i < totalItemsToSend) {
+        const uint64_t toSend = std::min(sendCountToLargerBlock, totalItemsToSend - sendCountToLargerBlock * i);
+        p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, d, GLOO_HIP_SLOT_DATA0, 0, ctorBufferOffset, 0, toSend));
+        ctorBufferOffset += toSend;
+      }
+      destOrdinal++;
+    }
+  }
+  p.arena = std::max<uint64_t>(p.arena, ctorBufferOffset);
+
+  // run() :225-362
+  uint64_t bufferOffset = 0;
+  uint64_t numItems = swb > 0 ? g.chunkSize << (g.steps - 1) : count;
+  for (uint32_t i = 0; i < swb; i++) {                                  // :244-259
+    if (g.sendOffsets[i] < count)
+      p.steps.push_back(mk(GLOO_HIP_STEP_SEND, g.dest[i], GLOO_HIP_SLOT_DATA0, 0, 0, g.sendOffsets[i],
+                           g.sendCounts[i]));
+    if (g.recvOffsets[i] < count) {
+      p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, g.dest[i], GLOO_HIP_SLOT_DATA0));
+      p.steps.push_back(mk(GLOO_HIP_STEP_REDUCE, -1, 0, GLOO_HIP_SRC_ARENA, g.recvOffsets[i],
+                           bufferOffset, g.recvCounts[i]));
+    }
+    bufferOffset += numItems;
+    p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, g.dest[i], GLOO_HIP_SLOT_NOTIFY));
+    numItems >>= 1;
+  }
+  if (bl.nextSmallerBlockSize != 0 && smallRecv) {                      // :266-273
+    p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, smallDest, GLOO_HIP_SLOT_DATA0));
+    p.steps.push_back(mk(GLOO_HIP_STEP_REDUCE, -1, 0, GLOO_HIP_SRC_ARENA, g.recvOffsets[swb - 1],
+                         bufferOffset, g.recvCounts[swb - 1]));
+  }
+  if (bl.nextLargerBlockSize != 0 && totalItemsToSend != 0) {           // :277-309
+    const uint64_t offset = swb > 0 ? g.recvOffsets[swb - 1] : 0;
+    const uint32_t numSR = bl.nextLargerBlockSize / bl.myBinaryBlockSize;
+    for (uint32_t i = 0; i < numSR; i++)
+      if (sendCountToLargerBlock * i < totalItemsToSend)
+        p.steps.push_back(mk(GLOO_HIP_STEP_SEND, largeDest[i], GLOO_HIP_SLOT_DATA0, 0, 0,
+                             offset + i * sendCountToLargerBlock,
+                             std::min(sendCountToLargerBlock, totalItemsToSend - sendCountToLargerBlock * i)));
+    for (uint32_t i = 0; i < numSR; i++)
+      if (sendCountToLargerBlock * i < totalItemsToSend)
+        p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, largeDest[i], GLOO_HIP_SLOT_DATA0));
+    p.steps.push_back(mk(GLOO_HIP_STEP_COPY, -1, 0, GLOO_HIP_SRC_ARENA, offset, bufferOffset,
+                         totalItemsToSend));
+  }
+  bool sentToSmallerBlock = false;                                      // :312-321
+  if (bl.nextSmallerBlockSize != 0) {
+    if (g.recvOffsets[swb - 1] < count) {
+      sentToSmallerBlock = true;
+      p.steps.push_back(mk(GLOO_HIP_STEP_SEND, smallDest, GLOO_HIP_SLOT_DATA0, 0, 0,
+                           g.recvOffsets[swb - 1], g.recvCounts[swb - 1]));
+    }
+  }
+  numItems = g.chunkSize << (g.steps - swb);                            // :324-346
+  for (int i = (int)swb - 1; i >= 0; i--) {
+    p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, g.dest[i], GLOO_HIP_SLOT_NOTIFY));
+    if (g.recvOffsets[i] < count)
+      p.steps.push_back(mk(GLOO_HIP_STEP_SEND, g.dest[i], GLOO_HIP_SLOT_DATA0, 0, 0, g.recvOffsets[i],
+                           g.recvCounts[i]));
+    bufferOffset -= numItems;
+    if (g.sendOffsets[i] < count) {
+      p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, g.dest[i], GLOO_HIP_SLOT_DATA0));
+      p.steps.push_back(mk(GLOO_HIP_STEP_COPY, -1, 0, GLOO_HIP_SRC_ARENA, g.sendOffsets[i],
+                           bufferOffset, g.sendCounts[i]));
+    }
+    numItems <<= 1;
+    p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, g.dest[i], GLOO_HIP_SLOT_NOTIFY));
+  }
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count));  // :349-352
+  for (int i = (int)swb - 1; i >= 0; i--)                               // :357-359
+    p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, g.dest[i], GLOO_HIP_SLOT_NOTIFY));
+  if (sentToSmallerBlock)                                               // :364-366
+    p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_SEND, smallDest, GLOO_HIP_SLOT_DATA0));
+  return p;
+}
+
+// ---------------------------------------------------------------------------
+// AllreduceRing (gloo/allreduce_ring.h:21-113), GPU twin
+// gloo/cuda_allreduce_ring.cc:73-121.  Arena = [inbox_ | outbox_].
+// ---------------------------------------------------------------------------
+Plan planRing(int rank, int size, uint64_t count, int nptrs) {
+  Plan p;
+  if (count == 0) return p;
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, 0, 0, 0, count));
+  if (size > 1) {
+    const int left = (size + rank - 1) % size, right = (rank + 1) % size;
+    const uint64_t inbox = 0, outbox = count;
+    p.arena = 2 * count;
+    p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, left, GLOO_HIP_SLOT_DATA0, 0, inbox, 0, count));
+    p.steps.push_back(mk(GLOO_HIP_STEP_COPY, -1, 0, GLOO_HIP_DST_ARENA, outbox, 0, count));  // :78
+    for (int round = 0; round < size - 1; round++) {
+      p.steps.push_back(mk(GLOO_HIP_STEP_SEND, right, GLOO_HIP_SLOT_DATA0, GLOO_HIP_SRC_ARENA, 0, outbox, count));
+      p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, left, GLOO_HIP_SLOT_DATA0));
+      p.steps.push_back(mk(GLOO_HIP_STEP_REDUCE, -1, 0, GLOO_HIP_SRC_ARENA, 0, inbox, count));
+      p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_SEND, right, GLOO_HIP_SLOT_DATA0));
+      if (round < size - 2)
+        p.steps.push_back(mk(GLOO_HIP_STEP_COPY, -1, 0, GLOO_HIP_SRC_ARENA | GLOO_HIP_DST_ARENA, outbox,
+                             inbox, count));
+      p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, left, GLOO_HIP_SLOT_NOTIFY));
+      p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, right, GLOO_HIP_SLOT_NOTIFY));
+    }
+  }
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count));
+  return p;
+}
+
+// AllreduceLocal (gloo/allreduce_local.cc:28-37).
+Plan planLocal(int, int, uint64_t count, int nptrs) {
+  Plan p;
+  if (nptrs > 1 && count > 0) {
+    p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, 0, 0, 0, count));
+    p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count));
+  }
+  return p;
+}
+
+// ---------------------------------------------------------------------------
+// ReduceScatterHalvingDoubling (gloo/reduce_scatter.h:112-442).
+// Arena = [recvBuf_ (chunkSize << steps) | recvBufDist_ (count)].
+// ---------------------------------------------------------------------------
+struct DistMap {
+  int rank;
+  uint64_t offset, itemCount;
+};
+
+// gloo/reduce_scatter.h:72-110
+void distributionMap(int size, uint64_t srcOffset, uint64_t srcCount, const std::vector<int>& recvCounts,
+                     bool reorder, std::vector<DistMap>& out) {
+  if (srcCount == 0) return;
+  uint64_t destOffset = 0;
+  const int n = reorder ? 1 << (int)ilog2(size) : size;
+  int start = 0;
+  for (; start < n; ++start) {
+    if (destOffset + (uint64_t)(int64_t)recvCounts[start] > srcOffset) break;
+    destOffset += recvCounts[start];
+  }
+  destOffset = srcOffset - destOffset;
+  uint64_t totalCount = srcCount;
+  for (int i = start; i < n; ++i) {
+    int64_t recvCount = recvCounts[i];
+    if (destOffset != 0) {
+      recvCount -= (int64_t)destOffset;
+      destOffset = 0;
+    }
+    const int r = reorder ? (int)reverseLastNBits(i, ilog2(size)) : i;
+    uint64_t rc = (uint64_t)recvCount;
+    rc = rc < totalCount ? rc : totalCount;
+    out.push_back({r, srcOffset, rc});
+    srcOffset += rc;
+    totalCount -= rc;
+    if (totalCount == 0) break;
+  }
+}
+
+Plan planReduceScatter(int rank, int size, uint64_t count, int nptrs, const std::vector<int>& recvElems) {
+  Plan p;
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, 0, 0, 0, count));
+  if (size == 1) {                                                       // run() :337-343
+    if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count));
+    return p;
+  }
+  const Blocks bl = binaryBlocks(rank, size);
+  HDGeometry g = hdGeometry(rank, size, count, bl);
+  const uint32_t swb = bl.stepsWithinBlock;
+  const uint64_t distBase = g.chunkSize << g.steps;
+  p.arena = distBase + count;
+  for (uint32_t i = 0; i < swb; i++)
+    p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, g.dest[i], GLOO_HIP_SLOT_DATA0, 0, g.regionOff[i], 0,
+                         g.chunkSize << (g.steps - 1) >> i));
+  int smallDest = -1;
+  bool smallRecv = false;
+  if (bl.nextSmallerBlockSize != 0) {                                    // :206-220
+    smallDest = bl.offsetToMyBinaryBlock + bl.myBinaryBlockSize + bl.rankInBinaryBlock % bl.nextSmallerBlockSize;
+    const uint64_t itemCount = g.recvCounts[swb - 1];
+    if (itemCount > 0) {
+      smallRecv = true;
+      p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, smallDest, GLOO_HIP_SLOT_DATA0, 0, g.bufferOffset, 0,
+                           itemCount));
+    }
+  }
+  std::vector<int> largeDest;
+  uint64_t sendCountToLargerBlock = 0;
+  if (bl.nextLargerBlockSize != 0) {                                     // :221-247
+    const uint32_t offsetToLargerBlock = bl.offsetToMyBinaryBlock - bl.nextLargerBlockSize;
+    const uint32_t numSR = bl.nextLargerBlockSize / bl.myBinaryBlockSize;
+    sendCountToLargerBlock = g.stepChunkSize >> (static_cast<uint64_t>(ilog2(numSR)) - 1);
+    const uint32_t srcOrdinal = reverseLastNBits(bl.rankInBinaryBlock, ilog2(bl.myBinaryBlockSize));
+    uint32_t destOrdinal = srcOrdinal * numSR;
+    for (uint32_t i = 0; i < numSR; i++) {
+      largeDest.push_back(offsetToLargerBlock + reverseLastNBits(destOrdinal, ilog2(bl.nextLargerBlockSize)));
+      destOrdinal++;
+    }
+  }
+  std::vector<DistMap> distSend, distRecv;                               // :255-327
+  if (bl.nextLargerBlockSize == 0 && swb > 0)
+    distributionMap(size, g.recvOffsets[swb - 1], g.recvCounts[swb - 1], recvElems, false, distSend);
+  if (recvElems[rank] > 0) {
+    std::vector<int> srcCounts;
+    uint64_t rem = count;
+    for (int i = 0; i < size; ++i) {
+      srcCounts.push_back((int)std::min(g.chunkSize, rem));
+      rem = rem > g.chunkSize ? rem - g.chunkSize : 0;
+    }
+    uint64_t offset = 0;
+    for (int i = 0; i < rank; ++i) offset += recvElems[i];
+    distributionMap(size, offset, recvElems[rank], srcCounts, true, distRecv);
+    for (const auto& d : distRecv)
+      if (d.rank != rank)
+        p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, d.rank, GLOO_HIP_SLOT_DIST, 0, distBase + d.offset, 0,
+                             d.itemCount));
+  }
+
+  // run() :329-442
+  uint64_t bufferOffset = 0;
+  uint64_t numItems = swb > 0 ? g.chunkSize << (g.steps - 1) : count;
+  for (uint32_t i = 0; i < swb; i++) {
+    if (g.sendOffsets[i] < count)
+      p.steps.push_back(mk(GLOO_HIP_STEP_SEND, g.dest[i], GLOO_HIP_SLOT_DATA0, 0, 0, g.sendOffsets[i],
+                           g.sendCounts[i]));
+    if (g.recvOffsets[i] < count) {
+      p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, g.dest[i], GLOO_HIP_SLOT_DATA0));
+      p.steps.push_back(mk(GLOO_HIP_STEP_REDUCE, -1, 0, GLOO_HIP_SRC_ARENA, g.recvOffsets[i], bufferOffset,
+                           g.recvCounts[i]));
+    }
+    bufferOffset += numItems;
+    p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, g.dest[i], GLOO_HIP_SLOT_NOTIFY));
+    numItems >>= 1;
+  }
+  if (bl.nextSmallerBlockSize != 0 && smallRecv) {
+    p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, smallDest, GLOO_HIP_SLOT_DATA0));
+    p.steps.push_back(mk(GLOO_HIP_STEP_REDUCE, -1, 0, GLOO_HIP_SRC_ARENA, g.recvOffsets[swb - 1],
+                         bufferOffset, g.recvCounts[swb - 1]));
+  }
+  const uint64_t totalItemsToSend = swb > 0 ? g.recvCounts[swb - 1] : count;
+  if (bl.nextLargerBlockSize != 0 && totalItemsToSend != 0) {
+    const uint64_t offset = swb > 0 ? g.recvOffsets[swb - 1] : 0;
+    const uint32_t numSR = bl.nextLargerBlockSize / bl.myBinaryBlockSize;
+    for (uint32_t i = 0; i < numSR; i++)
+      if (sendCountToLargerBlock * i < totalItemsToSend)
+        p.steps.push_back(mk(GLOO_HIP_STEP_SEND, largeDest[i], GLOO_HIP_SLOT_DATA0, 0, 0,
+                             offset + i * sendCountToLargerBlock,
+                             std::min(sendCountToLargerBlock, totalItemsToSend - sendCountToLargerBlock * i)));
+  }
+  for (const auto& d : distSend)
+    if (d.rank != rank)
+      p.steps.push_back(mk(GLOO_HIP_STEP_SEND, d.rank, GLOO_HIP_SLOT_DIST, 0, 0, d.offset, d.itemCount));
+  bufferOffset = 0;
+  for (const auto& d : distRecv) {
+    if (d.rank != rank) {
+      p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, d.rank, GLOO_HIP_SLOT_DIST));
+      p.steps.push_back(mk(GLOO_HIP_STEP_COPY, -1, 0, GLOO_HIP_SRC_ARENA, bufferOffset, distBase + d.offset,
+                           d.itemCount));
+      p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, d.rank, GLOO_HIP_SLOT_DIST_NOTIFY));
+    } else if (rank != 0) {  // data already in place for rank 0 (:418-425)
+      p.steps.push_back(mk(GLOO_HIP_STEP_COPY, -1, 0, 0, bufferOffset, d.offset, d.itemCount));
+    }
+    bufferOffset += d.itemCount;
+  }
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count));
+  for (uint32_t i = 0; i < swb; i++)                                     // :432-439
+    p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, g.dest[i], GLOO_HIP_SLOT_NOTIFY));
+  for (const auto& d : distSend)
+    if (d.rank != rank)
+      p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, d.rank, GLOO_HIP_SLOT_DIST_NOTIFY));
+  return p;
+}
+
+}  // namespace
+
+Plan makePlan(int algo, int rank, int size, uint64_t count, int nptrs, const std::vector<int>& recvElems) {
+  if (size < 1 || rank < 0 || rank >= size) throw std::invalid_argument("bad rank/size");
+  if (nptrs < 1) throw std::invalid_argument("need at least one pointer");
+  switch (algo) {
+    case GLOO_HIP_ALGO_RING_CHUNKED: return planRingChunked(rank, size, count, nptrs);
+    case GLOO_HIP_ALGO_HALVING_DOUBLING: return planHalvingDoubling(rank, size, count, nptrs);
+    case GLOO_HIP_ALGO_RING: return planRing(rank, size, count, nptrs);
+    case GLOO_HIP_ALGO_LOCAL: return planLocal(rank, size, count, nptrs);
+    case GLOO_HIP_ALGO_REDUCE_SCATTER:
+      if ((int)recvElems.size() != size) throw std::invalid_argument("recvElems must have size entries");
+      return planReduceScatter(rank, size, count, nptrs, recvElems);
+  }
+  throw std::invalid_argument("unknown algorithm");
+}
+
+}  // namespace gloo_amd
+
+extern "C" int gloo_hip_plan(int algo, int rank, int size, size_t count, int nptrs, const int* recv_elems,
+                             gloo_hip_step_t* steps, size_t capacity, size_t* nsteps, size_t* arena_elems) {
+  try {
+    std::vector<int> re;
+    if (algo == GLOO_HIP_ALGO_REDUCE_SCATTER) {
+      if (!recv_elems) return GLOO_HIP_EINVAL_ARG;
+      re.assign(recv_elems, recv_elems + size);
+    }
+    gloo_amd::Plan p = gloo_amd::makePlan(algo, rank, size, count, nptrs, re);
+    if (nsteps) *nsteps = p.steps.size();
+    if (arena_elems) *arena_elems = p.arena;
+    if (steps) {
+      if (capacity < p.steps.size()) return GLOO_HIP_EINVAL_ARG;
+      std::memcpy(steps, p.steps.data(), p.steps.size() * sizeof(gloo_hip_step_t));
+    }
+    return GLOO_HIP_OK;
+  } catch (const std::exception&) {
+    return GLOO_HIP_EINVAL_ARG;
+  }
+}

@@ -9,7 +9,9 @@
 //    64 lanes -> 1 KiB contiguous per wave-instruction, fully coalesced;
 //  * UNROLL independent 16-B packets per operand per lane are in flight
 //    before the first use (memory-level parallelism instead of occupancy);
-//  * the aligned body is a flat tile grid (one tile = 256 lanes x UNROLL
+//  * raw buffer loads/stores with the `nt` cache policy (data is streamed
+//    exactly once) through per-tile buffer descriptors;
+//  * the aligned body is a flat tile grid (one tile = 512 lanes x UNROLL
 //    packets), tiles dealt round-robin over the 8 XCDs by the dispatcher;
 //  * a chunk may start at any element offset (Gloo chunk offsets are
 //    arbitrary element counts, gloo/allreduce_ring_chunked.h:128): the first
@@ -172,15 +174,25 @@ __device__ __forceinline__ u32x4 apply_packet<TrU8, GLOO_HIP_SUM>(u32x4 a, u32x4
                swar_add8(a.w, b.w)};
 }
 
-template <bool NT>
-__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(p);
-  else return *p;
+// Buffer resources.  Each workgroup builds descriptors whose base is its own
+// tile (wave-uniform, SGPRs) and whose range is the bytes left in the body, so
+// 32-bit lane offsets suffice for any chunk size and the hardware range check
+// drops the out-of-range packets of a ragged last tile (loads return 0, stores
+// are discarded) without per-lane branches.
+constexpr int kRsrcFlags = 0x00020000;  // gfx950 raw-buffer word 3
+constexpr int kAuxNT = 2;               // cache policy `nt`: streamed once
+constexpr int kAuxSC1 = 16;             // cache policy `sc1`
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, kRsrcFlags);
 }
-template <bool NT>
-__device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
-  if constexpr (NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
+template <int AUX>
+__device__ __forceinline__ u32x4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
+}
+template <int AUX>
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, AUX);
 }
 
 // Element-wise head / tail: elements [0, head) and [tail0, n) of the chunk,
@@ -198,47 +210,38 @@ __device__ __forceinline__ void edges(typename Tr::Storage* c,
 }
 
 // Aligned body.  c, a, b are congruent modulo 16 B; `head` elements bring
-// them to a 16-B boundary.  Tile = kBlock lanes x UNROLL packets; within a
-// tile packet u of lane t is at t + u*kBlock (each wave-instruction covers
-// 1 KiB contiguous).  PERSIST: grid-stride over tiles with a capped grid.
-template <class Tr, int OP, int UNROLL, bool NTL, bool NTS, bool PERSIST>
-__global__ __launch_bounds__(kBlock) void reduce_vec_kernel(
+// them to a 16-B boundary.  One workgroup = one tile of BLOCK lanes x UNROLL
+// 16-B packets per operand; packet u of lane t sits at (t + u*BLOCK)*16 bytes
+// into the tile, so every wave-instruction covers 1 KiB contiguous.  All loads
+// of the tile are issued before the first use.  Measured on MI355X (profiles/
+// round1): `nt` on both loads and stores, UNROLL 2, BLOCK 512, one tile per
+// workgroup is the fastest of 126 variants for the 64 MiB fp32 chunk.
+template <class Tr, int OP, int UNROLL, int BLOCK, int LAUX, int SAUX>
+__global__ __launch_bounds__(BLOCK) void reduce_vec_kernel(
     typename Tr::Storage* c, const typename Tr::Storage* a,
     const typename Tr::Storage* b, size_t n, size_t head) {
   using S = typename Tr::Storage;
   constexpr int kV = 16 / sizeof(S);
-  constexpr size_t kTile = (size_t)kBlock * UNROLL;
+  constexpr uint32_t kTileBytes = (uint32_t)BLOCK * UNROLL * 16;
   const size_t nvec = (n - head) / kV;
-  u32x4* cv = reinterpret_cast<u32x4*>(c + head);
-  const u32x4* av = reinterpret_cast<const u32x4*>(a + head);
-  const u32x4* bv = reinterpret_cast<const u32x4*>(b + head);
-
   if (blockIdx.x == 0) edges<Tr, OP>(c, a, b, head, head + nvec * kV, n);
 
-  const size_t ntiles_full = nvec / kTile;
-  size_t tile = blockIdx.x;
-  const size_t step = PERSIST ? gridDim.x : ntiles_full + 1;
-  for (; tile < ntiles_full; tile += step) {
-    const size_t base = tile * kTile + threadIdx.x;
-    u32x4 ra[UNROLL], rb[UNROLL];
+  const size_t body = nvec * 16;
+  const size_t base = (size_t)blockIdx.x * kTileBytes;
+  if (base >= body) return;
+  const uint32_t bytes = (uint32_t)((body - base) < kTileBytes ? (body - base) : kTileBytes);
+  const auto ra = make_rsrc(reinterpret_cast<const char*>(a + head) + base, bytes);
+  const auto rb = make_rsrc(reinterpret_cast<const char*>(b + head) + base, bytes);
+  const auto rc = make_rsrc(reinterpret_cast<const char*>(c + head) + base, bytes);
+  const uint32_t lane_off = threadIdx.x * 16u;
+  u32x4 x[UNROLL], y[UNROLL];
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) ra[u] = ld16<NTL>(av + base + u * kBlock);
+  for (int u = 0; u < UNROLL; u++) x[u] = bload<LAUX>(ra, lane_off + u * BLOCK * 16);
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) rb[u] = ld16<NTL>(bv + base + u * kBlock);
+  for (int u = 0; u < UNROLL; u++) y[u] = bload<LAUX>(rb, lane_off + u * BLOCK * 16);
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++)
-      st16<NTS>(cv + base + u * kBlock, apply_packet<Tr, OP>(ra[u], rb[u]));
-    if constexpr (!PERSIST) return;
-  }
-  // Ragged last tile (at most one): guarded packets.
-  if (tile == ntiles_full) {
-    const size_t base = tile * kTile + threadIdx.x;
-#pragma unroll
-    for (int u = 0; u < UNROLL; u++) {
-      const size_t i = base + u * kBlock;
-      if (i < nvec) st16<NTS>(cv + i, apply_packet<Tr, OP>(ld16<NTL>(av + i), ld16<NTL>(bv + i)));
-    }
-  }
+  for (int u = 0; u < UNROLL; u++)
+    bstore<SAUX>(rc, lane_off + u * BLOCK * 16, apply_packet<Tr, OP>(x[u], y[u]));
 }
 
 // Operands with different misalignment: element-wise, coalesced (lane t of
@@ -270,12 +273,12 @@ struct SrcList {
   const void* p[GLOO_HIP_MAX_SRCS];
 };
 
-template <class Tr, int OP, int UNROLL>
-__global__ __launch_bounds__(kBlock) void reduce_multi_vec_kernel(
+template <class Tr, int OP, int UNROLL, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
     typename Tr::Storage* dst, SrcList srcs, int k, size_t n, size_t head) {
   using S = typename Tr::Storage;
   constexpr int kV = 16 / sizeof(S);
-  constexpr size_t kTile = (size_t)kBlock * UNROLL;
+  constexpr uint32_t kTileBytes = (uint32_t)BLOCK * UNROLL * 16;
   const size_t nvec = (n - head) / kV;
   const size_t tail0 = head + nvec * kV;
   if (blockIdx.x == 0) {
@@ -289,30 +292,31 @@ __global__ __launch_bounds__(kBlock) void reduce_multi_vec_kernel(
       }
     }
   }
-  const size_t base = (size_t)blockIdx.x * kTile + threadIdx.x;
+  const size_t body = nvec * 16;
+  const size_t base = (size_t)blockIdx.x * kTileBytes;
+  if (base >= body) return;
+  const uint32_t bytes = (uint32_t)((body - base) < kTileBytes ? (body - base) : kTileBytes);
+  const uint32_t lane_off = threadIdx.x * 16u;
+  auto src_rsrc = [&](int j) {
+    return make_rsrc(reinterpret_cast<const char*>(static_cast<const S*>(srcs.p[j]) + head) + base, bytes);
+  };
   u32x4 acc[UNROLL];
+  {
+    const auto r0 = src_rsrc(0);
 #pragma unroll
-  for (int u = 0; u < UNROLL; u++) {
-    const size_t i = base + u * kBlock;
-    if (i < nvec) acc[u] = reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[0]) + head)[i];
+    for (int u = 0; u < UNROLL; u++) acc[u] = bload<kAuxNT>(r0, lane_off + u * BLOCK * 16);
   }
   for (int j = 1; j < k; j++) {
-    const u32x4* sv = reinterpret_cast<const u32x4*>(static_cast<const S*>(srcs.p[j]) + head);
+    const auto rj = src_rsrc(j);
     u32x4 r[UNROLL];
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) {
-      const size_t i = base + u * kBlock;
-      if (i < nvec) r[u] = sv[i];
-    }
+    for (int u = 0; u < UNROLL; u++) r[u] = bload<kAuxNT>(rj, lane_off + u * BLOCK * 16);
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) acc[u] = apply_packet<Tr, OP>(acc[u], r[u]);
   }
-  u32x4* dv = reinterpret_cast<u32x4*>(dst + head);
+  const auto rd = make_rsrc(reinterpret_cast<const char*>(dst + head) + base, bytes);
 #pragma unroll
-  for (int u = 0; u < UNROLL; u++) {
-    const size_t i = base + u * kBlock;
-    if (i < nvec) dv[i] = acc[u];
-  }
+  for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rd, lane_off + u * BLOCK * 16, acc[u]);
 }
 
 template <class Tr, int OP, int UNROLL>
@@ -351,25 +355,21 @@ int check_launch(const char* name) {
   return GLOO_HIP_OK;
 }
 
-constexpr int kDefaultUnroll = 4;
+constexpr int kUnroll = 2;      // 16-B packets per operand per lane
+constexpr int kVecBlock = 512;  // lanes per workgroup on the vector body
 constexpr int kElemUnroll = 4;
 constexpr int kMultiUnroll = 2;
 
 inline size_t ceil_div(size_t a, size_t b) { return (a + b - 1) / b; }
 
-template <class Tr, int OP, int UNROLL, bool NTL, bool NTS, bool PERSIST>
-int launch_vec(void* c, const void* a, const void* b, size_t n, size_t head,
-               hipStream_t s) {
+template <class Tr, int OP, int UNROLL, int BLOCK, int LAUX, int SAUX>
+int launch_vec(void* c, const void* a, const void* b, size_t n, size_t head, hipStream_t s) {
   using S = typename Tr::Storage;
   constexpr int kV = 16 / sizeof(S);
   const size_t nvec = (n - head) / kV;
-  size_t grid = ceil_div(nvec, (size_t)kBlock * UNROLL);
+  size_t grid = ceil_div(nvec, (size_t)BLOCK * UNROLL);
   if (grid == 0) grid = 1;
-  if (PERSIST) {
-    const size_t cap = 256 * 8;  // 8 blocks per CU on 256 CUs
-    if (grid > cap) grid = cap;
-  }
-  reduce_vec_kernel<Tr, OP, UNROLL, NTL, NTS, PERSIST><<<dim3((unsigned)grid), dim3(kBlock), 0, s>>>(
+  reduce_vec_kernel<Tr, OP, UNROLL, BLOCK, LAUX, SAUX><<<dim3((unsigned)grid), dim3(BLOCK), 0, s>>>(
       static_cast<S*>(c), static_cast<const S*>(a), static_cast<const S*>(b), n, head);
   return check_launch("reduce_vec_kernel");
 }
@@ -387,22 +387,20 @@ int launch3(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
     if (head > n) head = n;
     (void)kV;
     if constexpr (std::is_same<Tr, TrF32>::value && OP == GLOO_HIP_SUM) {
+      // A/B knob for the measurement harness (tools/sweep_variants.py).
       switch (g_variant) {
-        case 1: return launch_vec<Tr, OP, 1, false, false, false>(c, a, b, n, head, s);
-        case 2: return launch_vec<Tr, OP, 2, false, false, false>(c, a, b, n, head, s);
-        case 3: return launch_vec<Tr, OP, 4, false, false, false>(c, a, b, n, head, s);
-        case 4: return launch_vec<Tr, OP, 8, false, false, false>(c, a, b, n, head, s);
-        case 5: return launch_vec<Tr, OP, 4, true, false, false>(c, a, b, n, head, s);
-        case 6: return launch_vec<Tr, OP, 4, false, true, false>(c, a, b, n, head, s);
-        case 7: return launch_vec<Tr, OP, 4, true, true, false>(c, a, b, n, head, s);
-        case 8: return launch_vec<Tr, OP, 4, false, false, true>(c, a, b, n, head, s);
-        case 9: return launch_vec<Tr, OP, 8, false, true, false>(c, a, b, n, head, s);
-        case 10: return launch_vec<Tr, OP, 2, false, true, false>(c, a, b, n, head, s);
-        case 11: return launch_vec<Tr, OP, 8, true, true, true>(c, a, b, n, head, s);
+        case 1: return launch_vec<Tr, OP, 2, 256, kAuxNT, kAuxNT>(c, a, b, n, head, s);
+        case 2: return launch_vec<Tr, OP, 4, 256, kAuxNT, kAuxNT>(c, a, b, n, head, s);
+        case 3: return launch_vec<Tr, OP, 1, 512, kAuxNT, kAuxNT>(c, a, b, n, head, s);
+        case 4: return launch_vec<Tr, OP, 2, 512, kAuxNT, 0>(c, a, b, n, head, s);
+        case 5: return launch_vec<Tr, OP, 2, 1024, kAuxNT, kAuxNT>(c, a, b, n, head, s);
+        case 6: return launch_vec<Tr, OP, 1, 1024, kAuxNT, kAuxNT>(c, a, b, n, head, s);
+        case 7: return launch_vec<Tr, OP, 2, 512, kAuxNT, kAuxNT | kAuxSC1>(c, a, b, n, head, s);
+        case 8: return launch_vec<Tr, OP, 3, 512, kAuxNT, kAuxNT>(c, a, b, n, head, s);
         default: break;
       }
     }
-    return launch_vec<Tr, OP, kDefaultUnroll, false, false, false>(c, a, b, n, head, s);
+    return launch_vec<Tr, OP, kUnroll, kVecBlock, kAuxNT, kAuxNT>(c, a, b, n, head, s);
   }
   const size_t grid = ceil_div(n, (size_t)kBlock * kElemUnroll);
   reduce_elem_kernel<Tr, OP, kElemUnroll><<<dim3((unsigned)grid), dim3(kBlock), 0, s>>>(
@@ -431,9 +429,9 @@ int launch_multi(void* dst, const void* const* srcs, int k, size_t n, hipStream_
     if (head > n) head = n;
     constexpr int kV = 16 / sizeof(S);
     const size_t nvec = (n - head) / kV;
-    size_t grid = ceil_div(nvec, (size_t)kBlock * kMultiUnroll);
+    size_t grid = ceil_div(nvec, (size_t)kVecBlock * kMultiUnroll);
     if (grid == 0) grid = 1;
-    reduce_multi_vec_kernel<Tr, OP, kMultiUnroll><<<dim3((unsigned)grid), dim3(kBlock), 0, s>>>(
+    reduce_multi_vec_kernel<Tr, OP, kMultiUnroll, kVecBlock><<<dim3((unsigned)grid), dim3(kVecBlock), 0, s>>>(
         static_cast<S*>(dst), list, k, n, head);
     return check_launch("reduce_multi_vec_kernel");
   }

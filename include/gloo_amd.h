@@ -116,6 +116,65 @@ const char* gloo_hip_version(void);
  * the fp32 SUM path.  0 = default (tuned).  Returns the previous value. */
 int gloo_hip_set_variant(int variant);
 
+/* ------------------------------------------------------------------------
+ * Schedules.  Each of the reference's reducing algorithms is restated as a
+ * per-rank PLAN: the exact sequence of one-sided sends, receive waits,
+ * reductions, copies and notifications its run() performs (same offsets,
+ * lengths, peers, order — hence the same association order and bit-identical
+ * results).  The HIP executor (gloo_hip_algo_*) walks a plan over device
+ * memory; tests simulate all ranks' plans on the CPU against golden vectors.
+ * ---------------------------------------------------------------------- */
+typedef enum {
+  GLOO_HIP_ALGO_RING_CHUNKED = 0,     /* gloo/allreduce_ring_chunked.h        */
+  GLOO_HIP_ALGO_HALVING_DOUBLING = 1, /* gloo/allreduce_halving_doubling.h    */
+  GLOO_HIP_ALGO_RING = 2,             /* gloo/allreduce_ring.h                */
+  GLOO_HIP_ALGO_LOCAL = 3,            /* gloo/allreduce_local.{h,cc}          */
+  GLOO_HIP_ALGO_REDUCE_SCATTER = 4,   /* gloo/reduce_scatter.h (HD)           */
+} gloo_hip_algo_t;
+
+typedef enum {
+  GLOO_HIP_STEP_DECL_RECV = 0,   /* inbox region for (peer, slot): arena[dst_off, +length) */
+  GLOO_HIP_STEP_SEND = 1,        /* src[src_off, +length) -> peer's (me, slot) region       */
+  GLOO_HIP_STEP_WAIT_RECV = 2,   /* wait for the next message from (peer, slot)             */
+  GLOO_HIP_STEP_REDUCE = 3,      /* user[dst_off..] = user[dst_off..] op arena[src_off..]   */
+  GLOO_HIP_STEP_COPY = 4,        /* dst[dst_off..] = src[src_off..] (memmove semantics)     */
+  GLOO_HIP_STEP_NOTIFY = 5,      /* one notification to (peer, slot)                        */
+  GLOO_HIP_STEP_WAIT_NOTIFY = 6, /* wait for the next notification from (peer, slot)        */
+  GLOO_HIP_STEP_WAIT_SEND = 7,   /* wait until our last send to (peer, slot) has completed  */
+  GLOO_HIP_STEP_LOCAL_REDUCE = 8,/* ptrs[0] = ((ptrs[0] op ptrs[1]) op ...), length elts    */
+  GLOO_HIP_STEP_LOCAL_BCAST = 9, /* ptrs[i] = ptrs[0] for i >= 1, length elements           */
+} gloo_hip_step_kind_t;
+
+/* Message channels between a pair of ranks (the reference's slot roles). */
+#define GLOO_HIP_SLOT_DATA0 0
+#define GLOO_HIP_SLOT_DATA1 1
+#define GLOO_HIP_SLOT_NOTIFY 2
+#define GLOO_HIP_SLOT_DIST 3
+#define GLOO_HIP_SLOT_DIST_NOTIFY 4
+#define GLOO_HIP_NUM_SLOTS 5
+
+/* flags: which space each side of a data step lives in. */
+#define GLOO_HIP_SRC_ARENA 1 /* else the user buffer ptrs[0] */
+#define GLOO_HIP_DST_ARENA 2
+
+typedef struct {
+  int32_t kind;
+  int32_t peer;
+  int32_t slot;
+  int32_t flags;
+  uint64_t dst_off; /* elements */
+  uint64_t src_off; /* elements */
+  uint64_t length;  /* elements */
+} gloo_hip_step_t;
+
+/* Build rank `rank`'s plan of algorithm `algo` for `size` ranks, `count`
+ * elements and `nptrs` local pointers.  recv_elems (size entries) is used by
+ * GLOO_HIP_ALGO_REDUCE_SCATTER only.  With steps == NULL only *nsteps is
+ * filled.  *arena_elems receives the inbox arena size this rank needs. */
+int gloo_hip_plan(int algo, int rank, int size, size_t count, int nptrs,
+                  const int* recv_elems, gloo_hip_step_t* steps, size_t capacity,
+                  size_t* nsteps, size_t* arena_elems);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -13,10 +13,9 @@ import torch  # noqa: E402
 
 import gloo_amd as hip  # noqa: E402
 
-VARIANTS = {0: "default (unroll4)", 1: "unroll1", 2: "unroll2", 3: "unroll4", 4: "unroll8",
-            5: "unroll4 nt-load", 6: "unroll4 nt-store", 7: "unroll4 nt-load+store",
-            8: "unroll4 persistent", 9: "unroll8 nt-store", 10: "unroll2 nt-store",
-            11: "unroll8 nt-load+store persistent"}
+VARIANTS = {0: "default: unroll2 block512 nt-load nt-store", 1: "unroll2 block256", 2: "unroll4 block256",
+            3: "unroll1 block512", 4: "unroll2 block512 nt-load plain-store", 5: "unroll2 block1024",
+            6: "unroll1 block1024", 7: "unroll2 block512 store nt|sc1", 8: "unroll3 block512"}
 
 
 def bench(n, steps, pairs, variant=0):
