@@ -1,0 +1,139 @@
+"""CPU simulation of gloo_amd plans — TEST INFRASTRUCTURE.
+
+Executes the per-rank step lists produced by gloo_hip_plan (the C++
+restatement of the reference schedules) for ALL ranks at once over numpy
+buffers, with the oracle restatement of gloo/math.h as the reduction.  Sends
+are one-sided writes into the receiver's declared inbox region, exactly the
+semantics of gloo::transport::Buffer::send (gloo/transport/buffer.h:26-34).
+The scheduler interleaves ranks in a seeded random order, and flags any send
+that would overwrite a message the receiver has not consumed yet (a broken
+notification protocol) and any deadlock.
+"""
+import ctypes
+import random
+
+import numpy as np
+
+import oracle
+
+KIND = dict(DECL_RECV=0, SEND=1, WAIT_RECV=2, REDUCE=3, COPY=4, NOTIFY=5, WAIT_NOTIFY=6,
+            WAIT_SEND=7, LOCAL_REDUCE=8, LOCAL_BCAST=9)
+ALGO = dict(ring_chunked=0, halving_doubling=1, ring=2, local=3, reduce_scatter=4)
+SRC_ARENA, DST_ARENA = 1, 2
+
+
+class Step(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("peer", ctypes.c_int32), ("slot", ctypes.c_int32),
+                ("flags", ctypes.c_int32), ("dst_off", ctypes.c_uint64), ("src_off", ctypes.c_uint64),
+                ("length", ctypes.c_uint64)]
+
+
+def get_plan(algo, rank, size, count, nptrs=1, recv=None):
+    import gloo_amd
+    L = gloo_amd.lib
+    n = ctypes.c_size_t()
+    arena = ctypes.c_size_t()
+    rp = None
+    if recv is not None:
+        recv = np.ascontiguousarray(recv, dtype=np.int32)
+        rp = recv.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+    L.gloo_hip_plan.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_int), ctypes.c_void_p, ctypes.c_size_t,
+                                ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
+    rc = L.gloo_hip_plan(ALGO[algo], rank, size, count, nptrs, rp, None, 0, ctypes.byref(n), ctypes.byref(arena))
+    if rc:
+        raise RuntimeError(f"gloo_hip_plan failed {rc}")
+    steps = (Step * max(1, n.value))()
+    rc = L.gloo_hip_plan(ALGO[algo], rank, size, count, nptrs, rp, ctypes.cast(steps, ctypes.c_void_p),
+                         n.value, ctypes.byref(n), ctypes.byref(arena))
+    if rc:
+        raise RuntimeError(f"gloo_hip_plan failed {rc}")
+    return [steps[i] for i in range(n.value)], arena.value
+
+
+class ProtocolError(AssertionError):
+    pass
+
+
+def simulate(algo, op, dtype, inputs, recv=None, seed=0):
+    """inputs: [P][k][n] array of the dtype's storage type.  Returns [P][k][n]."""
+    P, k, n = inputs.shape
+    plans = [get_plan(algo, r, P, n, k, recv) for r in range(P)]
+    user = [[inputs[r, j].copy() for j in range(k)] for r in range(P)]
+    arena = [np.zeros(max(1, a), dtype=inputs.dtype) for _, a in plans]
+    regions = {}
+    for r, (steps, _) in enumerate(plans):
+        for s in steps:
+            if s.kind == KIND["DECL_RECV"]:
+                key = (s.peer, r, s.slot)
+                if key in regions:
+                    raise ProtocolError(f"region {key} declared twice")
+                regions[key] = (s.dst_off, s.length)
+    sent, consumed = {}, {}
+    pc = [0] * P
+    rng = random.Random(seed)
+
+    def space(r, is_arena):
+        return arena[r] if is_arena else user[r][0]
+
+    def runnable(r):
+        steps = plans[r][0]
+        if pc[r] >= len(steps):
+            return False
+        s = steps[pc[r]]
+        if s.kind in (KIND["WAIT_RECV"], KIND["WAIT_NOTIFY"]):
+            key = (s.peer, r, s.slot)
+            return sent.get(key, 0) > consumed.get(key, 0)
+        return True
+
+    while True:
+        ready = [r for r in range(P) if runnable(r)]
+        if not ready:
+            if all(pc[r] >= len(plans[r][0]) for r in range(P)):
+                break
+            raise ProtocolError(f"deadlock at pcs {pc}")
+        r = rng.choice(ready)
+        s = plans[r][0][pc[r]]
+        pc[r] += 1
+        K = s.kind
+        if K == KIND["DECL_RECV"] or K == KIND["WAIT_SEND"]:
+            continue
+        if K == KIND["SEND"]:
+            key = (r, s.peer, s.slot)
+            if key not in regions:
+                raise ProtocolError(f"send to undeclared region {key}")
+            if sent.get(key, 0) > consumed.get(key, 0):
+                raise ProtocolError(f"send {key} overwrites an unconsumed message")
+            roff, cap = regions[key]
+            if s.length > cap:
+                raise ProtocolError(f"send {key} of {s.length} exceeds region {cap}")
+            src = space(r, s.flags & SRC_ARENA)
+            arena[s.peer][roff:roff + s.length] = src[s.src_off:s.src_off + s.length]
+            sent[key] = sent.get(key, 0) + 1
+        elif K in (KIND["WAIT_RECV"], KIND["WAIT_NOTIFY"]):
+            key = (s.peer, r, s.slot)
+            consumed[key] = consumed.get(key, 0) + 1
+        elif K == KIND["NOTIFY"]:
+            key = (r, s.peer, s.slot)
+            sent[key] = sent.get(key, 0) + 1
+        elif K == KIND["REDUCE"]:
+            dst = user[r][0]
+            a = dst[s.dst_off:s.dst_off + s.length]
+            b = arena[r][s.src_off:s.src_off + s.length]
+            dst[s.dst_off:s.dst_off + s.length] = oracle.reduce3(op, dtype, a, b)
+        elif K == KIND["COPY"]:
+            src = space(r, s.flags & SRC_ARENA)
+            dst = space(r, s.flags & DST_ARENA)
+            dst[s.dst_off:s.dst_off + s.length] = src[s.src_off:s.src_off + s.length].copy()
+        elif K == KIND["LOCAL_REDUCE"]:
+            for j in range(1, k):
+                user[r][0][:s.length] = oracle.reduce3(op, dtype, user[r][0][:s.length], user[r][j][:s.length])
+        elif K == KIND["LOCAL_BCAST"]:
+            for j in range(1, k):
+                user[r][j][:s.length] = user[r][0][:s.length]
+        else:
+            raise ProtocolError(f"unknown step kind {K}")
+    for key in sent:
+        if sent[key] != consumed.get(key, 0):
+            raise ProtocolError(f"{key}: {sent[key]} sent, {consumed.get(key, 0)} consumed")
+    return np.array([[user[r][j] for j in range(k)] for r in range(P)])

@@ -1,0 +1,114 @@
+"""CPU: the C++ schedule planners (gloo_amd/csrc/plan.cc) reproduce the
+reference's allreduce / reduce-scatter schedules bit for bit.
+
+tests/golden/sched_golden.npz holds outputs of the reference's own
+AllreduceRingChunked / AllreduceHalvingDoubling / AllreduceRing /
+AllreduceLocal / ReduceScatterHalvingDoubling (oracle/gen_golden.py, ranks as
+threads over the reference's TCP transport).  Here all ranks' plans are
+executed by tests/plan_sim.py with the oracle reduction, under several random
+interleavings, and compared byte for byte.
+"""
+import numpy as np
+import pytest
+
+from plan_sim import ProtocolError, get_plan, simulate
+
+import oracle
+
+
+def golden_cases(g):
+    keys = sorted({k.rsplit("/", 1)[0] for k in g.files})
+    return keys
+
+
+def _keys():
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "sched_golden.npz"))
+    return golden_cases(z)
+
+
+@pytest.mark.parametrize("case", _keys())
+def test_plan_matches_reference_golden(golden_sched, case):
+    parts = case.split("/")
+    algo, op, dtype = parts[0], parts[1], parts[2]
+    x = golden_sched[case + "/in"]
+    want = golden_sched[case + "/out"]
+    for seed in (0, 1, 2):
+        if algo == "reduce_scatter":
+            recv = golden_sched[case + "/recv"]
+            y = simulate(algo, op, dtype, x[:, None, :], recv=recv, seed=seed)
+            got = np.concatenate([y[r, 0, :recv[r]] for r in range(len(recv))])
+        elif algo == "ring":
+            y = simulate(algo, op, dtype, x, seed=seed)
+            got = y[:, 0]
+        else:
+            y = simulate(algo, op, dtype, x, seed=seed)
+            P, k = y.shape[:2]
+            for r in range(P):
+                for j in range(k):
+                    assert (y[r, j].view(np.uint8) == y[0, 0].view(np.uint8)).all()
+            got = y[0, 0]
+        assert got.shape == want.shape
+        bad = np.where(~(got.view(np.uint8).reshape(len(got.reshape(-1)), -1) ==
+                         want.view(np.uint8).reshape(len(want.reshape(-1)), -1)).all(1))[0]
+        assert bad.size == 0, f"{case} seed {seed}: {bad.size} mismatches, first {bad[:5]}"
+
+
+@pytest.mark.parametrize("algo", ["ring_chunked", "halving_doubling", "ring"])
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 6, 7, 8, 9, 13, 16])
+@pytest.mark.parametrize("n", [0, 1, 4, 100, 1000])
+def test_allreduce_grid_closed_form(algo, P, n):
+    """The reference test grid (gloo/test/allreduce_test.cc:241-269) with its
+    closed-form fixture (gloo/test/base_test.h:184-236): src[j] = j*P + rank,
+    sum over ranks = j*P*P + P*(P-1)/2."""
+    if algo == "ring" and P > 9:
+        pytest.skip("plain ring grid stops at 9 in this sweep")
+    x = np.array([[np.arange(n, dtype=np.float64) * P + r] for r in range(P)], dtype=np.float64)
+    y = simulate(algo, "sum", "f64", x, seed=P * 31 + n)
+    want = np.arange(n, dtype=np.float64) * P * P + P * (P - 1) / 2
+    for r in range(P):
+        assert (y[r, 0] == want).all()
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 6, 7, 8, 9, 13, 16, 24, 32])
+@pytest.mark.parametrize("n", [4, 100, 1000])
+def test_reduce_scatter_grid(P, n):
+    """gloo/test/reduce_scatter_test.cc:79-105 grid: every rank holds its rank,
+    rank r's block equals P(P-1)/2."""
+    chunk = (n + P - 1) // P
+    recv, rem = [], n
+    for _ in range(P):
+        recv.append(min(chunk, rem))
+        rem = rem - chunk if rem > chunk else 0
+    x = np.array([[np.full(n, r, dtype=np.float32)] for r in range(P)])
+    y = simulate("reduce_scatter", "sum", "f32", x, recv=np.array(recv, np.int32), seed=P)
+    for r in range(P):
+        assert (y[r, 0, :recv[r]] == P * (P - 1) / 2).all()
+
+
+def test_multi_pointer_and_plan_shapes():
+    steps, arena = get_plan("ring_chunked", 0, 4, 1000, 3)
+    kinds = [s.kind for s in steps]
+    assert kinds[0] == 8 and kinds[-1] == 9        # local reduce first, broadcast last
+    assert arena == 2 * 256                         # two inboxes of max(256, ceil(n/2P))
+    steps, arena = get_plan("local", 0, 1, 10, 1)
+    assert steps == [] and arena == 0
+
+
+def test_simulator_detects_protocol_violation():
+    """The simulator must reject a schedule whose notifications are dropped."""
+    import plan_sim
+    orig = plan_sim.get_plan
+
+    def broken(*a, **kw):
+        steps, arena = orig(*a, **kw)
+        return [s for s in steps if s.kind not in (plan_sim.KIND["NOTIFY"], plan_sim.KIND["WAIT_NOTIFY"])], arena
+
+    plan_sim.get_plan = broken
+    try:
+        x = np.random.default_rng(0).standard_normal((3, 1, 5000)).astype(np.float32)
+        with pytest.raises(ProtocolError):
+            for seed in range(20):
+                plan_sim.simulate("ring_chunked", "sum", "f32", x, seed=seed)
+    finally:
+        plan_sim.get_plan = orig
