@@ -48,7 +48,7 @@ OP_NAMES = {"sum": ReductionType.SUM, "product": ReductionType.PRODUCT,
 
 EXPORTED = ("gloo_hip_reduce", "gloo_hip_reduce3", "gloo_hip_reduce_multi",
             "gloo_hip_dtype_size", "gloo_hip_last_error", "gloo_hip_version",
-            "gloo_hip_set_variant")
+            "gloo_hip_set_variant", "gloo_hip_plan")
 
 
 class GlooHipError(RuntimeError):
