@@ -190,3 +190,87 @@ ReductionFunction.sum = ReductionFunction(ReductionType.SUM)
 ReductionFunction.product = ReductionFunction(ReductionType.PRODUCT)
 ReductionFunction.max = ReductionFunction(ReductionType.MAX)
 ReductionFunction.min = ReductionFunction(ReductionType.MIN)
+
+
+# ---- contexts and algorithms (GPU allreduce / reduce-scatter drop-ins) -----
+
+ALGORITHMS = {"ring_chunked": 0, "halving_doubling": 1, "ring": 2, "local": 3,
+              "reduce_scatter": 4}
+
+
+def _bind_collectives(L):
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.gloo_hip_context_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                          ctypes.c_int, ctypes.POINTER(vp)]
+    L.gloo_hip_context_destroy.argtypes = [vp]
+    L.gloo_hip_algorithm_create.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.POINTER(vp), ctypes.c_int, sz,
+                                            ctypes.POINTER(ctypes.c_int), vp, ctypes.POINTER(vp)]
+    L.gloo_hip_algorithm_run.argtypes = [vp]
+    L.gloo_hip_algorithm_destroy.argtypes = [vp]
+    L.gloo_hip_algorithm_wait_seconds.argtypes = [vp]
+    L.gloo_hip_algorithm_wait_seconds.restype = ctypes.c_double
+
+
+_bind_collectives(lib)
+EXPORTED = EXPORTED + ("gloo_hip_context_create", "gloo_hip_context_destroy",
+                       "gloo_hip_algorithm_create", "gloo_hip_algorithm_run",
+                       "gloo_hip_algorithm_destroy", "gloo_hip_algorithm_wait_seconds")
+
+
+class Context:
+    """rendezvous::Context(rank, size) + connectFullMesh(store, device)
+    (gloo/rendezvous/context.cc:25-35).  store_url: "file:<dir>" when ranks
+    are processes, "mem:<name>" when ranks are threads of one process."""
+
+    def __init__(self, rank, size, store_url, device=0, timeout_ms=30000):
+        self.rank, self.size = rank, size
+        h = ctypes.c_void_p()
+        _check(lib.gloo_hip_context_create(rank, size, store_url.encode(), device, timeout_ms,
+                                           ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if self._h:
+            _check(lib.gloo_hip_context_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Algorithm:
+    """A constructed GPU algorithm (CudaAllreduceRingChunked & co.); run() is
+    Algorithm::run() (gloo/algorithm.h:26).  ptrs: device pointers (ints)."""
+
+    def __init__(self, ctx, algo, op, dtype, ptrs, count, recv_elems=None, stream=0):
+        self.ctx = ctx
+        arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
+        rp = None
+        if recv_elems is not None:
+            rp = (ctypes.c_int * len(recv_elems))(*[int(x) for x in recv_elems])
+        h = ctypes.c_void_p()
+        a = ALGORITHMS[algo] if isinstance(algo, str) else int(algo)
+        _check(lib.gloo_hip_algorithm_create(ctx._h, a, _as_op(op), _as_dtype(dtype), arr, len(ptrs),
+                                             int(count), rp, stream or None, ctypes.byref(h)))
+        self._h = h
+
+    def run(self):
+        _check(lib.gloo_hip_algorithm_run(self._h))
+
+    def wait_seconds(self):
+        return lib.gloo_hip_algorithm_wait_seconds(self._h)
+
+    def close(self):
+        if self._h:
+            _check(lib.gloo_hip_algorithm_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,84 @@
+// capi.cc — C-ABI over Context / PlanExecutor; no exception crosses it.
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "gloo_amd.h"
+#include "gloo_amd/common.h"
+#include "gloo_amd/context.h"
+#include "gloo_amd/errors.h"
+#include "gloo_amd/executor.h"
+
+struct gloo_hip_context {
+  std::shared_ptr<gloo_amd::Context> ctx;
+};
+struct gloo_hip_algorithm {
+  std::unique_ptr<gloo_amd::PlanExecutor> exec;
+};
+
+namespace {
+template <typename F>
+int guarded(F&& f) {
+  try {
+    f();
+    return GLOO_HIP_OK;
+  } catch (const gloo_amd::IoException& e) {
+    return gloo_amd::setError(-5, std::string("IoException: ") + e.what());
+  } catch (const std::exception& e) {
+    return gloo_amd::setError(GLOO_HIP_EINVAL_ARG, e.what());
+  } catch (...) {
+    return gloo_amd::setError(GLOO_HIP_EINVAL_ARG, "unknown exception");
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int gloo_hip_context_create(int rank, int size, const char* store_url, int device, int timeout_ms,
+                            gloo_hip_context_t* out) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(out && store_url, "null argument");
+    auto c = std::make_unique<gloo_hip_context>();
+    c->ctx = std::make_shared<gloo_amd::Context>(
+        rank, size, std::chrono::milliseconds(timeout_ms > 0 ? timeout_ms : 30000));
+    c->ctx->connect(gloo_amd::openStore(store_url), device);
+    *out = c.release();
+  });
+}
+
+int gloo_hip_context_destroy(gloo_hip_context_t ctx) {
+  return guarded([&] { delete ctx; });
+}
+
+int gloo_hip_algorithm_create(gloo_hip_context_t ctx, int algo, int op, int dtype, void* const* ptrs, int nptrs,
+                              size_t count, const int* recv_elems, gloo_hip_stream_t stream,
+                              gloo_hip_algorithm_t* out) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(ctx && out && ptrs && nptrs >= 1, "bad arguments");
+    std::vector<int> re;
+    if (algo == GLOO_HIP_ALGO_REDUCE_SCATTER) {
+      GLOO_AMD_ENFORCE(recv_elems, "reduce-scatter needs recv_elems");
+      re.assign(recv_elems, recv_elems + ctx->ctx->size);
+    }
+    auto a = std::make_unique<gloo_hip_algorithm>();
+    a->exec = std::make_unique<gloo_amd::PlanExecutor>(ctx->ctx, algo, op, dtype,
+                                                       std::vector<void*>(ptrs, ptrs + nptrs), count, re,
+                                                       static_cast<hipStream_t>(stream));
+    *out = a.release();
+  });
+}
+
+int gloo_hip_algorithm_run(gloo_hip_algorithm_t a) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(a, "null algorithm");
+    a->exec->run();
+  });
+}
+
+int gloo_hip_algorithm_destroy(gloo_hip_algorithm_t a) {
+  return guarded([&] { delete a; });
+}
+
+double gloo_hip_algorithm_wait_seconds(gloo_hip_algorithm_t a) { return a ? a->exec->lastWaitSeconds() : 0.0; }
+
+}  // extern "C"

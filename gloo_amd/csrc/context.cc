@@ -1,0 +1,87 @@
+// context.cc — see context.h.
+#include "gloo_amd/context.h"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstring>
+#include <random>
+
+#include "gloo_amd.h"
+#include "gloo_amd/common.h"
+
+namespace gloo_amd {
+
+namespace {
+struct ShmHeader {
+  uint64_t magic;
+  uint64_t size;
+  uint64_t slots;
+  uint64_t pad;
+};
+constexpr uint64_t kMagic = 0x676c6f6f5f616d64ull;  // "gloo_amd"
+
+std::vector<char> bytes(const std::string& s) { return std::vector<char>(s.begin(), s.end()); }
+}  // namespace
+
+Context::Context(int r, int s, std::chrono::milliseconds timeout)
+    : rank(r), size(s), timeout_(timeout), pid_((int)::getpid()) {
+  GLOO_AMD_ENFORCE(size >= 1 && rank >= 0 && rank < size, "bad rank ", rank, " / size ", size);
+}
+
+Context::~Context() {
+  if (shm_) ::munmap(shm_, shmBytes_);
+}
+
+void Context::connect(std::shared_ptr<Store> store, int device) {
+  store_ = std::move(store);
+  device_ = device;
+  shmBytes_ = sizeof(ShmHeader) +
+              kMaxLiveInstances * (size_t)size * size * GLOO_HIP_NUM_SLOTS * sizeof(uint64_t);
+  if (rank == 0) {
+    std::random_device rd;
+    shmName_ = strcat_("/gloo_amd_", pid_, "_", rd(), rd());
+    int fd = ::shm_open(shmName_.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+    GLOO_AMD_ENFORCE(fd >= 0, "shm_open(create) failed for ", shmName_);
+    GLOO_AMD_ENFORCE(::ftruncate(fd, (off_t)shmBytes_) == 0, "ftruncate failed");
+    shm_ = ::mmap(nullptr, shmBytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    ::close(fd);
+    GLOO_AMD_ENFORCE(shm_ != MAP_FAILED, "mmap failed");
+    auto* h = static_cast<ShmHeader*>(shm_);
+    h->size = size;
+    h->slots = GLOO_HIP_NUM_SLOTS;
+    std::atomic_thread_fence(std::memory_order_release);
+    h->magic = kMagic;
+    store_->set("gloo_amd/shm", bytes(shmName_));
+  } else {
+    auto v = store_->get("gloo_amd/shm", timeout_);
+    shmName_.assign(v.begin(), v.end());
+    int fd = ::shm_open(shmName_.c_str(), O_RDWR, 0600);
+    GLOO_AMD_ENFORCE(fd >= 0, "shm_open failed for ", shmName_);
+    shm_ = ::mmap(nullptr, shmBytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    ::close(fd);
+    GLOO_AMD_ENFORCE(shm_ != MAP_FAILED, "mmap failed");
+    auto* h = static_cast<ShmHeader*>(shm_);
+    GLOO_AMD_ENFORCE(h->magic == kMagic && (int)h->size == size, "control block mismatch");
+  }
+  barrier("connect");
+  if (rank == 0) ::shm_unlink(shmName_.c_str());  // every rank has it mapped now
+}
+
+std::atomic<uint64_t>& Context::counter(uint64_t inst, int src, int dst, int slot) {
+  GLOO_AMD_ENFORCE(shm_ != nullptr, "context not connected");
+  auto* base = reinterpret_cast<std::atomic<uint64_t>*>(static_cast<char*>(shm_) + sizeof(ShmHeader));
+  const size_t i = (((inst % kMaxLiveInstances) * size + src) * size + dst) * GLOO_HIP_NUM_SLOTS + slot;
+  return base[i];
+}
+
+void Context::barrier(const std::string& tag) {
+  const uint64_t gen = barrierGen_++;
+  const std::string prefix = strcat_("gloo_amd/barrier/", tag, "/", gen, "/");
+  store_->set(prefix + std::to_string(rank), {'1'});
+  for (int r = 0; r < size; r++) store_->get(prefix + std::to_string(r), timeout_);
+}
+
+}  // namespace gloo_amd

@@ -1,0 +1,256 @@
+// executor.cc — see executor.h.
+#include "gloo_amd/executor.h"
+
+#include <sched.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <mutex>
+#include <cstring>
+#include <set>
+#include <thread>
+
+#include "gloo_amd.h"
+#include "gloo_amd/common.h"
+
+namespace gloo_amd {
+
+namespace {
+
+struct ArenaRecord {
+  int32_t pid;
+  int32_t device;
+  uint64_t ptr;
+  uint64_t bytes;
+  hipIpcMemHandle_t handle;
+};
+
+void bumpCounter(void* p) { static_cast<std::atomic<uint64_t>*>(p)->fetch_add(1, std::memory_order_acq_rel); }
+
+void enqueueBump(hipStream_t s, std::atomic<uint64_t>& c) {
+  GLOO_AMD_HIP_CHECK(hipLaunchHostFunc(s, bumpCounter, &c));
+}
+
+void checkRc(int rc, const char* what) {
+  if (rc != GLOO_HIP_OK) throw EnforceNotMet(strcat_(what, " failed (", rc, "): ", gloo_hip_last_error()));
+}
+
+// Device memmove: non-overlapping pieces, walking away from the overlap.
+void deviceMove(char* dst, const char* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0 || dst == src) return;
+  const bool overlap = (dst < src + bytes) && (src < dst + bytes);
+  if (!overlap) {
+    GLOO_AMD_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+    return;
+  }
+  const size_t gap = dst < src ? (size_t)(src - dst) : (size_t)(dst - src);
+  if (dst < src) {
+    for (size_t off = 0; off < bytes; off += gap) {
+      const size_t n = std::min(gap, bytes - off);
+      GLOO_AMD_HIP_CHECK(hipMemcpyAsync(dst + off, src + off, n, hipMemcpyDeviceToDevice, s));
+    }
+  } else {
+    for (size_t end = bytes; end > 0;) {
+      const size_t n = std::min(gap, end);
+      end -= n;
+      GLOO_AMD_HIP_CHECK(hipMemcpyAsync(dst + end, src + end, n, hipMemcpyDeviceToDevice, s));
+    }
+  }
+}
+
+std::set<std::pair<const Context*, uint64_t>>& liveInstances() {
+  static std::set<std::pair<const Context*, uint64_t>> s;
+  return s;
+}
+std::mutex& liveMutex() {
+  static std::mutex m;
+  return m;
+}
+
+}  // namespace
+
+PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int dtype,
+                           const std::vector<void*>& ptrs, size_t count, const std::vector<int>& recvElems,
+                           hipStream_t stream)
+    : ctx_(std::move(ctx)), algo_(algo), op_(op), dtype_(dtype), ptrs_(ptrs), count_(count),
+      recvElems_(recvElems) {
+  es_ = gloo_hip_dtype_size(dtype_);
+  GLOO_AMD_ENFORCE(es_ > 0, "unknown dtype ", dtype_);
+  GLOO_AMD_ENFORCE(op_ >= GLOO_HIP_SUM && op_ <= GLOO_HIP_MIN, "unknown op ", op_);
+  GLOO_AMD_ENFORCE(!ptrs_.empty(), "need at least one pointer");
+  for (void* p : ptrs_) GLOO_AMD_ENFORCE(p != nullptr || count_ == 0, "null device pointer");
+  const int me = ctx_->rank, P = ctx_->size;
+  plan_ = makePlan(algo_, me, P, count_, (int)ptrs_.size(), recvElems_);
+  inst_ = ctx_->nextInstance();
+  {
+    std::lock_guard<std::mutex> lk(liveMutex());
+    auto key = std::make_pair((const Context*)ctx_.get(), inst_ % Context::kMaxLiveInstances);
+    GLOO_AMD_ENFORCE(liveInstances().insert(key).second, "more than ", Context::kMaxLiveInstances,
+                     " live algorithm instances on one context");
+  }
+  GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
+  if (stream) {
+    stream_ = stream;
+  } else {
+    GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    ownStream_ = true;
+  }
+  // Baseline every incoming counter before anyone can signal this instance
+  // (instance slots are recycled modulo kMaxLiveInstances).
+  for (const Step& s : plan_.steps)
+    if (s.kind == GLOO_HIP_STEP_WAIT_RECV || s.kind == GLOO_HIP_STEP_WAIT_NOTIFY)
+      consumed_[{s.peer, s.slot}] = ctx_->counter(inst_, s.peer, me, s.slot).load(std::memory_order_acquire);
+
+  if (P == 1) return;  // no transport: local reduce / broadcast only
+  const size_t arenaBytes = std::max<size_t>(256, plan_.arena * es_);
+  GLOO_AMD_HIP_CHECK(hipMalloc(&arena_, arenaBytes));
+  ArenaRecord rec;
+  std::memset(&rec, 0, sizeof(rec));
+  rec.pid = ctx_->pid();
+  rec.device = ctx_->device();
+  rec.ptr = reinterpret_cast<uint64_t>(arena_);
+  rec.bytes = arenaBytes;
+  GLOO_AMD_HIP_CHECK(hipIpcGetMemHandle(&rec.handle, arena_));
+  std::vector<char> blob(sizeof(rec));
+  std::memcpy(blob.data(), &rec, sizeof(rec));
+  ctx_->store().set(strcat_("gloo_amd/inst", inst_, "/arena/", me), blob);
+
+  // Map the inbox arena of every peer this rank sends to, and find where in
+  // it the peer declared the region for our messages (its own plan).
+  peers_.resize(P);
+  std::set<int> sendPeers;
+  for (const Step& s : plan_.steps)
+    if (s.kind == GLOO_HIP_STEP_SEND) sendPeers.insert(s.peer);
+  for (int peer : sendPeers) {
+    auto v = ctx_->store().get(strcat_("gloo_amd/inst", inst_, "/arena/", peer), ctx_->timeout());
+    GLOO_AMD_ENFORCE(v.size() == sizeof(ArenaRecord), "bad arena record from rank ", peer);
+    ArenaRecord pr;
+    std::memcpy(&pr, v.data(), sizeof(pr));
+    if (pr.pid == ctx_->pid()) {
+      peers_[peer].base = reinterpret_cast<char*>(pr.ptr);
+      if (pr.device != ctx_->device()) {
+        hipError_t e = hipDeviceEnablePeerAccess(pr.device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
+        (void)hipGetLastError();
+      }
+    } else {
+      void* p = nullptr;
+      GLOO_AMD_HIP_CHECK(hipIpcOpenMemHandle(&p, pr.handle, hipIpcMemLazyEnablePeerAccess));
+      peers_[peer].base = static_cast<char*>(p);
+      peers_[peer].ipc = true;
+    }
+    const Plan theirs = makePlan(algo_, peer, P, count_, 1, recvElems_);
+    for (const Step& d : theirs.steps)
+      if (d.kind == GLOO_HIP_STEP_DECL_RECV && d.peer == me) {
+        GLOO_AMD_ENFORCE((d.dst_off + d.length) * es_ <= pr.bytes, "peer region outside its arena");
+        remoteRegion_[{peer, d.slot}] = d.dst_off;
+      }
+  }
+  for (const Step& s : plan_.steps)
+    if (s.kind == GLOO_HIP_STEP_SEND)
+      GLOO_AMD_ENFORCE(remoteRegion_.count({s.peer, s.slot}), "rank ", s.peer, " declared no region for rank ",
+                       me, " slot ", s.slot);
+  ctx_->barrier(strcat_("inst", inst_, "/ready"));
+}
+
+PlanExecutor::~PlanExecutor() {
+  try {
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    if (ctx_->size > 1) {
+      for (auto& p : peers_)
+        if (p.ipc && p.base) (void)hipIpcCloseMemHandle(p.base);
+      // nobody may free an arena a peer still maps
+      ctx_->barrier(strcat_("inst", inst_, "/closed"));
+      if (arena_) (void)hipFree(arena_);
+    }
+    if (ownStream_ && stream_) (void)hipStreamDestroy(stream_);
+  } catch (...) {
+    // teardown is best effort; never throw from a destructor
+  }
+  std::lock_guard<std::mutex> lk(liveMutex());
+  liveInstances().erase(std::make_pair((const Context*)ctx_.get(), inst_ % Context::kMaxLiveInstances));
+}
+
+void PlanExecutor::waitCounter(std::atomic<uint64_t>& c, uint64_t target, int peer, int slot) {
+  if (c.load(std::memory_order_acquire) >= target) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto deadline = t0 + ctx_->timeout();
+  for (uint64_t i = 0;; i++) {
+    if (c.load(std::memory_order_acquire) >= target) break;
+    if (i < 4096) {
+      __builtin_ia32_pause();
+    } else if (i < 8192) {
+      sched_yield();
+    } else {
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    if ((i & 255) == 255 && std::chrono::steady_clock::now() > deadline)
+      throw IoException(strcat_("Timed out waiting for rank ", peer, " (slot ", slot, ") on rank ", ctx_->rank,
+                                " after ", ctx_->timeout().count(), " ms"));
+  }
+  waitSeconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void PlanExecutor::run() {
+  GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
+  const int me = ctx_->rank;
+  waitSeconds_ = 0;
+  for (const Step& s : plan_.steps) {
+    switch (s.kind) {
+      case GLOO_HIP_STEP_DECL_RECV:
+        break;
+      case GLOO_HIP_STEP_SEND: {
+        char* dst = peers_[s.peer].base + (remoteRegion_[{s.peer, s.slot}] + s.dst_off) * es_;
+        const char* src = (s.flags & GLOO_HIP_SRC_ARENA ? arena_ : userPtr(0)) + s.src_off * es_;
+        if (s.length) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(dst, src, s.length * es_, hipMemcpyDeviceToDevice, stream_));
+        enqueueBump(stream_, ctx_->counter(inst_, me, s.peer, s.slot));
+        break;
+      }
+      case GLOO_HIP_STEP_WAIT_RECV:
+      case GLOO_HIP_STEP_WAIT_NOTIFY: {
+        const uint64_t target = ++consumed_[{s.peer, s.slot}];
+        waitCounter(ctx_->counter(inst_, s.peer, me, s.slot), target, s.peer, s.slot);
+        break;
+      }
+      case GLOO_HIP_STEP_REDUCE:
+        checkRc(gloo_hip_reduce(op_, dtype_, userPtr(0) + s.dst_off * es_, arena_ + s.src_off * es_, s.length,
+                                stream_),
+                "gloo_hip_reduce");
+        break;
+      case GLOO_HIP_STEP_COPY: {
+        char* dst = (s.flags & GLOO_HIP_DST_ARENA ? arena_ : userPtr(0)) + s.dst_off * es_;
+        const char* src = (s.flags & GLOO_HIP_SRC_ARENA ? arena_ : userPtr(0)) + s.src_off * es_;
+        deviceMove(dst, src, s.length * es_, stream_);
+        break;
+      }
+      case GLOO_HIP_STEP_NOTIFY:
+        enqueueBump(stream_, ctx_->counter(inst_, me, s.peer, s.slot));
+        break;
+      case GLOO_HIP_STEP_WAIT_SEND:
+        GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+        break;
+      case GLOO_HIP_STEP_LOCAL_REDUCE: {
+        // one fused pass over up to GLOO_HIP_MAX_SRCS pointers, then fold on
+        for (size_t j0 = 0; j0 + 1 < ptrs_.size();) {
+          std::vector<const void*> srcs{ptrs_[0]};
+          size_t j = j0 + 1;
+          for (; j < ptrs_.size() && srcs.size() < GLOO_HIP_MAX_SRCS; j++) srcs.push_back(ptrs_[j]);
+          checkRc(gloo_hip_reduce_multi(op_, dtype_, ptrs_[0], srcs.data(), (int)srcs.size(), s.length, stream_),
+                  "gloo_hip_reduce_multi");
+          j0 = j - 1;
+        }
+        break;
+      }
+      case GLOO_HIP_STEP_LOCAL_BCAST:
+        for (size_t j = 1; j < ptrs_.size(); j++)
+          GLOO_AMD_HIP_CHECK(hipMemcpyAsync(ptrs_[j], ptrs_[0], s.length * es_, hipMemcpyDeviceToDevice, stream_));
+        break;
+      default:
+        throw EnforceNotMet(strcat_("unknown plan step ", s.kind));
+    }
+  }
+  if (ownStream_) GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+}  // namespace gloo_amd

@@ -30,9 +30,11 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <string>
 #include <type_traits>
 
 #include "gloo_amd.h"
+#include "gloo_amd/errors.h"
 
 namespace gloo_amd {
 namespace {
@@ -338,20 +340,13 @@ __global__ __launch_bounds__(kBlock) void reduce_multi_elem_kernel(
 // ---------------------------------------------------------------------------
 // Host-side dispatch.
 // ---------------------------------------------------------------------------
-thread_local char g_last_error[512] = "";
 int g_variant = 0;  // fp32 SUM kernel variant (measurement knob)
 
-int set_error(int code, const char* what) {
-  snprintf(g_last_error, sizeof(g_last_error), "%s", what);
-  return code;
-}
+int set_error(int code, const char* what) { return setError(code, what); }
 
 int check_launch(const char* name) {
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    snprintf(g_last_error, sizeof(g_last_error), "%s: %s", name, hipGetErrorString(e));
-    return (int)e;
-  }
+  if (e != hipSuccess) return setError((int)e, std::string(name) + ": " + hipGetErrorString(e));
   return GLOO_HIP_OK;
 }
 
@@ -535,8 +530,6 @@ size_t gloo_hip_dtype_size(int dtype) {
   if (dtype < 0 || dtype >= GLOO_HIP_NUM_DTYPES) return 0;
   return kSizes[dtype];
 }
-
-const char* gloo_hip_last_error(void) { return g_last_error; }
 
 const char* gloo_hip_version(void) { return "0.1.0"; }
 

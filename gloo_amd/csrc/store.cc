@@ -1,0 +1,83 @@
+// store.cc — FileStore / HashStore (see store.h).
+#include "gloo_amd/store.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <fstream>
+#include <iterator>
+#include <thread>
+
+#include "gloo_amd/common.h"
+
+namespace gloo_amd {
+
+FileStore::FileStore(const std::string& dir) : dir_(dir) {
+  ::mkdir(dir_.c_str(), 0777);  // may already exist
+}
+
+std::string FileStore::path(const std::string& key) const {
+  std::string k;
+  for (char c : key) k += (c == '/') ? '%' : c;
+  return dir_ + "/" + k;
+}
+
+void FileStore::set(const std::string& key, const std::vector<char>& data) {
+  const std::string final_path = path(key);
+  const std::string tmp = final_path + ".tmp." + std::to_string(::getpid()) + "." +
+                          std::to_string(std::hash<std::thread::id>()(std::this_thread::get_id()));
+  {
+    std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+    GLOO_AMD_ENFORCE(f.good(), "cannot write ", tmp);
+    f.write(data.data(), (std::streamsize)data.size());
+  }
+  GLOO_AMD_ENFORCE(::rename(tmp.c_str(), final_path.c_str()) == 0, "rename failed for ", final_path);
+}
+
+std::vector<char> FileStore::get(const std::string& key, std::chrono::milliseconds timeout) {
+  const std::string p = path(key);
+  const auto deadline = std::chrono::steady_clock::now() + timeout;
+  auto sleep = std::chrono::microseconds(50);
+  for (;;) {
+    std::ifstream f(p, std::ios::binary);
+    if (f.good()) return std::vector<char>(std::istreambuf_iterator<char>(f), {});
+    if (std::chrono::steady_clock::now() > deadline)
+      throw IoException("FileStore: timed out waiting for key " + key);
+    std::this_thread::sleep_for(sleep);
+    if (sleep < std::chrono::milliseconds(5)) sleep *= 2;
+  }
+}
+
+void HashStore::set(const std::string& key, const std::vector<char>& data) {
+  std::lock_guard<std::mutex> lk(m_);
+  map_[key] = data;
+  cv_.notify_all();
+}
+
+std::vector<char> HashStore::get(const std::string& key, std::chrono::milliseconds timeout) {
+  std::unique_lock<std::mutex> lk(m_);
+  if (!cv_.wait_for(lk, timeout, [&] { return map_.count(key) > 0; }))
+    throw IoException("HashStore: timed out waiting for key " + key);
+  return map_[key];
+}
+
+std::shared_ptr<Store> openStore(const std::string& url) {
+  static std::mutex m;
+  static std::map<std::string, std::weak_ptr<Store>> named;
+  if (url.rfind("file:", 0) == 0) return std::make_shared<FileStore>(url.substr(5));
+  if (url.rfind("mem:", 0) == 0) {
+    std::lock_guard<std::mutex> lk(m);
+    auto sp = named[url].lock();
+    if (!sp) {
+      sp = std::make_shared<HashStore>();
+      named[url] = sp;
+    }
+    return sp;
+  }
+  throw EnforceNotMet("unknown store url (want file:<dir> or mem:<name>): " + url);
+}
+
+}  // namespace gloo_amd

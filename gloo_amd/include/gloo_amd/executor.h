@@ -1,0 +1,77 @@
+// executor.h — runs one rank's plan on its GPU.
+//
+// The device-side twin of the reference's GPU algorithms
+// (gloo/cuda_allreduce_ring_chunked.cc:130-273 and friends) with the inboxes
+// in device memory (the CudaDeviceWorkspace flavour, gloo/cuda_workspace.h:20-31)
+// on every rank:
+//   SEND        hipMemcpyAsync into the peer's inbox (IPC-mapped or same
+//               process), over xGMI when the peer is another GPU, then a
+//               stream-ordered host function bumps the arrival counter;
+//   WAIT_*      host waits on the control-block counter (bounded by the
+//               context timeout -> IoException);
+//   REDUCE      the HIP chunk-reduce kernel on the rank's stream, reading the
+//               local inbox from HBM (never a peer's memory);
+//   NOTIFY      stream-ordered counter bump, i.e. only after every reduction
+//               enqueued before it has finished reading the inbox.
+// Only the wait steps block the host; copies and kernels stay asynchronous,
+// so a rank's chunk reductions queue back to back on its stream.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <map>
+#include <memory>
+#include <utility>
+#include <vector>
+
+#include "gloo_amd/context.h"
+#include "gloo_amd/plan.h"
+
+namespace gloo_amd {
+
+class PlanExecutor {
+ public:
+  // stream == nullptr: the executor owns a stream and run() returns with the
+  // outputs complete (synchronizeDeviceOutputs_, gloo/cuda_allreduce_ring_chunked.cc:52).
+  // Otherwise work is enqueued on `stream` and the caller synchronises
+  // (docs/cuda.md:6-13 of the reference).
+  PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int dtype,
+               const std::vector<void*>& ptrs, size_t count, const std::vector<int>& recvElems,
+               hipStream_t stream);
+  ~PlanExecutor();
+  PlanExecutor(const PlanExecutor&) = delete;
+  PlanExecutor& operator=(const PlanExecutor&) = delete;
+
+  void run();
+
+  const Plan& plan() const { return plan_; }
+  hipStream_t stream() const { return stream_; }
+  // Host time spent blocked in WAIT steps during the last run(), seconds.
+  double lastWaitSeconds() const { return waitSeconds_; }
+
+ private:
+  struct Peer {
+    char* base = nullptr;
+    bool ipc = false;
+  };
+  void waitCounter(std::atomic<uint64_t>& c, uint64_t target, int peer, int slot);
+  char* userPtr(int j) const { return static_cast<char*>(ptrs_[j]); }
+
+  std::shared_ptr<Context> ctx_;
+  int algo_, op_, dtype_;
+  size_t es_;
+  std::vector<void*> ptrs_;
+  size_t count_;
+  std::vector<int> recvElems_;
+  Plan plan_;
+  uint64_t inst_;
+  char* arena_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  bool ownStream_ = false;
+  std::vector<Peer> peers_;
+  std::map<std::pair<int, int>, uint64_t> remoteRegion_;  // (peer, slot) -> elts into peer arena
+  std::map<std::pair<int, int>, uint64_t> consumed_;      // (src, slot) -> counter value consumed
+  double waitSeconds_ = 0;
+};
+
+}  // namespace gloo_amd

@@ -175,6 +175,46 @@ int gloo_hip_plan(int algo, int rank, int size, size_t count, int nptrs,
                   const int* recv_elems, gloo_hip_step_t* steps, size_t capacity,
                   size_t* nsteps, size_t* arena_elems);
 
+/* ------------------------------------------------------------------------
+ * Contexts and algorithms (the GPU allreduce / reduce-scatter drop-ins).
+ *
+ *   gloo_hip_context_create  <- rendezvous::Context(rank, size) +
+ *                               connectFullMesh(store, device)
+ *                               (gloo/rendezvous/context.cc:25-35); the store
+ *                               is "file:<dir>" (ranks = processes of one
+ *                               node) or "mem:<name>" (ranks = threads).
+ *   gloo_hip_algorithm_create <- the constructors of CudaAllreduceRingChunked
+ *                               (gloo/cuda_allreduce_ring_chunked.h:19-26),
+ *                               CudaAllreduceHalvingDoubling
+ *                               (gloo/cuda_allreduce_halving_doubling.h:25-30),
+ *                               CudaAllreduceRing, CudaAllreduceLocal and
+ *                               ReduceScatterHalvingDoubling
+ *                               (gloo/reduce_scatter.h:112-117): device
+ *                               pointers `ptrs` (nptrs of them, on this
+ *                               rank's device), `count` elements each.
+ *                               Collective: every rank creates its
+ *                               algorithms in the same order.
+ *   gloo_hip_algorithm_run   <- Algorithm::run() (gloo/algorithm.h:26).  With
+ *                               stream == NULL outputs are complete on
+ *                               return; otherwise the work is ordered on
+ *                               `stream` and the caller synchronises.
+ * ---------------------------------------------------------------------- */
+typedef struct gloo_hip_context* gloo_hip_context_t;
+typedef struct gloo_hip_algorithm* gloo_hip_algorithm_t;
+
+int gloo_hip_context_create(int rank, int size, const char* store_url, int device,
+                            int timeout_ms, gloo_hip_context_t* out);
+int gloo_hip_context_destroy(gloo_hip_context_t ctx);
+
+int gloo_hip_algorithm_create(gloo_hip_context_t ctx, int algo, int op, int dtype,
+                              void* const* ptrs, int nptrs, size_t count,
+                              const int* recv_elems, gloo_hip_stream_t stream,
+                              gloo_hip_algorithm_t* out);
+int gloo_hip_algorithm_run(gloo_hip_algorithm_t algo);
+int gloo_hip_algorithm_destroy(gloo_hip_algorithm_t algo);
+/* Host seconds the last run() spent blocked waiting for peers. */
+double gloo_hip_algorithm_wait_seconds(gloo_hip_algorithm_t algo);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif
