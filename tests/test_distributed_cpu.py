@@ -1,0 +1,156 @@
+"""CPU, multi-process: the N>1 path without a GPU.
+
+1. The per-rank plans from gloo_hip_plan executed by separate processes that
+   exchange messages over torch.distributed's gloo backend (world_size 2 and
+   3, 127.0.0.1), reductions by the oracle restatement of gloo/math.h; results
+   compared byte for byte with the reference's schedule goldens.
+2. The C++ Context rendezvous (FileStore + shared-memory control block,
+   gloo_amd/csrc/context.cc) created and torn down by separate processes.
+"""
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+PLAN_WORKER = r'''
+import os, sys
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"]); sys.path.insert(0, os.path.join(os.environ["GLOO_AMD_ROOT"], "tests"))
+import numpy as np, torch, torch.distributed as dist
+import oracle
+from plan_sim import KIND, SRC_ARENA, DST_ARENA, get_plan
+rank, size, port, case, outdir = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
+dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=size)
+g = np.load(os.path.join(os.environ["GLOO_AMD_ROOT"], "tests", "golden", "sched_golden.npz"))
+algo, op, dtype = case.split("/")[:3]
+x = g[case + "/in"]
+recv = g[case + "/recv"] if algo == "reduce_scatter" else None
+if algo == "reduce_scatter":
+    x = x[:, None, :]
+P, k, n = x.shape
+steps, arena_n = get_plan(algo, rank, P, n, k, recv)
+user = [x[rank, j].copy() for j in range(k)]
+arena = np.zeros(max(1, arena_n), dtype=x.dtype)
+regions = {(s.peer, s.slot): (s.dst_off, s.length) for s in steps if s.kind == KIND["DECL_RECV"]}
+as_t = lambda a: torch.from_numpy(a.view(np.uint8).copy())
+pending = []
+for s in steps:
+    K = s.kind
+    if K == KIND["SEND"]:
+        src = arena if s.flags & SRC_ARENA else user[0]
+        payload = src[s.src_off:s.src_off + s.length]
+        pending.append(dist.isend(torch.tensor([s.length], dtype=torch.int64), s.peer, tag=10 * s.slot))
+        pending.append(dist.isend(as_t(payload), s.peer, tag=10 * s.slot + 1))
+    elif K == KIND["WAIT_RECV"]:
+        hdr = torch.zeros(1, dtype=torch.int64)
+        dist.recv(hdr, s.peer, tag=10 * s.slot)
+        ln = int(hdr[0]); off, cap = regions[(s.peer, s.slot)]
+        assert ln <= cap
+        buf = torch.zeros(ln * x.dtype.itemsize, dtype=torch.uint8)
+        dist.recv(buf, s.peer, tag=10 * s.slot + 1)
+        arena[off:off + ln] = buf.numpy().view(x.dtype)
+    elif K == KIND["NOTIFY"]:
+        pending.append(dist.isend(torch.zeros(1), s.peer, tag=10 * s.slot + 5))
+    elif K == KIND["WAIT_NOTIFY"]:
+        dist.recv(torch.zeros(1), s.peer, tag=10 * s.slot + 5)
+    elif K == KIND["REDUCE"]:
+        d = user[0][s.dst_off:s.dst_off + s.length]
+        user[0][s.dst_off:s.dst_off + s.length] = oracle.reduce3(op, dtype, d, arena[s.src_off:s.src_off + s.length])
+    elif K == KIND["COPY"]:
+        src = arena if s.flags & SRC_ARENA else user[0]
+        dst = arena if s.flags & DST_ARENA else user[0]
+        dst[s.dst_off:s.dst_off + s.length] = src[s.src_off:s.src_off + s.length].copy()
+    elif K == KIND["LOCAL_REDUCE"]:
+        for j in range(1, k):
+            user[0][:s.length] = oracle.reduce3(op, dtype, user[0][:s.length], user[j][:s.length])
+    elif K == KIND["LOCAL_BCAST"]:
+        for j in range(1, k):
+            user[j][:s.length] = user[0][:s.length]
+for p in pending:
+    p.wait()
+dist.barrier()
+np.save(os.path.join(outdir, f"out{rank}.npy"), np.array(user))
+dist.destroy_process_group()
+'''
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+CASES = ["ring_chunked/sum/f32/P2/k1/n1000", "halving_doubling/sum/f32/P2/k1/n1000",
+         "halving_doubling/sum/f32/P3/k1/n1000", "ring_chunked/sum/f32/P3/k2/n1000",
+         "reduce_scatter/sum/f32/P2/n100", "reduce_scatter/sum/f32/P3/n10007",
+         "ring/sum/f32/P3/k1/n1000"]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_plans_over_gloo_processes(golden_sched, case):
+    algo = case.split("/")[0]
+    P = int(case.split("/")[3][1:])
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(PLAN_WORKER)
+        env = dict(os.environ, GLOO_AMD_ROOT=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+        port = str(free_port())
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), port, case, d], env=env)
+                 for r in range(P)]
+        assert [p.wait(timeout=240) for p in procs] == [0] * P
+        outs = [np.load(os.path.join(d, f"out{r}.npy")) for r in range(P)]
+    want = golden_sched[case + "/out"]
+    if algo == "reduce_scatter":
+        recv = golden_sched[case + "/recv"]
+        got = np.concatenate([outs[r][0, :recv[r]] for r in range(P)])
+        assert (got.view(np.uint8) == want.view(np.uint8)).all()
+    elif algo == "ring":
+        for r in range(P):
+            assert (outs[r][0].view(np.uint8) == want[r].view(np.uint8)).all()
+    else:
+        for r in range(P):
+            for j in range(outs[r].shape[0]):
+                assert (outs[r][j].view(np.uint8) == want.view(np.uint8)).all(), (r, j)
+
+
+CTX_WORKER = r'''
+import os, sys
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import gloo_amd
+rank, size, store = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+c = gloo_amd.Context(rank, size, store, device=0, timeout_ms=60000)
+c.close()
+print("ok", rank)
+'''
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_context_rendezvous_processes(P):
+    """Context::connect across processes needs no GPU: FileStore exchange of
+    the control-block name, shm_open/mmap, store barrier."""
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "c.py")
+        open(w, "w").write(CTX_WORKER)
+        env = dict(os.environ, GLOO_AMD_ROOT=ROOT)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s")], env=env,
+                                  stdout=subprocess.PIPE, text=True) for r in range(P)]
+        outs = [p.communicate(timeout=120)[0] for p in procs]
+        assert [p.returncode for p in procs] == [0] * P
+        assert all(f"ok {r}" in outs[r] for r in range(P))
+
+
+def test_context_timeout_is_io_exception():
+    """A rank whose peers never arrive times out with IoException, like
+    gloo's context timeout (gloo/context.cc:61-64)."""
+    import gloo_amd
+    with tempfile.TemporaryDirectory() as d:
+        with pytest.raises(gloo_amd.GlooHipError) as e:
+            gloo_amd.Context(1, 2, "file:" + os.path.join(d, "s"), device=0, timeout_ms=300)
+        assert "timed out" in str(e.value).lower()
