@@ -53,6 +53,10 @@ def parse():
     p.add_argument("--no-host-staged", action="store_true")
     p.add_argument("--variant", type=int, default=0, help="kernel variant (tuning)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--no-allreduce", action="store_true",
+                   help="N>1: skip the config-3 xGMI ring-chunked allreduce section")
+    p.add_argument("--allreduce-mib", type=int, default=256, help="config 3: MiB per rank")
+    p.add_argument("--allreduce-iters", type=int, default=5)
     return p.parse_args()
 
 
@@ -158,6 +162,72 @@ def copy_ceiling(torch, dev, nbytes=1 << 30, iters=10):
     return round(2.0 * nbytes / t / 1e9, 1)
 
 
+def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
+    """BASELINE config 3: AllreduceRingChunked fp32 sum, `world` ranks, one per
+    GPU, 256 MiB per rank; chunks move GPU->GPU into the peer's HBM inbox
+    (xGMI), every arriving chunk is reduced by the HIP kernel on the receiving
+    GPU.  Reports the slowest rank's time per allreduce and the reduce
+    kernel's own GiB/s measured with HIP events around each chunk reduction
+    while the exchange runs (per-GPU efficiency vs the 1-GPU figure)."""
+    import tempfile
+    obj = [tempfile.mkdtemp(prefix="gloo_amd_bench_")] if rank == 0 else [None]
+    dist.broadcast_object_list(obj, src=0)
+    n = args.allreduce_mib * (1 << 20) // 4
+    res = {}
+    try:
+        buf = torch.ones(n, device=dev)
+        torch.cuda.synchronize(dev)
+        ctx = hip.Context(rank, world, "file:" + obj[0], device=dev.index, timeout_ms=60000)
+        a = hip.Algorithm(ctx, "ring_chunked", "sum", "f32", [buf.data_ptr()], n)
+        a.set_profiling(True)
+        a.run()
+        times, red_s, red_b, wait_s = [], 0.0, 0.0, 0.0
+        for _ in range(args.allreduce_iters):
+            dist.barrier()
+            t0 = time.perf_counter()
+            a.run()
+            times.append(time.perf_counter() - t0)
+            st = a.stats()
+            red_s += st["reduce_s"]
+            red_b += st["reduce_bytes"]
+            wait_s += st["wait_s"]
+        runs = 1 + args.allreduce_iters
+        want = float(world) ** runs
+        ok = bool((buf[:: max(1, n // 4096)] == want).all()) if want < 2 ** 24 else None
+        a.close()
+        ctx.close()
+        res = {"ms": [round(t * 1e3, 3) for t in times], "reduce_s": red_s, "reduce_b": red_b,
+               "wait_ms_per_run": round(wait_s / args.allreduce_iters * 1e3, 3), "verified": ok}
+    except Exception as e:  # noqa: BLE001
+        res = {"error": repr(e)}
+    gathered = [None] * world
+    dist.all_gather_object(gathered, res)
+    errs = [g["error"] for g in gathered if "error" in g]
+    if errs:
+        return {"error": errs[0]}
+    ms = [max(g["ms"][i] for g in gathered) for i in range(args.allreduce_iters)]
+    ms.sort()
+    t = ms[len(ms) // 2] / 1e3
+    per_gpu = [g["reduce_b"] / g["reduce_s"] / GIB for g in gathered if g["reduce_s"] > 0]
+    ngpu = torch.cuda.device_count()
+    return {"config": "allreduce_ring_chunked fp32 sum, %d ranks, %d MiB/rank" % (world, args.allreduce_mib),
+            "data_path": "xGMI peer copies" if ngpu >= world else f"{world} ranks on {ngpu} GPU(s)",
+            "ms_p50": round(t * 1e3, 3), "algbw_gib_s": round(n * 4 / t / GIB, 2),
+            "busbw_gib_s": round(2 * (world - 1) / world * n * 4 / t / GIB, 2),
+            "reduce_kernel_gib_s_per_gpu": [round(x, 1) for x in per_gpu],
+            "reduce_kernel_gib_s_min": round(min(per_gpu), 1) if per_gpu else None,
+            "host_wait_ms_per_run_max": max(g["wait_ms_per_run"] for g in gathered),
+            "verified": all(g["verified"] is not False for g in gathered)}
+
+
+def arm_watchdog(seconds, on_fire):
+    import threading
+    t = threading.Timer(seconds, on_fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -172,7 +242,9 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    dev = torch.device(f"cuda:{local_rank}")
+    # one GPU per rank; ranks wrap around the visible GPUs (rehearsals of the
+    # multi-rank path on a 1-GPU box put every rank on cuda:0)
+    dev = torch.device(f"cuda:{local_rank % max(1, torch.cuda.device_count())}")
     torch.cuda.set_device(dev)
     hip.set_variant(args.variant)
 
@@ -228,6 +300,7 @@ def main():
     value = world * args.steps * alg_bytes / tmax / GIB
     achieved_gbs = alg_bytes / (kern_ms / 1e3) / 1e9
 
+    out = None
     if rank == 0:
         traffic = None
         if os.path.exists(args.traffic_json):
@@ -266,6 +339,24 @@ def main():
                 out["host_staged"] = host_staged(torch, hip, n, dev)
             if not args.no_cpu:
                 out["cpu_baseline"] = cpu_baseline(args, n)
+
+    if world > 1 and not args.no_allreduce:
+        # A failure in the collective must never cost the headline line: every
+        # rank arms a watchdog; if it fires, rank 0 prints the headline with
+        # the section marked as timed out, and the process exits.
+        def fire():
+            if rank == 0:
+                out["xgmi_allreduce"] = {"error": "watchdog: section exceeded 240 s"}
+                print(json.dumps(out), flush=True)
+            os._exit(0)
+
+        wd = arm_watchdog(240, fire)
+        xr = xgmi_allreduce(torch, dist, hip, rank, world, dev, args)
+        wd.cancel()
+        if rank == 0:
+            out["xgmi_allreduce"] = xr
+
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

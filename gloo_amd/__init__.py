@@ -210,12 +210,15 @@ def _bind_collectives(L):
     L.gloo_hip_algorithm_destroy.argtypes = [vp]
     L.gloo_hip_algorithm_wait_seconds.argtypes = [vp]
     L.gloo_hip_algorithm_wait_seconds.restype = ctypes.c_double
+    L.gloo_hip_algorithm_set_profiling.argtypes = [vp, ctypes.c_int]
+    L.gloo_hip_algorithm_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
 
 
 _bind_collectives(lib)
 EXPORTED = EXPORTED + ("gloo_hip_context_create", "gloo_hip_context_destroy",
                        "gloo_hip_algorithm_create", "gloo_hip_algorithm_run",
-                       "gloo_hip_algorithm_destroy", "gloo_hip_algorithm_wait_seconds")
+                       "gloo_hip_algorithm_destroy", "gloo_hip_algorithm_wait_seconds",
+                       "gloo_hip_algorithm_set_profiling", "gloo_hip_algorithm_stats")
 
 
 class Context:
@@ -263,6 +266,16 @@ class Algorithm:
 
     def wait_seconds(self):
         return lib.gloo_hip_algorithm_wait_seconds(self._h)
+
+    def set_profiling(self, on=True):
+        _check(lib.gloo_hip_algorithm_set_profiling(self._h, 1 if on else 0))
+
+    def stats(self):
+        """After run(): reduce-kernel seconds, algorithmic bytes reduced, chunk
+        reductions, host seconds blocked on peers (profiling must be on)."""
+        out = (ctypes.c_double * 4)()
+        _check(lib.gloo_hip_algorithm_stats(self._h, out))
+        return {"reduce_s": out[0], "reduce_bytes": out[1], "reductions": int(out[2]), "wait_s": out[3]}
 
     def close(self):
         if self._h:

@@ -81,4 +81,21 @@ int gloo_hip_algorithm_destroy(gloo_hip_algorithm_t a) {
 
 double gloo_hip_algorithm_wait_seconds(gloo_hip_algorithm_t a) { return a ? a->exec->lastWaitSeconds() : 0.0; }
 
+int gloo_hip_algorithm_set_profiling(gloo_hip_algorithm_t a, int on) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(a, "null algorithm");
+    a->exec->setProfiling(on != 0);
+  });
+}
+
+int gloo_hip_algorithm_stats(gloo_hip_algorithm_t a, double* stats) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(a && stats, "null argument");
+    stats[0] = a->exec->lastReduceSeconds();
+    stats[1] = a->exec->lastReduceBytes();
+    stats[2] = (double)a->exec->lastReduceCount();
+    stats[3] = a->exec->lastWaitSeconds();
+  });
+}
+
 }  // extern "C"

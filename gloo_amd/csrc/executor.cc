@@ -164,6 +164,7 @@ PlanExecutor::~PlanExecutor() {
       ctx_->barrier(strcat_("inst", inst_, "/closed"));
       if (arena_) (void)hipFree(arena_);
     }
+    for (hipEvent_t e : events_) (void)hipEventDestroy(e);
     if (ownStream_ && stream_) (void)hipStreamDestroy(stream_);
   } catch (...) {
     // teardown is best effort; never throw from a destructor
@@ -196,6 +197,17 @@ void PlanExecutor::run() {
   GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
   const int me = ctx_->rank;
   waitSeconds_ = 0;
+  reduceSeconds_ = reduceBytes_ = 0;
+  reduceCount_ = 0;
+  size_t ev = 0;
+  auto event = [&]() {
+    if (ev == events_.size()) {
+      hipEvent_t e;
+      GLOO_AMD_HIP_CHECK(hipEventCreate(&e));
+      events_.push_back(e);
+    }
+    return events_[ev++];
+  };
   for (const Step& s : plan_.steps) {
     switch (s.kind) {
       case GLOO_HIP_STEP_DECL_RECV:
@@ -214,9 +226,15 @@ void PlanExecutor::run() {
         break;
       }
       case GLOO_HIP_STEP_REDUCE:
+        if (profiling_) GLOO_AMD_HIP_CHECK(hipEventRecord(event(), stream_));
         checkRc(gloo_hip_reduce(op_, dtype_, userPtr(0) + s.dst_off * es_, arena_ + s.src_off * es_, s.length,
                                 stream_),
                 "gloo_hip_reduce");
+        if (profiling_) {
+          GLOO_AMD_HIP_CHECK(hipEventRecord(event(), stream_));
+          reduceBytes_ += 3.0 * s.length * es_;
+          reduceCount_++;
+        }
         break;
       case GLOO_HIP_STEP_COPY: {
         char* dst = (s.flags & GLOO_HIP_DST_ARENA ? arena_ : userPtr(0)) + s.dst_off * es_;
@@ -250,7 +268,12 @@ void PlanExecutor::run() {
         throw EnforceNotMet(strcat_("unknown plan step ", s.kind));
     }
   }
-  if (ownStream_) GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+  if (ownStream_ || profiling_) GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+  for (size_t i = 0; profiling_ && i + 1 < ev; i += 2) {
+    float ms = 0;
+    GLOO_AMD_HIP_CHECK(hipEventElapsedTime(&ms, events_[i], events_[i + 1]));
+    reduceSeconds_ += ms * 1e-3;
+  }
 }
 
 }  // namespace gloo_amd

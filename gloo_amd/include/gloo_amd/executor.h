@@ -48,6 +48,12 @@ class PlanExecutor {
   hipStream_t stream() const { return stream_; }
   // Host time spent blocked in WAIT steps during the last run(), seconds.
   double lastWaitSeconds() const { return waitSeconds_; }
+  // When enabled, every REDUCE of run() is bracketed by HIP events; after the
+  // run: summed kernel seconds and algorithmic bytes (3 * n * sizeof(T)).
+  void setProfiling(bool on) { profiling_ = on; }
+  double lastReduceSeconds() const { return reduceSeconds_; }
+  double lastReduceBytes() const { return reduceBytes_; }
+  size_t lastReduceCount() const { return reduceCount_; }
 
  private:
   struct Peer {
@@ -72,6 +78,10 @@ class PlanExecutor {
   std::map<std::pair<int, int>, uint64_t> remoteRegion_;  // (peer, slot) -> elts into peer arena
   std::map<std::pair<int, int>, uint64_t> consumed_;      // (src, slot) -> counter value consumed
   double waitSeconds_ = 0;
+  bool profiling_ = false;
+  std::vector<hipEvent_t> events_;
+  double reduceSeconds_ = 0, reduceBytes_ = 0;
+  size_t reduceCount_ = 0;
 };
 
 }  // namespace gloo_amd

@@ -1,0 +1,163 @@
+// hip_allreduce.h — C++ drop-in surface for Gloo's GPU reducing algorithms.
+//
+//   gloo::CudaReductionFunction<T>      -> gloo_amd::HipReductionFunction<T>
+//                                          (gloo/cuda.h:286-358)
+//   gloo::CudaAllreduceRingChunked<T,W> -> gloo_amd::HipAllreduceRingChunked<T>
+//                                          (gloo/cuda_allreduce_ring_chunked.h:19-26)
+//   gloo::CudaAllreduceHalvingDoubling  -> gloo_amd::HipAllreduceHalvingDoubling<T>
+//                                          (gloo/cuda_allreduce_halving_doubling.h:25-30)
+//   gloo::CudaAllreduceRing             -> gloo_amd::HipAllreduceRing<T>
+//   gloo::CudaAllreduceLocal            -> gloo_amd::HipAllreduceLocal<T>
+//   gloo::ReduceScatterHalvingDoubling  -> gloo_amd::HipReduceScatterHalvingDoubling<T>
+//                                          (gloo/reduce_scatter.h:112-117)
+// Same constructor shapes (context, ptrs, count[, recvElems][, streams][, fn])
+// and run().  Differences, by design: one rank drives one GPU (all `ptrs` of
+// a rank live on that rank's device — ranks are processes or threads), the
+// workspace is always device memory (inboxes in HBM, chunks moved over
+// xGMI), and `count` is computed in size_t internally.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "gloo_amd.h"
+#include "gloo_amd/common.h"
+#include "gloo_amd/context.h"
+#include "gloo_amd/executor.h"
+
+namespace gloo_amd {
+
+// 16-bit float storage types (gloo::float16, gloo/types.h:96; c10::BFloat16).
+struct float16 {
+  uint16_t x;
+};
+struct bfloat16 {
+  uint16_t x;
+};
+
+template <typename T> struct DType;
+template <> struct DType<int8_t> { static constexpr int value = GLOO_HIP_I8; };
+template <> struct DType<uint8_t> { static constexpr int value = GLOO_HIP_U8; };
+template <> struct DType<int32_t> { static constexpr int value = GLOO_HIP_I32; };
+template <> struct DType<uint32_t> { static constexpr int value = GLOO_HIP_U32; };
+template <> struct DType<int64_t> { static constexpr int value = GLOO_HIP_I64; };
+template <> struct DType<uint64_t> { static constexpr int value = GLOO_HIP_U64; };
+template <> struct DType<float16> { static constexpr int value = GLOO_HIP_F16; };
+template <> struct DType<bfloat16> { static constexpr int value = GLOO_HIP_BF16; };
+template <> struct DType<float> { static constexpr int value = GLOO_HIP_F32; };
+template <> struct DType<double> { static constexpr int value = GLOO_HIP_F64; };
+
+// gloo::ReductionType values (gloo/algorithm.h:49-57).
+enum ReductionType { SUM = GLOO_HIP_SUM, PRODUCT = GLOO_HIP_PRODUCT, MAX = GLOO_HIP_MAX, MIN = GLOO_HIP_MIN };
+
+// Device reduction function: call() enqueues dst = dst op src on `stream`
+// (the device overload of CudaReductionFunction<T>::call, gloo/cuda.h:326-333).
+template <typename T>
+class HipReductionFunction {
+ public:
+  static const HipReductionFunction<T>* sum;
+  static const HipReductionFunction<T>* product;
+  static const HipReductionFunction<T>* min;
+  static const HipReductionFunction<T>* max;
+
+  explicit HipReductionFunction(ReductionType t) : type_(t) {}
+  ReductionType type() const { return type_; }
+  void call(T* dst, const T* src, size_t n, hipStream_t stream) const {
+    const int rc = gloo_hip_reduce(type_, DType<T>::value, dst, src, n, stream);
+    if (rc != GLOO_HIP_OK) throw EnforceNotMet(gloo_hip_last_error());
+  }
+
+ private:
+  ReductionType type_;
+};
+template <typename T>
+const HipReductionFunction<T>* HipReductionFunction<T>::sum = new HipReductionFunction<T>(SUM);
+template <typename T>
+const HipReductionFunction<T>* HipReductionFunction<T>::product = new HipReductionFunction<T>(PRODUCT);
+template <typename T>
+const HipReductionFunction<T>* HipReductionFunction<T>::min = new HipReductionFunction<T>(MIN);
+template <typename T>
+const HipReductionFunction<T>* HipReductionFunction<T>::max = new HipReductionFunction<T>(MAX);
+
+// gloo::Algorithm (gloo/algorithm.h:20-38).
+class Algorithm {
+ public:
+  explicit Algorithm(const std::shared_ptr<Context>& context)
+      : context_(context), contextRank_(context->rank), contextSize_(context->size) {}
+  virtual ~Algorithm() = default;
+  virtual void run() = 0;
+
+ protected:
+  std::shared_ptr<Context> context_;
+  const int contextRank_;
+  const int contextSize_;
+};
+
+template <typename T, int ALGO>
+class HipPlanAlgorithm : public Algorithm {
+ public:
+  HipPlanAlgorithm(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
+                   const std::vector<int>& recvElems, const std::vector<hipStream_t>& streams,
+                   const HipReductionFunction<T>* fn)
+      : Algorithm(context) {
+    std::vector<void*> p(ptrs.begin(), ptrs.end());
+    exec_ = std::make_unique<PlanExecutor>(context, ALGO, fn->type(), DType<T>::value, p,
+                                           static_cast<size_t>(count), recvElems,
+                                           streams.empty() ? nullptr : streams[0]);
+  }
+  void run() override { exec_->run(); }
+
+ protected:
+  std::unique_ptr<PlanExecutor> exec_;
+};
+
+template <typename T>
+class HipAllreduceRingChunked : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING_CHUNKED> {
+ public:
+  HipAllreduceRingChunked(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
+                          const std::vector<hipStream_t>& streams = {},
+                          const HipReductionFunction<T>* fn = HipReductionFunction<T>::sum)
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING_CHUNKED>(context, ptrs, count, {}, streams, fn) {}
+};
+
+template <typename T>
+class HipAllreduceHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING> {
+ public:
+  HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
+                              const std::vector<hipStream_t>& streams = {},
+                              const HipReductionFunction<T>* fn = HipReductionFunction<T>::sum)
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING>(context, ptrs, count, {}, streams, fn) {}
+};
+
+template <typename T>
+class HipAllreduceRing : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING> {
+ public:
+  HipAllreduceRing(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
+                   const std::vector<hipStream_t>& streams = {},
+                   const HipReductionFunction<T>* fn = HipReductionFunction<T>::sum)
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING>(context, ptrs, count, {}, streams, fn) {}
+};
+
+template <typename T>
+class HipAllreduceLocal : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_LOCAL> {
+ public:
+  HipAllreduceLocal(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
+                    const std::vector<hipStream_t>& streams = {},
+                    const HipReductionFunction<T>* fn = HipReductionFunction<T>::sum)
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_LOCAL>(context, ptrs, count, {}, streams, fn) {}
+};
+
+template <typename T>
+class HipReduceScatterHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_REDUCE_SCATTER> {
+ public:
+  HipReduceScatterHalvingDoubling(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
+                                  int count, const std::vector<int>& recvElems,
+                                  const std::vector<hipStream_t>& streams = {},
+                                  const HipReductionFunction<T>* fn = HipReductionFunction<T>::sum)
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_REDUCE_SCATTER>(context, ptrs, count, recvElems, streams, fn) {}
+};
+
+}  // namespace gloo_amd

@@ -214,6 +214,12 @@ int gloo_hip_algorithm_run(gloo_hip_algorithm_t algo);
 int gloo_hip_algorithm_destroy(gloo_hip_algorithm_t algo);
 /* Host seconds the last run() spent blocked waiting for peers. */
 double gloo_hip_algorithm_wait_seconds(gloo_hip_algorithm_t algo);
+/* Measurement: bracket every chunk reduction of run() with HIP events.  After
+ * a run: stats[0] = summed reduce-kernel seconds, stats[1] = algorithmic
+ * bytes reduced (3 * n * sizeof(T) per chunk), stats[2] = chunks reduced,
+ * stats[3] = host seconds blocked on peers. */
+int gloo_hip_algorithm_set_profiling(gloo_hip_algorithm_t algo, int on);
+int gloo_hip_algorithm_stats(gloo_hip_algorithm_t algo, double* stats4);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -264,6 +264,30 @@ int ref_reduce_scatter(int op, int dtype, int P, size_t n, const int* recvElems,
   DISPATCH(dtype, reduce_scatter<T>(op, P, n, recvElems, in, out));
 }
 
+// BASELINE config 1 timing: construct the reference algorithm once per rank,
+// then time `iters` run() calls (threads over TCP localhost, the reference's
+// own benchmark shape, gloo/benchmark/runner.cc:279-366).  Returns the
+// slowest rank's mean seconds per run in *sec.
+int ref_allreduce_timed(int algo, int P, size_t n, int iters, double* sec) {
+  std::vector<float> data((size_t)P * n, 1.0f);
+  std::vector<double> per(P, 0.0);
+  const auto* fn = gloo::ReductionFunction<float>::sum;
+  int rc = spawn(P, [&](std::shared_ptr<gloo::Context> ctx) {
+    std::vector<float*> ptrs{data.data() + (size_t)ctx->rank * n};
+    std::unique_ptr<gloo::Algorithm> a;
+    if (algo == ALGO_RING_CHUNKED) a.reset(new gloo::AllreduceRingChunked<float>(ctx, ptrs, (int)n, fn));
+    else a.reset(new gloo::AllreduceHalvingDoubling<float>(ctx, ptrs, (int)n, fn));
+    a->run();  // warmup
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < iters; i++) a->run();
+    per[ctx->rank] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / iters;
+  });
+  double m = 0;
+  for (double v : per) m = v > m ? v : m;
+  *sec = m;
+  return rc;
+}
+
 const char* ref_last_error() { return g_err.c_str(); }
 
 }  // extern "C"

@@ -186,3 +186,47 @@ def test_processes_ipc(torch, algo):
             y = np.load(os.path.join(d, f"out{r}.npy"))
             # run 1: every element = total; run 2 reduces that again: P * total
             assert (y == P * total).all(), (r, y[:5])
+
+
+def test_profiling_stats(torch):
+    """Measurement hook: every chunk reduction is timed with HIP events and
+    the algorithmic bytes add up to the reduce-scatter part of the schedule."""
+    import gloo_amd
+    P, n = 4, 1 << 20
+    url = "mem:" + uuid.uuid4().hex
+    bufs = [torch.ones(n, device=f"cuda:{dev_of(torch, r)}") for r in range(P)]
+    torch.cuda.synchronize()
+    out = [None] * P
+
+    def body(r):
+        torch.cuda.set_device(dev_of(torch, r))
+        ctx = gloo_amd.Context(r, P, url, device=dev_of(torch, r))
+        a = gloo_amd.Algorithm(ctx, "ring_chunked", "sum", "f32", [bufs[r].data_ptr()], n)
+        a.set_profiling(True)
+        a.run()
+        out[r] = a.stats()
+        a.close()
+        ctx.close()
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(P)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for r in range(P):
+        st = out[r]
+        # 2(P-1) chunks of n/(2P) elements reduced per rank
+        assert st["reductions"] == 2 * (P - 1)
+        assert st["reduce_bytes"] == 3 * 4 * (n // (2 * P)) * 2 * (P - 1)
+        assert st["reduce_s"] > 0
+    assert float(bufs[0][0]) == P
+
+
+def test_cpp_example_program():
+    """The C++ drop-in surface (gloo_amd/include/gloo_amd/hip_allreduce.h)."""
+    exe = os.path.join(ROOT, "examples", "allreduce_ring_chunked")
+    if not os.path.exists(exe):
+        pytest.skip("example not built")
+    r = subprocess.run([exe, "4", "100003"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok" in r.stdout
