@@ -12,6 +12,8 @@
 #include "gloo_amd.h"
 #include "gloo_amd/common.h"
 
+#include <hip/hip_runtime_api.h>
+
 namespace gloo_amd {
 
 namespace {
@@ -32,14 +34,16 @@ Context::Context(int r, int s, std::chrono::milliseconds timeout)
 }
 
 Context::~Context() {
+  if (shmDev_) (void)hipHostUnregister(shm_);
   if (shm_) ::munmap(shm_, shmBytes_);
 }
 
 void Context::connect(std::shared_ptr<Store> store, int device) {
   store_ = std::move(store);
   device_ = device;
-  shmBytes_ = sizeof(ShmHeader) +
-              kMaxLiveInstances * (size_t)size * size * GLOO_HIP_NUM_SLOTS * sizeof(uint64_t);
+  countersBytes_ = kMaxLiveInstances * (size_t)size * size * GLOO_HIP_NUM_SLOTS * sizeof(uint64_t);
+  shmBytes_ = sizeof(ShmHeader) + countersBytes_ + ((size_t)size * sizeof(uint32_t) + 63) / 64 * 64;
+  shmBytes_ = (shmBytes_ + 4095) / 4096 * 4096;
   if (rank == 0) {
     std::random_device rd;
     shmName_ = strcat_("/gloo_amd_", pid_, "_", rd(), rd());
@@ -75,6 +79,31 @@ std::atomic<uint64_t>& Context::counter(uint64_t inst, int src, int dst, int slo
   auto* base = reinterpret_cast<std::atomic<uint64_t>*>(static_cast<char*>(shm_) + sizeof(ShmHeader));
   const size_t i = (((inst % kMaxLiveInstances) * size + src) * size + dst) * GLOO_HIP_NUM_SLOTS + slot;
   return base[i];
+}
+
+void Context::ensureDeviceMapped() {
+  if (shmDev_) return;
+  GLOO_AMD_HIP_CHECK(hipHostRegister(shm_, shmBytes_, hipHostRegisterMapped | hipHostRegisterPortable));
+  void* d = nullptr;
+  GLOO_AMD_HIP_CHECK(hipHostGetDevicePointer(&d, shm_, 0));
+  shmDev_ = d;
+}
+
+uint64_t* Context::counterDevicePtr(uint64_t inst, int src, int dst, int slot) {
+  ensureDeviceMapped();
+  const size_t off = reinterpret_cast<char*>(&counter(inst, src, dst, slot)) - static_cast<char*>(shm_);
+  return reinterpret_cast<uint64_t*>(static_cast<char*>(shmDev_) + off);
+}
+
+std::atomic<uint32_t>& Context::errorWord(int r) {
+  auto* base = reinterpret_cast<std::atomic<uint32_t>*>(static_cast<char*>(shm_) + sizeof(ShmHeader) + countersBytes_);
+  return base[r];
+}
+
+uint32_t* Context::errorWordDevicePtr(int r) {
+  ensureDeviceMapped();
+  const size_t off = reinterpret_cast<char*>(&errorWord(r)) - static_cast<char*>(shm_);
+  return reinterpret_cast<uint32_t*>(static_cast<char*>(shmDev_) + off);
 }
 
 void Context::barrier(const std::string& tag) {

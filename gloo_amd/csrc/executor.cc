@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <mutex>
 #include <cstring>
 #include <set>
@@ -13,6 +14,7 @@
 
 #include "gloo_amd.h"
 #include "gloo_amd/common.h"
+#include "gloo_amd/signal.h"
 
 namespace gloo_amd {
 
@@ -102,9 +104,55 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     if (s.kind == GLOO_HIP_STEP_WAIT_RECV || s.kind == GLOO_HIP_STEP_WAIT_NOTIFY)
       consumed_[{s.peer, s.slot}] = ctx_->counter(inst_, s.peer, me, s.slot).load(std::memory_order_acquire);
 
+  for (const Step& s : plan_.steps)
+    if (s.kind == GLOO_HIP_STEP_SEND || s.kind == GLOO_HIP_STEP_NOTIFY)
+      sent_[{s.peer, s.slot}] = ctx_->counter(inst_, me, s.peer, s.slot).load(std::memory_order_acquire);
+
   if (P == 1) return;  // no transport: local reduce / broadcast only
+
+  // Phase 1: who is where.  Every rank publishes (pid, device); each rank
+  // reads the records of every peer its plan talks to.
+  std::set<int> planPeers, sendPeers, recvPeers;
+  for (const Step& s : plan_.steps) {
+    if (s.peer >= 0) planPeers.insert(s.peer);
+    if (s.kind == GLOO_HIP_STEP_SEND) sendPeers.insert(s.peer);
+    if (s.kind == GLOO_HIP_STEP_DECL_RECV) recvPeers.insert(s.peer);
+  }
+  {
+    int32_t hello[2] = {ctx_->pid(), ctx_->device()};
+    std::vector<char> blob(sizeof(hello));
+    std::memcpy(blob.data(), hello, sizeof(hello));
+    ctx_->store().set(strcat_("gloo_amd/inst", inst_, "/where/", me), blob);
+  }
+  peers_.resize(P);
+  bool sharesDeviceInProcess = false, crossDeviceSender = false;
+  for (int peer : planPeers) {
+    auto v = ctx_->store().get(strcat_("gloo_amd/inst", inst_, "/where/", peer), ctx_->timeout());
+    GLOO_AMD_ENFORCE(v.size() == 2 * sizeof(int32_t), "bad record from rank ", peer);
+    int32_t w[2];
+    std::memcpy(w, v.data(), sizeof(w));
+    peers_[peer].pid = w[0];
+    peers_[peer].device = w[1];
+    if (w[0] == ctx_->pid() && w[1] == ctx_->device()) sharesDeviceInProcess = true;
+    if (recvPeers.count(peer) && w[1] != ctx_->device()) crossDeviceSender = true;
+  }
+  const char* sig = std::getenv("GLOO_AMD_SIGNAL");
+  const std::string sigMode = sig ? sig : "auto";
+  deviceSignal_ = sigMode == "device" || (sigMode == "auto" && !sharesDeviceInProcess);
+  // A peer GPU writes this rank's inboxes over xGMI; keep them in
+  // fine-grained memory so no stale line of this GPU's L2 can be read.
+  const char* ar = std::getenv("GLOO_AMD_ARENA");
+  const std::string arMode = ar ? ar : "auto";
+  fineArena_ = arMode == "fine" || (arMode == "auto" && crossDeviceSender);
+
+  // Phase 2: the inbox arena.
   const size_t arenaBytes = std::max<size_t>(256, plan_.arena * es_);
-  GLOO_AMD_HIP_CHECK(hipMalloc(&arena_, arenaBytes));
+  if (fineArena_) {
+    GLOO_AMD_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), arenaBytes,
+                                             hipDeviceMallocFinegrained));
+  } else {
+    GLOO_AMD_HIP_CHECK(hipMalloc(&arena_, arenaBytes));
+  }
   ArenaRecord rec;
   std::memset(&rec, 0, sizeof(rec));
   rec.pid = ctx_->pid();
@@ -118,10 +166,6 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
 
   // Map the inbox arena of every peer this rank sends to, and find where in
   // it the peer declared the region for our messages (its own plan).
-  peers_.resize(P);
-  std::set<int> sendPeers;
-  for (const Step& s : plan_.steps)
-    if (s.kind == GLOO_HIP_STEP_SEND) sendPeers.insert(s.peer);
   for (int peer : sendPeers) {
     auto v = ctx_->store().get(strcat_("gloo_amd/inst", inst_, "/arena/", peer), ctx_->timeout());
     GLOO_AMD_ENFORCE(v.size() == sizeof(ArenaRecord), "bad arena record from rank ", peer);
@@ -151,6 +195,10 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     if (s.kind == GLOO_HIP_STEP_SEND)
       GLOO_AMD_ENFORCE(remoteRegion_.count({s.peer, s.slot}), "rank ", s.peer, " declared no region for rank ",
                        me, " slot ", s.slot);
+  if (deviceSignal_) {
+    (void)ctx_->counterDevicePtr(inst_, 0, 0, 0);  // register the control block now
+    ctx_->errorWord(me).store(0);
+  }
   ctx_->barrier(strcat_("inst", inst_, "/ready"));
 }
 
@@ -196,6 +244,17 @@ void PlanExecutor::waitCounter(std::atomic<uint64_t>& c, uint64_t target, int pe
 void PlanExecutor::run() {
   GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
   const int me = ctx_->rank;
+  const uint64_t timeoutTicks = (uint64_t)ctx_->timeout().count() * 100000ull;  // 100 MHz realtime clock
+  auto signal = [&](int peer, int slot) {
+    const uint64_t seq = ++sent_[{peer, slot}];
+    if (deviceSignal_) {
+      GLOO_AMD_HIP_CHECK(launchSignal(ctx_->counterDevicePtr(inst_, me, peer, slot), seq, stream_));
+    } else {
+      enqueueBump(stream_, ctx_->counter(inst_, me, peer, slot));
+    }
+  };
+  if (deviceSignal_ && ctx_->errorWord(me).load() != 0)
+    throw IoException(strcat_("rank ", me, ": a device-side wait of a previous run timed out"));
   waitSeconds_ = 0;
   reduceSeconds_ = reduceBytes_ = 0;
   reduceCount_ = 0;
@@ -216,13 +275,18 @@ void PlanExecutor::run() {
         char* dst = peers_[s.peer].base + (remoteRegion_[{s.peer, s.slot}] + s.dst_off) * es_;
         const char* src = (s.flags & GLOO_HIP_SRC_ARENA ? arena_ : userPtr(0)) + s.src_off * es_;
         if (s.length) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(dst, src, s.length * es_, hipMemcpyDeviceToDevice, stream_));
-        enqueueBump(stream_, ctx_->counter(inst_, me, s.peer, s.slot));
+        signal(s.peer, s.slot);
         break;
       }
       case GLOO_HIP_STEP_WAIT_RECV:
       case GLOO_HIP_STEP_WAIT_NOTIFY: {
         const uint64_t target = ++consumed_[{s.peer, s.slot}];
-        waitCounter(ctx_->counter(inst_, s.peer, me, s.slot), target, s.peer, s.slot);
+        if (deviceSignal_) {
+          GLOO_AMD_HIP_CHECK(launchWait(ctx_->counterDevicePtr(inst_, s.peer, me, s.slot), target, timeoutTicks,
+                                        ctx_->errorWordDevicePtr(me), stream_));
+        } else {
+          waitCounter(ctx_->counter(inst_, s.peer, me, s.slot), target, s.peer, s.slot);
+        }
         break;
       }
       case GLOO_HIP_STEP_REDUCE:
@@ -243,10 +307,12 @@ void PlanExecutor::run() {
         break;
       }
       case GLOO_HIP_STEP_NOTIFY:
-        enqueueBump(stream_, ctx_->counter(inst_, me, s.peer, s.slot));
+        signal(s.peer, s.slot);
         break;
       case GLOO_HIP_STEP_WAIT_SEND:
-        GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+        // stream order already puts every later use of the buffer after the
+        // copy; only host-side waiting needs the explicit drain
+        if (!deviceSignal_) GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
         break;
       case GLOO_HIP_STEP_LOCAL_REDUCE: {
         // one fused pass over up to GLOO_HIP_MAX_SRCS pointers, then fold on
@@ -268,7 +334,14 @@ void PlanExecutor::run() {
         throw EnforceNotMet(strcat_("unknown plan step ", s.kind));
     }
   }
-  if (ownStream_ || profiling_) GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+  if (ownStream_ || profiling_) {
+    const auto t0 = std::chrono::steady_clock::now();
+    GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (deviceSignal_) waitSeconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (deviceSignal_ && ctx_->errorWord(me).exchange(0) != 0)
+      throw IoException(strcat_("Timed out on rank ", me, " waiting for a peer (device-side wait, ",
+                                ctx_->timeout().count(), " ms)"));
+  }
   for (size_t i = 0; profiling_ && i + 1 < ev; i += 2) {
     float ms = 0;
     GLOO_AMD_HIP_CHECK(hipEventElapsedTime(&ms, events_[i], events_[i + 1]));

@@ -47,6 +47,12 @@ class Context : public std::enable_shared_from_this<Context> {
 
   // Counter for messages src -> dst on `slot` of instance `inst`.
   std::atomic<uint64_t>& counter(uint64_t inst, int src, int dst, int slot);
+  // The same counter as a GPU-addressable pointer (the control block is
+  // registered with hipHostRegister on first use).
+  uint64_t* counterDevicePtr(uint64_t inst, int src, int dst, int slot);
+  // Per-rank error word written by device-side waits that time out.
+  std::atomic<uint32_t>& errorWord(int r);
+  uint32_t* errorWordDevicePtr(int r);
 
   // Store-based barrier among all ranks (setup / teardown only).
   void barrier(const std::string& tag);
@@ -59,7 +65,10 @@ class Context : public std::enable_shared_from_this<Context> {
   uint64_t nextInstance_ = 0;
   std::string shmName_;
   void* shm_ = nullptr;
+  void* shmDev_ = nullptr;
   size_t shmBytes_ = 0;
+  size_t countersBytes_ = 0;
+  void ensureDeviceMapped();
   uint64_t barrierGen_ = 0;
 };
 

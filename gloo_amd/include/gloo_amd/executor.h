@@ -15,6 +15,16 @@
 //               enqueued before it has finished reading the inbox.
 // Only the wait steps block the host; copies and kernels stay asynchronous,
 // so a rank's chunk reductions queue back to back on its stream.
+//
+// Device signalling (default whenever no other rank shares this rank's GPU
+// inside the same process): SEND / NOTIFY become a one-wave signal kernel
+// writing the channel's next sequence number, WAIT_* a one-wave wait kernel
+// (signal.h) — the whole plan is enqueued without a single host round trip.
+// Within one process, ranks that share a GPU share its hardware queues, where
+// a spinning wait could block the very signal it waits for; those ranks keep
+// the host-side waits.  Both styles write the same monotonically increasing
+// sequence numbers, so they interoperate.  GLOO_AMD_SIGNAL=host|device
+// overrides the choice.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -46,6 +56,8 @@ class PlanExecutor {
 
   const Plan& plan() const { return plan_; }
   hipStream_t stream() const { return stream_; }
+  bool deviceSignalling() const { return deviceSignal_; }
+  bool fineGrainedArena() const { return fineArena_; }
   // Host time spent blocked in WAIT steps during the last run(), seconds.
   double lastWaitSeconds() const { return waitSeconds_; }
   // When enabled, every REDUCE of run() is bracketed by HIP events; after the
@@ -59,6 +71,8 @@ class PlanExecutor {
   struct Peer {
     char* base = nullptr;
     bool ipc = false;
+    int pid = -1;
+    int device = -1;
   };
   void waitCounter(std::atomic<uint64_t>& c, uint64_t target, int peer, int slot);
   char* userPtr(int j) const { return static_cast<char*>(ptrs_[j]); }
@@ -77,6 +91,9 @@ class PlanExecutor {
   std::vector<Peer> peers_;
   std::map<std::pair<int, int>, uint64_t> remoteRegion_;  // (peer, slot) -> elts into peer arena
   std::map<std::pair<int, int>, uint64_t> consumed_;      // (src, slot) -> counter value consumed
+  std::map<std::pair<int, int>, uint64_t> sent_;          // (dst, slot) -> last sequence signalled
+  bool deviceSignal_ = false;  // stream-ordered signal/wait kernels instead of host waits
+  bool fineArena_ = false;     // inbox arena in fine-grained (cross-device coherent) memory
   double waitSeconds_ = 0;
   bool profiling_ = false;
   std::vector<hipEvent_t> events_;

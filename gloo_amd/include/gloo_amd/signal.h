@@ -1,0 +1,25 @@
+// signal.h — stream-ordered cross-rank signalling kernels (internal).
+//
+// A rank's chunk exchange is a sequence of (copy, signal) on the sender's
+// stream and (wait, reduce) on the receiver's stream.  These two one-wave
+// kernels make both ends stream-ordered, so a whole plan is enqueued without
+// host round trips:
+//   signal: system-scope release, then the flag word := value
+//   wait:   poll the flag (system-scope acquire) until >= target, sleeping
+//           between polls; give up after `timeout_ticks` of the 100 MHz
+//           realtime counter and set *err (the host raises IoException).
+// Flags are 64-bit counters in the node's shared control block, registered
+// with hipHostRegister so every GPU of every rank can address them.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+namespace gloo_amd {
+
+hipError_t launchSignal(uint64_t* flag, uint64_t value, hipStream_t stream);
+hipError_t launchWait(const uint64_t* flag, uint64_t target, uint64_t timeoutTicks, uint32_t* err,
+                      hipStream_t stream);
+
+}  // namespace gloo_amd

@@ -164,18 +164,25 @@ np.save(out, buf.cpu().numpy().view(np.float32))
 '''
 
 
-@pytest.mark.parametrize("algo", ["ring_chunked", "halving_doubling"])
-def test_processes_ipc(torch, algo):
+@pytest.mark.parametrize("algo,P,env", [
+    ("ring_chunked", 4, {}),                                  # auto: device-side signalling
+    ("halving_doubling", 4, {}),
+    ("halving_doubling", 5, {}),                              # non-power-of-2 binary blocks
+    ("ring_chunked", 3, {"GLOO_AMD_SIGNAL": "host"}),         # host waits across processes
+    ("halving_doubling", 4, {"GLOO_AMD_ARENA": "fine"}),      # fine-grained inboxes over IPC
+    ("ring_chunked", 8, {"GLOO_AMD_ARENA": "fine"}),
+])
+def test_processes_ipc(torch, algo, P, env):
     """Ranks as processes: inbox arenas exchanged as HIP IPC handles through a
     FileStore; run twice (x2 of the sum, exact for these integers)."""
-    P, n = 4, 100_003
+    n = 100_003
     x = np.array([np.arange(n, dtype=np.float32) * 0 + r + 1 for r in range(P)], dtype=np.float32)
     with tempfile.TemporaryDirectory() as d:
         inp = os.path.join(d, "in.npy")
         np.save(inp, x)
         worker = os.path.join(d, "w.py")
         open(worker, "w").write(WORKER)
-        env = dict(os.environ, GLOO_AMD_ROOT=ROOT)
+        env = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
         procs = [subprocess.Popen([sys.executable, worker, str(r), str(P), "file:" + os.path.join(d, "store"),
                                    algo, inp, os.path.join(d, f"out{r}.npy")], env=env)
                  for r in range(P)]
@@ -230,3 +237,16 @@ def test_cpp_example_program():
     r = subprocess.run([exe, "4", "100003"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ok" in r.stdout
+
+
+@pytest.mark.parametrize("env", [{"GLOO_AMD_SIGNAL": "host"}, {"GLOO_AMD_ARENA": "fine"}])
+def test_threads_forced_modes(torch, golden_sched, env, monkeypatch):
+    """Thread ranks under the non-default transport settings still match the
+    reference bit for bit (fine-grained inboxes; explicit host waits)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    case = "halving_doubling/sum/f32/P5/k1/n10007"
+    x, want = golden_sched[case + "/in"], golden_sched[case + "/out"]
+    y = run_threads(torch, "halving_doubling", "sum", "f32", x)
+    for r in range(y.shape[0]):
+        assert same_bytes(y[r, 0], want)

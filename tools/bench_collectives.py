@@ -82,6 +82,42 @@ def run_collective(torch, algo, op, dtype, P, n, iters, profile=True, recv=None)
     return per_iter, stats
 
 
+def run_collective_procs(torch, dist, algo, op, dtype, P, n, iters, store, profile=True, recv=None):
+    """Same measurement with THIS process as one rank (torch.distributed.run
+    launch); timings gathered over torch.distributed's gloo backend."""
+    import gloo_amd
+    rank = dist.get_rank()
+    ndev = torch.cuda.device_count()
+    dev = rank % ndev
+    torch.cuda.set_device(dev)
+    es = gloo_amd.dtype_size(dtype)
+    buf = torch.zeros(max(4, n * es), dtype=torch.uint8, device=f"cuda:{dev}")
+    if dtype == "f32":
+        buf.view(torch.float32)[:n].fill_(1.0)
+    torch.cuda.synchronize()
+    ctx = gloo_amd.Context(rank, P, store, device=dev, timeout_ms=120000)
+    a = gloo_amd.Algorithm(ctx, algo, op, dtype, [buf.data_ptr()], n, recv_elems=recv)
+    a.set_profiling(profile)
+    a.run()
+    times, acc = [], {"reduce_s": 0.0, "reduce_bytes": 0.0, "reductions": 0, "wait_s": 0.0}
+    for _ in range(iters):
+        dist.barrier()
+        t0 = time.perf_counter()
+        a.run()
+        times.append(time.perf_counter() - t0)
+        st = a.stats()
+        for k in acc:
+            acc[k] += st[k]
+    a.close()
+    ctx.close()
+    allt = [None] * P
+    alls = [None] * P
+    dist.all_gather_object(allt, times)
+    dist.all_gather_object(alls, acc)
+    per_iter = sorted(max(allt[r][i] for r in range(P)) for i in range(iters))
+    return per_iter, alls
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--ranks", type=int, default=8)
@@ -89,7 +125,37 @@ def main():
     p.add_argument("--iters", type=int, default=5)
     args = p.parse_args()
     cfgs = set(args.configs.split(","))
-    if "1" in cfgs:
+    import torch
+    ndev = torch.cuda.device_count()
+    P = args.ranks
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    emit = True
+    if world:
+        # ranks are processes: one per GPU (wrapping on a small box)
+        import tempfile
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        P = world
+        emit = dist.get_rank() == 0
+        obj = [tempfile.mkdtemp(prefix="gloo_amd_coll_")] if emit else [None]
+        dist.broadcast_object_list(obj, src=0)
+        counter = [0]
+
+        def run_collective(torch, algo, op, dtype, P, n, iters, profile=True, recv=None):  # noqa: F811
+            counter[0] += 1
+            return run_collective_procs(torch, dist, algo, op, dtype, P, n, iters,
+                                        "file:%s/%d" % (obj[0], counter[0]), profile, recv)
+    else:
+        run_collective = globals()["run_collective"]
+    layout = "processes" if world else "threads"
+    where = ("xGMI peer copies" if ndev >= P else f"{P} ranks on {ndev} GPU(s): HBM-local copies") + \
+        f", ranks as {layout}"
+    _print = print
+
+    def print(*a, **k):  # noqa: A001
+        if emit:
+            _print(*a, **k)
+    if "1" in cfgs and emit:
         import ctypes
         import oracle
         if oracle.ref_available():
@@ -103,10 +169,6 @@ def main():
                                   "ranks": 2, "transport": "tcp loopback (threads)", "elements": n,
                                   "rc": rc, "ms": round(sec.value * 1e3, 3),
                                   "payload_gib_s": round(n * 4 / sec.value / GIB, 3)}), flush=True)
-    import torch
-    ndev = torch.cuda.device_count()
-    P = args.ranks
-    where = "xGMI peer copies" if ndev >= P else f"{P} ranks on {ndev} GPU(s): HBM-local copies"
     if "3" in cfgs:
         n = 64 << 20  # 256 MiB of fp32 per rank
         per, st = run_collective(torch, "ring_chunked", "sum", "f32", P, n, args.iters)
