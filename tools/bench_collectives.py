@@ -150,7 +150,8 @@ def main():
     layout = "processes" if world else "threads"
     where = ("xGMI peer copies" if ndev >= P else f"{P} ranks on {ndev} GPU(s): HBM-local copies") + \
         f", ranks as {layout}"
-    _print = print
+    import builtins
+    _print = builtins.print
 
     def print(*a, **k):  # noqa: A001
         if emit:

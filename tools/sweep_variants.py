@@ -43,8 +43,36 @@ def bench(n, steps, pairs, variant=0):
     return mean, med
 
 
+def bench_misaligned(n, steps, pairs, src_off_elems, dtype_bytes=4):
+    """dst 16-B aligned, src shifted by src_off_elems elements: the
+    relatively-misaligned case an arbitrary Gloo chunk offset produces."""
+    dev = torch.device("cuda:0")
+    bufs = [(torch.rand(n + 8, device=dev), torch.rand(n + 8, device=dev)) for _ in range(pairs)]
+    s = torch.cuda.current_stream().cuda_stream
+    es = dtype_bytes
+    for i in range(5):
+        d, x = bufs[i % pairs]
+        hip.reduce_ptr("sum", "f32", d.data_ptr(), x.data_ptr() + src_off_elems * es, n, s)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(steps):
+        d, x = bufs[i % pairs]
+        hip.reduce_ptr("sum", "f32", d.data_ptr(), x.data_ptr() + src_off_elems * es, n, s)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / steps
+    del bufs
+    torch.cuda.empty_cache()
+    return us
+
+
 def main():
     n = 16 << 20
+    for off in (0, 1, 2, 3):
+        us = bench_misaligned(n, 300, 6, off)
+        print(json.dumps({"sweep": "relative_misalignment", "src_offset_elems": off, "us_mean": round(us, 2),
+                          "GBs": round(3 * n * 4 / (us / 1e3) / 1e9, 1)}), flush=True)
     for v in VARIANTS:
         mean, med = bench(n, 300, 6, v)
         print(json.dumps({"sweep": "variant", "variant": v, "name": VARIANTS[v],
