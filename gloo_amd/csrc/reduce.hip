@@ -17,8 +17,9 @@
 //    arbitrary element counts, gloo/allreduce_ring_chunked.h:128): the first
 //    `head` elements up to the 16-B boundary of the destination and the
 //    ragged tail are done element-wise by block 0 inside the same launch;
-//  * operands whose misalignment differs (relative offset not a multiple of
-//    16 B) take an element-wise coalesced path with the same tile shape;
+//  * operands whose misalignment differs from the destination's (relative
+//    offset not a multiple of 16 B) still move in 16-B accesses: their
+//    misalignment rides in the buffer instruction's scalar offset;
 //  * 64-bit indices throughout (the reference uses `int`, Appendix A.4).
 //
 // Arithmetic is bit-exact with gloo/math.h evaluated in the same order: see
@@ -39,7 +40,6 @@
 namespace gloo_amd {
 namespace {
 
-constexpr int kBlock = 256;  // 4 waves of 64 lanes
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
@@ -183,14 +183,28 @@ __device__ __forceinline__ u32x4 apply_packet<TrU8, GLOO_HIP_SUM>(u32x4 a, u32x4
 // are discarded) without per-lane branches.
 constexpr int kRsrcFlags = 0x00020000;  // gfx950 raw-buffer word 3
 constexpr int kAuxNT = 2;               // cache policy `nt`: streamed once
-constexpr int kAuxSC1 = 16;             // cache policy `sc1`
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, kRsrcFlags);
 }
 template <int AUX>
-__device__ __forceinline__ u32x4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
+__device__ __forceinline__ u32x4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff = 0) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, AUX);
+}
+
+// A source operand of the vector body: its first body byte sits `mis` bytes
+// past a 16-B boundary (0 when it is congruent with the destination).  The
+// descriptor is based at the aligned-down address and `mis` rides in the
+// instruction's scalar offset, so a relatively misaligned operand still
+// moves in 16-B accesses (gfx950 runs global/buffer accesses in unaligned
+// mode; the compiler itself emits dwordx4 for byte-aligned data).
+struct Src {
+  const char* base;  // 16-B aligned
+  uint32_t mis;      // 0..15
+};
+__device__ __forceinline__ Src src_of(const void* body) {
+  const uintptr_t p = reinterpret_cast<uintptr_t>(body);
+  return Src{reinterpret_cast<const char*>(p & ~uintptr_t(15)), (uint32_t)(p & 15)};
 }
 template <int AUX>
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
@@ -211,8 +225,8 @@ __device__ __forceinline__ void edges(typename Tr::Storage* c,
   if (j < n) c[j] = apply<Tr, OP>(a[j], b[j]);
 }
 
-// Aligned body.  c, a, b are congruent modulo 16 B; `head` elements bring
-// them to a 16-B boundary.  One workgroup = one tile of BLOCK lanes x UNROLL
+// Vector body.  `head` elements bring the destination c to a 16-B boundary;
+// a and b may sit at any element offset relative to it (Src).  One workgroup = one tile of BLOCK lanes x UNROLL
 // 16-B packets per operand; packet u of lane t sits at (t + u*BLOCK)*16 bytes
 // into the tile, so every wave-instruction covers 1 KiB contiguous.  All loads
 // of the tile are issued before the first use.  Measured on MI355X (profiles/
@@ -232,42 +246,19 @@ __global__ __launch_bounds__(BLOCK) void reduce_vec_kernel(
   const size_t base = (size_t)blockIdx.x * kTileBytes;
   if (base >= body) return;
   const uint32_t bytes = (uint32_t)((body - base) < kTileBytes ? (body - base) : kTileBytes);
-  const auto ra = make_rsrc(reinterpret_cast<const char*>(a + head) + base, bytes);
-  const auto rb = make_rsrc(reinterpret_cast<const char*>(b + head) + base, bytes);
+  const Src sa = src_of(a + head), sb = src_of(b + head);
+  const auto ra = make_rsrc(sa.base + base, bytes + sa.mis);
+  const auto rb = make_rsrc(sb.base + base, bytes + sb.mis);
   const auto rc = make_rsrc(reinterpret_cast<const char*>(c + head) + base, bytes);
   const uint32_t lane_off = threadIdx.x * 16u;
   u32x4 x[UNROLL], y[UNROLL];
 #pragma unroll
-  for (int u = 0; u < UNROLL; u++) x[u] = bload<LAUX>(ra, lane_off + u * BLOCK * 16);
+  for (int u = 0; u < UNROLL; u++) x[u] = bload<LAUX>(ra, lane_off + u * BLOCK * 16, sa.mis);
 #pragma unroll
-  for (int u = 0; u < UNROLL; u++) y[u] = bload<LAUX>(rb, lane_off + u * BLOCK * 16);
+  for (int u = 0; u < UNROLL; u++) y[u] = bload<LAUX>(rb, lane_off + u * BLOCK * 16, sb.mis);
 #pragma unroll
   for (int u = 0; u < UNROLL; u++)
     bstore<SAUX>(rc, lane_off + u * BLOCK * 16, apply_packet<Tr, OP>(x[u], y[u]));
-}
-
-// Operands with different misalignment: element-wise, coalesced (lane t of
-// a wave touches element t), UNROLL elements per lane in flight.
-template <class Tr, int OP, int UNROLL>
-__global__ __launch_bounds__(kBlock) void reduce_elem_kernel(
-    typename Tr::Storage* c, const typename Tr::Storage* a,
-    const typename Tr::Storage* b, size_t n) {
-  using S = typename Tr::Storage;
-  const size_t base = (size_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
-  S ra[UNROLL], rb[UNROLL];
-#pragma unroll
-  for (int u = 0; u < UNROLL; u++) {
-    const size_t i = base + (size_t)u * kBlock;
-    if (i < n) {
-      ra[u] = a[i];
-      rb[u] = b[i];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < UNROLL; u++) {
-    const size_t i = base + (size_t)u * kBlock;
-    if (i < n) c[i] = apply<Tr, OP>(ra[u], rb[u]);
-  }
 }
 
 // Multi-source left fold dst = ((s0 op s1) op s2) ... in one pass.
@@ -299,42 +290,25 @@ __global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
   if (base >= body) return;
   const uint32_t bytes = (uint32_t)((body - base) < kTileBytes ? (body - base) : kTileBytes);
   const uint32_t lane_off = threadIdx.x * 16u;
-  auto src_rsrc = [&](int j) {
-    return make_rsrc(reinterpret_cast<const char*>(static_cast<const S*>(srcs.p[j]) + head) + base, bytes);
-  };
   u32x4 acc[UNROLL];
   {
-    const auto r0 = src_rsrc(0);
+    const Src s0 = src_of(static_cast<const S*>(srcs.p[0]) + head);
+    const auto r0 = make_rsrc(s0.base + base, bytes + s0.mis);
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) acc[u] = bload<kAuxNT>(r0, lane_off + u * BLOCK * 16);
+    for (int u = 0; u < UNROLL; u++) acc[u] = bload<kAuxNT>(r0, lane_off + u * BLOCK * 16, s0.mis);
   }
   for (int j = 1; j < k; j++) {
-    const auto rj = src_rsrc(j);
+    const Src sj = src_of(static_cast<const S*>(srcs.p[j]) + head);
+    const auto rj = make_rsrc(sj.base + base, bytes + sj.mis);
     u32x4 r[UNROLL];
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) r[u] = bload<kAuxNT>(rj, lane_off + u * BLOCK * 16);
+    for (int u = 0; u < UNROLL; u++) r[u] = bload<kAuxNT>(rj, lane_off + u * BLOCK * 16, sj.mis);
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) acc[u] = apply_packet<Tr, OP>(acc[u], r[u]);
   }
   const auto rd = make_rsrc(reinterpret_cast<const char*>(dst + head) + base, bytes);
 #pragma unroll
   for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rd, lane_off + u * BLOCK * 16, acc[u]);
-}
-
-template <class Tr, int OP, int UNROLL>
-__global__ __launch_bounds__(kBlock) void reduce_multi_elem_kernel(
-    typename Tr::Storage* dst, SrcList srcs, int k, size_t n) {
-  using S = typename Tr::Storage;
-  const size_t base = (size_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
-#pragma unroll
-  for (int u = 0; u < UNROLL; u++) {
-    const size_t i = base + (size_t)u * kBlock;
-    if (i < n) {
-      S acc = static_cast<const S*>(srcs.p[0])[i];
-      for (int j = 1; j < k; j++) acc = apply<Tr, OP>(acc, static_cast<const S*>(srcs.p[j])[i]);
-      dst[i] = acc;
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -352,7 +326,6 @@ int check_launch(const char* name) {
 
 constexpr int kUnroll = 2;      // 16-B packets per operand per lane
 constexpr int kVecBlock = 512;  // lanes per workgroup on the vector body
-constexpr int kElemUnroll = 4;
 constexpr int kMultiUnroll = 2;
 
 inline size_t ceil_div(size_t a, size_t b) { return (a + b - 1) / b; }
@@ -377,30 +350,21 @@ int launch3(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
   const uintptr_t pc = (uintptr_t)c, pa = (uintptr_t)a, pb = (uintptr_t)b;
   if ((pc % sizeof(S)) || (pa % sizeof(S)) || (pb % sizeof(S)))
     return set_error(GLOO_HIP_EINVAL_PTR, "pointer not aligned to the element size");
-  if (((pc ^ pa) & 15) == 0 && ((pc ^ pb) & 15) == 0) {
-    size_t head = ((16 - (pc & 15)) & 15) / sizeof(S);
-    if (head > n) head = n;
-    (void)kV;
-    if constexpr (std::is_same<Tr, TrF32>::value && OP == GLOO_HIP_SUM) {
-      // A/B knob for the measurement harness (tools/sweep_variants.py).
-      switch (g_variant) {
-        case 1: return launch_vec<Tr, OP, 2, 256, kAuxNT, kAuxNT>(c, a, b, n, head, s);
-        case 2: return launch_vec<Tr, OP, 4, 256, kAuxNT, kAuxNT>(c, a, b, n, head, s);
-        case 3: return launch_vec<Tr, OP, 1, 512, kAuxNT, kAuxNT>(c, a, b, n, head, s);
-        case 4: return launch_vec<Tr, OP, 2, 512, kAuxNT, 0>(c, a, b, n, head, s);
-        case 5: return launch_vec<Tr, OP, 2, 1024, kAuxNT, kAuxNT>(c, a, b, n, head, s);
-        case 6: return launch_vec<Tr, OP, 1, 1024, kAuxNT, kAuxNT>(c, a, b, n, head, s);
-        case 7: return launch_vec<Tr, OP, 2, 512, kAuxNT, kAuxNT | kAuxSC1>(c, a, b, n, head, s);
-        case 8: return launch_vec<Tr, OP, 3, 512, kAuxNT, kAuxNT>(c, a, b, n, head, s);
-        default: break;
-      }
+  size_t head = ((16 - (pc & 15)) & 15) / sizeof(S);
+  if (head > n) head = n;
+  (void)kV;
+  if constexpr (std::is_same<Tr, TrF32>::value && OP == GLOO_HIP_SUM) {
+    // A/B knob for the measurement harness (tools/sweep_variants.py).
+    switch (g_variant) {
+      case 1: return launch_vec<Tr, OP, 2, 256, kAuxNT, kAuxNT>(c, a, b, n, head, s);
+      case 2: return launch_vec<Tr, OP, 4, 256, kAuxNT, kAuxNT>(c, a, b, n, head, s);
+      case 3: return launch_vec<Tr, OP, 1, 512, kAuxNT, kAuxNT>(c, a, b, n, head, s);
+      case 4: return launch_vec<Tr, OP, 2, 512, kAuxNT, 0>(c, a, b, n, head, s);
+      case 5: return launch_vec<Tr, OP, 2, 1024, kAuxNT, kAuxNT>(c, a, b, n, head, s);
+      default: break;
     }
-    return launch_vec<Tr, OP, kUnroll, kVecBlock, kAuxNT, kAuxNT>(c, a, b, n, head, s);
   }
-  const size_t grid = ceil_div(n, (size_t)kBlock * kElemUnroll);
-  reduce_elem_kernel<Tr, OP, kElemUnroll><<<dim3((unsigned)grid), dim3(kBlock), 0, s>>>(
-      static_cast<S*>(c), static_cast<const S*>(a), static_cast<const S*>(b), n);
-  return check_launch("reduce_elem_kernel");
+  return launch_vec<Tr, OP, kUnroll, kVecBlock, kAuxNT, kAuxNT>(c, a, b, n, head, s);
 }
 
 template <class Tr, int OP>
@@ -411,29 +375,21 @@ int launch_multi(void* dst, const void* const* srcs, int k, size_t n, hipStream_
   memset(&list, 0, sizeof(list));
   const uintptr_t pd = (uintptr_t)dst;
   if (pd % sizeof(S)) return set_error(GLOO_HIP_EINVAL_PTR, "dst not aligned to the element size");
-  bool congruent = true;
   for (int j = 0; j < k; j++) {
     if (srcs[j] == nullptr) return set_error(GLOO_HIP_EINVAL_PTR, "null source pointer");
     const uintptr_t p = (uintptr_t)srcs[j];
     if (p % sizeof(S)) return set_error(GLOO_HIP_EINVAL_PTR, "source not aligned to the element size");
-    if ((p ^ pd) & 15) congruent = false;
     list.p[j] = srcs[j];
   }
-  if (congruent) {
-    size_t head = ((16 - (pd & 15)) & 15) / sizeof(S);
-    if (head > n) head = n;
-    constexpr int kV = 16 / sizeof(S);
-    const size_t nvec = (n - head) / kV;
-    size_t grid = ceil_div(nvec, (size_t)kVecBlock * kMultiUnroll);
-    if (grid == 0) grid = 1;
-    reduce_multi_vec_kernel<Tr, OP, kMultiUnroll, kVecBlock><<<dim3((unsigned)grid), dim3(kVecBlock), 0, s>>>(
-        static_cast<S*>(dst), list, k, n, head);
-    return check_launch("reduce_multi_vec_kernel");
-  }
-  const size_t grid = ceil_div(n, (size_t)kBlock * kElemUnroll);
-  reduce_multi_elem_kernel<Tr, OP, kElemUnroll><<<dim3((unsigned)grid), dim3(kBlock), 0, s>>>(
-      static_cast<S*>(dst), list, k, n);
-  return check_launch("reduce_multi_elem_kernel");
+  size_t head = ((16 - (pd & 15)) & 15) / sizeof(S);
+  if (head > n) head = n;
+  constexpr int kV = 16 / sizeof(S);
+  const size_t nvec = (n - head) / kV;
+  size_t grid = ceil_div(nvec, (size_t)kVecBlock * kMultiUnroll);
+  if (grid == 0) grid = 1;
+  reduce_multi_vec_kernel<Tr, OP, kMultiUnroll, kVecBlock><<<dim3((unsigned)grid), dim3(kVecBlock), 0, s>>>(
+      static_cast<S*>(dst), list, k, n, head);
+  return check_launch("reduce_multi_vec_kernel");
 }
 
 template <class Tr>

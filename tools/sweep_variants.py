@@ -67,8 +67,44 @@ def bench_misaligned(n, steps, pairs, src_off_elems, dtype_bytes=4):
     return us
 
 
+def bench_finegrained_src(n, steps, pairs):
+    """dst coarse-grained (hipMalloc), src in fine-grained device memory
+    (hipExtMallocWithFlags(hipDeviceMallocFinegrained)) — the inbox arenas a
+    peer GPU writes over xGMI."""
+    import ctypes
+    hiprt = ctypes.CDLL("libamdhip64.so")
+    hiprt.hipExtMallocWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    hiprt.hipFree.argtypes = [ctypes.c_void_p]
+    dev = torch.device("cuda:0")
+    dsts = [torch.rand(n, device=dev) for _ in range(pairs)]
+    srcs = []
+    for _ in range(pairs):
+        p = ctypes.c_void_p()
+        assert hiprt.hipExtMallocWithFlags(ctypes.byref(p), n * 4, 0x1) == 0  # hipDeviceMallocFinegrained
+        srcs.append(p.value)
+    s = torch.cuda.current_stream().cuda_stream
+    for i in range(5):
+        hip.reduce_ptr("sum", "f32", dsts[i % pairs].data_ptr(), srcs[i % pairs], n, s)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(steps):
+        hip.reduce_ptr("sum", "f32", dsts[i % pairs].data_ptr(), srcs[i % pairs], n, s)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / steps
+    for p in srcs:
+        hiprt.hipFree(p)
+    del dsts
+    torch.cuda.empty_cache()
+    return us
+
+
 def main():
     n = 16 << 20
+    us = bench_finegrained_src(n, 300, 6)
+    print(json.dumps({"sweep": "finegrained_src", "us_mean": round(us, 2),
+                      "GBs": round(3 * n * 4 / (us / 1e3) / 1e9, 1)}), flush=True)
     for off in (0, 1, 2, 3):
         us = bench_misaligned(n, 300, 6, off)
         print(json.dumps({"sweep": "relative_misalignment", "src_offset_elems": off, "us_mean": round(us, 2),
