@@ -287,3 +287,42 @@ class Algorithm:
             self.close()
         except Exception:
             pass
+
+
+# ---- new-style function API: gloo::allreduce(opts) -------------------------
+
+class AllreduceOptions(ctypes.Structure):
+    """gloo_hip_allreduce_options_t (mirrors gloo::AllreduceOptions,
+    gloo/allreduce.h:89-193)."""
+    _fields_ = [("algorithm", ctypes.c_int), ("op", ctypes.c_int), ("dtype", ctypes.c_int),
+                ("inputs", ctypes.POINTER(ctypes.c_void_p)), ("ninputs", ctypes.c_int),
+                ("outputs", ctypes.POINTER(ctypes.c_void_p)), ("noutputs", ctypes.c_int),
+                ("elements", ctypes.c_size_t), ("max_segment_bytes", ctypes.c_size_t),
+                ("tag", ctypes.c_uint32), ("stream", ctypes.c_void_p)]
+
+
+lib.gloo_hip_allreduce.argtypes = [ctypes.c_void_p, ctypes.POINTER(AllreduceOptions)]
+EXPORTED = EXPORTED + ("gloo_hip_allreduce", "gloo_hip_plan_ex")
+
+
+def allreduce(ctx, outputs, elements, dtype, op="sum", inputs=None, max_segment_bytes=0, tag=0,
+              stream=0):
+    """gloo::allreduce(opts) with RING (gloo/allreduce.cc:147-392) on device
+    pointers; every output receives the reduction of all inputs (or of the
+    outputs when no inputs are given) over all ranks."""
+    inputs = list(inputs or [])
+    o = AllreduceOptions()
+    o.algorithm = 1
+    o.op = _as_op(op)
+    o.dtype = _as_dtype(dtype)
+    ins = (ctypes.c_void_p * max(1, len(inputs)))(*inputs)
+    outs = (ctypes.c_void_p * len(outputs))(*outputs)
+    o.inputs = ins if inputs else None
+    o.ninputs = len(inputs)
+    o.outputs = outs
+    o.noutputs = len(outputs)
+    o.elements = int(elements)
+    o.max_segment_bytes = int(max_segment_bytes)
+    o.tag = tag
+    o.stream = stream or None
+    _check(lib.gloo_hip_allreduce(ctx._h, ctypes.byref(o)))

@@ -1,4 +1,5 @@
 // capi.cc — C-ABI over Context / PlanExecutor; no exception crosses it.
+#include <list>
 #include <memory>
 #include <string>
 #include <vector>
@@ -11,6 +12,9 @@
 
 struct gloo_hip_context {
   std::shared_ptr<gloo_amd::Context> ctx;
+  // function-style allreduce: one executor per option set, least recently
+  // used first (every rank makes the same calls, so hits and evictions agree)
+  std::list<std::pair<std::string, std::unique_ptr<gloo_amd::PlanExecutor>>> cache;
 };
 struct gloo_hip_algorithm {
   std::unique_ptr<gloo_amd::PlanExecutor> exec;
@@ -47,7 +51,10 @@ int gloo_hip_context_create(int rank, int size, const char* store_url, int devic
 }
 
 int gloo_hip_context_destroy(gloo_hip_context_t ctx) {
-  return guarded([&] { delete ctx; });
+  return guarded([&] {
+    if (ctx) ctx->cache.clear();  // executors tear down before the context
+    delete ctx;
+  });
 }
 
 int gloo_hip_algorithm_create(gloo_hip_context_t ctx, int algo, int op, int dtype, void* const* ptrs, int nptrs,
@@ -77,6 +84,38 @@ int gloo_hip_algorithm_run(gloo_hip_algorithm_t a) {
 
 int gloo_hip_algorithm_destroy(gloo_hip_algorithm_t a) {
   return guarded([&] { delete a; });
+}
+
+int gloo_hip_allreduce(gloo_hip_context_t ctx, const gloo_hip_allreduce_options_t* o) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(ctx && o, "null argument");
+    GLOO_AMD_ENFORCE(o->algorithm == 0 || o->algorithm == GLOO_HIP_ALLREDUCE_RING, "only RING is implemented");
+    GLOO_AMD_ENFORCE(o->noutputs >= 1 && o->outputs, "need at least one output");
+    GLOO_AMD_ENFORCE(o->ninputs == 0 || o->inputs, "null inputs");
+    if (o->elements == 0) return;  // gloo/allreduce.cc:98-100
+    std::vector<void*> ins(o->inputs, o->inputs + o->ninputs), outs(o->outputs, o->outputs + o->noutputs);
+    const std::string key = gloo_amd::strcat_(o->op, "/", o->dtype, "/", o->ninputs, "/", o->noutputs, "/",
+                                              o->elements, "/", o->max_segment_bytes, "/", o->tag, "/",
+                                              reinterpret_cast<uintptr_t>(o->stream));
+    auto& cache = ctx->cache;
+    auto it = cache.begin();
+    for (; it != cache.end(); ++it)
+      if (it->first == key) break;
+    if (it == cache.end()) {
+      constexpr size_t kMaxCached = 16;
+      if (cache.size() == kMaxCached) cache.pop_back();
+      cache.emplace_front(key, std::make_unique<gloo_amd::PlanExecutor>(
+                                   ctx->ctx, GLOO_HIP_ALGO_ALLREDUCE_RING, o->op, o->dtype, outs, o->elements,
+                                   std::vector<int>{}, static_cast<hipStream_t>(o->stream), ins,
+                                   o->max_segment_bytes));
+      it = cache.begin();
+    } else if (it != cache.begin()) {
+      cache.splice(cache.begin(), cache, it);
+      it = cache.begin();
+    }
+    it->second->setBuffers(ins, outs);
+    it->second->run();
+  });
 }
 
 double gloo_hip_algorithm_wait_seconds(gloo_hip_algorithm_t a) { return a ? a->exec->lastWaitSeconds() : 0.0; }

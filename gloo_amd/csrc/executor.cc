@@ -72,18 +72,41 @@ std::mutex& liveMutex() {
 
 }  // namespace
 
+namespace {
+Plan planFor(int algo, int rank, int size, size_t count, int nin, int nout, size_t es, size_t maxSeg,
+             const std::vector<int>& recvElems) {
+  if (algo == GLOO_HIP_ALGO_ALLREDUCE_RING) {
+    NewStyleOptions o;
+    o.ninputs = nin;
+    o.noutputs = nout;
+    o.elemSize = es;
+    o.maxSegmentBytes = maxSeg;
+    return makeAllreducePlan(rank, size, count, o);
+  }
+  return makePlan(algo, rank, size, count, nout, recvElems);
+}
+}  // namespace
+
+void PlanExecutor::setBuffers(const std::vector<void*>& inputs, const std::vector<void*>& outputs) {
+  GLOO_AMD_ENFORCE(inputs.size() == inputs_.size() && outputs.size() == ptrs_.size(),
+                   "buffer count differs from the one the algorithm was built for");
+  inputs_ = inputs;
+  ptrs_ = outputs;
+}
+
 PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int dtype,
                            const std::vector<void*>& ptrs, size_t count, const std::vector<int>& recvElems,
-                           hipStream_t stream)
-    : ctx_(std::move(ctx)), algo_(algo), op_(op), dtype_(dtype), ptrs_(ptrs), count_(count),
-      recvElems_(recvElems) {
+                           hipStream_t stream, const std::vector<void*>& inputs, size_t maxSegmentBytes)
+    : ctx_(std::move(ctx)), algo_(algo), op_(op), dtype_(dtype), ptrs_(ptrs), inputs_(inputs), count_(count),
+      maxSegmentBytes_(maxSegmentBytes), recvElems_(recvElems) {
   es_ = gloo_hip_dtype_size(dtype_);
   GLOO_AMD_ENFORCE(es_ > 0, "unknown dtype ", dtype_);
   GLOO_AMD_ENFORCE(op_ >= GLOO_HIP_SUM && op_ <= GLOO_HIP_MIN, "unknown op ", op_);
   GLOO_AMD_ENFORCE(!ptrs_.empty(), "need at least one pointer");
   for (void* p : ptrs_) GLOO_AMD_ENFORCE(p != nullptr || count_ == 0, "null device pointer");
   const int me = ctx_->rank, P = ctx_->size;
-  plan_ = makePlan(algo_, me, P, count_, (int)ptrs_.size(), recvElems_);
+  plan_ = planFor(algo_, me, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_, maxSegmentBytes_,
+                  recvElems_);
   inst_ = ctx_->nextInstance();
   {
     std::lock_guard<std::mutex> lk(liveMutex());
@@ -184,7 +207,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       peers_[peer].base = static_cast<char*>(p);
       peers_[peer].ipc = true;
     }
-    const Plan theirs = makePlan(algo_, peer, P, count_, 1, recvElems_);
+    const Plan theirs = planFor(algo_, peer, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
     for (const Step& d : theirs.steps)
       if (d.kind == GLOO_HIP_STEP_DECL_RECV && d.peer == me) {
         GLOO_AMD_ENFORCE((d.dst_off + d.length) * es_ <= pr.bytes, "peer region outside its arena");
@@ -315,20 +338,35 @@ void PlanExecutor::run() {
         if (!deviceSignal_) GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
         break;
       case GLOO_HIP_STEP_LOCAL_REDUCE: {
-        // one fused pass over up to GLOO_HIP_MAX_SRCS pointers, then fold on
-        for (size_t j0 = 0; j0 + 1 < ptrs_.size();) {
-          std::vector<const void*> srcs{ptrs_[0]};
-          size_t j = j0 + 1;
-          for (; j < ptrs_.size() && srcs.size() < GLOO_HIP_MAX_SRCS; j++) srcs.push_back(ptrs_[j]);
-          checkRc(gloo_hip_reduce_multi(op_, dtype_, ptrs_[0], srcs.data(), (int)srcs.size(), s.length, stream_),
+        // out[0][range] = ((src0 op src1) op src2) ... with src = the
+        // separate inputs (FROM_INPUTS; one input = a copy) or the outputs;
+        // one fused pass per GLOO_HIP_MAX_SRCS sources.
+        const size_t off = s.dst_off * es_;
+        const std::vector<void*>& from = (s.flags & GLOO_HIP_FROM_INPUTS) ? inputs_ : ptrs_;
+        char* out0 = userPtr(0) + off;
+        if (from.size() == 1) {
+          deviceMove(out0, static_cast<const char*>(from[0]) + off, s.length * es_, stream_);
+          break;
+        }
+        std::vector<const void*> srcs;
+        size_t j = 0;
+        for (; j < from.size() && srcs.size() < GLOO_HIP_MAX_SRCS; j++)
+          srcs.push_back(static_cast<const char*>(from[j]) + off);
+        checkRc(gloo_hip_reduce_multi(op_, dtype_, out0, srcs.data(), (int)srcs.size(), s.length, stream_),
+                "gloo_hip_reduce_multi");
+        while (j < from.size()) {
+          srcs.assign(1, out0);
+          for (; j < from.size() && srcs.size() < GLOO_HIP_MAX_SRCS; j++)
+            srcs.push_back(static_cast<const char*>(from[j]) + off);
+          checkRc(gloo_hip_reduce_multi(op_, dtype_, out0, srcs.data(), (int)srcs.size(), s.length, stream_),
                   "gloo_hip_reduce_multi");
-          j0 = j - 1;
         }
         break;
       }
       case GLOO_HIP_STEP_LOCAL_BCAST:
         for (size_t j = 1; j < ptrs_.size(); j++)
-          GLOO_AMD_HIP_CHECK(hipMemcpyAsync(ptrs_[j], ptrs_[0], s.length * es_, hipMemcpyDeviceToDevice, stream_));
+          GLOO_AMD_HIP_CHECK(hipMemcpyAsync(userPtr(j) + s.dst_off * es_, userPtr(0) + s.dst_off * es_,
+                                            s.length * es_, hipMemcpyDeviceToDevice, stream_));
         break;
       default:
         throw EnforceNotMet(strcat_("unknown plan step ", s.kind));

@@ -518,7 +518,114 @@ Plan planReduceScatter(int rank, int size, uint64_t count, int nptrs, const std:
   return p;
 }
 
+// ---------------------------------------------------------------------------
+// New-style gloo::allreduce(opts), RING (gloo/allreduce.cc:97-392).
+// The reference's two-sided unbound buffers are restated one-sidedly: posting
+// a receive becomes a credit (NOTIFY) to the sender, which waits for it
+// before writing (WAIT_NOTIFY + SEND); the reduce-scatter receives land in
+// two segment inboxes (tmp, :219-226), the allgather receives in two more and
+// are copied to out[0] at their offset (the reference receives in place).
+// Arena = [tmp0 | tmp1 | ag0 | ag1], one segment each.
+// ---------------------------------------------------------------------------
+Plan planAllreduceRing(int rank, int size, uint64_t count, const NewStyleOptions& o) {
+  Plan p;
+  if (count == 0) return p;                                             // :98-100
+  const uint64_t es = o.elemSize;
+  const bool localReduce = o.ninputs > 0 || o.noutputs > 1;
+  const int fromInputs = o.ninputs > 0 ? GLOO_HIP_FROM_INPUTS : 0;
+  auto reduceInputs = [&](uint64_t off, uint64_t len) {                 // :42-84
+    if (localReduce) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, fromInputs, off, 0, len));
+  };
+  auto broadcastOutputs = [&](uint64_t off, uint64_t len) {             // :89-98
+    if (o.noutputs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, off, 0, len));
+  };
+  if (size == 1) {                                                      // :125-129
+    reduceInputs(0, count);
+    broadcastOutputs(0, count);
+    return p;
+  }
+  const uint64_t totalBytes = count * es;
+  const uint64_t maxSegmentBytes = es * std::max<uint64_t>(1, (o.maxSegmentBytes ? o.maxSegmentBytes : 1024 * 1024) / es);
+  auto roundUp = [](uint64_t v, uint64_t m) { return v % m == 0 ? v : v + m - v % m; };
+  const uint64_t numSegments =
+      roundUp(std::max<uint64_t>((totalBytes + (maxSegmentBytes - 1)) / maxSegmentBytes, (uint64_t)size * 2),
+              (uint64_t)size);                                          // :202-207
+  const uint64_t nspr = numSegments / size;
+  const uint64_t segBytes = roundUp((totalBytes + numSegments - 1) / numSegments, es);  // :211-212
+  const uint64_t seg = segBytes / es;  // elements
+  const int recvRank = (size + rank + 1) % size, sendRank = (size + rank - 1) % size;  // :158-159
+  p.arena = 4 * seg;
+  p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, recvRank, GLOO_HIP_SLOT_DATA0, 0, 0, 0, seg));
+  p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, recvRank, GLOO_HIP_SLOT_DATA1, 0, seg, 0, seg));
+  p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, recvRank, GLOO_HIP_SLOT_AUX0, 0, 2 * seg, 0, seg));
+  p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, recvRank, GLOO_HIP_SLOT_AUX1, 0, 3 * seg, 0, seg));
+  struct Off {
+    uint64_t sendOffset, recvOffset;
+    int64_t sendLength, recvLength;
+  };
+  auto offsets = [&](uint64_t i, int sendShift, int recvShift) {        // :231-257, :312-335
+    Off r;
+    r.sendOffset = ((((uint64_t)rank + sendShift) * nspr + i) * seg) % (numSegments * seg);
+    r.recvOffset = ((((uint64_t)rank + recvShift) * nspr + i) * seg) % (numSegments * seg);
+    r.sendLength = std::min<int64_t>((int64_t)seg, (int64_t)count - (int64_t)r.sendOffset);
+    r.recvLength = std::min<int64_t>((int64_t)seg, (int64_t)count - (int64_t)r.recvOffset);
+    return r;
+  };
+  const uint64_t iters = numSegments - nspr + 2;
+  for (uint64_t i = 0; i < iters; i++) {                                // reduce/scatter :268-306
+    const int buf = (int)(i & 1);
+    if (i >= 2) {
+      const Off prev = offsets(i - 2, 1, 2);
+      if (prev.recvLength > 0) {
+        reduceInputs(prev.recvOffset, prev.recvLength);
+        p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, recvRank, GLOO_HIP_SLOT_DATA0 + buf));
+        p.steps.push_back(mk(GLOO_HIP_STEP_REDUCE, -1, 0, GLOO_HIP_SRC_ARENA, prev.recvOffset, buf * seg,
+                             prev.recvLength));
+      }
+    }
+    if (i < numSegments - nspr) {
+      const Off cur = offsets(i, 1, 2);
+      if (cur.recvLength > 0) p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, recvRank, GLOO_HIP_SLOT_NOTIFY));
+      if (cur.sendLength > 0) {
+        if (i < nspr) reduceInputs(cur.sendOffset, cur.sendLength);
+        p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, sendRank, GLOO_HIP_SLOT_NOTIFY));
+        p.steps.push_back(mk(GLOO_HIP_STEP_SEND, sendRank, GLOO_HIP_SLOT_DATA0 + buf, 0, 0, cur.sendOffset,
+                             cur.sendLength));
+      }
+    }
+  }
+  for (uint64_t i = 0; i < iters; i++) {                                // allgather :345-377
+    const int buf = (int)(i & 1);
+    if (i >= 2) {
+      const Off prev = offsets(i - 2, 0, 1);
+      if (prev.recvLength > 0) {
+        p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, recvRank, GLOO_HIP_SLOT_AUX0 + buf));
+        p.steps.push_back(mk(GLOO_HIP_STEP_COPY, -1, 0, GLOO_HIP_SRC_ARENA, prev.recvOffset, (2 + buf) * seg,
+                             prev.recvLength));
+        broadcastOutputs(prev.recvOffset, prev.recvLength);
+      }
+    }
+    if (i < numSegments - nspr) {
+      const Off cur = offsets(i, 0, 1);
+      if (cur.recvLength > 0) p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, recvRank, GLOO_HIP_SLOT_AUX_NOTIFY));
+      if (cur.sendLength > 0) {
+        p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, sendRank, GLOO_HIP_SLOT_AUX_NOTIFY));
+        p.steps.push_back(mk(GLOO_HIP_STEP_SEND, sendRank, GLOO_HIP_SLOT_AUX0 + buf, 0, 0, cur.sendOffset,
+                             cur.sendLength));
+        if (i < nspr) broadcastOutputs(cur.sendOffset, cur.sendLength);
+      }
+    }
+  }
+  return p;
+}
+
 }  // namespace
+
+Plan makeAllreducePlan(int rank, int size, uint64_t count, const NewStyleOptions& o) {
+  if (size < 1 || rank < 0 || rank >= size) throw std::invalid_argument("bad rank/size");
+  if (o.noutputs < 1 || o.ninputs < 0 || o.elemSize == 0) throw std::invalid_argument("bad options");
+  return planAllreduceRing(rank, size, count, o);
+}
 
 Plan makePlan(int algo, int rank, int size, uint64_t count, int nptrs, const std::vector<int>& recvElems) {
   if (size < 1 || rank < 0 || rank >= size) throw std::invalid_argument("bad rank/size");
@@ -539,13 +646,30 @@ Plan makePlan(int algo, int rank, int size, uint64_t count, int nptrs, const std
 
 extern "C" int gloo_hip_plan(int algo, int rank, int size, size_t count, int nptrs, const int* recv_elems,
                              gloo_hip_step_t* steps, size_t capacity, size_t* nsteps, size_t* arena_elems) {
+  return gloo_hip_plan_ex(algo, rank, size, count, 0, nptrs, 4, 0, recv_elems, steps, capacity, nsteps,
+                          arena_elems);
+}
+
+extern "C" int gloo_hip_plan_ex(int algo, int rank, int size, size_t count, int ninputs, int noutputs,
+                                size_t elem_size, size_t max_segment_bytes, const int* recv_elems,
+                                gloo_hip_step_t* steps, size_t capacity, size_t* nsteps, size_t* arena_elems) {
   try {
     std::vector<int> re;
     if (algo == GLOO_HIP_ALGO_REDUCE_SCATTER) {
       if (!recv_elems) return GLOO_HIP_EINVAL_ARG;
       re.assign(recv_elems, recv_elems + size);
     }
-    gloo_amd::Plan p = gloo_amd::makePlan(algo, rank, size, count, nptrs, re);
+    gloo_amd::Plan p;
+    if (algo == GLOO_HIP_ALGO_ALLREDUCE_RING) {
+      gloo_amd::NewStyleOptions o;
+      o.ninputs = ninputs;
+      o.noutputs = noutputs;
+      o.elemSize = elem_size;
+      o.maxSegmentBytes = max_segment_bytes;
+      p = gloo_amd::makeAllreducePlan(rank, size, count, o);
+    } else {
+      p = gloo_amd::makePlan(algo, rank, size, count, noutputs, re);
+    }
     if (nsteps) *nsteps = p.steps.size();
     if (arena_elems) *arena_elems = p.arena;
     if (steps) {

@@ -47,7 +47,11 @@ class PlanExecutor {
   // (docs/cuda.md:6-13 of the reference).
   PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int dtype,
                const std::vector<void*>& ptrs, size_t count, const std::vector<int>& recvElems,
-               hipStream_t stream);
+               hipStream_t stream, const std::vector<void*>& inputs = {}, size_t maxSegmentBytes = 0);
+
+  // Function-style calls (gloo::allreduce(opts)) reuse one executor for a
+  // given option set and rebind the buffers before each run.
+  void setBuffers(const std::vector<void*>& inputs, const std::vector<void*>& outputs);
   ~PlanExecutor();
   PlanExecutor(const PlanExecutor&) = delete;
   PlanExecutor& operator=(const PlanExecutor&) = delete;
@@ -80,8 +84,10 @@ class PlanExecutor {
   std::shared_ptr<Context> ctx_;
   int algo_, op_, dtype_;
   size_t es_;
-  std::vector<void*> ptrs_;
+  std::vector<void*> ptrs_;     // outputs (the reference's ptrs_ / out)
+  std::vector<void*> inputs_;   // separate inputs (new-style allreduce), may be empty
   size_t count_;
+  size_t maxSegmentBytes_ = 0;
   std::vector<int> recvElems_;
   Plan plan_;
   uint64_t inst_;

@@ -19,4 +19,13 @@ struct Plan {
 Plan makePlan(int algo, int rank, int size, uint64_t count, int nptrs,
               const std::vector<int>& recvElems = {});
 
+// New-style allreduce parameters (gloo/allreduce.h:89-193).
+struct NewStyleOptions {
+  int ninputs = 0;
+  int noutputs = 1;
+  size_t elemSize = 4;
+  size_t maxSegmentBytes = 1024 * 1024;  // kMaxSegmentSize, gloo/allreduce.h:78
+};
+Plan makeAllreducePlan(int rank, int size, uint64_t count, const NewStyleOptions& o);
+
 }  // namespace gloo_amd

@@ -130,6 +130,8 @@ typedef enum {
   GLOO_HIP_ALGO_RING = 2,             /* gloo/allreduce_ring.h                */
   GLOO_HIP_ALGO_LOCAL = 3,            /* gloo/allreduce_local.{h,cc}          */
   GLOO_HIP_ALGO_REDUCE_SCATTER = 4,   /* gloo/reduce_scatter.h (HD)           */
+  GLOO_HIP_ALGO_ALLREDUCE_RING = 5,   /* new-style gloo::allreduce(opts), RING
+                                         (gloo/allreduce.cc:147-392)          */
 } gloo_hip_algo_t;
 
 typedef enum {
@@ -151,11 +153,18 @@ typedef enum {
 #define GLOO_HIP_SLOT_NOTIFY 2
 #define GLOO_HIP_SLOT_DIST 3
 #define GLOO_HIP_SLOT_DIST_NOTIFY 4
-#define GLOO_HIP_NUM_SLOTS 5
+#define GLOO_HIP_SLOT_AUX0 5
+#define GLOO_HIP_SLOT_AUX1 6
+#define GLOO_HIP_SLOT_AUX_NOTIFY 7
+#define GLOO_HIP_NUM_SLOTS 8
 
 /* flags: which space each side of a data step lives in. */
 #define GLOO_HIP_SRC_ARENA 1 /* else the user buffer ptrs[0] */
 #define GLOO_HIP_DST_ARENA 2
+/* LOCAL_REDUCE over [dst_off, +length) folds the separate INPUT buffers into
+ * output 0 (new-style allreduce; one input = copy), instead of folding the
+ * outputs into output 0. */
+#define GLOO_HIP_FROM_INPUTS 4
 
 typedef struct {
   int32_t kind;
@@ -174,6 +183,14 @@ typedef struct {
 int gloo_hip_plan(int algo, int rank, int size, size_t count, int nptrs,
                   const int* recv_elems, gloo_hip_step_t* steps, size_t capacity,
                   size_t* nsteps, size_t* arena_elems);
+
+/* Full form: `ninputs` separate input buffers (0 = the outputs are the
+ * inputs), `noutputs` outputs, element size and the new-style allreduce's
+ * maximum segment size in bytes (0 = 1 MiB, gloo/allreduce.h:78). */
+int gloo_hip_plan_ex(int algo, int rank, int size, size_t count, int ninputs, int noutputs,
+                     size_t elem_size, size_t max_segment_bytes, const int* recv_elems,
+                     gloo_hip_step_t* steps, size_t capacity, size_t* nsteps,
+                     size_t* arena_elems);
 
 /* ------------------------------------------------------------------------
  * Contexts and algorithms (the GPU allreduce / reduce-scatter drop-ins).
@@ -220,6 +237,32 @@ double gloo_hip_algorithm_wait_seconds(gloo_hip_algorithm_t algo);
  * stats[3] = host seconds blocked on peers. */
 int gloo_hip_algorithm_set_profiling(gloo_hip_algorithm_t algo, int on);
 int gloo_hip_algorithm_stats(gloo_hip_algorithm_t algo, double* stats4);
+
+/* ------------------------------------------------------------------------
+ * New-style function API: gloo::allreduce(const AllreduceOptions&)
+ * (gloo/allreduce.h:89-193, gloo/allreduce.cc:97-145), RING algorithm.
+ * inputs may be empty (the outputs are the inputs); every output receives
+ * the result.  Collective: all ranks call with the same options in the same
+ * order.  The first call with a given option set builds the schedule and
+ * inbox arena (a store exchange); later calls reuse it with the buffers of
+ * the call.
+ * ---------------------------------------------------------------------- */
+#define GLOO_HIP_ALLREDUCE_RING 1 /* AllreduceOptions::Algorithm::RING */
+typedef struct {
+  int algorithm;            /* 0 (unspecified) or GLOO_HIP_ALLREDUCE_RING */
+  int op;                   /* gloo_hip_op_t: the reduce Func             */
+  int dtype;                /* gloo_hip_dtype_t: setInputs<T>/setOutputs<T> */
+  void* const* inputs;      /* device pointers, may be NULL               */
+  int ninputs;
+  void* const* outputs;     /* device pointers, at least one              */
+  int noutputs;
+  size_t elements;
+  size_t max_segment_bytes; /* setMaxSegmentSize; 0 = 1 MiB               */
+  uint32_t tag;             /* setTag                                     */
+  gloo_hip_stream_t stream; /* NULL: outputs complete on return           */
+} gloo_hip_allreduce_options_t;
+
+int gloo_hip_allreduce(gloo_hip_context_t ctx, const gloo_hip_allreduce_options_t* opts);
 
 #ifdef __cplusplus
 } /* extern "C" */

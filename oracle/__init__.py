@@ -74,6 +74,9 @@ def ref():
         L.ref_reduce_scatter.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]
+        L.ref_allreduce_new.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
+                                        ctypes.c_void_p, ctypes.c_void_p]
         L.ref_last_error.restype = ctypes.c_char_p
         _ref = L
     return _ref

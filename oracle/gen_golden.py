@@ -174,6 +174,34 @@ def gen_sched():
         out[key + "/recv"] = recv
         # only rank r's reduced block out[r, :recv[r]] is defined; concatenate
         out[key + "/out"] = np.concatenate([y[r, :recv[r]] for r in range(P)])
+    # New-style gloo::allreduce(opts), ring (gloo/allreduce.cc:147-392).
+    new_cases = []
+    for P in (2, 3, 5, 8):
+        for n in (1, 1000, 4099):
+            new_cases.append(("sum", "f32", P, 0, 1, n, 0))
+    new_cases += [("sum", "f32", 3, 1, 1, 1000, 128), ("sum", "f32", 3, 3, 2, 1000, 128),
+                  ("sum", "f32", 4, 2, 1, 4099, 256), ("sum", "f32", 5, 0, 3, 777, 100),
+                  ("max", "f32", 4, 0, 1, 3000, 128), ("sum", "bf16", 4, 2, 2, 2000, 256),
+                  ("sum", "u64", 4, 0, 1, 1000, 128), ("product", "f64", 3, 2, 1, 999, 64)]
+    for op, dtype, P, nin, nout, n, seg in new_cases:
+        x = sched_inputs(dtype, op, (P, max(nin, 1), n), rng) if dtype not in ("u64",) else \
+            rng.integers(0, 1 << 40, (P, max(nin, 1), n), dtype=np.uint64)
+        init = sched_inputs(dtype, op, (P, nout, n), rng) if dtype not in ("u64",) else \
+            rng.integers(0, 1 << 40, (P, nout, n), dtype=np.uint64)
+        code, npt = oracle.DTYPES[dtype]
+        y = np.ascontiguousarray(init.copy())
+        xin = np.ascontiguousarray(x[:, :nin]) if nin else np.zeros(1, dtype=npt)
+        rc = oracle.ref().ref_allreduce_new(oracle.OPS[op], code, P, nin, nout, n, seg,
+                                            xin.ctypes.data, y.ctypes.data)
+        if rc:
+            raise RuntimeError(f"ref_allreduce_new failed {rc}: {oracle.ref().ref_last_error()}")
+        key = f"allreduce_new/{op}/{dtype}/P{P}/i{nin}/o{nout}/n{n}/s{seg}"
+        assert all((y[r, j].view(np.uint8) == y[0, 0].view(np.uint8)).all()
+                   for r in range(P) for j in range(nout)), key
+        if nin:
+            out[key + "/in"] = x[:, :nin]
+        out[key + "/init"] = init
+        out[key + "/out"] = y[0, 0].copy()
     np.savez_compressed(os.path.join(OUT, "sched_golden.npz"), **out)
     print("sched_golden.npz:", len(out), "arrays")
 

@@ -32,6 +32,7 @@
 
 #include <c10/util/BFloat16.h>
 
+#include "gloo/allreduce.h"
 #include "gloo/allreduce_halving_doubling.h"
 #include "gloo/allreduce_local.h"
 #include "gloo/allreduce_ring.h"
@@ -212,6 +213,29 @@ int reduce_scatter(int op, int P, size_t n, const int* recvElems, const void* in
   });
 }
 
+// New-style gloo::allreduce(opts), ring algorithm (gloo/allreduce.cc:147-392).
+// in: [P][nin][n] (nin may be 0: outputs are the inputs); out: [P][nout][n].
+template <typename T>
+int allreduce_new(int op, int P, int nin, int nout, size_t n, size_t maxSeg, const void* in, void* out) {
+  Fn3<T> fn = pick3<T>(op);
+  if (!fn) return -1;
+  std::vector<T> inputs((size_t)P * nin * n);
+  if (nin) std::memcpy(inputs.data(), in, inputs.size() * sizeof(T));
+  T* o = static_cast<T*>(out);
+  return spawn(P, [&](std::shared_ptr<gloo::Context> ctx) {
+    gloo::AllreduceOptions opts(ctx);
+    std::vector<T*> ip, op_;
+    for (int j = 0; j < nin; j++) ip.push_back(inputs.data() + ((size_t)ctx->rank * nin + j) * n);
+    for (int j = 0; j < nout; j++) op_.push_back(o + ((size_t)ctx->rank * nout + j) * n);
+    if (nin) opts.setInputs(ip, n);
+    opts.setOutputs(op_, n);
+    opts.setAlgorithm(gloo::AllreduceOptions::Algorithm::RING);
+    opts.setReduceFunction(fn);
+    if (maxSeg) opts.setMaxSegmentSize(maxSeg);
+    gloo::allreduce(opts);
+  });
+}
+
 #define DISPATCH(dtype, CALL)                     \
   switch (dtype) {                                \
     case I8: { using T = int8_t; return CALL; }   \
@@ -256,6 +280,12 @@ int ref_reduce3_f16_scalar(int op, void* c, const void* a, const void* b, size_t
 int ref_allreduce(int algo, int op, int dtype, int P, int k, size_t n, const void* in,
                   void* out) {
   DISPATCH(dtype, allreduce<T>(algo, op, P, k, n, in, out));
+}
+
+// New-style allreduce; out holds the initial outputs and receives the result.
+int ref_allreduce_new(int op, int dtype, int P, int nin, int nout, size_t n, size_t maxSeg,
+                      const void* in, void* out) {
+  DISPATCH(dtype, allreduce_new<T>(op, P, nin, nout, n, maxSeg, in, out));
 }
 
 // P ranks x n elements; rank r's reduced block lands at out[r][0:recvElems[r]].

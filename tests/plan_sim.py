@@ -18,8 +18,8 @@ import oracle
 
 KIND = dict(DECL_RECV=0, SEND=1, WAIT_RECV=2, REDUCE=3, COPY=4, NOTIFY=5, WAIT_NOTIFY=6,
             WAIT_SEND=7, LOCAL_REDUCE=8, LOCAL_BCAST=9)
-ALGO = dict(ring_chunked=0, halving_doubling=1, ring=2, local=3, reduce_scatter=4)
-SRC_ARENA, DST_ARENA = 1, 2
+ALGO = dict(ring_chunked=0, halving_doubling=1, ring=2, local=3, reduce_scatter=4, allreduce_new=5)
+SRC_ARENA, DST_ARENA, FROM_INPUTS = 1, 2, 4
 
 
 class Step(ctypes.Structure):
@@ -28,7 +28,7 @@ class Step(ctypes.Structure):
                 ("length", ctypes.c_uint64)]
 
 
-def get_plan(algo, rank, size, count, nptrs=1, recv=None):
+def get_plan(algo, rank, size, count, nptrs=1, recv=None, nin=0, elem_size=4, max_seg=0):
     import gloo_amd
     L = gloo_amd.lib
     n = ctypes.c_size_t()
@@ -37,15 +37,17 @@ def get_plan(algo, rank, size, count, nptrs=1, recv=None):
     if recv is not None:
         recv = np.ascontiguousarray(recv, dtype=np.int32)
         rp = recv.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
-    L.gloo_hip_plan.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
-                                ctypes.POINTER(ctypes.c_int), ctypes.c_void_p, ctypes.c_size_t,
-                                ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
-    rc = L.gloo_hip_plan(ALGO[algo], rank, size, count, nptrs, rp, None, 0, ctypes.byref(n), ctypes.byref(arena))
+    L.gloo_hip_plan_ex.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
+                                   ctypes.POINTER(ctypes.c_int), ctypes.c_void_p, ctypes.c_size_t,
+                                   ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
+    args = (ALGO[algo], rank, size, count, nin, nptrs, elem_size, max_seg, rp)
+    rc = L.gloo_hip_plan_ex(*args, None, 0, ctypes.byref(n), ctypes.byref(arena))
     if rc:
         raise RuntimeError(f"gloo_hip_plan failed {rc}")
     steps = (Step * max(1, n.value))()
-    rc = L.gloo_hip_plan(ALGO[algo], rank, size, count, nptrs, rp, ctypes.cast(steps, ctypes.c_void_p),
-                         n.value, ctypes.byref(n), ctypes.byref(arena))
+    rc = L.gloo_hip_plan_ex(*args, ctypes.cast(steps, ctypes.c_void_p), n.value, ctypes.byref(n),
+                            ctypes.byref(arena))
     if rc:
         raise RuntimeError(f"gloo_hip_plan failed {rc}")
     return [steps[i] for i in range(n.value)], arena.value
@@ -55,10 +57,14 @@ class ProtocolError(AssertionError):
     pass
 
 
-def simulate(algo, op, dtype, inputs, recv=None, seed=0):
-    """inputs: [P][k][n] array of the dtype's storage type.  Returns [P][k][n]."""
+def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0):
+    """inputs: [P][k][n] array of the dtype's storage type (the outputs'
+    initial contents); ins: optional [P][kin][n] separate inputs (new-style
+    allreduce).  Returns the outputs [P][k][n]."""
     P, k, n = inputs.shape
-    plans = [get_plan(algo, r, P, n, k, recv) for r in range(P)]
+    nin = 0 if ins is None else ins.shape[1]
+    es = inputs.dtype.itemsize
+    plans = [get_plan(algo, r, P, n, k, recv, nin=nin, elem_size=es, max_seg=max_seg) for r in range(P)]
     user = [[inputs[r, j].copy() for j in range(k)] for r in range(P)]
     arena = [np.zeros(max(1, a), dtype=inputs.dtype) for _, a in plans]
     regions = {}
@@ -126,11 +132,22 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0):
             dst = space(r, s.flags & DST_ARENA)
             dst[s.dst_off:s.dst_off + s.length] = src[s.src_off:s.src_off + s.length].copy()
         elif K == KIND["LOCAL_REDUCE"]:
-            for j in range(1, k):
-                user[r][0][:s.length] = oracle.reduce3(op, dtype, user[r][0][:s.length], user[r][j][:s.length])
+            lo, hi = s.dst_off, s.dst_off + s.length
+            out0 = user[r][0]
+            if s.flags & FROM_INPUTS:
+                if nin == 1:
+                    out0[lo:hi] = ins[r, 0, lo:hi]
+                else:
+                    out0[lo:hi] = oracle.reduce3(op, dtype, ins[r, 0, lo:hi], ins[r, 1, lo:hi])
+                    for j in range(2, nin):
+                        out0[lo:hi] = oracle.reduce3(op, dtype, out0[lo:hi], ins[r, j, lo:hi])
+            else:
+                for j in range(1, k):
+                    out0[lo:hi] = oracle.reduce3(op, dtype, out0[lo:hi], user[r][j][lo:hi])
         elif K == KIND["LOCAL_BCAST"]:
+            lo, hi = s.dst_off, s.dst_off + s.length
             for j in range(1, k):
-                user[r][j][:s.length] = user[r][0][:s.length]
+                user[r][j][lo:hi] = user[r][0][lo:hi]
         else:
             raise ProtocolError(f"unknown step kind {K}")
     for key in sent:

@@ -250,3 +250,50 @@ def test_threads_forced_modes(torch, golden_sched, env, monkeypatch):
     y = run_threads(torch, "halving_doubling", "sum", "f32", x)
     for r in range(y.shape[0]):
         assert same_bytes(y[r, 0], want)
+
+
+def new_style_keys():
+    z = np.load(os.path.join(ROOT, "tests", "golden", "sched_golden.npz"))
+    return sorted({k.rsplit("/", 1)[0] for k in z.files if k.startswith("allreduce_new/")})
+
+
+@pytest.mark.parametrize("case", new_style_keys())
+def test_new_style_allreduce_golden(torch, golden_sched, case):
+    """gloo::allreduce(opts) RING through gloo_hip_allreduce, ranks as
+    threads, against the reference's own outputs; called twice to exercise
+    the cached schedule with rebound buffers."""
+    import gloo_amd
+    parts = case.split("/")
+    op, dtype, P = parts[1], parts[2], int(parts[3][1:])
+    nin, nout, n, seg = int(parts[4][1:]), int(parts[5][1:]), int(parts[6][1:]), int(parts[7][1:])
+    init = golden_sched[case + "/init"]
+    ins = golden_sched[case + "/in"] if nin else None
+    want = golden_sched[case + "/out"]
+    url = "mem:" + uuid.uuid4().hex
+    dev = lambda r: torch.device("cuda", dev_of(torch, r))  # noqa: E731
+    results, errors = {}, []
+
+    def body(r):
+        try:
+            torch.cuda.set_device(dev_of(torch, r))
+            ctx = gloo_amd.Context(r, P, url, device=dev_of(torch, r), timeout_ms=60000)
+            for rep in range(2):
+                outs = [torch.from_numpy(init[r, j].view(np.uint8).copy()).to(dev(r)) for j in range(nout)]
+                inb = [torch.from_numpy(ins[r, j].view(np.uint8).copy()).to(dev(r)) for j in range(nin)]
+                torch.cuda.synchronize()
+                gloo_amd.allreduce(ctx, [t.data_ptr() for t in outs], n, dtype, op,
+                                   inputs=[t.data_ptr() for t in inb], max_segment_bytes=seg)
+                results[(r, rep)] = [t.cpu().numpy().view(init.dtype) for t in outs]
+            ctx.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append((r, repr(e)))
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(P)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    for (r, rep), outs in results.items():
+        for j, y in enumerate(outs):
+            assert same_bytes(y, want), (r, rep, j)

@@ -31,10 +31,20 @@ def _keys():
 def test_plan_matches_reference_golden(golden_sched, case):
     parts = case.split("/")
     algo, op, dtype = parts[0], parts[1], parts[2]
-    x = golden_sched[case + "/in"]
+    x = golden_sched[case + "/in"] if case + "/in" in golden_sched.files else None
     want = golden_sched[case + "/out"]
     for seed in (0, 1, 2):
-        if algo == "reduce_scatter":
+        if algo == "allreduce_new":
+            nin = int(parts[4][1:])
+            seg = int(parts[7][1:])
+            init = golden_sched[case + "/init"]
+            ins = golden_sched[case + "/in"] if nin else None
+            y = simulate(algo, op, dtype, init, seed=seed, ins=ins, max_seg=seg)
+            for r in range(y.shape[0]):
+                for j in range(y.shape[1]):
+                    assert (y[r, j].view(np.uint8) == want.view(np.uint8)).all(), (r, j)
+            got = y[0, 0]
+        elif algo == "reduce_scatter":
             recv = golden_sched[case + "/recv"]
             y = simulate(algo, op, dtype, x[:, None, :], recv=recv, seed=seed)
             got = np.concatenate([y[r, 0, :recv[r]] for r in range(len(recv))])
@@ -112,3 +122,16 @@ def test_simulator_detects_protocol_violation():
                 plan_sim.simulate("ring_chunked", "sum", "f32", x, seed=seed)
     finally:
         plan_sim.get_plan = orig
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 7])
+@pytest.mark.parametrize("n,seg", [(1, 0), (100, 128), (1000, 128), (5000, 256), (3, 4)])
+def test_new_style_allreduce_closed_form(P, n, seg):
+    """The new-style ring at many segment counts (gloo/test/allreduce_test.cc:
+    307-378 exercises maxSegmentSize=128): every element j sums to
+    j*P*P + P*(P-1)/2 and every output equals output 0."""
+    x = np.array([[np.arange(n, dtype=np.float64) * P + r] * 2 for r in range(P)], dtype=np.float64)
+    y = simulate("allreduce_new", "sum", "f64", x, seed=n + P, max_seg=seg)
+    want = np.arange(n, dtype=np.float64) * P * P * 2 + 2 * P * (P - 1) / 2
+    for r in range(P):
+        assert (y[r, 0] == want).all() and (y[r, 1] == want).all()
