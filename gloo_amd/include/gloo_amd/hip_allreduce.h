@@ -10,6 +10,8 @@
 //   gloo::CudaAllreduceLocal            -> gloo_amd::HipAllreduceLocal<T>
 //   gloo::ReduceScatterHalvingDoubling  -> gloo_amd::HipReduceScatterHalvingDoubling<T>
 //                                          (gloo/reduce_scatter.h:112-117)
+//   gloo::allreduce(AllreduceOptions)   -> gloo_amd::allreduce(AllreduceOptions)
+//                                          (gloo/allreduce.h:89-193), RING
 // Same constructor shapes (context, ptrs, count[, recvElems][, streams][, fn])
 // and run().  Differences, by design: one rank drives one GPU (all `ptrs` of
 // a rank live on that rank's device — ranks are processes or threads), the
@@ -159,5 +161,50 @@ class HipReduceScatterHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO
                                   const HipReductionFunction<T>* fn = HipReductionFunction<T>::sum)
       : HipPlanAlgorithm<T, GLOO_HIP_ALGO_REDUCE_SCATTER>(context, ptrs, count, recvElems, streams, fn) {}
 };
+
+// New-style function API (gloo/allreduce.h:89-193): options object + free
+// function; RING algorithm.  Same setter names as gloo::AllreduceOptions.
+class AllreduceOptions {
+ public:
+  explicit AllreduceOptions(const std::shared_ptr<Context>& context) : context_(context) {}
+  template <typename T>
+  void setInputs(std::vector<T*> ptrs, size_t elements) {
+    inputs_.assign(ptrs.begin(), ptrs.end());
+    elements_ = elements;
+    dtype_ = DType<T>::value;
+  }
+  template <typename T>
+  void setInput(T* ptr, size_t elements) { setInputs(std::vector<T*>{ptr}, elements); }
+  template <typename T>
+  void setOutputs(std::vector<T*> ptrs, size_t elements) {
+    outputs_.assign(ptrs.begin(), ptrs.end());
+    elements_ = elements;
+    dtype_ = DType<T>::value;
+  }
+  template <typename T>
+  void setOutput(T* ptr, size_t elements) { setOutputs(std::vector<T*>{ptr}, elements); }
+  void setReduceFunction(ReductionType op) { op_ = op; }   // built-in ops only on the device
+  void setTag(uint32_t tag) { tag_ = tag; }
+  void setMaxSegmentSize(size_t bytes) { maxSegmentBytes_ = bytes; }
+  void setStream(hipStream_t s) { stream_ = s; }
+
+  std::shared_ptr<Context> context_;
+  std::vector<void*> inputs_, outputs_;
+  size_t elements_ = 0;
+  int dtype_ = GLOO_HIP_F32;
+  ReductionType op_ = SUM;
+  uint32_t tag_ = 0;
+  size_t maxSegmentBytes_ = 0;
+  hipStream_t stream_ = nullptr;
+};
+
+// One call = one allreduce (builds a PlanExecutor each time; the C-ABI
+// gloo_hip_allreduce caches them per option set).
+inline void allreduce(const AllreduceOptions& o) {
+  if (o.elements_ == 0) return;
+  PlanExecutor exec(o.context_, GLOO_HIP_ALGO_ALLREDUCE_RING, o.op_, o.dtype_, o.outputs_, o.elements_, {},
+                    o.stream_, o.inputs_, o.maxSegmentBytes_);
+  exec.run();
+}
 
 }  // namespace gloo_amd
