@@ -298,3 +298,40 @@ def test_new_style_allreduce_golden(torch, golden_sched, case):
     for (r, rep), outs in results.items():
         for j, y in enumerate(outs):
             assert same_bytes(y, want), (r, rep, j)
+
+
+DEAD_PEER_WORKER = r'''
+import os, sys, time, numpy as np
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, size, store = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+torch.cuda.set_device(0)
+buf = torch.ones(1 << 16, device="cuda:0")
+torch.cuda.synchronize()
+ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=3000)
+a = gloo_amd.Algorithm(ctx, "ring_chunked", "sum", "f32", [buf.data_ptr()], 1 << 16)
+if rank == 1:
+    os._exit(0)          # the peer dies after construction
+t0 = time.time()
+try:
+    a.run()
+    print("NO-ERROR")
+except gloo_amd.GlooHipError as e:
+    print("RAISED", round(time.time() - t0, 1), str(e)[:200])
+'''
+
+
+@pytest.mark.parametrize("mode", ["device", "host"])
+def test_dead_peer_times_out(torch, mode):
+    """Failure detection (SURVEY §5: context timeout -> IoException): a peer
+    that disappears makes run() raise after the timeout instead of hanging —
+    through the device-side wait kernel's bounded spin, or the host wait."""
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(DEAD_PEER_WORKER)
+        env = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_SIGNAL=mode)
+        procs = [subprocess.Popen([sys.executable, w, str(r), "2", "file:" + os.path.join(d, "s")], env=env,
+                                  stdout=subprocess.PIPE, text=True) for r in range(2)]
+        outs = [p.communicate(timeout=120)[0] for p in procs]
+    assert "RAISED" in outs[0], outs[0]
+    assert "timed out" in outs[0].lower()
