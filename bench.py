@@ -210,7 +210,39 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
     t = ms[len(ms) // 2] / 1e3
     per_gpu = [g["reduce_b"] / g["reduce_s"] / GIB for g in gathered if g["reduce_s"] > 0]
     ngpu = torch.cuda.device_count()
+    hd = []
+    for nbytes in (1 << 10, 1 << 20, 64 << 20):  # config 4: latency and bandwidth regimes
+        m = max(1, nbytes // 4)
+        try:
+            b2 = torch.ones(m, device=dev)
+            torch.cuda.synchronize(dev)
+            ctx2 = hip.Context(rank, world, "file:" + obj[0] + "/hd%d" % nbytes, device=dev.index,
+                               timeout_ms=60000)
+            a2 = hip.Algorithm(ctx2, "halving_doubling", "sum", "f32", [b2.data_ptr()], m)
+            a2.run()
+            ts = []
+            for _ in range(10):
+                dist.barrier()
+                t0 = time.perf_counter()
+                a2.run()
+                ts.append(time.perf_counter() - t0)
+            a2.close()
+            ctx2.close()
+            hd.append({"bytes": nbytes, "us": [round(t * 1e6, 1) for t in ts]})
+        except Exception as e:  # noqa: BLE001
+            hd.append({"bytes": nbytes, "error": repr(e)})
+    hd_all = [None] * world
+    dist.all_gather_object(hd_all, hd)
+    hd_summary = []
+    for i, nbytes in enumerate((1 << 10, 1 << 20, 64 << 20)):
+        if any("error" in h[i] for h in hd_all):
+            hd_summary.append({"bytes": nbytes, "error": next(h[i]["error"] for h in hd_all if "error" in h[i])})
+            continue
+        per = sorted(max(h[i]["us"][k] for h in hd_all) for k in range(10))
+        hd_summary.append({"bytes": nbytes, "us_p50": per[5], "us_max": per[-1],
+                           "busbw_gib_s": round(2 * (world - 1) / world * nbytes / (per[5] / 1e6) / GIB, 3)})
     return {"config": "allreduce_ring_chunked fp32 sum, %d ranks, %d MiB/rank" % (world, args.allreduce_mib),
+            "halving_doubling": hd_summary,
             "data_path": "xGMI peer copies" if ngpu >= world else f"{world} ranks on {ngpu} GPU(s)",
             "ms_p50": round(t * 1e3, 3), "algbw_gib_s": round(n * 4 / t / GIB, 2),
             "busbw_gib_s": round(2 * (world - 1) / world * n * 4 / t / GIB, 2),
