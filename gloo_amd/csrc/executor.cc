@@ -290,7 +290,68 @@ void PlanExecutor::run() {
     }
     return events_[ev++];
   };
-  for (const Step& s : plan_.steps) {
+  // Small-message fusion (device signalling only): a plan's
+  //   WAIT_* -> {REDUCE | COPY | SEND} -> [NOTIFY]   or a lone small SEND
+  // becomes ONE one-workgroup launch (launchFusedSmall): below a few KiB a
+  // hop costs dispatches, not bytes.  Off while profiling reduce kernels.
+  static const size_t kFuseBytes = [] {
+    const char* e = std::getenv("GLOO_AMD_FUSE_BYTES");
+    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)(64 << 10);
+  }();
+  const bool fuse = deviceSignal_ && !profiling_ && kFuseBytes > 0;
+  auto userOrArena = [&](bool arena) { return arena ? arena_ : userPtr(0); };
+  const std::vector<Step>& steps = plan_.steps;
+  for (size_t i = 0; i < steps.size(); i++) {
+    const Step& s = steps[i];
+    if (fuse) {
+      const bool isWait = s.kind == GLOO_HIP_STEP_WAIT_RECV || s.kind == GLOO_HIP_STEP_WAIT_NOTIFY;
+      const Step* t = isWait && i + 1 < steps.size() ? &steps[i + 1] : &s;
+      const bool body = t->kind == GLOO_HIP_STEP_REDUCE || t->kind == GLOO_HIP_STEP_COPY ||
+                        t->kind == GLOO_HIP_STEP_SEND;
+      if (body && t->length * es_ <= kFuseBytes && (isWait || t->kind == GLOO_HIP_STEP_SEND)) {
+        int op = 0;
+        char* dst = nullptr;
+        const char* src = nullptr;
+        if (t->kind == GLOO_HIP_STEP_REDUCE) {
+          op = op_;
+          dst = userPtr(0) + t->dst_off * es_;
+          src = arena_ + t->src_off * es_;
+        } else if (t->kind == GLOO_HIP_STEP_COPY) {
+          dst = userOrArena(t->flags & GLOO_HIP_DST_ARENA) + t->dst_off * es_;
+          src = userOrArena(t->flags & GLOO_HIP_SRC_ARENA) + t->src_off * es_;
+        } else {
+          dst = peers_[t->peer].base + (remoteRegion_[{t->peer, t->slot}] + t->dst_off) * es_;
+          src = userOrArena(t->flags & GLOO_HIP_SRC_ARENA) + t->src_off * es_;
+        }
+        const size_t bytes = t->length * es_;
+        const bool overlap = dst < src + bytes && src < dst + bytes && dst != src;
+        if (!(t->kind == GLOO_HIP_STEP_COPY && overlap)) {
+          const uint64_t* wf = nullptr;
+          uint64_t wt = 0;
+          if (isWait) {
+            wt = ++consumed_[{s.peer, s.slot}];
+            wf = ctx_->counterDevicePtr(inst_, s.peer, me, s.slot);
+          }
+          uint64_t* sf = nullptr;
+          uint64_t sv = 0;
+          size_t consumed = isWait ? 2 : 1;
+          if (t->kind == GLOO_HIP_STEP_SEND) {
+            sv = ++sent_[{t->peer, t->slot}];
+            sf = ctx_->counterDevicePtr(inst_, me, t->peer, t->slot);
+          } else if (isWait && i + 2 < steps.size() && steps[i + 2].kind == GLOO_HIP_STEP_NOTIFY) {
+            const Step& nt = steps[i + 2];
+            sv = ++sent_[{nt.peer, nt.slot}];
+            sf = ctx_->counterDevicePtr(inst_, me, nt.peer, nt.slot);
+            consumed = 3;
+          }
+          checkRc(launchFusedSmall(op, dtype_, dst, src, t->length, wf, wt, timeoutTicks, ctx_->errorWordDevicePtr(me),
+                                   sf, sv, stream_),
+                  "fused step");
+          i += consumed - 1;
+          continue;
+        }
+      }
+    }
     switch (s.kind) {
       case GLOO_HIP_STEP_DECL_RECV:
         break;

@@ -312,6 +312,73 @@ __global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Fused small-message step: [wait for a flag] -> dst (op)= src over n
+// elements (OP 0: plain copy) -> [signal a flag].  One workgroup: for chunks
+// of a few KiB a schedule hop is dispatch-bound, so the executor folds the
+// wait / reduce-or-copy / notify chain of a plan into this one launch.
+// Protocol (MI355X_MICROARCH.md, inter-workgroup visibility): ONE lane polls
+// relaxed, ONE system-scope acquire, barrier, then plain loads; every wave
+// drains its memory ops (vmcnt(0)) before the barrier that precedes the
+// single system-scope release + flag store.
+// ---------------------------------------------------------------------------
+constexpr int kFusedBlock = 512;
+
+template <class Tr, int OP>
+__global__ __launch_bounds__(kFusedBlock) void fused_small_kernel(
+    typename Tr::Storage* dst, const typename Tr::Storage* src, size_t n, const uint64_t* waitFlag,
+    uint64_t waitTarget, uint64_t timeoutTicks, uint32_t* err, uint64_t* sigFlag, uint64_t sigValue) {
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    int good = 1;
+    if (waitFlag) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(waitFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < waitTarget) {
+        __builtin_amdgcn_s_sleep(4);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > timeoutTicks) {
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          good = 0;
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    }
+    ok = good;
+  }
+  __syncthreads();
+  if (!ok) return;  // timed out: no work, no signal (the host raises)
+  for (size_t i = threadIdx.x; i < n; i += kFusedBlock) {
+    if constexpr (OP == 0) dst[i] = src[i];
+    else dst[i] = apply<Tr, OP>(dst[i], src[i]);
+  }
+  if (sigFlag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(sigFlag, sigValue, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+template <class Tr>
+int launch_fused(int op, void* dst, const void* src, size_t n, const uint64_t* wf, uint64_t wt, uint64_t tt,
+                 uint32_t* err, uint64_t* sf, uint64_t sv, hipStream_t s) {
+  using S = typename Tr::Storage;
+  S* d = static_cast<S*>(dst);
+  const S* x = static_cast<const S*>(src);
+  switch (op) {
+    case 0: fused_small_kernel<Tr, 0><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv); break;
+    case GLOO_HIP_SUM: fused_small_kernel<Tr, GLOO_HIP_SUM><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv); break;
+    case GLOO_HIP_PRODUCT: fused_small_kernel<Tr, GLOO_HIP_PRODUCT><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv); break;
+    case GLOO_HIP_MAX: fused_small_kernel<Tr, GLOO_HIP_MAX><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv); break;
+    case GLOO_HIP_MIN: fused_small_kernel<Tr, GLOO_HIP_MIN><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv); break;
+    default: return GLOO_HIP_EINVAL_OP;
+  }
+  return GLOO_HIP_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Host-side dispatch.
 // ---------------------------------------------------------------------------
 int g_variant = 0;  // fp32 SUM kernel variant (measurement knob)
@@ -449,6 +516,29 @@ int dispatch_multi(int op, int dtype, void* d, const void* const* srcs, int k, s
 }
 
 }  // namespace
+
+// Internal entry for the plan executor (see gloo_amd/signal.h).
+int launchFusedSmall(int op, int dtype, void* dst, const void* src, size_t n, const uint64_t* waitFlag,
+                     uint64_t waitTarget, uint64_t timeoutTicks, uint32_t* err, uint64_t* sigFlag,
+                     uint64_t sigValue, hipStream_t s) {
+  int rc;
+  switch (dtype) {
+    case GLOO_HIP_I8: rc = launch_fused<TrI8>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
+    case GLOO_HIP_U8: rc = launch_fused<TrU8>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
+    case GLOO_HIP_I32: rc = launch_fused<TrI32>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
+    case GLOO_HIP_U32: rc = launch_fused<TrU32>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
+    case GLOO_HIP_I64: rc = launch_fused<TrI64>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
+    case GLOO_HIP_U64: rc = launch_fused<TrU64>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
+    case GLOO_HIP_F16: rc = launch_fused<TrF16>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
+    case GLOO_HIP_BF16: rc = launch_fused<TrBF16>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
+    case GLOO_HIP_F32: rc = launch_fused<TrF32>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
+    case GLOO_HIP_F64: rc = launch_fused<TrF64>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
+    default: return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
+  }
+  if (rc != GLOO_HIP_OK) return set_error(rc, "fused step: bad op");
+  return check_launch("fused_small_kernel");
+}
+
 }  // namespace gloo_amd
 
 using namespace gloo_amd;

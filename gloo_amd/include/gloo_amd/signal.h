@@ -22,4 +22,11 @@ hipError_t launchSignal(uint64_t* flag, uint64_t value, hipStream_t stream);
 hipError_t launchWait(const uint64_t* flag, uint64_t target, uint64_t timeoutTicks, uint32_t* err,
                       hipStream_t stream);
 
+// One-workgroup fused step for small messages (reduce.hip): optionally wait
+// for `waitFlag >= waitTarget`, then dst[i] = dst[i] op src[i] (op 0: copy),
+// then optionally signal `*sigFlag = sigValue`.  Returns a gloo_hip status.
+int launchFusedSmall(int op, int dtype, void* dst, const void* src, size_t n, const uint64_t* waitFlag,
+                     uint64_t waitTarget, uint64_t timeoutTicks, uint32_t* err, uint64_t* sigFlag,
+                     uint64_t sigValue, hipStream_t stream);
+
 }  // namespace gloo_amd

@@ -335,3 +335,56 @@ def test_dead_peer_times_out(torch, mode):
         outs = [p.communicate(timeout=120)[0] for p in procs]
     assert "RAISED" in outs[0], outs[0]
     assert "timed out" in outs[0].lower()
+
+
+GOLDEN_PROC_WORKER = r'''
+import os, sys, numpy as np
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, size, store, case, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
+g = np.load(os.path.join(os.environ["GLOO_AMD_ROOT"], "tests", "golden", "sched_golden.npz"))
+algo, op, dtype = case.split("/")[:3]
+x = g[case + "/in"]
+recv = g[case + "/recv"] if algo == "reduce_scatter" else None
+xr = x[rank] if algo == "reduce_scatter" else x[rank, 0]
+torch.cuda.set_device(0)
+buf = torch.from_numpy(xr.view(np.uint8).copy()).to("cuda:0")
+torch.cuda.synchronize()
+ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=60000)
+a = gloo_amd.Algorithm(ctx, algo, op, dtype, [buf.data_ptr()], xr.size, recv_elems=recv)
+a.run()
+a.close(); ctx.close()
+np.save(out, buf.cpu().numpy().view(xr.dtype))
+'''
+
+
+@pytest.mark.parametrize("case,env", [
+    ("halving_doubling/sum/f32/P5/k1/n10007", {}),
+    ("halving_doubling/sum/f32/P8/k1/n1000", {}),
+    ("ring_chunked/sum/f32/P8/k1/n10007", {}),
+    ("reduce_scatter/max/bf16/P8/n4096", {}),
+    ("reduce_scatter/sum/f32/P5/n100", {}),
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0"}),
+    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0"}),
+])
+def test_processes_golden_device_signalling(torch, golden_sched, case, env):
+    """Ranks as processes on the box's GPU(s): device-side signalling with the
+    small-step fusion (default) and without it; bytes vs the reference."""
+    algo = case.split("/")[0]
+    P = int(case.split("/")[3][1:])
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(GOLDEN_PROC_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), case,
+                                   os.path.join(d, f"o{r}.npy")], env=e) for r in range(P)]
+        assert [p.wait(timeout=300) for p in procs] == [0] * P
+        outs = [np.load(os.path.join(d, f"o{r}.npy")) for r in range(P)]
+    want = golden_sched[case + "/out"]
+    if algo == "reduce_scatter":
+        recv = golden_sched[case + "/recv"]
+        got = np.concatenate([outs[r][:recv[r]] for r in range(P)])
+        assert same_bytes(got, want)
+    else:
+        for r in range(P):
+            assert same_bytes(outs[r], want), r
