@@ -92,6 +92,34 @@ void PlanExecutor::setBuffers(const std::vector<void*>& inputs, const std::vecto
                    "buffer count differs from the one the algorithm was built for");
   inputs_ = inputs;
   ptrs_ = outputs;
+  classifyPointers();
+}
+
+void PlanExecutor::classifyPointers() {
+  const char* forced = std::getenv("GLOO_AMD_FORCE_STAGING");  // tests: stage even same-device pointers
+  const bool force = forced && forced[0] == '1';
+  auto classify = [&](const std::vector<void*>& v, std::vector<bool>& remote, std::vector<char*>& stage,
+                      size_t first) {
+    remote.assign(v.size(), false);
+    stage.resize(v.size(), nullptr);
+    for (size_t j = first; j < v.size(); j++) {
+      if (!v[j]) continue;
+      hipPointerAttribute_t attr;
+      int dev = ctx_->device();
+      if (hipPointerGetAttributes(&attr, v[j]) == hipSuccess) dev = attr.device;
+      (void)hipGetLastError();
+      remote[j] = force || dev != ctx_->device();
+      if (remote[j] && dev != ctx_->device()) {
+        hipError_t e = hipDeviceEnablePeerAccess(dev, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
+        (void)hipGetLastError();
+      }
+      if (remote[j] && !stage[j]) GLOO_AMD_HIP_CHECK(hipMalloc(&stage[j], std::max<size_t>(256, count_ * es_)));
+      anyRemote_ = anyRemote_ || remote[j];
+    }
+  };
+  classify(ptrs_, outRemote_, outStage_, 1);   // output 0 is the rank's working buffer
+  classify(inputs_, inRemote_, inStage_, 0);
 }
 
 PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int dtype,
@@ -107,6 +135,8 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   const int me = ctx_->rank, P = ctx_->size;
   plan_ = planFor(algo_, me, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_, maxSegmentBytes_,
                   recvElems_);
+  GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
+  classifyPointers();
   inst_ = ctx_->nextInstance();
   {
     std::lock_guard<std::mutex> lk(liveMutex());
@@ -236,6 +266,10 @@ PlanExecutor::~PlanExecutor() {
       if (arena_) (void)hipFree(arena_);
     }
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+    for (char* p : outStage_)
+      if (p) (void)hipFree(p);
+    for (char* p : inStage_)
+      if (p) (void)hipFree(p);
     if (ownStream_ && stream_) (void)hipStreamDestroy(stream_);
   } catch (...) {
     // teardown is best effort; never throw from a destructor
@@ -403,7 +437,18 @@ void PlanExecutor::run() {
         // separate inputs (FROM_INPUTS; one input = a copy) or the outputs;
         // one fused pass per GLOO_HIP_MAX_SRCS sources.
         const size_t off = s.dst_off * es_;
-        const std::vector<void*>& from = (s.flags & GLOO_HIP_FROM_INPUTS) ? inputs_ : ptrs_;
+        const bool fromInputs = s.flags & GLOO_HIP_FROM_INPUTS;
+        std::vector<void*> from = fromInputs ? inputs_ : ptrs_;
+        if (anyRemote_) {
+          const std::vector<bool>& remote = fromInputs ? inRemote_ : outRemote_;
+          const std::vector<char*>& stage = fromInputs ? inStage_ : outStage_;
+          for (size_t j = 0; j < from.size(); j++)
+            if (remote[j]) {  // pull the range over the peer link into local HBM
+              GLOO_AMD_HIP_CHECK(hipMemcpyAsync(stage[j] + off, static_cast<const char*>(from[j]) + off,
+                                                s.length * es_, hipMemcpyDeviceToDevice, stream_));
+              from[j] = stage[j];
+            }
+        }
         char* out0 = userPtr(0) + off;
         if (from.size() == 1) {
           deviceMove(out0, static_cast<const char*>(from[0]) + off, s.length * es_, stream_);

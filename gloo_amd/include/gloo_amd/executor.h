@@ -89,6 +89,14 @@ class PlanExecutor {
   size_t count_;
   size_t maxSegmentBytes_ = 0;
   std::vector<int> recvElems_;
+  // Local pointers on other GPUs of this process (the reference's
+  // multi-GPU-per-process form, gloo/cuda_collectives_native.h:22-146):
+  // their ranges are pulled into local staging buffers by peer copies before
+  // the fused local fold, and the broadcast pushes back by peer copies.
+  std::vector<bool> outRemote_, inRemote_;
+  std::vector<char*> outStage_, inStage_;
+  bool anyRemote_ = false;
+  void classifyPointers();
   Plan plan_;
   uint64_t inst_;
   char* arena_ = nullptr;

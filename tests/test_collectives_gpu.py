@@ -388,3 +388,38 @@ def test_processes_golden_device_signalling(torch, golden_sched, case, env):
     else:
         for r in range(P):
             assert same_bytes(outs[r], want), r
+
+
+@pytest.mark.parametrize("case", ["ring_chunked/sum/f32/P3/k2/n1000", "halving_doubling/sum/f32/P3/k3/n500",
+                                  "local/sum/f32/P1/k4/n1000"])
+def test_multi_pointer_staging(torch, golden_sched, case, monkeypatch):
+    """Local pointers that live on another GPU are pulled into local HBM by
+    peer copies before the fused fold (the reference's multi-GPU-per-process
+    form).  GLOO_AMD_FORCE_STAGING exercises that path on a single GPU."""
+    monkeypatch.setenv("GLOO_AMD_FORCE_STAGING", "1")
+    algo = case.split("/")[0]
+    x, want = golden_sched[case + "/in"], golden_sched[case + "/out"]
+    y = run_threads(torch, algo, "sum", "f32", x)
+    for r in range(y.shape[0]):
+        for j in range(y.shape[1]):
+            assert same_bytes(y[r, j], want), (r, j)
+
+
+def test_multi_pointer_across_gpus(torch, golden_sched):
+    """One rank, one pointer per GPU (gloo/test/cuda_allreduce_test.cc
+    MultiPointer); needs >= 2 GPUs."""
+    import gloo_amd
+    ndev = torch.cuda.device_count()
+    if ndev < 2:
+        pytest.skip("needs 2+ GPUs")
+    case = "local/sum/f32/P1/k4/n1000"
+    x, want = golden_sched[case + "/in"], golden_sched[case + "/out"]
+    bufs = [torch.from_numpy(x[0, j].copy()).to(f"cuda:{j % ndev}") for j in range(x.shape[1])]
+    torch.cuda.synchronize()
+    ctx = gloo_amd.Context(0, 1, "mem:" + uuid.uuid4().hex, device=0)
+    a = gloo_amd.Algorithm(ctx, "local", "sum", "f32", [b.data_ptr() for b in bufs], x.shape[2])
+    a.run()
+    a.close()
+    ctx.close()
+    for b in bufs:
+        assert same_bytes(b.cpu().numpy(), want)
