@@ -163,55 +163,79 @@ def copy_ceiling(torch, dev, nbytes=1 << 30, iters=10):
 
 
 def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
-    """BASELINE config 3: AllreduceRingChunked fp32 sum, `world` ranks, one per
-    GPU, 256 MiB per rank; chunks move GPU->GPU into the peer's HBM inbox
-    (xGMI), every arriving chunk is reduced by the HIP kernel on the receiving
-    GPU.  Reports the slowest rank's time per allreduce and the reduce
-    kernel's own GiB/s measured with HIP events around each chunk reduction
-    while the exchange runs (per-GPU efficiency vs the 1-GPU figure)."""
+    """BASELINE config 3 (+ a config-4 sweep) at N > 1 ranks, one per GPU.
+
+    Config 3: AllreduceRingChunked fp32 sum, 256 MiB per rank.  Chunks move
+    GPU->GPU into the peer's HBM inbox (xGMI) and every arriving chunk is
+    reduced by the HIP kernel on the receiving GPU.  Reported: the slowest
+    rank's time per allreduce, bus bandwidth, and the reduce kernel's own
+    GiB/s measured with HIP events around each chunk reduction while the
+    exchange runs (per-GPU efficiency vs the 1-GPU figure) — once with
+    hipMemcpyAsync peer copies, once with the fused copy+signal kernel.
+    Config 4: halving-doubling at 1 KiB / 1 MiB / 64 MiB per rank."""
     import tempfile
     obj = [tempfile.mkdtemp(prefix="gloo_amd_bench_")] if rank == 0 else [None]
     dist.broadcast_object_list(obj, src=0)
     n = args.allreduce_mib * (1 << 20) // 4
-    res = {}
-    try:
-        buf = torch.ones(n, device=dev)
-        torch.cuda.synchronize(dev)
-        ctx = hip.Context(rank, world, "file:" + obj[0], device=dev.index, timeout_ms=60000)
-        a = hip.Algorithm(ctx, "ring_chunked", "sum", "f32", [buf.data_ptr()], n)
-        a.set_profiling(True)
-        a.run()
-        times, red_s, red_b, wait_s = [], 0.0, 0.0, 0.0
-        for _ in range(args.allreduce_iters):
-            dist.barrier()
-            t0 = time.perf_counter()
+
+    def gather(res):
+        g = [None] * world
+        dist.all_gather_object(g, res)
+        return g
+
+    def ring_once(engine):
+        os.environ["GLOO_AMD_COPY"] = engine
+        res = {}
+        try:
+            buf = torch.ones(n, device=dev)
+            torch.cuda.synchronize(dev)
+            ctx = hip.Context(rank, world, "file:" + obj[0] + "/ring_" + engine, device=dev.index,
+                              timeout_ms=60000)
+            a = hip.Algorithm(ctx, "ring_chunked", "sum", "f32", [buf.data_ptr()], n)
+            a.set_profiling(True)
             a.run()
-            times.append(time.perf_counter() - t0)
-            st = a.stats()
-            red_s += st["reduce_s"]
-            red_b += st["reduce_bytes"]
-            wait_s += st["wait_s"]
-        runs = 1 + args.allreduce_iters
-        want = float(world) ** runs
-        ok = bool((buf[:: max(1, n // 4096)] == want).all()) if want < 2 ** 24 else None
-        a.close()
-        ctx.close()
-        res = {"ms": [round(t * 1e3, 3) for t in times], "reduce_s": red_s, "reduce_b": red_b,
-               "wait_ms_per_run": round(wait_s / args.allreduce_iters * 1e3, 3), "verified": ok}
-    except Exception as e:  # noqa: BLE001
-        res = {"error": repr(e)}
-    gathered = [None] * world
-    dist.all_gather_object(gathered, res)
-    errs = [g["error"] for g in gathered if "error" in g]
-    if errs:
-        return {"error": errs[0]}
-    ms = [max(g["ms"][i] for g in gathered) for i in range(args.allreduce_iters)]
-    ms.sort()
-    t = ms[len(ms) // 2] / 1e3
-    per_gpu = [g["reduce_b"] / g["reduce_s"] / GIB for g in gathered if g["reduce_s"] > 0]
-    ngpu = torch.cuda.device_count()
+            times, red_s, red_b, wait_s = [], 0.0, 0.0, 0.0
+            for _ in range(args.allreduce_iters):
+                dist.barrier()
+                t0 = time.perf_counter()
+                a.run()
+                times.append(time.perf_counter() - t0)
+                st = a.stats()
+                red_s += st["reduce_s"]
+                red_b += st["reduce_bytes"]
+                wait_s += st["wait_s"]
+            want = float(world) ** (1 + args.allreduce_iters)
+            ok = bool((buf[:: max(1, n // 4096)] == want).all()) if want < 2 ** 24 else None
+            a.close()
+            ctx.close()
+            res = {"ms": [round(t * 1e3, 3) for t in times], "reduce_s": red_s, "reduce_b": red_b,
+                   "wait_ms_per_run": round(wait_s / args.allreduce_iters * 1e3, 3), "verified": ok}
+        except Exception as e:  # noqa: BLE001
+            res = {"error": repr(e)}
+        finally:
+            os.environ.pop("GLOO_AMD_COPY", None)
+        gathered = gather(res)
+        errs = [g["error"] for g in gathered if "error" in g]
+        if errs:
+            return {"copy_engine": engine, "error": errs[0]}
+        ms = sorted(max(g["ms"][i] for g in gathered) for i in range(args.allreduce_iters))
+        t = ms[len(ms) // 2] / 1e3
+        per_gpu = [g["reduce_b"] / g["reduce_s"] / GIB for g in gathered if g["reduce_s"] > 0]
+        return {"copy_engine": engine, "ms_p50": round(t * 1e3, 3), "algbw_gib_s": round(n * 4 / t / GIB, 2),
+                "busbw_gib_s": round(2 * (world - 1) / world * n * 4 / t / GIB, 2),
+                "reduce_kernel_gib_s_per_gpu": [round(x, 1) for x in per_gpu],
+                "reduce_kernel_gib_s_min": round(min(per_gpu), 1) if per_gpu else None,
+                "host_wait_ms_per_run_max": max(g["wait_ms_per_run"] for g in gathered),
+                "verified": all(g["verified"] is not False for g in gathered)}
+
+    ring = ring_once("memcpy")
+    if "error" in ring:
+        return ring
+    ring_kernel = ring_once("kernel")
+
+    sizes = (1 << 10, 1 << 20, 64 << 20)
     hd = []
-    for nbytes in (1 << 10, 1 << 20, 64 << 20):  # config 4: latency and bandwidth regimes
+    for nbytes in sizes:
         m = max(1, nbytes // 4)
         try:
             b2 = torch.ones(m, device=dev)
@@ -231,25 +255,22 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
             hd.append({"bytes": nbytes, "us": [round(t * 1e6, 1) for t in ts]})
         except Exception as e:  # noqa: BLE001
             hd.append({"bytes": nbytes, "error": repr(e)})
-    hd_all = [None] * world
-    dist.all_gather_object(hd_all, hd)
+    hd_all = gather(hd)
     hd_summary = []
-    for i, nbytes in enumerate((1 << 10, 1 << 20, 64 << 20)):
+    for i, nbytes in enumerate(sizes):
         if any("error" in h[i] for h in hd_all):
             hd_summary.append({"bytes": nbytes, "error": next(h[i]["error"] for h in hd_all if "error" in h[i])})
             continue
         per = sorted(max(h[i]["us"][k] for h in hd_all) for k in range(10))
         hd_summary.append({"bytes": nbytes, "us_p50": per[5], "us_max": per[-1],
                            "busbw_gib_s": round(2 * (world - 1) / world * nbytes / (per[5] / 1e6) / GIB, 3)})
-    return {"config": "allreduce_ring_chunked fp32 sum, %d ranks, %d MiB/rank" % (world, args.allreduce_mib),
-            "halving_doubling": hd_summary,
-            "data_path": "xGMI peer copies" if ngpu >= world else f"{world} ranks on {ngpu} GPU(s)",
-            "ms_p50": round(t * 1e3, 3), "algbw_gib_s": round(n * 4 / t / GIB, 2),
-            "busbw_gib_s": round(2 * (world - 1) / world * n * 4 / t / GIB, 2),
-            "reduce_kernel_gib_s_per_gpu": [round(x, 1) for x in per_gpu],
-            "reduce_kernel_gib_s_min": round(min(per_gpu), 1) if per_gpu else None,
-            "host_wait_ms_per_run_max": max(g["wait_ms_per_run"] for g in gathered),
-            "verified": all(g["verified"] is not False for g in gathered)}
+    ngpu = torch.cuda.device_count()
+    out = {"config": "allreduce_ring_chunked fp32 sum, %d ranks, %d MiB/rank" % (world, args.allreduce_mib),
+           "data_path": "xGMI peer copies" if ngpu >= world else f"{world} ranks on {ngpu} GPU(s)"}
+    out.update(ring)
+    out["kernel_copy_engine"] = ring_kernel
+    out["halving_doubling"] = hd_summary
+    return out
 
 
 def arm_watchdog(seconds, on_fire):

@@ -251,6 +251,13 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   if (deviceSignal_) {
     (void)ctx_->counterDevicePtr(inst_, 0, 0, 0);  // register the control block now
     ctx_->errorWord(me).store(0);
+    const char* cp = std::getenv("GLOO_AMD_COPY");
+    kernelCopy_ = cp && std::string(cp) == "kernel";
+    if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS")) copyBlocks_ = (unsigned)std::max(1, std::atoi(cb));
+    if (kernelCopy_) {
+      GLOO_AMD_HIP_CHECK(hipMalloc(&ticket_, 256));
+      GLOO_AMD_HIP_CHECK(hipMemset(ticket_, 0, 256));
+    }
   }
   ctx_->barrier(strcat_("inst", inst_, "/ready"));
 }
@@ -266,6 +273,7 @@ PlanExecutor::~PlanExecutor() {
       if (arena_) (void)hipFree(arena_);
     }
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+    if (ticket_) (void)hipFree(ticket_);
     for (char* p : outStage_)
       if (p) (void)hipFree(p);
     for (char* p : inStage_)
@@ -392,6 +400,15 @@ void PlanExecutor::run() {
       case GLOO_HIP_STEP_SEND: {
         char* dst = peers_[s.peer].base + (remoteRegion_[{s.peer, s.slot}] + s.dst_off) * es_;
         const char* src = (s.flags & GLOO_HIP_SRC_ARENA ? arena_ : userPtr(0)) + s.src_off * es_;
+        if (kernelCopy_) {
+          const uint64_t seq = ++sent_[{s.peer, s.slot}];
+          const unsigned grid = copySignalGrid(s.length * es_, copyBlocks_);
+          checkRc(launchCopySignal(dst, src, s.length * es_, ctx_->counterDevicePtr(inst_, me, s.peer, s.slot), seq,
+                                   ticket_, ticketNext_, grid, stream_),
+                  "copy_signal_kernel");
+          ticketNext_ += grid;
+          break;
+        }
         if (s.length) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(dst, src, s.length * es_, hipMemcpyDeviceToDevice, stream_));
         signal(s.peer, s.slot);
         break;

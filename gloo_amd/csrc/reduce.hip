@@ -379,6 +379,58 @@ int launch_fused(int op, void* dst, const void* src, size_t n, const uint64_t* w
 }
 
 // ---------------------------------------------------------------------------
+// Peer copy with the arrival signal fused in: the SEND of a plan as one
+// launch.  A capped grid walks 16 KiB tiles (512 lanes x 2 x 16 B): loads
+// from local HBM (`nt`, any misalignment via soffset), 16-B stores into the
+// peer's inbox (over xGMI when it is another GPU).  Completion: every wave
+// drains (vmcnt 0), the workgroup syncs, one lane releases at system scope
+// and takes a ticket; the workgroup holding the last ticket of this launch
+// publishes `*flag = seq` (MI355X_MICROARCH.md: counter fan-in + flag).
+// Tickets only grow; the host passes the launch's first ticket.
+// ---------------------------------------------------------------------------
+constexpr int kCopyBlock = 512;
+constexpr int kCopyUnroll = 2;
+
+__global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(
+    char* dst, const char* src, size_t bytes, uint64_t* flag, uint64_t seq, unsigned* ticket,
+    unsigned ticketBase) {
+  // dst head up to a 16-B boundary and the ragged tail: block 0, bytewise
+  const size_t head = ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) < bytes
+                          ? ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) : bytes;
+  const size_t nvec = (bytes - head) / 16;
+  const size_t tail0 = head + nvec * 16;
+  if (blockIdx.x == 0) {
+    for (size_t i = threadIdx.x; i < head; i += kCopyBlock) dst[i] = src[i];
+    for (size_t i = tail0 + threadIdx.x; i < bytes; i += kCopyBlock) dst[i] = src[i];
+  }
+  constexpr uint32_t kTileBytes = kCopyBlock * kCopyUnroll * 16;
+  const size_t body = nvec * 16;
+  const Src ss = src_of(src + head);
+  for (size_t base = (size_t)blockIdx.x * kTileBytes; base < body; base += (size_t)gridDim.x * kTileBytes) {
+    const uint32_t n = (uint32_t)((body - base) < kTileBytes ? (body - base) : kTileBytes);
+    const auto rs = make_rsrc(ss.base + base, n + ss.mis);
+    const auto rd = make_rsrc(dst + head + base, n);
+    const uint32_t lane_off = threadIdx.x * 16u;
+    u32x4 v[kCopyUnroll];
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; u++) v[u] = bload<kAuxNT>(rs, lane_off + u * kCopyBlock * 16, ss.mis);
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; u++) bstore<kAuxNT>(rd, lane_off + u * kCopyBlock * 16, v[u]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == ticketBase + gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host-side dispatch.
 // ---------------------------------------------------------------------------
 int g_variant = 0;  // fp32 SUM kernel variant (measurement knob)
@@ -516,6 +568,19 @@ int dispatch_multi(int op, int dtype, void* d, const void* const* srcs, int k, s
 }
 
 }  // namespace
+
+unsigned copySignalGrid(size_t bytes, unsigned maxBlocks) {
+  const size_t tiles = (bytes + (size_t)kCopyBlock * kCopyUnroll * 16 - 1) / ((size_t)kCopyBlock * kCopyUnroll * 16);
+  size_t g = tiles < maxBlocks ? tiles : maxBlocks;
+  return (unsigned)(g == 0 ? 1 : g);
+}
+
+int launchCopySignal(void* dst, const void* src, size_t bytes, uint64_t* flag, uint64_t seq, unsigned* ticket,
+                     unsigned ticketBase, unsigned grid, hipStream_t s) {
+  copy_signal_kernel<<<grid, kCopyBlock, 0, s>>>(static_cast<char*>(dst), static_cast<const char*>(src), bytes,
+                                                 flag, seq, ticket, ticketBase);
+  return check_launch("copy_signal_kernel");
+}
 
 // Internal entry for the plan executor (see gloo_amd/signal.h).
 int launchFusedSmall(int op, int dtype, void* dst, const void* src, size_t n, const uint64_t* waitFlag,

@@ -25,6 +25,11 @@
 // the host-side waits.  Both styles write the same monotonically increasing
 // sequence numbers, so they interoperate.  GLOO_AMD_SIGNAL=host|device
 // overrides the choice.
+//
+// Copy engine of a SEND (device signalling): hipMemcpyAsync + signal kernel
+// (default), or GLOO_AMD_COPY=kernel: copy_signal_kernel, one launch that
+// copies with GLOO_AMD_COPY_BLOCKS workgroups (default 64) and publishes the
+// arrival itself.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -62,6 +67,7 @@ class PlanExecutor {
   hipStream_t stream() const { return stream_; }
   bool deviceSignalling() const { return deviceSignal_; }
   bool fineGrainedArena() const { return fineArena_; }
+  bool kernelCopy() const { return kernelCopy_; }
   // Host time spent blocked in WAIT steps during the last run(), seconds.
   double lastWaitSeconds() const { return waitSeconds_; }
   // When enabled, every REDUCE of run() is bracketed by HIP events; after the
@@ -108,6 +114,10 @@ class PlanExecutor {
   std::map<std::pair<int, int>, uint64_t> sent_;          // (dst, slot) -> last sequence signalled
   bool deviceSignal_ = false;  // stream-ordered signal/wait kernels instead of host waits
   bool fineArena_ = false;     // inbox arena in fine-grained (cross-device coherent) memory
+  bool kernelCopy_ = false;    // SEND = copy_signal_kernel instead of hipMemcpyAsync + signal
+  unsigned copyBlocks_ = 64;
+  unsigned* ticket_ = nullptr; // completion tickets of copy_signal_kernel (device memory)
+  unsigned ticketNext_ = 0;
   double waitSeconds_ = 0;
   bool profiling_ = false;
   std::vector<hipEvent_t> events_;

@@ -29,4 +29,12 @@ int launchFusedSmall(int op, int dtype, void* dst, const void* src, size_t n, co
                      uint64_t waitTarget, uint64_t timeoutTicks, uint32_t* err, uint64_t* sigFlag,
                      uint64_t sigValue, hipStream_t stream);
 
+// Peer copy + fused arrival signal (reduce.hip): `grid` workgroups copy
+// `bytes` from src (local) to dst (a peer's inbox); the workgroup that takes
+// ticket ticketBase + grid - 1 publishes *flag = seq.  copySignalGrid() sizes
+// the grid (capped at maxBlocks: a link, not HBM, bounds a peer copy).
+unsigned copySignalGrid(size_t bytes, unsigned maxBlocks);
+int launchCopySignal(void* dst, const void* src, size_t bytes, uint64_t* flag, uint64_t seq, unsigned* ticket,
+                     unsigned ticketBase, unsigned grid, hipStream_t stream);
+
 }  // namespace gloo_amd

@@ -366,6 +366,11 @@ np.save(out, buf.cpu().numpy().view(xr.dtype))
     ("reduce_scatter/sum/f32/P5/n100", {}),
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0"}),
     ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0"}),
+    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0", "GLOO_AMD_COPY": "kernel"}),
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0", "GLOO_AMD_COPY": "kernel",
+                                               "GLOO_AMD_COPY_BLOCKS": "3"}),
+    ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_COPY": "kernel"}),
+    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_FUSE_BYTES": "0", "GLOO_AMD_COPY": "kernel"}),
 ])
 def test_processes_golden_device_signalling(torch, golden_sched, case, env):
     """Ranks as processes on the box's GPU(s): device-side signalling with the
