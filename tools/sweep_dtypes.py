@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Every dtype x op of the chunk-reduce kernel at 64 MiB per operand
+(in place, 6 rotated pairs = 768 MiB footprint): time per launch and
+algorithmic GB/s (3 x 64 MiB per launch).  One JSON line each."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import gloo_amd as hip  # noqa: E402
+
+NBYTES = 64 << 20
+DTYPES = ["i8", "u8", "i32", "u32", "i64", "u64", "f16", "bf16", "f32", "f64"]
+OPS = ["sum", "product", "max", "min"]
+
+
+def main():
+    dev = torch.device("cuda:0")
+    pairs = [(torch.randint(0, 255, (NBYTES,), dtype=torch.uint8, device=dev),
+              torch.randint(0, 255, (NBYTES,), dtype=torch.uint8, device=dev)) for _ in range(6)]
+    s = torch.cuda.current_stream().cuda_stream
+    for dt in DTYPES:
+        n = NBYTES // hip.dtype_size(dt)
+        for op in OPS:
+            for i in range(6):
+                d, x = pairs[i]
+                hip.reduce_ptr(op, dt, d.data_ptr(), x.data_ptr(), n, s)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            steps = 120
+            e0.record()
+            for i in range(steps):
+                d, x = pairs[i % 6]
+                hip.reduce_ptr(op, dt, d.data_ptr(), x.data_ptr(), n, s)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / steps
+            print(json.dumps({"dtype": dt, "op": op, "us": round(us, 2),
+                              "GBs": round(3 * NBYTES / (us / 1e3) / 1e9, 1),
+                              "frac_of_8TBs": round(3 * NBYTES / (us / 1e3) / 8e12, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
