@@ -38,8 +38,8 @@ def main():
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / steps
             print(json.dumps({"dtype": dt, "op": op, "us": round(us, 2),
-                              "GBs": round(3 * NBYTES / (us / 1e3) / 1e9, 1),
-                              "frac_of_8TBs": round(3 * NBYTES / (us / 1e3) / 8e12, 4)}), flush=True)
+                              "GBs": round(3 * NBYTES / (us / 1e6) / 1e9, 1),
+                              "frac_of_8TBs": round(3 * NBYTES / (us / 1e6) / 8e12, 4)}), flush=True)
 
 
 if __name__ == "__main__":
