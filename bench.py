@@ -264,6 +264,10 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
         per = sorted(max(h[i]["us"][k] for h in hd_all) for k in range(10))
         hd_summary.append({"bytes": nbytes, "us_p50": per[5], "us_max": per[-1],
                            "busbw_gib_s": round(2 * (world - 1) / world * nbytes / (per[5] / 1e6) / GIB, 3)})
+    dist.barrier()
+    if rank == 0:
+        import shutil
+        shutil.rmtree(obj[0], ignore_errors=True)
     ngpu = torch.cuda.device_count()
     out = {"config": "allreduce_ring_chunked fp32 sum, %d ranks, %d MiB/rank" % (world, args.allreduce_mib),
            "data_path": "xGMI peer copies" if ngpu >= world else f"{world} ranks on {ngpu} GPU(s)"}
