@@ -183,37 +183,55 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
         dist.all_gather_object(g, res)
         return g
 
-    def ring_once(engine):
-        os.environ["GLOO_AMD_COPY"] = engine
-        res = {}
+    def with_env(env, fn):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
         try:
+            return fn()
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+    def ring_once(engine):
+        def body():
             buf = torch.ones(n, device=dev)
             torch.cuda.synchronize(dev)
             ctx = hip.Context(rank, world, "file:" + obj[0] + "/ring_" + engine, device=dev.index,
                               timeout_ms=60000)
             a = hip.Algorithm(ctx, "ring_chunked", "sum", "f32", [buf.data_ptr()], n)
-            a.set_profiling(True)
             a.run()
-            times, red_s, red_b, wait_s = [], 0.0, 0.0, 0.0
+            # timed: steady state (the plan replays as a hipGraph from run 3 on)
+            times = []
             for _ in range(args.allreduce_iters):
                 dist.barrier()
                 t0 = time.perf_counter()
                 a.run()
                 times.append(time.perf_counter() - t0)
+            graphed = a.mode()["graph"]
+            # profiled: every chunk reduction bracketed by HIP events (eager)
+            a.set_profiling(True)
+            red_s = red_b = wait_s = 0.0
+            for _ in range(3):
+                dist.barrier()
+                a.run()
                 st = a.stats()
                 red_s += st["reduce_s"]
                 red_b += st["reduce_bytes"]
                 wait_s += st["wait_s"]
-            want = float(world) ** (1 + args.allreduce_iters)
+            runs = 1 + args.allreduce_iters + 3
+            want = float(world) ** runs
             ok = bool((buf[:: max(1, n // 4096)] == want).all()) if want < 2 ** 24 else None
             a.close()
             ctx.close()
-            res = {"ms": [round(t * 1e3, 3) for t in times], "reduce_s": red_s, "reduce_b": red_b,
-                   "wait_ms_per_run": round(wait_s / args.allreduce_iters * 1e3, 3), "verified": ok}
+            return {"ms": [round(t * 1e3, 3) for t in times], "reduce_s": red_s, "reduce_b": red_b,
+                    "wait_ms_per_run": round(wait_s / 3 * 1e3, 3), "verified": ok, "graph": graphed}
+        try:
+            res = with_env({"GLOO_AMD_COPY": engine}, body)
         except Exception as e:  # noqa: BLE001
             res = {"error": repr(e)}
-        finally:
-            os.environ.pop("GLOO_AMD_COPY", None)
         gathered = gather(res)
         errs = [g["error"] for g in gathered if "error" in g]
         if errs:
@@ -221,11 +239,12 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
         ms = sorted(max(g["ms"][i] for g in gathered) for i in range(args.allreduce_iters))
         t = ms[len(ms) // 2] / 1e3
         per_gpu = [g["reduce_b"] / g["reduce_s"] / GIB for g in gathered if g["reduce_s"] > 0]
-        return {"copy_engine": engine, "ms_p50": round(t * 1e3, 3), "algbw_gib_s": round(n * 4 / t / GIB, 2),
+        return {"copy_engine": engine, "graph": all(g["graph"] for g in gathered),
+                "ms_p50": round(t * 1e3, 3), "algbw_gib_s": round(n * 4 / t / GIB, 2),
                 "busbw_gib_s": round(2 * (world - 1) / world * n * 4 / t / GIB, 2),
                 "reduce_kernel_gib_s_per_gpu": [round(x, 1) for x in per_gpu],
                 "reduce_kernel_gib_s_min": round(min(per_gpu), 1) if per_gpu else None,
-                "host_wait_ms_per_run_max": max(g["wait_ms_per_run"] for g in gathered),
+                "host_wait_ms_per_run_max_profiled": max(g["wait_ms_per_run"] for g in gathered),
                 "verified": all(g["verified"] is not False for g in gathered)}
 
     ring = ring_once("memcpy")
@@ -233,37 +252,54 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
         return ring
     ring_kernel = ring_once("kernel")
 
-    sizes = (1 << 10, 1 << 20, 64 << 20)
-    hd = []
-    for nbytes in sizes:
-        m = max(1, nbytes // 4)
-        try:
-            b2 = torch.ones(m, device=dev)
-            torch.cuda.synchronize(dev)
-            ctx2 = hip.Context(rank, world, "file:" + obj[0] + "/hd%d" % nbytes, device=dev.index,
-                               timeout_ms=60000)
-            a2 = hip.Algorithm(ctx2, "halving_doubling", "sum", "f32", [b2.data_ptr()], m)
-            a2.run()
-            ts = []
-            for _ in range(10):
-                dist.barrier()
-                t0 = time.perf_counter()
-                a2.run()
-                ts.append(time.perf_counter() - t0)
-            a2.close()
-            ctx2.close()
-            hd.append({"bytes": nbytes, "us": [round(t * 1e6, 1) for t in ts]})
-        except Exception as e:  # noqa: BLE001
-            hd.append({"bytes": nbytes, "error": repr(e)})
-    hd_all = gather(hd)
-    hd_summary = []
-    for i, nbytes in enumerate(sizes):
-        if any("error" in h[i] for h in hd_all):
-            hd_summary.append({"bytes": nbytes, "error": next(h[i]["error"] for h in hd_all if "error" in h[i])})
-            continue
-        per = sorted(max(h[i]["us"][k] for h in hd_all) for k in range(10))
-        hd_summary.append({"bytes": nbytes, "us_p50": per[5], "us_max": per[-1],
-                           "busbw_gib_s": round(2 * (world - 1) / world * nbytes / (per[5] / 1e6) / GIB, 3)})
+    sizes = (1 << 10, 64 << 10, 1 << 20, 64 << 20)
+    iters = 20
+
+    def hd_sweep(label, env):
+        def body():
+            hd = []
+            for nbytes in sizes:
+                m = max(1, nbytes // 4)
+                try:
+                    b2 = torch.ones(m, device=dev)
+                    torch.cuda.synchronize(dev)
+                    ctx2 = hip.Context(rank, world, "file:%s/hd_%s_%d" % (obj[0], label, nbytes),
+                                       device=dev.index, timeout_ms=60000)
+                    a2 = hip.Algorithm(ctx2, "halving_doubling", "sum", "f32", [b2.data_ptr()], m)
+                    a2.run()
+                    a2.run()
+                    ts = []
+                    for _ in range(iters):
+                        dist.barrier()
+                        t0 = time.perf_counter()
+                        a2.run()
+                        ts.append(time.perf_counter() - t0)
+                    g = a2.mode()["graph"]
+                    a2.close()
+                    ctx2.close()
+                    hd.append({"bytes": nbytes, "us": [round(t * 1e6, 1) for t in ts], "graph": g})
+                except Exception as e:  # noqa: BLE001
+                    hd.append({"bytes": nbytes, "error": repr(e)})
+            return hd
+        hd_all = gather(with_env(env, body))
+        summary = []
+        for i, nbytes in enumerate(sizes):
+            if any("error" in h[i] for h in hd_all):
+                summary.append({"bytes": nbytes,
+                                "error": next(h[i]["error"] for h in hd_all if "error" in h[i])})
+                continue
+            per = sorted(max(h[i]["us"][k] for h in hd_all) for k in range(iters))
+            summary.append({"bytes": nbytes, "us_p50": per[iters // 2], "us_max": per[-1],
+                            "graph": all(h[i]["graph"] for h in hd_all),
+                            "busbw_gib_s": round(2 * (world - 1) / world * nbytes / (per[iters // 2] / 1e6) / GIB,
+                                                 3)})
+        return summary
+
+    hd_variants = {"memcpy_graph": {"GLOO_AMD_COPY": "memcpy"},
+                   "kernel_graph": {"GLOO_AMD_COPY": "kernel"},
+                   "memcpy_eager": {"GLOO_AMD_COPY": "memcpy", "GLOO_AMD_GRAPH": "0"},
+                   "kernel_eager": {"GLOO_AMD_COPY": "kernel", "GLOO_AMD_GRAPH": "0"}}
+    hd_summary = {k: hd_sweep(k, v) for k, v in hd_variants.items()}
     dist.barrier()
     if rank == 0:
         import shutil

@@ -212,13 +212,15 @@ def _bind_collectives(L):
     L.gloo_hip_algorithm_wait_seconds.restype = ctypes.c_double
     L.gloo_hip_algorithm_set_profiling.argtypes = [vp, ctypes.c_int]
     L.gloo_hip_algorithm_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+    L.gloo_hip_algorithm_mode.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
 
 
 _bind_collectives(lib)
 EXPORTED = EXPORTED + ("gloo_hip_context_create", "gloo_hip_context_destroy",
                        "gloo_hip_algorithm_create", "gloo_hip_algorithm_run",
                        "gloo_hip_algorithm_destroy", "gloo_hip_algorithm_wait_seconds",
-                       "gloo_hip_algorithm_set_profiling", "gloo_hip_algorithm_stats")
+                       "gloo_hip_algorithm_set_profiling", "gloo_hip_algorithm_stats",
+                       "gloo_hip_algorithm_mode")
 
 
 class Context:
@@ -276,6 +278,19 @@ class Algorithm:
         out = (ctypes.c_double * 4)()
         _check(lib.gloo_hip_algorithm_stats(self._h, out))
         return {"reduce_s": out[0], "reduce_bytes": out[1], "reductions": int(out[2]), "wait_s": out[3]}
+
+    def mode(self):
+        """How run() executes: device-side signalling, fine-grained inboxes,
+        kernel copy engine, hipGraph replay; 'graph_error' says why capture
+        was abandoned (empty if it was not)."""
+        out = (ctypes.c_int * 4)()
+        _check(lib.gloo_hip_algorithm_mode(self._h, out))
+        err = lib.gloo_hip_last_error()
+        err = err.decode() if isinstance(err, bytes) else (err or "")
+        return {"device_signal": bool(out[0]), "fine_arena": bool(out[1]), "kernel_copy": bool(out[2]),
+                "graph": bool(out[3]),
+                "graph_error": err[len("graph capture abandoned: "):]
+                if err.startswith("graph capture abandoned: ") else ""}
 
     def close(self):
         if self._h:

@@ -137,4 +137,15 @@ int gloo_hip_algorithm_stats(gloo_hip_algorithm_t a, double* stats) {
   });
 }
 
+int gloo_hip_algorithm_mode(gloo_hip_algorithm_t a, int* mode) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(a && mode, "null argument");
+    mode[0] = a->exec->deviceSignalling() ? 1 : 0;
+    mode[1] = a->exec->fineGrainedArena() ? 1 : 0;
+    mode[2] = a->exec->kernelCopy() ? 1 : 0;
+    mode[3] = a->exec->graphed() ? 1 : 0;
+    gloo_amd::setError(0, a->exec->graphError().empty() ? "" : "graph capture abandoned: " + a->exec->graphError());
+  });
+}
+
 }  // extern "C"

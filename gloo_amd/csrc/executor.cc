@@ -61,6 +61,15 @@ void deviceMove(char* dst, const char* src, size_t bytes, hipStream_t s) {
   }
 }
 
+// Largest message whose wait / body / notify chain is fused into one launch.
+size_t fuseBytes() {
+  static const size_t v = [] {
+    const char* e = std::getenv("GLOO_AMD_FUSE_BYTES");
+    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)(64 << 10);
+  }();
+  return v;
+}
+
 std::set<std::pair<const Context*, uint64_t>>& liveInstances() {
   static std::set<std::pair<const Context*, uint64_t>> s;
   return s;
@@ -90,9 +99,20 @@ Plan planFor(int algo, int rank, int size, size_t count, int nin, int nout, size
 void PlanExecutor::setBuffers(const std::vector<void*>& inputs, const std::vector<void*>& outputs) {
   GLOO_AMD_ENFORCE(inputs.size() == inputs_.size() && outputs.size() == ptrs_.size(),
                    "buffer count differs from the one the algorithm was built for");
+  if (inputs != inputs_ || outputs != ptrs_) {
+    dropGraph();
+    stableRuns_ = 0;
+  }
   inputs_ = inputs;
   ptrs_ = outputs;
   classifyPointers();
+}
+
+void PlanExecutor::dropGraph() {
+  if (!graphExec_) return;
+  if (stream_) (void)hipStreamSynchronize(stream_);
+  (void)hipGraphExecDestroy(graphExec_);
+  graphExec_ = nullptr;
 }
 
 void PlanExecutor::classifyPointers() {
@@ -151,15 +171,33 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     ownStream_ = true;
   }
-  // Baseline every incoming counter before anyone can signal this instance
-  // (instance slots are recycled modulo kMaxLiveInstances).
-  for (const Step& s : plan_.steps)
-    if (s.kind == GLOO_HIP_STEP_WAIT_RECV || s.kind == GLOO_HIP_STEP_WAIT_NOTIFY)
-      consumed_[{s.peer, s.slot}] = ctx_->counter(inst_, s.peer, me, s.slot).load(std::memory_order_acquire);
-
-  for (const Step& s : plan_.steps)
-    if (s.kind == GLOO_HIP_STEP_SEND || s.kind == GLOO_HIP_STEP_NOTIFY)
-      sent_[{s.peer, s.slot}] = ctx_->counter(inst_, me, s.peer, s.slot).load(std::memory_order_acquire);
+  // Baseline every channel before anyone can signal this instance (instance
+  // slots are recycled modulo kMaxLiveInstances), count its messages per
+  // run, and give every step its sequence number (StepSeq).
+  {
+    std::map<std::pair<int, int>, uint64_t> base, perRun, seen;
+    auto isWait = [](int k) { return k == GLOO_HIP_STEP_WAIT_RECV || k == GLOO_HIP_STEP_WAIT_NOTIFY; };
+    auto isSend = [](int k) { return k == GLOO_HIP_STEP_SEND || k == GLOO_HIP_STEP_NOTIFY; };
+    for (const Step& s : plan_.steps) {
+      if (!isWait(s.kind) && !isSend(s.kind)) continue;
+      // waits count the peer->me channel, sends the me->peer one; keep the
+      // two apart in the maps by the sign of the key
+      const std::pair<int, int> key{isWait(s.kind) ? -1 - s.peer : s.peer, s.slot};
+      if (!base.count(key))
+        base[key] = isWait(s.kind) ? ctx_->counter(inst_, s.peer, me, s.slot).load(std::memory_order_acquire)
+                                   : ctx_->counter(inst_, me, s.peer, s.slot).load(std::memory_order_acquire);
+      perRun[key]++;
+    }
+    stepSeq_.resize(plan_.steps.size());
+    for (size_t i = 0; i < plan_.steps.size(); i++) {
+      const Step& s = plan_.steps[i];
+      if (!isWait(s.kind) && !isSend(s.kind)) continue;
+      const std::pair<int, int> key{isWait(s.kind) ? -1 - s.peer : s.peer, s.slot};
+      const uint64_t j = seen[key]++;
+      stepSeq_[i].base = base[key] + j + 1 - perRun[key];
+      stepSeq_[i].perRun = perRun[key];
+    }
+  }
 
   if (P == 1) return;  // no transport: local reduce / broadcast only
 
@@ -257,6 +295,26 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     if (kernelCopy_) {
       GLOO_AMD_HIP_CHECK(hipMalloc(&ticket_, 256));
       GLOO_AMD_HIP_CHECK(hipMemset(ticket_, 0, 256));
+      for (size_t i = 0; i < plan_.steps.size(); i++)
+        if (plan_.steps[i].kind == GLOO_HIP_STEP_SEND) {
+          stepSeq_[i].ticket = ticketsPerRun_;
+          ticketsPerRun_ += copySignalGrid(plan_.steps[i].length * es_, copyBlocks_);
+        }
+    }
+    // Graph replay pays off once a plan has steps that are not fused
+    // one-workgroup launches (measured); "1" / "0" force it.
+    const char* gm = std::getenv("GLOO_AMD_GRAPH");
+    const std::string gmode = gm ? gm : "auto";
+    bool unfused = fuseBytes() == 0;
+    for (const Step& s : plan_.steps)
+      if ((s.kind == GLOO_HIP_STEP_SEND || s.kind == GLOO_HIP_STEP_REDUCE || s.kind == GLOO_HIP_STEP_COPY ||
+           s.kind == GLOO_HIP_STEP_LOCAL_REDUCE || s.kind == GLOO_HIP_STEP_LOCAL_BCAST) &&
+          s.length * es_ > fuseBytes())
+        unfused = true;
+    graphMode_ = gmode == "1" || (gmode == "auto" && unfused);
+    if (graphMode_) {
+      GLOO_AMD_HIP_CHECK(hipMalloc(&epoch_, sizeof(uint64_t)));
+      GLOO_AMD_HIP_CHECK(hipMemset(epoch_, 0, sizeof(uint64_t)));
     }
   }
   ctx_->barrier(strcat_("inst", inst_, "/ready"));
@@ -273,6 +331,8 @@ PlanExecutor::~PlanExecutor() {
       if (arena_) (void)hipFree(arena_);
     }
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+    if (graphExec_) (void)hipGraphExecDestroy(graphExec_);
+    if (epoch_) (void)hipFree(epoch_);
     if (ticket_) (void)hipFree(ticket_);
     for (char* p : outStage_)
       if (p) (void)hipFree(p);
@@ -306,40 +366,110 @@ void PlanExecutor::waitCounter(std::atomic<uint64_t>& c, uint64_t target, int pe
   waitSeconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+Seq PlanExecutor::seqOf(size_t i, uint64_t r, bool graph) const {
+  const StepSeq& q = stepSeq_[i];
+  return graph ? Seq{q.base, q.perRun} : Seq{q.base + r * q.perRun, 0};
+}
+
+Seq PlanExecutor::ticketOf(size_t i, uint64_t r, bool graph) const {
+  const uint64_t base = (uint64_t)stepSeq_[i].ticket - ticketsPerRun_;
+  return graph ? Seq{base, ticketsPerRun_} : Seq{base + r * ticketsPerRun_, 0};
+}
+
 void PlanExecutor::run() {
   GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
   const int me = ctx_->rank;
-  const uint64_t timeoutTicks = (uint64_t)ctx_->timeout().count() * 100000ull;  // 100 MHz realtime clock
-  auto signal = [&](int peer, int slot) {
-    const uint64_t seq = ++sent_[{peer, slot}];
-    if (deviceSignal_) {
-      GLOO_AMD_HIP_CHECK(launchSignal(ctx_->counterDevicePtr(inst_, me, peer, slot), seq, stream_));
-    } else {
-      enqueueBump(stream_, ctx_->counter(inst_, me, peer, slot));
-    }
-  };
   if (deviceSignal_ && ctx_->errorWord(me).load() != 0)
     throw IoException(strcat_("rank ", me, ": a device-side wait of a previous run timed out"));
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  GLOO_AMD_HIP_CHECK(hipStreamIsCapturing(stream_, &cs));
+  GLOO_AMD_ENFORCE(cs == hipStreamCaptureStatusNone,
+                   "run() on a stream under capture: the executor captures and replays its own graph");
   waitSeconds_ = 0;
   reduceSeconds_ = reduceBytes_ = 0;
   reduceCount_ = 0;
-  size_t ev = 0;
+  const uint64_t r = runs_ + 1;
+  const bool graphable = deviceSignal_ && graphMode_ && !profiling_;
+  if (graphable && !graphExec_ && stableRuns_ >= 1) tryCapture(r);
+  if (graphable && graphExec_) {
+    GLOO_AMD_HIP_CHECK(hipGraphLaunch(graphExec_, stream_));
+  } else {
+    enqueue(r, false);
+  }
+  runs_ = r;
+  stableRuns_++;
+  if (ownStream_ || profiling_) {
+    const auto t0 = std::chrono::steady_clock::now();
+    GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (deviceSignal_) waitSeconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (deviceSignal_ && ctx_->errorWord(me).exchange(0) != 0)
+      throw IoException(strcat_("Timed out on rank ", me, " waiting for a peer (device-side wait, ",
+                                ctx_->timeout().count(), " ms)"));
+  }
+  for (size_t i = 0; profiling_ && i + 1 < evUsed_; i += 2) {
+    float ms = 0;
+    GLOO_AMD_HIP_CHECK(hipEventElapsedTime(&ms, events_[i], events_[i + 1]));
+    reduceSeconds_ += ms * 1e-3;
+  }
+}
+
+void PlanExecutor::tryCapture(uint64_t r) {
+  // The device epoch holds the number of runs already executed; the graph's
+  // first node advances it, and every node derives its sequence numbers
+  // from it.  Capture failures are not fatal: the plan keeps being enqueued
+  // eagerly (graphError() says why).
+  GLOO_AMD_HIP_CHECK(launchEpochSet(epoch_, r - 1, stream_));
+  GLOO_AMD_HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+  hipGraph_t g = nullptr;
+  try {
+    GLOO_AMD_HIP_CHECK(launchEpochBump(epoch_, stream_));
+    enqueue(r, true);
+  } catch (const std::exception& ex) {
+    (void)hipStreamEndCapture(stream_, &g);
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    graphMode_ = false;
+    graphError_ = ex.what();
+    return;
+  }
+  hipError_t e = hipStreamEndCapture(stream_, &g);
+  if (e == hipSuccess) e = hipGraphInstantiate(&graphExec_, g, nullptr, nullptr, 0);
+  if (g) (void)hipGraphDestroy(g);
+  if (e != hipSuccess) {
+    graphExec_ = nullptr;
+    graphMode_ = false;
+    graphError_ = hipGetErrorString(e);
+    (void)hipGetLastError();
+  }
+}
+
+void PlanExecutor::enqueue(uint64_t r, bool graph) {
+  const int me = ctx_->rank;
+  const uint64_t timeoutTicks = (uint64_t)ctx_->timeout().count() * 100000ull;  // 100 MHz realtime clock
+  const uint64_t* epoch = graph ? epoch_ : nullptr;
+  auto signal = [&](size_t i) {
+    const Step& s = plan_.steps[i];
+    if (deviceSignal_) {
+      GLOO_AMD_HIP_CHECK(launchSignal(ctx_->counterDevicePtr(inst_, me, s.peer, s.slot), seqOf(i, r, graph), epoch,
+                                      stream_));
+    } else {
+      enqueueBump(stream_, ctx_->counter(inst_, me, s.peer, s.slot));
+    }
+  };
+  evUsed_ = 0;
   auto event = [&]() {
-    if (ev == events_.size()) {
+    if (evUsed_ == events_.size()) {
       hipEvent_t e;
       GLOO_AMD_HIP_CHECK(hipEventCreate(&e));
       events_.push_back(e);
     }
-    return events_[ev++];
+    return events_[evUsed_++];
   };
   // Small-message fusion (device signalling only): a plan's
   //   WAIT_* -> {REDUCE | COPY | SEND} -> [NOTIFY]   or a lone small SEND
   // becomes ONE one-workgroup launch (launchFusedSmall): below a few KiB a
   // hop costs dispatches, not bytes.  Off while profiling reduce kernels.
-  static const size_t kFuseBytes = [] {
-    const char* e = std::getenv("GLOO_AMD_FUSE_BYTES");
-    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)(64 << 10);
-  }();
+  const size_t kFuseBytes = fuseBytes();
   const bool fuse = deviceSignal_ && !profiling_ && kFuseBytes > 0;
   auto userOrArena = [&](bool arena) { return arena ? arena_ : userPtr(0); };
   const std::vector<Step>& steps = plan_.steps;
@@ -369,25 +499,25 @@ void PlanExecutor::run() {
         const bool overlap = dst < src + bytes && src < dst + bytes && dst != src;
         if (!(t->kind == GLOO_HIP_STEP_COPY && overlap)) {
           const uint64_t* wf = nullptr;
-          uint64_t wt = 0;
+          Seq wt;
           if (isWait) {
-            wt = ++consumed_[{s.peer, s.slot}];
+            wt = seqOf(i, r, graph);
             wf = ctx_->counterDevicePtr(inst_, s.peer, me, s.slot);
           }
           uint64_t* sf = nullptr;
-          uint64_t sv = 0;
+          Seq sv;
           size_t consumed = isWait ? 2 : 1;
           if (t->kind == GLOO_HIP_STEP_SEND) {
-            sv = ++sent_[{t->peer, t->slot}];
+            sv = seqOf(isWait ? i + 1 : i, r, graph);
             sf = ctx_->counterDevicePtr(inst_, me, t->peer, t->slot);
           } else if (isWait && i + 2 < steps.size() && steps[i + 2].kind == GLOO_HIP_STEP_NOTIFY) {
             const Step& nt = steps[i + 2];
-            sv = ++sent_[{nt.peer, nt.slot}];
+            sv = seqOf(i + 2, r, graph);
             sf = ctx_->counterDevicePtr(inst_, me, nt.peer, nt.slot);
             consumed = 3;
           }
           checkRc(launchFusedSmall(op, dtype_, dst, src, t->length, wf, wt, timeoutTicks, ctx_->errorWordDevicePtr(me),
-                                   sf, sv, stream_),
+                                   sf, sv, epoch, stream_),
                   "fused step");
           i += consumed - 1;
           continue;
@@ -401,26 +531,23 @@ void PlanExecutor::run() {
         char* dst = peers_[s.peer].base + (remoteRegion_[{s.peer, s.slot}] + s.dst_off) * es_;
         const char* src = (s.flags & GLOO_HIP_SRC_ARENA ? arena_ : userPtr(0)) + s.src_off * es_;
         if (kernelCopy_) {
-          const uint64_t seq = ++sent_[{s.peer, s.slot}];
           const unsigned grid = copySignalGrid(s.length * es_, copyBlocks_);
-          checkRc(launchCopySignal(dst, src, s.length * es_, ctx_->counterDevicePtr(inst_, me, s.peer, s.slot), seq,
-                                   ticket_, ticketNext_, grid, stream_),
+          checkRc(launchCopySignal(dst, src, s.length * es_, ctx_->counterDevicePtr(inst_, me, s.peer, s.slot),
+                                   seqOf(i, r, graph), ticket_, ticketOf(i, r, graph), epoch, grid, stream_),
                   "copy_signal_kernel");
-          ticketNext_ += grid;
           break;
         }
         if (s.length) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(dst, src, s.length * es_, hipMemcpyDeviceToDevice, stream_));
-        signal(s.peer, s.slot);
+        signal(i);
         break;
       }
       case GLOO_HIP_STEP_WAIT_RECV:
       case GLOO_HIP_STEP_WAIT_NOTIFY: {
-        const uint64_t target = ++consumed_[{s.peer, s.slot}];
         if (deviceSignal_) {
-          GLOO_AMD_HIP_CHECK(launchWait(ctx_->counterDevicePtr(inst_, s.peer, me, s.slot), target, timeoutTicks,
-                                        ctx_->errorWordDevicePtr(me), stream_));
+          GLOO_AMD_HIP_CHECK(launchWait(ctx_->counterDevicePtr(inst_, s.peer, me, s.slot), seqOf(i, r, graph), epoch,
+                                        timeoutTicks, ctx_->errorWordDevicePtr(me), stream_));
         } else {
-          waitCounter(ctx_->counter(inst_, s.peer, me, s.slot), target, s.peer, s.slot);
+          waitCounter(ctx_->counter(inst_, s.peer, me, s.slot), seqOf(i, r, false).base, s.peer, s.slot);
         }
         break;
       }
@@ -442,7 +569,7 @@ void PlanExecutor::run() {
         break;
       }
       case GLOO_HIP_STEP_NOTIFY:
-        signal(s.peer, s.slot);
+        signal(i);
         break;
       case GLOO_HIP_STEP_WAIT_SEND:
         // stream order already puts every later use of the buffer after the
@@ -494,19 +621,6 @@ void PlanExecutor::run() {
       default:
         throw EnforceNotMet(strcat_("unknown plan step ", s.kind));
     }
-  }
-  if (ownStream_ || profiling_) {
-    const auto t0 = std::chrono::steady_clock::now();
-    GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
-    if (deviceSignal_) waitSeconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (deviceSignal_ && ctx_->errorWord(me).exchange(0) != 0)
-      throw IoException(strcat_("Timed out on rank ", me, " waiting for a peer (device-side wait, ",
-                                ctx_->timeout().count(), " ms)"));
-  }
-  for (size_t i = 0; profiling_ && i + 1 < ev; i += 2) {
-    float ms = 0;
-    GLOO_AMD_HIP_CHECK(hipEventElapsedTime(&ms, events_[i], events_[i + 1]));
-    reduceSeconds_ += ms * 1e-3;
   }
 }
 

@@ -36,6 +36,7 @@
 
 #include "gloo_amd.h"
 #include "gloo_amd/errors.h"
+#include "gloo_amd/signal.h"
 
 namespace gloo_amd {
 namespace {
@@ -326,11 +327,12 @@ constexpr int kFusedBlock = 512;
 template <class Tr, int OP>
 __global__ __launch_bounds__(kFusedBlock) void fused_small_kernel(
     typename Tr::Storage* dst, const typename Tr::Storage* src, size_t n, const uint64_t* waitFlag,
-    uint64_t waitTarget, uint64_t timeoutTicks, uint32_t* err, uint64_t* sigFlag, uint64_t sigValue) {
+    Seq wait, uint64_t timeoutTicks, uint32_t* err, uint64_t* sigFlag, Seq sig, const uint64_t* epoch) {
   __shared__ int ok;
   if (threadIdx.x == 0) {
     int good = 1;
     if (waitFlag) {
+      const uint64_t waitTarget = epoch ? wait.base + *epoch * wait.perRun : wait.base;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load(waitFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < waitTarget) {
         __builtin_amdgcn_s_sleep(4);
@@ -354,6 +356,7 @@ __global__ __launch_bounds__(kFusedBlock) void fused_small_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
+      const uint64_t sigValue = epoch ? sig.base + *epoch * sig.perRun : sig.base;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(sigFlag, sigValue, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -362,17 +365,17 @@ __global__ __launch_bounds__(kFusedBlock) void fused_small_kernel(
 }
 
 template <class Tr>
-int launch_fused(int op, void* dst, const void* src, size_t n, const uint64_t* wf, uint64_t wt, uint64_t tt,
-                 uint32_t* err, uint64_t* sf, uint64_t sv, hipStream_t s) {
+int launch_fused(int op, void* dst, const void* src, size_t n, const uint64_t* wf, Seq wt, uint64_t tt,
+                 uint32_t* err, uint64_t* sf, Seq sv, const uint64_t* ep, hipStream_t s) {
   using S = typename Tr::Storage;
   S* d = static_cast<S*>(dst);
   const S* x = static_cast<const S*>(src);
   switch (op) {
-    case 0: fused_small_kernel<Tr, 0><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv); break;
-    case GLOO_HIP_SUM: fused_small_kernel<Tr, GLOO_HIP_SUM><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv); break;
-    case GLOO_HIP_PRODUCT: fused_small_kernel<Tr, GLOO_HIP_PRODUCT><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv); break;
-    case GLOO_HIP_MAX: fused_small_kernel<Tr, GLOO_HIP_MAX><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv); break;
-    case GLOO_HIP_MIN: fused_small_kernel<Tr, GLOO_HIP_MIN><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv); break;
+    case 0: fused_small_kernel<Tr, 0><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv, ep); break;
+    case GLOO_HIP_SUM: fused_small_kernel<Tr, GLOO_HIP_SUM><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv, ep); break;
+    case GLOO_HIP_PRODUCT: fused_small_kernel<Tr, GLOO_HIP_PRODUCT><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv, ep); break;
+    case GLOO_HIP_MAX: fused_small_kernel<Tr, GLOO_HIP_MAX><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv, ep); break;
+    case GLOO_HIP_MIN: fused_small_kernel<Tr, GLOO_HIP_MIN><<<1, kFusedBlock, 0, s>>>(d, x, n, wf, wt, tt, err, sf, sv, ep); break;
     default: return GLOO_HIP_EINVAL_OP;
   }
   return GLOO_HIP_OK;
@@ -392,8 +395,8 @@ constexpr int kCopyBlock = 512;
 constexpr int kCopyUnroll = 2;
 
 __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(
-    char* dst, const char* src, size_t bytes, uint64_t* flag, uint64_t seq, unsigned* ticket,
-    unsigned ticketBase) {
+    char* dst, const char* src, size_t bytes, uint64_t* flag, Seq seqv, unsigned* ticket, Seq ticketv,
+    const uint64_t* epoch) {
   // dst head up to a 16-B boundary and the ragged tail: block 0, bytewise
   const size_t head = ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) < bytes
                           ? ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) : bytes;
@@ -422,10 +425,12 @@ __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t ep = epoch ? *epoch : 0;
+    const unsigned ticketBase = (unsigned)(ticketv.base + ep * ticketv.perRun);
     const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
     if (t == ticketBase + gridDim.x - 1) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(flag, seqv.base + ep * seqv.perRun, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -575,29 +580,29 @@ unsigned copySignalGrid(size_t bytes, unsigned maxBlocks) {
   return (unsigned)(g == 0 ? 1 : g);
 }
 
-int launchCopySignal(void* dst, const void* src, size_t bytes, uint64_t* flag, uint64_t seq, unsigned* ticket,
-                     unsigned ticketBase, unsigned grid, hipStream_t s) {
+int launchCopySignal(void* dst, const void* src, size_t bytes, uint64_t* flag, Seq seq, unsigned* ticket,
+                     Seq ticketv, const uint64_t* epoch, unsigned grid, hipStream_t s) {
   copy_signal_kernel<<<grid, kCopyBlock, 0, s>>>(static_cast<char*>(dst), static_cast<const char*>(src), bytes,
-                                                 flag, seq, ticket, ticketBase);
+                                                 flag, seq, ticket, ticketv, epoch);
   return check_launch("copy_signal_kernel");
 }
 
 // Internal entry for the plan executor (see gloo_amd/signal.h).
 int launchFusedSmall(int op, int dtype, void* dst, const void* src, size_t n, const uint64_t* waitFlag,
-                     uint64_t waitTarget, uint64_t timeoutTicks, uint32_t* err, uint64_t* sigFlag,
-                     uint64_t sigValue, hipStream_t s) {
+                     Seq waitTarget, uint64_t timeoutTicks, uint32_t* err, uint64_t* sigFlag, Seq sigValue,
+                     const uint64_t* epoch, hipStream_t s) {
   int rc;
   switch (dtype) {
-    case GLOO_HIP_I8: rc = launch_fused<TrI8>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
-    case GLOO_HIP_U8: rc = launch_fused<TrU8>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
-    case GLOO_HIP_I32: rc = launch_fused<TrI32>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
-    case GLOO_HIP_U32: rc = launch_fused<TrU32>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
-    case GLOO_HIP_I64: rc = launch_fused<TrI64>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
-    case GLOO_HIP_U64: rc = launch_fused<TrU64>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
-    case GLOO_HIP_F16: rc = launch_fused<TrF16>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
-    case GLOO_HIP_BF16: rc = launch_fused<TrBF16>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
-    case GLOO_HIP_F32: rc = launch_fused<TrF32>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
-    case GLOO_HIP_F64: rc = launch_fused<TrF64>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, s); break;
+    case GLOO_HIP_I8: rc = launch_fused<TrI8>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, epoch, s); break;
+    case GLOO_HIP_U8: rc = launch_fused<TrU8>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, epoch, s); break;
+    case GLOO_HIP_I32: rc = launch_fused<TrI32>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, epoch, s); break;
+    case GLOO_HIP_U32: rc = launch_fused<TrU32>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, epoch, s); break;
+    case GLOO_HIP_I64: rc = launch_fused<TrI64>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, epoch, s); break;
+    case GLOO_HIP_U64: rc = launch_fused<TrU64>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, epoch, s); break;
+    case GLOO_HIP_F16: rc = launch_fused<TrF16>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, epoch, s); break;
+    case GLOO_HIP_BF16: rc = launch_fused<TrBF16>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, epoch, s); break;
+    case GLOO_HIP_F32: rc = launch_fused<TrF32>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, epoch, s); break;
+    case GLOO_HIP_F64: rc = launch_fused<TrF64>(op, dst, src, n, waitFlag, waitTarget, timeoutTicks, err, sigFlag, sigValue, epoch, s); break;
     default: return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
   }
   if (rc != GLOO_HIP_OK) return set_error(rc, "fused step: bad op");

@@ -6,19 +6,30 @@
 namespace gloo_amd {
 namespace {
 
-__global__ __launch_bounds__(64) void signal_kernel(uint64_t* flag, uint64_t value) {
+__device__ __forceinline__ uint64_t seqValue(uint64_t base, uint64_t perRun, const uint64_t* epoch) {
+  return epoch ? base + *epoch * perRun : base;
+}
+
+__global__ __launch_bounds__(64) void epoch_kernel(uint64_t* epoch, int set, uint64_t value) {
+  if (threadIdx.x == 0) *epoch = set ? value : *epoch + 1;
+}
+
+__global__ __launch_bounds__(64) void signal_kernel(uint64_t* flag, uint64_t base, uint64_t perRun,
+                                                    const uint64_t* epoch) {
   if (threadIdx.x == 0) {
     // every write that precedes this kernel on the stream (the chunk copy,
     // the reduction that consumed an inbox) is performed at system scope
     // before the flag can be observed
+    const uint64_t v = seqValue(base, perRun, epoch);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
-__global__ __launch_bounds__(64) void wait_kernel(const uint64_t* flag, uint64_t target, uint64_t timeout_ticks,
-                                                  uint32_t* err) {
+__global__ __launch_bounds__(64) void wait_kernel(const uint64_t* flag, uint64_t base, uint64_t perRun,
+                                                  const uint64_t* epoch, uint64_t timeout_ticks, uint32_t* err) {
   if (threadIdx.x != 0) return;
+  const uint64_t target = seqValue(base, perRun, epoch);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   // relaxed polls, ONE acquire after the match (an acquire per poll would
   // invalidate the caches on every iteration)
@@ -34,14 +45,24 @@ __global__ __launch_bounds__(64) void wait_kernel(const uint64_t* flag, uint64_t
 
 }  // namespace
 
-hipError_t launchSignal(uint64_t* flag, uint64_t value, hipStream_t stream) {
-  signal_kernel<<<1, 64, 0, stream>>>(flag, value);
+hipError_t launchEpochBump(uint64_t* epoch, hipStream_t stream) {
+  epoch_kernel<<<1, 64, 0, stream>>>(epoch, 0, 0);
   return hipGetLastError();
 }
 
-hipError_t launchWait(const uint64_t* flag, uint64_t target, uint64_t timeoutTicks, uint32_t* err,
-                      hipStream_t stream) {
-  wait_kernel<<<1, 64, 0, stream>>>(flag, target, timeoutTicks, err);
+hipError_t launchEpochSet(uint64_t* epoch, uint64_t value, hipStream_t stream) {
+  epoch_kernel<<<1, 64, 0, stream>>>(epoch, 1, value);
+  return hipGetLastError();
+}
+
+hipError_t launchSignal(uint64_t* flag, Seq value, const uint64_t* epoch, hipStream_t stream) {
+  signal_kernel<<<1, 64, 0, stream>>>(flag, value.base, value.perRun, epoch);
+  return hipGetLastError();
+}
+
+hipError_t launchWait(const uint64_t* flag, Seq target, const uint64_t* epoch, uint64_t timeoutTicks,
+                      uint32_t* err, hipStream_t stream) {
+  wait_kernel<<<1, 64, 0, stream>>>(flag, target.base, target.perRun, epoch, timeoutTicks, err);
   return hipGetLastError();
 }
 

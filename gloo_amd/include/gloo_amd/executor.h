@@ -26,6 +26,14 @@
 // sequence numbers, so they interoperate.  GLOO_AMD_SIGNAL=host|device
 // overrides the choice.
 //
+// hipGraph replay (device signalling, GLOO_AMD_GRAPH=1, the default): once a
+// plan has run with the same buffers, the next run() captures the whole
+// enqueue — epoch bump, waits, copies, reductions, signals — into a hipGraph
+// and every later run() is ONE hipGraphLaunch.  Sequence numbers are
+// replayable (signal.h: base + epoch * perRun with a device-side run epoch),
+// so the graph never needs its kernel arguments updated.  New buffers
+// (setBuffers) drop the graph; profiling runs are enqueued eagerly.
+//
 // Copy engine of a SEND (device signalling): hipMemcpyAsync + signal kernel
 // (default), or GLOO_AMD_COPY=kernel: copy_signal_kernel, one launch that
 // copies with GLOO_AMD_COPY_BLOCKS workgroups (default 64) and publishes the
@@ -35,12 +43,14 @@
 #include <hip/hip_runtime_api.h>
 
 #include <map>
+#include <string>
 #include <memory>
 #include <utility>
 #include <vector>
 
 #include "gloo_amd/context.h"
 #include "gloo_amd/plan.h"
+#include "gloo_amd/signal.h"
 
 namespace gloo_amd {
 
@@ -68,6 +78,10 @@ class PlanExecutor {
   bool deviceSignalling() const { return deviceSignal_; }
   bool fineGrainedArena() const { return fineArena_; }
   bool kernelCopy() const { return kernelCopy_; }
+  // True once run() replays a captured hipGraph.
+  bool graphed() const { return graphExec_ != nullptr; }
+  // Why graph capture was abandoned (empty if it was not).
+  const std::string& graphError() const { return graphError_; }
   // Host time spent blocked in WAIT steps during the last run(), seconds.
   double lastWaitSeconds() const { return waitSeconds_; }
   // When enabled, every REDUCE of run() is bracketed by HIP events; after the
@@ -85,6 +99,13 @@ class PlanExecutor {
     int device = -1;
   };
   void waitCounter(std::atomic<uint64_t>& c, uint64_t target, int peer, int slot);
+  // Enqueue run `r` (1-based) of the plan.  graph: sequence numbers read the
+  // device epoch (a capture); otherwise they are computed on the host.
+  void enqueue(uint64_t r, bool graph);
+  void tryCapture(uint64_t r);
+  void dropGraph();
+  Seq seqOf(size_t step, uint64_t r, bool graph) const;
+  Seq ticketOf(size_t step, uint64_t r, bool graph) const;
   char* userPtr(int j) const { return static_cast<char*>(ptrs_[j]); }
 
   std::shared_ptr<Context> ctx_;
@@ -110,17 +131,31 @@ class PlanExecutor {
   bool ownStream_ = false;
   std::vector<Peer> peers_;
   std::map<std::pair<int, int>, uint64_t> remoteRegion_;  // (peer, slot) -> elts into peer arena
-  std::map<std::pair<int, int>, uint64_t> consumed_;      // (src, slot) -> counter value consumed
-  std::map<std::pair<int, int>, uint64_t> sent_;          // (dst, slot) -> last sequence signalled
+  // Sequence numbers.  Channel (peer, slot) carries perRun messages per run;
+  // the j-th message of run r on it has number
+  //   baseline + (r - 1) * perRun + j + 1 = base + r * perRun
+  // with base = baseline + j + 1 - perRun precomputed per step (StepSeq).
+  struct StepSeq {
+    uint64_t base = 0, perRun = 0;
+    uint32_t ticket = 0;  // kernel-copy SEND: first ticket within the run
+  };
+  std::vector<StepSeq> stepSeq_;
+  uint32_t ticketsPerRun_ = 0;
+  uint64_t runs_ = 0;          // runs enqueued so far
+  uint64_t* epoch_ = nullptr;  // device: the run being executed (graph replay)
+  hipGraphExec_t graphExec_ = nullptr;
+  bool graphMode_ = false;
+  uint64_t stableRuns_ = 0;    // runs since the buffers last changed
+  std::string graphError_;
   bool deviceSignal_ = false;  // stream-ordered signal/wait kernels instead of host waits
   bool fineArena_ = false;     // inbox arena in fine-grained (cross-device coherent) memory
   bool kernelCopy_ = false;    // SEND = copy_signal_kernel instead of hipMemcpyAsync + signal
   unsigned copyBlocks_ = 64;
   unsigned* ticket_ = nullptr; // completion tickets of copy_signal_kernel (device memory)
-  unsigned ticketNext_ = 0;
   double waitSeconds_ = 0;
   bool profiling_ = false;
   std::vector<hipEvent_t> events_;
+  size_t evUsed_ = 0;
   double reduceSeconds_ = 0, reduceBytes_ = 0;
   size_t reduceCount_ = 0;
 };

@@ -1,15 +1,23 @@
 // signal.h — stream-ordered cross-rank signalling kernels (internal).
 //
 // A rank's chunk exchange is a sequence of (copy, signal) on the sender's
-// stream and (wait, reduce) on the receiver's stream.  These two one-wave
-// kernels make both ends stream-ordered, so a whole plan is enqueued without
-// host round trips:
+// stream and (wait, reduce) on the receiver's stream.  These kernels make
+// both ends stream-ordered, so a whole plan is enqueued — and captured into
+// a hipGraph — without host round trips:
 //   signal: system-scope release, then the flag word := value
-//   wait:   poll the flag (system-scope acquire) until >= target, sleeping
-//           between polls; give up after `timeout_ticks` of the 100 MHz
-//           realtime counter and set *err (the host raises IoException).
+//   wait:   poll the flag (relaxed) until >= target, sleeping between polls;
+//           ONE system-scope acquire after the match; give up after
+//           `timeoutTicks` of the 100 MHz realtime counter and set *err (the
+//           host raises IoException).
 // Flags are 64-bit counters in the node's shared control block, registered
 // with hipHostRegister so every GPU of every rank can address them.
+//
+// Replayable sequence numbers: every value a kernel waits for or writes is
+//   Seq{base, perRun}.value(epoch) = base + epoch * perRun   (mod 2^64)
+// where `epoch` is the rank-local run counter in device memory that the
+// first node of each run increments (launchEpochBump).  A captured plan can
+// therefore be replayed unchanged: run r computes its own targets.  With a
+// null epoch pointer the value is `base` (host-computed).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -18,23 +26,32 @@
 
 namespace gloo_amd {
 
-hipError_t launchSignal(uint64_t* flag, uint64_t value, hipStream_t stream);
-hipError_t launchWait(const uint64_t* flag, uint64_t target, uint64_t timeoutTicks, uint32_t* err,
-                      hipStream_t stream);
+struct Seq {
+  uint64_t base = 0;
+  uint64_t perRun = 0;
+};
+
+hipError_t launchEpochBump(uint64_t* epoch, hipStream_t stream);            // *epoch += 1
+hipError_t launchEpochSet(uint64_t* epoch, uint64_t value, hipStream_t stream);  // *epoch = value
+hipError_t launchSignal(uint64_t* flag, Seq value, const uint64_t* epoch, hipStream_t stream);
+hipError_t launchWait(const uint64_t* flag, Seq target, const uint64_t* epoch, uint64_t timeoutTicks,
+                      uint32_t* err, hipStream_t stream);
 
 // One-workgroup fused step for small messages (reduce.hip): optionally wait
-// for `waitFlag >= waitTarget`, then dst[i] = dst[i] op src[i] (op 0: copy),
-// then optionally signal `*sigFlag = sigValue`.  Returns a gloo_hip status.
-int launchFusedSmall(int op, int dtype, void* dst, const void* src, size_t n, const uint64_t* waitFlag,
-                     uint64_t waitTarget, uint64_t timeoutTicks, uint32_t* err, uint64_t* sigFlag,
-                     uint64_t sigValue, hipStream_t stream);
+// for `*waitFlag >= wait`, then dst[i] = dst[i] op src[i] (op 0: copy), then
+// optionally signal `*sigFlag = sig`.  Returns a gloo_hip status.
+int launchFusedSmall(int op, int dtype, void* dst, const void* src, size_t n, const uint64_t* waitFlag, Seq wait,
+                     uint64_t timeoutTicks, uint32_t* err, uint64_t* sigFlag, Seq sig, const uint64_t* epoch,
+                     hipStream_t stream);
 
 // Peer copy + fused arrival signal (reduce.hip): `grid` workgroups copy
 // `bytes` from src (local) to dst (a peer's inbox); the workgroup that takes
-// ticket ticketBase + grid - 1 publishes *flag = seq.  copySignalGrid() sizes
-// the grid (capped at maxBlocks: a link, not HBM, bounds a peer copy).
+// the launch's last ticket publishes *flag = seq.  Tickets are 32-bit and
+// only grow: this launch's first ticket is ticket.value(epoch) (mod 2^32).
+// copySignalGrid() sizes the grid (capped at maxBlocks: a link, not HBM,
+// bounds a peer copy).
 unsigned copySignalGrid(size_t bytes, unsigned maxBlocks);
-int launchCopySignal(void* dst, const void* src, size_t bytes, uint64_t* flag, uint64_t seq, unsigned* ticket,
-                     unsigned ticketBase, unsigned grid, hipStream_t stream);
+int launchCopySignal(void* dst, const void* src, size_t bytes, uint64_t* flag, Seq seq, unsigned* ticketCounter,
+                     Seq ticket, const uint64_t* epoch, unsigned grid, hipStream_t stream);
 
 }  // namespace gloo_amd

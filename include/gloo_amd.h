@@ -238,6 +238,12 @@ double gloo_hip_algorithm_wait_seconds(gloo_hip_algorithm_t algo);
 int gloo_hip_algorithm_set_profiling(gloo_hip_algorithm_t algo, int on);
 int gloo_hip_algorithm_stats(gloo_hip_algorithm_t algo, double* stats4);
 
+/* How the algorithm executes (no reference counterpart; for tests and
+ * tools): mode4[0] = device-side signalling, [1] = fine-grained inbox arena,
+ * [2] = kernel copy engine, [3] = run() replays a captured hipGraph.  If graph
+ * capture was abandoned, gloo_hip_last_error() says why. */
+int gloo_hip_algorithm_mode(gloo_hip_algorithm_t algo, int* mode4);
+
 /* ------------------------------------------------------------------------
  * New-style function API: gloo::allreduce(const AllreduceOptions&)
  * (gloo/allreduce.h:89-193, gloo/allreduce.cc:97-145), RING algorithm.

@@ -10,6 +10,7 @@ Expected values: tests/golden/sched_golden.npz (the reference's own
 AllreduceRingChunked / HalvingDoubling / Ring / ReduceScatter outputs) and the
 closed-form fixture of gloo/test/base_test.h:184-236.
 """
+import json
 import os
 import subprocess
 import sys
@@ -428,3 +429,118 @@ def test_multi_pointer_across_gpus(torch, golden_sched):
     ctx.close()
     for b in bufs:
         assert same_bytes(b.cpu().numpy(), want)
+
+
+GRAPH_WORKER = r'''
+import os, sys, json, numpy as np
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, size, store, case, out, runs = (int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5],
+                                      int(sys.argv[6]))
+g = np.load(os.path.join(os.environ["GLOO_AMD_ROOT"], "tests", "golden", "sched_golden.npz"))
+algo, op, dtype = case.split("/")[:3]
+x = g[case + "/in"]
+recv = g[case + "/recv"] if algo == "reduce_scatter" else None
+xr = x[rank] if algo == "reduce_scatter" else x[rank, 0]
+torch.cuda.set_device(0)
+src = torch.from_numpy(xr.view(np.uint8).copy()).to("cuda:0")
+buf = torch.empty_like(src)
+ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=60000)
+a = gloo_amd.Algorithm(ctx, algo, op, dtype, [buf.data_ptr()], xr.size, recv_elems=recv)
+modes = []
+for it in range(runs):
+    buf.copy_(src)
+    torch.cuda.synchronize()
+    a.run()
+    modes.append(a.mode())
+    np.save(out + f".{it}.npy", buf.cpu().numpy().view(xr.dtype))
+a.close(); ctx.close()
+print("MODES", json.dumps(modes))
+'''
+
+
+@pytest.mark.parametrize("case,env,graph", [
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, True),  # fused small steps in the graph
+    ("halving_doubling/sum/f32/P8/k1/n1000", {"GLOO_AMD_GRAPH": "1"}, True),
+    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_FUSE_BYTES": "0"}, True),   # auto: unfused steps
+    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0", "GLOO_AMD_COPY": "kernel"}, True),
+    ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_COPY": "kernel",
+                                          "GLOO_AMD_COPY_BLOCKS": "3"}, True),
+    ("reduce_scatter/max/bf16/P8/n4096", {"GLOO_AMD_GRAPH": "1"}, True),
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "1024"}, True),  # mixed fused/unfused
+    ("halving_doubling/sum/f32/P5/k1/n10007", {}, False),  # auto: every step fused -> eager is faster
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_FUSE_BYTES": "0"}, False),
+    ("ring_chunked/sum/f32/P3/k1/n1000", {"GLOO_AMD_SIGNAL": "host", "GLOO_AMD_GRAPH": "1"}, False),
+])
+def test_processes_graph_replay(torch, golden_sched, case, env, graph):
+    """hipGraph replay: run 1 is enqueued eagerly, run 2 captures the plan and
+    runs 3.. replay it; sequence numbers come from the device run epoch.  The
+    buffer is reset to the input before every run, so every run must equal
+    the reference's output byte for byte."""
+    algo = case.split("/")[0]
+    P = int(case.split("/")[3][1:])
+    runs = 5
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(GRAPH_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), case,
+                                   os.path.join(d, f"o{r}"), str(runs)], env=e, stdout=subprocess.PIPE, text=True)
+                 for r in range(P)]
+        outs = [p.communicate(timeout=300)[0] for p in procs]
+        assert [p.returncode for p in procs] == [0] * P
+        ys = [[np.load(os.path.join(d, f"o{r}.{it}.npy")) for it in range(runs)] for r in range(P)]
+    want = golden_sched[case + "/out"]
+    for it in range(runs):
+        if algo == "reduce_scatter":
+            recv = golden_sched[case + "/recv"]
+            assert same_bytes(np.concatenate([ys[r][it][:recv[r]] for r in range(P)]), want), it
+        else:
+            for r in range(P):
+                assert same_bytes(ys[r][it], want), (r, it)
+    for r in range(P):
+        modes = json.loads(outs[r].split("MODES", 1)[1])
+        assert not modes[0]["graph"]
+        assert [m["graph"] for m in modes[1:]] == [graph] * (runs - 1), modes
+        assert modes[-1]["graph_error"] == "", modes[-1]
+
+
+NEW_STYLE_GRAPH_WORKER = r'''
+import os, sys, numpy as np
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, size, store, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+n = 400_000
+torch.cuda.set_device(0)
+ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=60000)
+sets = [[torch.empty(n, device="cuda:0") for _ in range(2)] for _ in range(2)]
+res = []
+for it, s in enumerate([0, 0, 0, 1, 1, 0, 1, 0, 0]):
+    ins, outs = sets[s]
+    ins.copy_(torch.arange(n, device="cuda:0", dtype=torch.float32) * 0 + (rank + 1) * (it + 1))
+    outs.fill_(-1)
+    torch.cuda.synchronize()
+    gloo_amd.allreduce(ctx, [outs.data_ptr()], n, "f32", "sum", inputs=[ins.data_ptr()])
+    res.append(outs.cpu().numpy())
+ctx.close()
+np.save(out, np.array(res))
+'''
+
+
+def test_processes_new_style_rebinding_graph(torch):
+    """Function-style allreduce (1.6 MB per rank: unfused steps, so the plan
+    is captured) called with alternating buffer sets: every rebinding drops
+    the captured graph, the next steady call re-captures it.
+    Each call sums (rank + 1) * (it + 1) over the ranks exactly."""
+    P = 4
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(NEW_STYLE_GRAPH_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"),
+                                   os.path.join(d, f"o{r}.npy")], env=e) for r in range(P)]
+        assert [p.wait(timeout=300) for p in procs] == [0] * P
+        ys = [np.load(os.path.join(d, f"o{r}.npy")) for r in range(P)]
+    for r in range(P):
+        for it in range(ys[r].shape[0]):
+            assert (ys[r][it] == (it + 1) * P * (P + 1) / 2).all(), (r, it)

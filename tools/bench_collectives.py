@@ -123,6 +123,7 @@ def main():
     p.add_argument("--ranks", type=int, default=8)
     p.add_argument("--configs", default="1,3,4,5")
     p.add_argument("--iters", type=int, default=5)
+    p.add_argument("--max-lg", type=int, default=30, help="config 4: largest size, log2 bytes per rank")
     args = p.parse_args()
     cfgs = set(args.configs.split(","))
     import torch
@@ -185,12 +186,14 @@ def main():
                           "host_wait_ms_per_run": round(max(s["wait_s"] for s in st) / args.iters * 1e3, 3)}),
               flush=True)
     if "4" in cfgs:
-        for lg in range(10, 31, 2):  # 1 KiB .. 1 GiB per rank
+        for lg in range(10, args.max_lg + 1, 2):  # 1 KiB .. 1 GiB per rank
             n = max(1, (1 << lg) // 4)
             it = args.iters if lg < 28 else 3
-            per, st = run_collective(torch, "halving_doubling", "sum", "f32", P, n, max(it, 3))
+            # latency: no profiling events, so the plan replays as a hipGraph
+            per, st = run_collective(torch, "halving_doubling", "sum", "f32", P, n, max(it, 3), profile=False)
             print(json.dumps({"config": 4, "algo": "halving_doubling", "ranks": P, "gpus": ndev,
                               "data_path": where, "bytes_per_rank": n * 4,
+                              "env": {k: v for k, v in os.environ.items() if k.startswith("GLOO_AMD_")},
                               "us_p50": round(per[len(per) // 2] * 1e6, 1),
                               "us_max": round(per[-1] * 1e6, 1),
                               "busbw_gib_s": round(2 * (P - 1) / P * n * 4 / per[len(per) // 2] / GIB, 3)}),
