@@ -4,11 +4,15 @@
 // around the visible GPUs), fp32 sum over device buffers, checked against the
 // closed form of gloo/test/base_test.h:184-236.
 //
-//   ./examples/allreduce_ring_chunked [ranks=4] [count=1048576]
+// With "host" as the third argument the inboxes live in pinned host memory
+// (HipHostWorkspace, the reference's CudaHostWorkspace placement).
+//
+//   ./examples/allreduce_ring_chunked [ranks=4] [count=1048576] [device|host]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -18,6 +22,7 @@
 int main(int argc, char** argv) {
   const int P = argc > 1 ? std::atoi(argv[1]) : 4;
   const int count = argc > 2 ? std::atoi(argv[2]) : (1 << 20);
+  const bool hostWs = argc > 3 && std::string(argv[3]) == "host";
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     std::fprintf(stderr, "no GPU\n");
@@ -37,8 +42,13 @@ int main(int argc, char** argv) {
       float* d = nullptr;
       (void)hipMalloc(&d, count * sizeof(float));
       (void)hipMemcpy(d, host.data(), count * sizeof(float), hipMemcpyHostToDevice);
-      gloo_amd::HipAllreduceRingChunked<float> algo(ctx, {d}, count);
-      algo.run();
+      if (hostWs) {
+        gloo_amd::HipAllreduceRingChunked<float, gloo_amd::HipHostWorkspace<float>> algo(ctx, {d}, count);
+        algo.run();
+      } else {
+        gloo_amd::HipAllreduceRingChunked<float> algo(ctx, {d}, count);
+        algo.run();
+      }
       (void)hipMemcpy(host.data(), d, count * sizeof(float), hipMemcpyDeviceToHost);
       for (int j = 0; j < count; j++) {
         const float want = float(j % 1000) * P * P + P * (P - 1) / 2.0f;
@@ -50,6 +60,7 @@ int main(int argc, char** argv) {
   for (auto& t : ts) t.join();
   int total = 0;
   for (int r = 0; r < P; r++) total += bad[r];
-  std::printf("allreduce_ring_chunked: %d ranks x %d floats: %s\n", P, count, total ? "MISMATCH" : "ok");
+  std::printf("allreduce_ring_chunked: %d ranks x %d floats (%s workspace): %s\n", P, count,
+              hostWs ? "host" : "device", total ? "MISMATCH" : "ok");
   return total ? 1 : 0;
 }

@@ -206,6 +206,9 @@ def _bind_collectives(L):
     L.gloo_hip_algorithm_create.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.POINTER(vp), ctypes.c_int, sz,
                                             ctypes.POINTER(ctypes.c_int), vp, ctypes.POINTER(vp)]
+    L.gloo_hip_algorithm_create_ws.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.POINTER(vp), ctypes.c_int, sz,
+                                               ctypes.POINTER(ctypes.c_int), vp, ctypes.c_int, ctypes.POINTER(vp)]
     L.gloo_hip_algorithm_run.argtypes = [vp]
     L.gloo_hip_algorithm_destroy.argtypes = [vp]
     L.gloo_hip_algorithm_wait_seconds.argtypes = [vp]
@@ -220,7 +223,9 @@ EXPORTED = EXPORTED + ("gloo_hip_context_create", "gloo_hip_context_destroy",
                        "gloo_hip_algorithm_create", "gloo_hip_algorithm_run",
                        "gloo_hip_algorithm_destroy", "gloo_hip_algorithm_wait_seconds",
                        "gloo_hip_algorithm_set_profiling", "gloo_hip_algorithm_stats",
-                       "gloo_hip_algorithm_mode")
+                       "gloo_hip_algorithm_mode", "gloo_hip_algorithm_create_ws")
+
+WORKSPACES = {"device": 0, "host": 1}
 
 
 class Context:
@@ -249,9 +254,11 @@ class Context:
 
 class Algorithm:
     """A constructed GPU algorithm (CudaAllreduceRingChunked & co.); run() is
-    Algorithm::run() (gloo/algorithm.h:26).  ptrs: device pointers (ints)."""
+    Algorithm::run() (gloo/algorithm.h:26).  ptrs: device pointers (ints).
+    workspace: "device" (inboxes in HBM) or "host" (pinned host-memory
+    inboxes, the CudaHostWorkspace placement; gloo/cuda_workspace.h:20-31)."""
 
-    def __init__(self, ctx, algo, op, dtype, ptrs, count, recv_elems=None, stream=0):
+    def __init__(self, ctx, algo, op, dtype, ptrs, count, recv_elems=None, stream=0, workspace="device"):
         self.ctx = ctx
         arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
         rp = None
@@ -259,8 +266,9 @@ class Algorithm:
             rp = (ctypes.c_int * len(recv_elems))(*[int(x) for x in recv_elems])
         h = ctypes.c_void_p()
         a = ALGORITHMS[algo] if isinstance(algo, str) else int(algo)
-        _check(lib.gloo_hip_algorithm_create(ctx._h, a, _as_op(op), _as_dtype(dtype), arr, len(ptrs),
-                                             int(count), rp, stream or None, ctypes.byref(h)))
+        ws = WORKSPACES[workspace] if isinstance(workspace, str) else int(workspace)
+        _check(lib.gloo_hip_algorithm_create_ws(ctx._h, a, _as_op(op), _as_dtype(dtype), arr, len(ptrs),
+                                                int(count), rp, stream or None, ws, ctypes.byref(h)))
         self._h = h
 
     def run(self):
@@ -287,7 +295,8 @@ class Algorithm:
         _check(lib.gloo_hip_algorithm_mode(self._h, out))
         err = lib.gloo_hip_last_error()
         err = err.decode() if isinstance(err, bytes) else (err or "")
-        return {"device_signal": bool(out[0]), "fine_arena": bool(out[1]), "kernel_copy": bool(out[2]),
+        return {"device_signal": bool(out[0]), "fine_arena": out[1] == 1,
+                "host_arena": out[1] == 2, "kernel_copy": bool(out[2]),
                 "graph": bool(out[3]),
                 "graph_error": err[len("graph capture abandoned: "):]
                 if err.startswith("graph capture abandoned: ") else ""}

@@ -57,9 +57,9 @@ int gloo_hip_context_destroy(gloo_hip_context_t ctx) {
   });
 }
 
-int gloo_hip_algorithm_create(gloo_hip_context_t ctx, int algo, int op, int dtype, void* const* ptrs, int nptrs,
-                              size_t count, const int* recv_elems, gloo_hip_stream_t stream,
-                              gloo_hip_algorithm_t* out) {
+int gloo_hip_algorithm_create_ws(gloo_hip_context_t ctx, int algo, int op, int dtype, void* const* ptrs, int nptrs,
+                                 size_t count, const int* recv_elems, gloo_hip_stream_t stream, int workspace,
+                                 gloo_hip_algorithm_t* out) {
   return guarded([&] {
     GLOO_AMD_ENFORCE(ctx && out && ptrs && nptrs >= 1, "bad arguments");
     std::vector<int> re;
@@ -70,9 +70,17 @@ int gloo_hip_algorithm_create(gloo_hip_context_t ctx, int algo, int op, int dtyp
     auto a = std::make_unique<gloo_hip_algorithm>();
     a->exec = std::make_unique<gloo_amd::PlanExecutor>(ctx->ctx, algo, op, dtype,
                                                        std::vector<void*>(ptrs, ptrs + nptrs), count, re,
-                                                       static_cast<hipStream_t>(stream));
+                                                       static_cast<hipStream_t>(stream), std::vector<void*>{}, 0,
+                                                       workspace);
     *out = a.release();
   });
+}
+
+int gloo_hip_algorithm_create(gloo_hip_context_t ctx, int algo, int op, int dtype, void* const* ptrs, int nptrs,
+                              size_t count, const int* recv_elems, gloo_hip_stream_t stream,
+                              gloo_hip_algorithm_t* out) {
+  return gloo_hip_algorithm_create_ws(ctx, algo, op, dtype, ptrs, nptrs, count, recv_elems, stream,
+                                      GLOO_HIP_WORKSPACE_DEVICE, out);
 }
 
 int gloo_hip_algorithm_run(gloo_hip_algorithm_t a) {
@@ -141,7 +149,7 @@ int gloo_hip_algorithm_mode(gloo_hip_algorithm_t a, int* mode) {
   return guarded([&] {
     GLOO_AMD_ENFORCE(a && mode, "null argument");
     mode[0] = a->exec->deviceSignalling() ? 1 : 0;
-    mode[1] = a->exec->fineGrainedArena() ? 1 : 0;
+    mode[1] = a->exec->hostArena() ? 2 : a->exec->fineGrainedArena() ? 1 : 0;
     mode[2] = a->exec->kernelCopy() ? 1 : 0;
     mode[3] = a->exec->graphed() ? 1 : 0;
     gloo_amd::setError(0, a->exec->graphError().empty() ? "" : "graph capture abandoned: " + a->exec->graphError());

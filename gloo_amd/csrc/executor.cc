@@ -1,7 +1,9 @@
 // executor.cc — see executor.h.
 #include "gloo_amd/executor.h"
 
+#include <fcntl.h>
 #include <sched.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -9,6 +11,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <cstring>
+#include <random>
 #include <set>
 #include <thread>
 
@@ -25,7 +28,9 @@ struct ArenaRecord {
   int32_t device;
   uint64_t ptr;
   uint64_t bytes;
-  hipIpcMemHandle_t handle;
+  hipIpcMemHandle_t handle;  // DEVICE workspace
+  int32_t host;              // HOST workspace: the arena is the shm segment `shm`
+  char shm[60];
 };
 
 void bumpCounter(void* p) { static_cast<std::atomic<uint64_t>*>(p)->fetch_add(1, std::memory_order_acq_rel); }
@@ -80,6 +85,65 @@ std::mutex& liveMutex() {
 }
 
 }  // namespace
+
+// A pinned host-memory segment every rank of the node can map (HOST workspace).
+struct PlanExecutor::HostShm {
+  std::string name;
+  void* host = nullptr;
+  void* dev = nullptr;
+  size_t bytes = 0;
+  bool owner = false;
+
+  static std::unique_ptr<HostShm> create(size_t bytes) {
+    auto h = std::make_unique<HostShm>();
+    std::random_device rd;
+    h->name = strcat_("/gloo_amd_ws_", ::getpid(), "_", rd(), rd());
+    h->bytes = bytes;
+    h->owner = true;
+    const int fd = ::shm_open(h->name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+    GLOO_AMD_ENFORCE(fd >= 0, "shm_open(create) failed for ", h->name);
+    const bool sized = ::ftruncate(fd, (off_t)bytes) == 0;
+    if (sized) h->host = ::mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    ::close(fd);
+    if (!sized || h->host == MAP_FAILED) {
+      h->host = nullptr;
+      ::shm_unlink(h->name.c_str());
+      throw EnforceNotMet(strcat_("cannot map a ", bytes, "-byte host workspace"));
+    }
+    h->map();
+    return h;
+  }
+  static std::unique_ptr<HostShm> open(const std::string& name, size_t bytes) {
+    auto h = std::make_unique<HostShm>();
+    h->name = name;
+    h->bytes = bytes;
+    const int fd = ::shm_open(name.c_str(), O_RDWR, 0600);
+    GLOO_AMD_ENFORCE(fd >= 0, "shm_open failed for ", name);
+    h->host = ::mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    ::close(fd);
+    if (h->host == MAP_FAILED) {
+      h->host = nullptr;
+      throw EnforceNotMet(strcat_("cannot map host workspace ", name));
+    }
+    h->map();
+    return h;
+  }
+  void map() {
+    GLOO_AMD_HIP_CHECK(hipHostRegister(host, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    GLOO_AMD_HIP_CHECK(hipHostGetDevicePointer(&dev, host, 0));
+  }
+  void unlink() {
+    if (owner && !name.empty()) ::shm_unlink(name.c_str());
+    owner = false;
+  }
+  ~HostShm() {
+    if (host) {
+      (void)hipHostUnregister(host);
+      ::munmap(host, bytes);
+    }
+    unlink();
+  }
+};
 
 namespace {
 Plan planFor(int algo, int rank, int size, size_t count, int nin, int nout, size_t es, size_t maxSeg,
@@ -144,7 +208,8 @@ void PlanExecutor::classifyPointers() {
 
 PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int dtype,
                            const std::vector<void*>& ptrs, size_t count, const std::vector<int>& recvElems,
-                           hipStream_t stream, const std::vector<void*>& inputs, size_t maxSegmentBytes)
+                           hipStream_t stream, const std::vector<void*>& inputs, size_t maxSegmentBytes,
+                           int workspace)
     : ctx_(std::move(ctx)), algo_(algo), op_(op), dtype_(dtype), ptrs_(ptrs), inputs_(inputs), count_(count),
       maxSegmentBytes_(maxSegmentBytes), recvElems_(recvElems) {
   es_ = gloo_hip_dtype_size(dtype_);
@@ -234,11 +299,17 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   // fine-grained memory so no stale line of this GPU's L2 can be read.
   const char* ar = std::getenv("GLOO_AMD_ARENA");
   const std::string arMode = ar ? ar : "auto";
-  fineArena_ = arMode == "fine" || (arMode == "auto" && crossDeviceSender);
+  GLOO_AMD_ENFORCE(workspace == GLOO_HIP_WORKSPACE_DEVICE || workspace == GLOO_HIP_WORKSPACE_HOST,
+                   "unknown workspace ", workspace);
+  hostArena_ = workspace == GLOO_HIP_WORKSPACE_HOST || arMode == "host";
+  fineArena_ = !hostArena_ && (arMode == "fine" || (arMode == "auto" && crossDeviceSender));
 
   // Phase 2: the inbox arena.
   const size_t arenaBytes = std::max<size_t>(256, plan_.arena * es_);
-  if (fineArena_) {
+  if (hostArena_) {
+    arenaShm_ = HostShm::create(arenaBytes);
+    arena_ = static_cast<char*>(arenaShm_->dev);
+  } else if (fineArena_) {
     GLOO_AMD_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), arenaBytes,
                                              hipDeviceMallocFinegrained));
   } else {
@@ -250,7 +321,13 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   rec.device = ctx_->device();
   rec.ptr = reinterpret_cast<uint64_t>(arena_);
   rec.bytes = arenaBytes;
-  GLOO_AMD_HIP_CHECK(hipIpcGetMemHandle(&rec.handle, arena_));
+  if (hostArena_) {
+    rec.host = 1;
+    GLOO_AMD_ENFORCE(arenaShm_->name.size() < sizeof(rec.shm), "shm name too long");
+    std::memcpy(rec.shm, arenaShm_->name.c_str(), arenaShm_->name.size() + 1);
+  } else {
+    GLOO_AMD_HIP_CHECK(hipIpcGetMemHandle(&rec.handle, arena_));
+  }
   std::vector<char> blob(sizeof(rec));
   std::memcpy(blob.data(), &rec, sizeof(rec));
   ctx_->store().set(strcat_("gloo_amd/inst", inst_, "/arena/", me), blob);
@@ -262,7 +339,12 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     GLOO_AMD_ENFORCE(v.size() == sizeof(ArenaRecord), "bad arena record from rank ", peer);
     ArenaRecord pr;
     std::memcpy(&pr, v.data(), sizeof(pr));
-    if (pr.pid == ctx_->pid()) {
+    if (pr.host && pr.pid != ctx_->pid()) {
+      // another process's host workspace: map the same pages here
+      peerShm_.push_back(HostShm::open(std::string(pr.shm), pr.bytes));
+      peers_[peer].base = static_cast<char*>(peerShm_.back()->dev);
+    } else if (pr.host || pr.pid == ctx_->pid()) {
+      // same process: registered portable (host) or peer-accessible (device)
       peers_[peer].base = reinterpret_cast<char*>(pr.ptr);
       if (pr.device != ctx_->device()) {
         hipError_t e = hipDeviceEnablePeerAccess(pr.device, 0);
@@ -318,6 +400,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     }
   }
   ctx_->barrier(strcat_("inst", inst_, "/ready"));
+  if (arenaShm_) arenaShm_->unlink();  // every peer has mapped it by now
 }
 
 PlanExecutor::~PlanExecutor() {
@@ -328,7 +411,12 @@ PlanExecutor::~PlanExecutor() {
         if (p.ipc && p.base) (void)hipIpcCloseMemHandle(p.base);
       // nobody may free an arena a peer still maps
       ctx_->barrier(strcat_("inst", inst_, "/closed"));
-      if (arena_) (void)hipFree(arena_);
+      peerShm_.clear();
+      if (arenaShm_) {
+        arenaShm_.reset();
+      } else if (arena_) {
+        (void)hipFree(arena_);
+      }
     }
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
     if (graphExec_) (void)hipGraphExecDestroy(graphExec_);

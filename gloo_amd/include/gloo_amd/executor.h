@@ -34,6 +34,12 @@
 // so the graph never needs its kernel arguments updated.  New buffers
 // (setBuffers) drop the graph; profiling runs are enqueued eagerly.
 //
+// Workspace (gloo/cuda_workspace.h:20-31): DEVICE inboxes in HBM (default),
+// or HOST inboxes in pinned host memory shared by the node's ranks (POSIX shm
+// registered with hipHostRegister), the placement of a transport that
+// receives from a socket/NIC.  Peers write HOST inboxes over PCIe; REDUCE
+// reads them in place (zero-copy) and accumulates into the device buffer.
+//
 // Copy engine of a SEND (device signalling): hipMemcpyAsync + signal kernel
 // (default), or GLOO_AMD_COPY=kernel: copy_signal_kernel, one launch that
 // copies with GLOO_AMD_COPY_BLOCKS workgroups (default 64) and publishes the
@@ -62,7 +68,8 @@ class PlanExecutor {
   // (docs/cuda.md:6-13 of the reference).
   PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int dtype,
                const std::vector<void*>& ptrs, size_t count, const std::vector<int>& recvElems,
-               hipStream_t stream, const std::vector<void*>& inputs = {}, size_t maxSegmentBytes = 0);
+               hipStream_t stream, const std::vector<void*>& inputs = {}, size_t maxSegmentBytes = 0,
+               int workspace = 0 /* GLOO_HIP_WORKSPACE_DEVICE */);
 
   // Function-style calls (gloo::allreduce(opts)) reuse one executor for a
   // given option set and rebind the buffers before each run.
@@ -77,6 +84,7 @@ class PlanExecutor {
   hipStream_t stream() const { return stream_; }
   bool deviceSignalling() const { return deviceSignal_; }
   bool fineGrainedArena() const { return fineArena_; }
+  bool hostArena() const { return hostArena_; }
   bool kernelCopy() const { return kernelCopy_; }
   // True once run() replays a captured hipGraph.
   bool graphed() const { return graphExec_ != nullptr; }
@@ -126,7 +134,11 @@ class PlanExecutor {
   void classifyPointers();
   Plan plan_;
   uint64_t inst_;
-  char* arena_ = nullptr;
+  char* arena_ = nullptr;       // device-visible address of this rank's inboxes
+  bool hostArena_ = false;      // inboxes in shared pinned host memory (HOST workspace)
+  struct HostShm;
+  std::unique_ptr<HostShm> arenaShm_;
+  std::vector<std::unique_ptr<HostShm>> peerShm_;
   hipStream_t stream_ = nullptr;
   bool ownStream_ = false;
   std::vector<Peer> peers_;

@@ -98,7 +98,19 @@ class Algorithm {
   const int contextSize_;
 };
 
-template <typename T, int ALGO>
+// Workspaces (gloo/cuda_workspace.h:20-31): where the inboxes live.  The
+// reference defaults to the host workspace with CPU reductions; here both
+// reduce on the GPU, and the device workspace is the default.
+template <typename T>
+struct HipDeviceWorkspace {
+  static constexpr int kind = GLOO_HIP_WORKSPACE_DEVICE;
+};
+template <typename T>
+struct HipHostWorkspace {
+  static constexpr int kind = GLOO_HIP_WORKSPACE_HOST;
+};
+
+template <typename T, int ALGO, typename W = HipDeviceWorkspace<T>>
 class HipPlanAlgorithm : public Algorithm {
  public:
   HipPlanAlgorithm(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
@@ -108,7 +120,8 @@ class HipPlanAlgorithm : public Algorithm {
     std::vector<void*> p(ptrs.begin(), ptrs.end());
     exec_ = std::make_unique<PlanExecutor>(context, ALGO, fn->type(), DType<T>::value, p,
                                            static_cast<size_t>(count), recvElems,
-                                           streams.empty() ? nullptr : streams[0]);
+                                           streams.empty() ? nullptr : streams[0], std::vector<void*>{}, 0,
+                                           W::kind);
   }
   void run() override { exec_->run(); }
 
@@ -116,50 +129,50 @@ class HipPlanAlgorithm : public Algorithm {
   std::unique_ptr<PlanExecutor> exec_;
 };
 
-template <typename T>
-class HipAllreduceRingChunked : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING_CHUNKED> {
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipAllreduceRingChunked : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING_CHUNKED, W> {
  public:
   HipAllreduceRingChunked(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
                           const std::vector<hipStream_t>& streams = {},
                           const HipReductionFunction<T>* fn = HipReductionFunction<T>::sum)
-      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING_CHUNKED>(context, ptrs, count, {}, streams, fn) {}
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING_CHUNKED, W>(context, ptrs, count, {}, streams, fn) {}
 };
 
-template <typename T>
-class HipAllreduceHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING> {
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipAllreduceHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING, W> {
  public:
   HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
                               const std::vector<hipStream_t>& streams = {},
                               const HipReductionFunction<T>* fn = HipReductionFunction<T>::sum)
-      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING>(context, ptrs, count, {}, streams, fn) {}
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING, W>(context, ptrs, count, {}, streams, fn) {}
 };
 
-template <typename T>
-class HipAllreduceRing : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING> {
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipAllreduceRing : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING, W> {
  public:
   HipAllreduceRing(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
                    const std::vector<hipStream_t>& streams = {},
                    const HipReductionFunction<T>* fn = HipReductionFunction<T>::sum)
-      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING>(context, ptrs, count, {}, streams, fn) {}
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING, W>(context, ptrs, count, {}, streams, fn) {}
 };
 
-template <typename T>
-class HipAllreduceLocal : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_LOCAL> {
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipAllreduceLocal : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_LOCAL, W> {
  public:
   HipAllreduceLocal(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
                     const std::vector<hipStream_t>& streams = {},
                     const HipReductionFunction<T>* fn = HipReductionFunction<T>::sum)
-      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_LOCAL>(context, ptrs, count, {}, streams, fn) {}
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_LOCAL, W>(context, ptrs, count, {}, streams, fn) {}
 };
 
-template <typename T>
-class HipReduceScatterHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_REDUCE_SCATTER> {
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipReduceScatterHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_REDUCE_SCATTER, W> {
  public:
   HipReduceScatterHalvingDoubling(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
                                   int count, const std::vector<int>& recvElems,
                                   const std::vector<hipStream_t>& streams = {},
                                   const HipReductionFunction<T>* fn = HipReductionFunction<T>::sum)
-      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_REDUCE_SCATTER>(context, ptrs, count, recvElems, streams, fn) {}
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_REDUCE_SCATTER, W>(context, ptrs, count, recvElems, streams, fn) {}
 };
 
 // New-style function API (gloo/allreduce.h:89-193): options object + free

@@ -227,6 +227,20 @@ int gloo_hip_algorithm_create(gloo_hip_context_t ctx, int algo, int op, int dtyp
                               void* const* ptrs, int nptrs, size_t count,
                               const int* recv_elems, gloo_hip_stream_t stream,
                               gloo_hip_algorithm_t* out);
+/* Where the inboxes (the transport's receive buffers) live — the reference's
+ * workspace template argument (gloo/cuda_workspace.h:20-31):
+ *   DEVICE  HBM of the rank's GPU (CudaDeviceWorkspace; the default here);
+ *   HOST    pinned host memory shared by the node's ranks (CudaHostWorkspace:
+ *           chunks arrive in host memory, as from a socket/NIC); peers write
+ *           them over PCIe and the reduce kernel reads them in place
+ *           (zero-copy) while accumulating into the device buffer. */
+typedef enum { GLOO_HIP_WORKSPACE_DEVICE = 0, GLOO_HIP_WORKSPACE_HOST = 1 } gloo_hip_workspace_t;
+
+/* gloo_hip_algorithm_create with an explicit workspace. */
+int gloo_hip_algorithm_create_ws(gloo_hip_context_t ctx, int algo, int op, int dtype, void* const* ptrs, int nptrs,
+                                 size_t count, const int* recv_elems, gloo_hip_stream_t stream, int workspace,
+                                 gloo_hip_algorithm_t* out);
+
 int gloo_hip_algorithm_run(gloo_hip_algorithm_t algo);
 int gloo_hip_algorithm_destroy(gloo_hip_algorithm_t algo);
 /* Host seconds the last run() spent blocked waiting for peers. */
@@ -239,7 +253,8 @@ int gloo_hip_algorithm_set_profiling(gloo_hip_algorithm_t algo, int on);
 int gloo_hip_algorithm_stats(gloo_hip_algorithm_t algo, double* stats4);
 
 /* How the algorithm executes (no reference counterpart; for tests and
- * tools): mode4[0] = device-side signalling, [1] = fine-grained inbox arena,
+ * tools): mode4[0] = device-side signalling, [1] = inbox arena (0 device
+ * coarse-grained, 1 device fine-grained, 2 pinned host),
  * [2] = kernel copy engine, [3] = run() replays a captured hipGraph.  If graph
  * capture was abandoned, gloo_hip_last_error() says why. */
 int gloo_hip_algorithm_mode(gloo_hip_algorithm_t algo, int* mode4);

@@ -231,12 +231,14 @@ def test_profiling_stats(torch):
     assert float(bufs[0][0]) == P
 
 
-def test_cpp_example_program():
-    """The C++ drop-in surface (gloo_amd/include/gloo_amd/hip_allreduce.h)."""
+@pytest.mark.parametrize("workspace", ["device", "host"])
+def test_cpp_example_program(workspace):
+    """The C++ drop-in surface (gloo_amd/include/gloo_amd/hip_allreduce.h),
+    with both workspaces (HipDeviceWorkspace / HipHostWorkspace)."""
     exe = os.path.join(ROOT, "examples", "allreduce_ring_chunked")
     if not os.path.exists(exe):
         pytest.skip("example not built")
-    r = subprocess.run([exe, "4", "100003"], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, "4", "100003", workspace], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ok" in r.stdout
 
@@ -544,3 +546,65 @@ def test_processes_new_style_rebinding_graph(torch):
     for r in range(P):
         for it in range(ys[r].shape[0]):
             assert (ys[r][it] == (it + 1) * P * (P + 1) / 2).all(), (r, it)
+
+
+HOST_WS_WORKER = r"""
+import os, sys, json, numpy as np
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, size, store, case, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
+g = np.load(os.path.join(os.environ["GLOO_AMD_ROOT"], "tests", "golden", "sched_golden.npz"))
+algo, op, dtype = case.split("/")[:3]
+x = g[case + "/in"]
+recv = g[case + "/recv"] if algo == "reduce_scatter" else None
+xr = x[rank] if algo == "reduce_scatter" else x[rank, 0]
+torch.cuda.set_device(0)
+src = torch.from_numpy(xr.view(np.uint8).copy()).to("cuda:0")
+buf = torch.empty_like(src)
+ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=60000)
+a = gloo_amd.Algorithm(ctx, algo, op, dtype, [buf.data_ptr()], xr.size, recv_elems=recv, workspace="host")
+for it in range(3):
+    buf.copy_(src)
+    torch.cuda.synchronize()
+    a.run()
+    np.save(out + f".{it}.npy", buf.cpu().numpy().view(xr.dtype))
+print("MODE", json.dumps(a.mode()))
+a.close(); ctx.close()
+"""
+
+
+@pytest.mark.parametrize("case,env", [
+    ("ring_chunked/max/f32/P5/k1/n999", {}),
+    ("halving_doubling/sum/f32/P5/k1/n10007", {}),
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0"}),
+    ("reduce_scatter/max/bf16/P8/n4096", {"GLOO_AMD_COPY": "kernel"}),
+    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_FUSE_BYTES": "0", "GLOO_AMD_GRAPH": "1"}),
+    ("ring_chunked/sum/f32/P3/k1/n1000", {"GLOO_AMD_SIGNAL": "host"}),
+])
+def test_processes_host_workspace(torch, golden_sched, case, env):
+    """HOST workspace (the reference's CudaHostWorkspace placement): every
+    rank's inboxes are pinned host memory shared through POSIX shm; peers
+    write them over PCIe and the reduce kernel reads them in place.  Ranks as
+    processes; three runs, each against the reference's bytes."""
+    algo = case.split("/")[0]
+    P = int(case.split("/")[3][1:])
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(HOST_WS_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), case,
+                                   os.path.join(d, f"o{r}")], env=e, stdout=subprocess.PIPE, text=True)
+                 for r in range(P)]
+        outs = [p.communicate(timeout=300)[0] for p in procs]
+        assert [p.returncode for p in procs] == [0] * P
+        ys = [[np.load(os.path.join(d, f"o{r}.{it}.npy")) for it in range(3)] for r in range(P)]
+    want = golden_sched[case + "/out"]
+    for it in range(3):
+        if algo == "reduce_scatter":
+            recv = golden_sched[case + "/recv"]
+            assert same_bytes(np.concatenate([ys[r][it][:recv[r]] for r in range(P)]), want), it
+        else:
+            for r in range(P):
+                assert same_bytes(ys[r][it], want), (r, it)
+    for r in range(P):
+        assert json.loads(outs[r].split("MODE", 1)[1])["host_arena"]
