@@ -226,13 +226,14 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
     """BASELINE config 3 (+ a config-4 sweep) at N > 1 ranks, one per GPU.
 
     Config 3: AllreduceRingChunked fp32 sum, 256 MiB per rank.  Chunks move
-    GPU->GPU into the peer's HBM inbox (xGMI) and every arriving chunk is
-    reduced by the HIP kernel on the receiving GPU.  Reported: the slowest
-    rank's time per allreduce, bus bandwidth, and the reduce kernel's own
-    GiB/s measured with HIP events around each chunk reduction while the
-    exchange runs (per-GPU efficiency vs the 1-GPU figure) — once with
-    hipMemcpyAsync peer copies, once with the fused copy+signal kernel.
-    Config 4: halving-doubling at 1 KiB / 1 MiB / 64 MiB per rank."""
+    GPU->GPU into the peer's HBM inbox (xGMI) and are reduced by the HIP
+    kernel on the receiving GPU.  Default: the mesh plan (the ring's bytes,
+    every link at once); variants: forked hipMemcpyAsync sends, the classic
+    ring with either copy engine, the HOST workspace.  Reported: the slowest
+    rank's time per allreduce, bus bandwidth, and the reduction kernels' own
+    GiB/s measured with HIP events while the exchange runs (per-GPU
+    efficiency vs the 1-GPU figure).
+    Config 4: halving-doubling at 1 KiB / 64 KiB / 1 MiB / 64 MiB per rank."""
     import tempfile
     obj = [tempfile.mkdtemp(prefix="gloo_amd_bench_")] if rank == 0 else [None]
     dist.broadcast_object_list(obj, src=0)
@@ -255,12 +256,12 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
                 else:
                     os.environ[k] = v
 
-    def ring_once(engine, workspace="device"):
+    def ring_once(engine, workspace="device", mesh="1"):
         def body():
             buf = torch.ones(n, device=dev)
             torch.cuda.synchronize(dev)
-            ctx = hip.Context(rank, world, "file:%s/ring_%s_%s" % (obj[0], engine, workspace), device=dev.index,
-                              timeout_ms=60000)
+            ctx = hip.Context(rank, world, "file:%s/ring_%s_%s_%s" % (obj[0], engine, workspace, mesh),
+                              device=dev.index, timeout_ms=60000)
             a = hip.Algorithm(ctx, "ring_chunked", "sum", "f32", [buf.data_ptr()], n, workspace=workspace)
             a.run()
             # timed: steady state (the plan replays as a hipGraph from run 3 on)
@@ -289,7 +290,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
             return {"ms": [round(t * 1e3, 3) for t in times], "reduce_s": red_s, "reduce_b": red_b,
                     "wait_ms_per_run": round(wait_s / 3 * 1e3, 3), "verified": ok, "graph": graphed}
         try:
-            res = with_env({"GLOO_AMD_COPY": engine}, body)
+            res = with_env({"GLOO_AMD_COPY": engine, "GLOO_AMD_RING_MESH": mesh}, body)
         except Exception as e:  # noqa: BLE001
             res = {"error": repr(e)}
         gathered = gather(res)
@@ -299,7 +300,8 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
         ms = sorted(max(g["ms"][i] for g in gathered) for i in range(args.allreduce_iters))
         t = ms[len(ms) // 2] / 1e3
         per_gpu = [g["reduce_b"] / g["reduce_s"] / GIB for g in gathered if g["reduce_s"] > 0]
-        return {"copy_engine": engine, "workspace": workspace, "graph": all(g["graph"] for g in gathered),
+        return {"plan": "mesh" if mesh == "1" and world <= 8 else "ring", "copy_engine": engine,
+                "workspace": workspace, "graph": all(g["graph"] for g in gathered),
                 "ms_p50": round(t * 1e3, 3), "algbw_gib_s": round(n * 4 / t / GIB, 2),
                 "busbw_gib_s": round(2 * (world - 1) / world * n * 4 / t / GIB, 2),
                 "reduce_kernel_gib_s_per_gpu": [round(x, 1) for x in per_gpu],
@@ -307,11 +309,14 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
                 "host_wait_ms_per_run_max_profiled": max(g["wait_ms_per_run"] for g in gathered),
                 "verified": all(g["verified"] is not False for g in gathered)}
 
-    ring = ring_once("memcpy")
+    # default: the mesh plan (batched sends = one multi-destination copy kernel)
+    ring = ring_once("auto")
     if "error" in ring:
         return ring
-    ring_kernel = ring_once("kernel")
-    ring_host = ring_once("memcpy", "host")
+    variants = {"mesh_memcpy_forked": ring_once("memcpy"),
+                "ring_memcpy": ring_once("memcpy", mesh="0"),
+                "ring_kernel": ring_once("kernel", mesh="0"),
+                "mesh_host_workspace": ring_once("auto", "host")}
 
     sizes = (1 << 10, 64 << 10, 1 << 20, 64 << 20)
     iters = 20
@@ -369,8 +374,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
     out = {"config": "allreduce_ring_chunked fp32 sum, %d ranks, %d MiB/rank" % (world, args.allreduce_mib),
            "data_path": "xGMI peer copies" if ngpu >= world else f"{world} ranks on {ngpu} GPU(s)"}
     out.update(ring)
-    out["kernel_copy_engine"] = ring_kernel
-    out["host_workspace"] = ring_host
+    out["variants"] = variants
     out["halving_doubling"] = hd_summary
     return out
 

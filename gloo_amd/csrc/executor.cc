@@ -218,7 +218,16 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   GLOO_AMD_ENFORCE(!ptrs_.empty(), "need at least one pointer");
   for (void* p : ptrs_) GLOO_AMD_ENFORCE(p != nullptr || count_ == 0, "null device pointer");
   const int me = ctx_->rank, P = ctx_->size;
-  plan_ = planFor(algo_, me, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_, maxSegmentBytes_,
+  // AllreduceRingChunked's result with mesh data movement (plan.cc
+  // planRingChunkedMesh): same bytes, two all-to-all hops over every xGMI
+  // link instead of 2(P-1) hops around the ring.  Every rank must choose
+  // alike, so the choice depends only on the environment and P.
+  planAlgo_ = algo_;
+  if (algo_ == GLOO_HIP_ALGO_RING_CHUNKED && P >= 2 && P <= GLOO_HIP_MAX_SRCS) {
+    const char* m = std::getenv("GLOO_AMD_RING_MESH");
+    if (!(m && m[0] == '0')) planAlgo_ = GLOO_HIP_ALGO_RING_CHUNKED_MESH;
+  }
+  plan_ = planFor(planAlgo_, me, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_, maxSegmentBytes_,
                   recvElems_);
   GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
   classifyPointers();
@@ -357,7 +366,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       peers_[peer].base = static_cast<char*>(p);
       peers_[peer].ipc = true;
     }
-    const Plan theirs = planFor(algo_, peer, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
+    const Plan theirs = planFor(planAlgo_, peer, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
     for (const Step& d : theirs.steps)
       if (d.kind == GLOO_HIP_STEP_DECL_RECV && d.peer == me) {
         GLOO_AMD_ENFORCE((d.dst_off + d.length) * es_ <= pr.bytes, "peer region outside its arena");
@@ -371,18 +380,18 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   if (deviceSignal_) {
     (void)ctx_->counterDevicePtr(inst_, 0, 0, 0);  // register the control block now
     ctx_->errorWord(me).store(0);
+    // Copy engine: a lone SEND is hipMemcpyAsync + signal ("memcpy", the
+    // default) or the copy+signal kernel ("kernel"); a batch of consecutive
+    // SENDs (one per peer) is one multi-destination copy kernel (default),
+    // or with "memcpy" one hipMemcpyAsync per forked stream.
     const char* cp = std::getenv("GLOO_AMD_COPY");
-    kernelCopy_ = cp && std::string(cp) == "kernel";
+    const std::string cmode = cp ? cp : "auto";
+    kernelCopy_ = cmode == "kernel";
+    batchKernelCopy_ = cmode != "memcpy";
     if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS")) copyBlocks_ = (unsigned)std::max(1, std::atoi(cb));
-    if (kernelCopy_) {
-      GLOO_AMD_HIP_CHECK(hipMalloc(&ticket_, 256));
-      GLOO_AMD_HIP_CHECK(hipMemset(ticket_, 0, 256));
-      for (size_t i = 0; i < plan_.steps.size(); i++)
-        if (plan_.steps[i].kind == GLOO_HIP_STEP_SEND) {
-          stepSeq_[i].ticket = ticketsPerRun_;
-          ticketsPerRun_ += copySignalGrid(plan_.steps[i].length * es_, copyBlocks_);
-        }
-    }
+    const size_t tickets = std::max<size_t>(256, (size_t)P * GLOO_HIP_NUM_SLOTS * sizeof(unsigned));
+    GLOO_AMD_HIP_CHECK(hipMalloc(&ticket_, tickets));
+    GLOO_AMD_HIP_CHECK(hipMemset(ticket_, 0, tickets));
     // Graph replay pays off once a plan has steps that are not fused
     // one-workgroup launches (measured); "1" / "0" force it.
     const char* gm = std::getenv("GLOO_AMD_GRAPH");
@@ -419,6 +428,8 @@ PlanExecutor::~PlanExecutor() {
       }
     }
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+    for (hipEvent_t e : forkEvents_) (void)hipEventDestroy(e);
+    for (hipStream_t a : aux_) (void)hipStreamDestroy(a);
     if (graphExec_) (void)hipGraphExecDestroy(graphExec_);
     if (epoch_) (void)hipFree(epoch_);
     if (ticket_) (void)hipFree(ticket_);
@@ -454,14 +465,29 @@ void PlanExecutor::waitCounter(std::atomic<uint64_t>& c, uint64_t target, int pe
   waitSeconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+hipStream_t PlanExecutor::auxStream(size_t k) {
+  const size_t kMaxAux = 7;
+  k %= kMaxAux;
+  while (aux_.size() <= k) {
+    hipStream_t a;
+    GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
+    aux_.push_back(a);
+  }
+  return aux_[k];
+}
+
+hipEvent_t PlanExecutor::forkEvent(size_t k) {
+  while (forkEvents_.size() <= k) {
+    hipEvent_t e;
+    GLOO_AMD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    forkEvents_.push_back(e);
+  }
+  return forkEvents_[k];
+}
+
 Seq PlanExecutor::seqOf(size_t i, uint64_t r, bool graph) const {
   const StepSeq& q = stepSeq_[i];
   return graph ? Seq{q.base, q.perRun} : Seq{q.base + r * q.perRun, 0};
-}
-
-Seq PlanExecutor::ticketOf(size_t i, uint64_t r, bool graph) const {
-  const uint64_t base = (uint64_t)stepSeq_[i].ticket - ticketsPerRun_;
-  return graph ? Seq{base, ticketsPerRun_} : Seq{base + r * ticketsPerRun_, 0};
 }
 
 void PlanExecutor::run() {
@@ -561,8 +587,72 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
   const bool fuse = deviceSignal_ && !profiling_ && kFuseBytes > 0;
   auto userOrArena = [&](bool arena) { return arena ? arena_ : userPtr(0); };
   const std::vector<Step>& steps = plan_.steps;
+  auto sendDst = [&](const Step& t) {
+    return peers_[t.peer].base + (remoteRegion_[{t.peer, t.slot}] + t.dst_off) * es_;
+  };
+  auto isWaitKind = [](int k) { return k == GLOO_HIP_STEP_WAIT_RECV || k == GLOO_HIP_STEP_WAIT_NOTIFY; };
+  std::vector<const void*> foldSrcs;
   for (size_t i = 0; i < steps.size(); i++) {
     const Step& s = steps[i];
+    // A run of consecutive SENDs (a mesh schedule's sends to every peer):
+    // all in flight at once.
+    if (s.kind == GLOO_HIP_STEP_SEND && i + 1 < steps.size() && steps[i + 1].kind == GLOO_HIP_STEP_SEND) {
+      size_t j = i;
+      while (j < steps.size() && steps[j].kind == GLOO_HIP_STEP_SEND) j++;
+      if (deviceSignal_ && batchKernelCopy_) {
+        for (size_t b = i; b < j; b += kMaxCopyEntries) {
+          CopyDesc d[kMaxCopyEntries];
+          int nd = 0;
+          for (size_t k = b; k < std::min(j, b + kMaxCopyEntries); k++) {
+            const Step& t = steps[k];
+            const size_t bytes = t.length * es_;
+            d[nd++] = CopyDesc{sendDst(t), userOrArena(t.flags & GLOO_HIP_SRC_ARENA) + t.src_off * es_, bytes,
+                               ctx_->counterDevicePtr(inst_, me, t.peer, t.slot), seqOf(k, r, graph),
+                               ticket_ + (size_t)t.peer * GLOO_HIP_NUM_SLOTS + t.slot,
+                               copySignalGrid(bytes, copyBlocks_)};
+          }
+          checkRc(launchCopySignalMulti(d, nd, epoch, stream_), "copy_signal_kernel (batch)");
+        }
+      } else {
+        // fork: one hipMemcpyAsync + arrival signal per auxiliary stream, joined
+        // back before anything later on the rank's stream
+        hipEvent_t fork = forkEvent(0);
+        GLOO_AMD_HIP_CHECK(hipEventRecord(fork, stream_));
+        for (size_t k = i; k < j; k++) {
+          const Step& t = steps[k];
+          hipStream_t a = auxStream(k - i);
+          GLOO_AMD_HIP_CHECK(hipStreamWaitEvent(a, fork, 0));
+          if (t.length)
+            GLOO_AMD_HIP_CHECK(hipMemcpyAsync(sendDst(t), userOrArena(t.flags & GLOO_HIP_SRC_ARENA) + t.src_off * es_,
+                                              t.length * es_, hipMemcpyDeviceToDevice, a));
+          if (deviceSignal_) {
+            GLOO_AMD_HIP_CHECK(launchSignal(ctx_->counterDevicePtr(inst_, me, t.peer, t.slot), seqOf(k, r, graph),
+                                            epoch, a));
+          } else {
+            enqueueBump(a, ctx_->counter(inst_, me, t.peer, t.slot));
+          }
+          hipEvent_t join = forkEvent(1 + (k - i));
+          GLOO_AMD_HIP_CHECK(hipEventRecord(join, a));
+          GLOO_AMD_HIP_CHECK(hipStreamWaitEvent(stream_, join, 0));
+        }
+      }
+      i = j - 1;
+      continue;
+    }
+    // A run of consecutive waits: one launch polls them all.
+    if (deviceSignal_ && isWaitKind(s.kind) && i + 1 < steps.size() && isWaitKind(steps[i + 1].kind)) {
+      size_t j = i;
+      std::vector<const uint64_t*> flags;
+      std::vector<Seq> targets;
+      for (; j < steps.size() && isWaitKind(steps[j].kind); j++) {
+        flags.push_back(ctx_->counterDevicePtr(inst_, steps[j].peer, me, steps[j].slot));
+        targets.push_back(seqOf(j, r, graph));
+      }
+      GLOO_AMD_HIP_CHECK(launchWaitMulti(flags.data(), targets.data(), (int)flags.size(), epoch, timeoutTicks,
+                                         ctx_->errorWordDevicePtr(me), stream_));
+      i = j - 1;
+      continue;
+    }
     if (fuse) {
       const bool isWait = s.kind == GLOO_HIP_STEP_WAIT_RECV || s.kind == GLOO_HIP_STEP_WAIT_NOTIFY;
       const Step* t = isWait && i + 1 < steps.size() ? &steps[i + 1] : &s;
@@ -621,7 +711,8 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         if (kernelCopy_) {
           const unsigned grid = copySignalGrid(s.length * es_, copyBlocks_);
           checkRc(launchCopySignal(dst, src, s.length * es_, ctx_->counterDevicePtr(inst_, me, s.peer, s.slot),
-                                   seqOf(i, r, graph), ticket_, ticketOf(i, r, graph), epoch, grid, stream_),
+                                   seqOf(i, r, graph), ticket_ + (size_t)s.peer * GLOO_HIP_NUM_SLOTS + s.slot, epoch,
+                                   grid, stream_),
                   "copy_signal_kernel");
           break;
         }
@@ -699,6 +790,24 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
           checkRc(gloo_hip_reduce_multi(op_, dtype_, out0, srcs.data(), (int)srcs.size(), s.length, stream_),
                   "gloo_hip_reduce_multi");
         }
+        break;
+      }
+      case GLOO_HIP_STEP_FOLD_SRC:
+        foldSrcs.push_back(userOrArena(s.flags & GLOO_HIP_SRC_ARENA) + s.src_off * es_);
+        break;
+      case GLOO_HIP_STEP_FOLD: {
+        // one pass over every source, in the plan's order (plan.cc FOLD)
+        GLOO_AMD_ENFORCE(!foldSrcs.empty() && foldSrcs.size() <= GLOO_HIP_MAX_SRCS, "bad fold");
+        if (profiling_) GLOO_AMD_HIP_CHECK(hipEventRecord(event(), stream_));
+        checkRc(launchFold(op_, dtype_, userPtr(0) + s.dst_off * es_, foldSrcs.data(), (int)foldSrcs.size(),
+                           s.length, (s.flags & GLOO_HIP_FOLD_REVERSE) != 0, stream_),
+                "fold");
+        if (profiling_) {
+          GLOO_AMD_HIP_CHECK(hipEventRecord(event(), stream_));
+          reduceBytes_ += (foldSrcs.size() + 1.0) * s.length * es_;
+          reduceCount_ += foldSrcs.size() - 1;
+        }
+        foldSrcs.clear();
         break;
       }
       case GLOO_HIP_STEP_LOCAL_BCAST:

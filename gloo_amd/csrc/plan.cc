@@ -208,6 +208,96 @@ Plan planRingChunked(int rank, int size, uint64_t count, int nptrs) {
 }
 
 // ---------------------------------------------------------------------------
+// AllreduceRingChunked's result, mesh data movement.
+//
+// In the ring (planRingChunked above) the chunk pair q = {2q, 2q+1} starts
+// on rank q (copyChunkAtOffset(2 * rank), :102-103) and every later rank
+// q+1, q+2, ... reduces `local op incoming` (fn_->call(&ptrs_[0][offset],
+// inbox, ...), :148-151) on its still-untouched local chunk, so the ring
+// finishes the pair on rank o = q-1 with
+//     x_{q+P-1} op ( ... op (x_{q+2} op (x_{q+1} op x_q)))
+// and broadcasts it.  Here every rank sends its raw pair straight to o, all
+// pairs at once (one xGMI link per peer on an 8-GPU node), o evaluates the
+// same expression in one pass (FOLD, REVERSE: acc = s_k op acc, s_0 = x_q),
+// and sends the result to every rank: 2 hops instead of 2(P-1), every link
+// busy, identical bits.
+//
+// Arena: RS[p] = [2p * cs, +2cs) receives p's raw pair of MY range,
+//        AG[p] = [2(P+p) * cs, +2cs) receives owner p's finished range.
+// Inbox reuse needs no extra handshake: my next-run RS send to p is stream-
+// ordered after my WAIT on p's AG message, which p sends after its FOLD;
+// p's next AG send needs my next RS data, sent after my COPY out of AG[p].
+// ---------------------------------------------------------------------------
+Plan planRingChunkedMesh(int rank, int size, uint64_t count, int nptrs) {
+  if (size > GLOO_HIP_MAX_SRCS) throw std::invalid_argument("mesh ring-chunked needs size <= 8");
+  Plan p;
+  if (count == 0) return p;
+  const uint64_t chunks = 2ull * size;
+  const uint64_t cs = std::max<uint64_t>(256, (count + chunks - 1) / chunks);
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, 0, 0, 0, count));
+  if (size == 1) {
+    if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count));
+    return p;
+  }
+  // owner o finishes pair q = o + 1: elements [2q*cs, min(count, (2q+2)*cs))
+  auto range = [&](int owner, uint64_t& off, uint64_t& len) {
+    const uint64_t q = (uint64_t)((owner + 1) % size);
+    off = 2 * q * cs;
+    const uint64_t end = std::min<uint64_t>(count, off + 2 * cs);
+    len = off < end ? end - off : 0;
+  };
+  p.arena = 4ull * size * cs;
+  uint64_t myOff, myLen;
+  range(rank, myOff, myLen);
+  for (int d = 1; d < size; d++) {
+    const int peer = (rank + d) % size;
+    uint64_t o, l;
+    range(peer, o, l);
+    if (myLen) p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, peer, GLOO_HIP_SLOT_DATA0, 0, 2ull * peer * cs, 0, 2 * cs));
+    if (l) p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, peer, GLOO_HIP_SLOT_DATA1, 0, 2ull * (size + peer) * cs, 0,
+                                2 * cs));
+  }
+  // reduce-scatter: my raw piece of every other owner's range, all at once
+  for (int d = 1; d < size; d++) {
+    const int peer = (rank + d) % size;
+    uint64_t o, l;
+    range(peer, o, l);
+    if (l) p.steps.push_back(mk(GLOO_HIP_STEP_SEND, peer, GLOO_HIP_SLOT_DATA0, 0, 0, o, l));
+  }
+  if (myLen) {
+    for (int d = 1; d < size; d++)
+      p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, (rank + d) % size, GLOO_HIP_SLOT_DATA0));
+    // s_0 = x_q, s_1 = x_{q+1}, ..., s_{P-1} = x_o (local, in place)
+    const int q = (rank + 1) % size;
+    for (int k = 0; k < size; k++) {
+      const int src = (q + k) % size;
+      if (src == rank)
+        p.steps.push_back(mk(GLOO_HIP_STEP_FOLD_SRC, -1, 0, 0, 0, myOff, myLen));
+      else
+        p.steps.push_back(mk(GLOO_HIP_STEP_FOLD_SRC, src, 0, GLOO_HIP_SRC_ARENA, 0, 2ull * src * cs, myLen));
+    }
+    p.steps.push_back(mk(GLOO_HIP_STEP_FOLD, -1, 0, GLOO_HIP_FOLD_REVERSE, myOff, 0, myLen));
+    // allgather: the finished range to every rank, all at once
+    for (int d = 1; d < size; d++)
+      p.steps.push_back(mk(GLOO_HIP_STEP_SEND, (rank + d) % size, GLOO_HIP_SLOT_DATA1, 0, 0, myOff, myLen));
+  }
+  for (int d = 1; d < size; d++) {
+    const int peer = (rank + d) % size;
+    uint64_t o, l;
+    range(peer, o, l);
+    if (l) p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, peer, GLOO_HIP_SLOT_DATA1));
+  }
+  for (int d = 1; d < size; d++) {
+    const int peer = (rank + d) % size;
+    uint64_t o, l;
+    range(peer, o, l);
+    if (l) p.steps.push_back(mk(GLOO_HIP_STEP_COPY, -1, 0, GLOO_HIP_SRC_ARENA, o, 2ull * (size + peer) * cs, l));
+  }
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count));
+  return p;
+}
+
+// ---------------------------------------------------------------------------
 // AllreduceHalvingDoubling (gloo/allreduce_halving_doubling.h:67-362), GPU
 // twin gloo/cuda_allreduce_halving_doubling.cc:246-410.
 // ---------------------------------------------------------------------------
@@ -632,6 +722,7 @@ Plan makePlan(int algo, int rank, int size, uint64_t count, int nptrs, const std
   if (nptrs < 1) throw std::invalid_argument("need at least one pointer");
   switch (algo) {
     case GLOO_HIP_ALGO_RING_CHUNKED: return planRingChunked(rank, size, count, nptrs);
+    case GLOO_HIP_ALGO_RING_CHUNKED_MESH: return planRingChunkedMesh(rank, size, count, nptrs);
     case GLOO_HIP_ALGO_HALVING_DOUBLING: return planHalvingDoubling(rank, size, count, nptrs);
     case GLOO_HIP_ALGO_RING: return planRing(rank, size, count, nptrs);
     case GLOO_HIP_ALGO_LOCAL: return planLocal(rank, size, count, nptrs);

@@ -267,7 +267,9 @@ struct SrcList {
   const void* p[GLOO_HIP_MAX_SRCS];
 };
 
-template <class Tr, int OP, int UNROLL, int BLOCK>
+// REV: each new source is the left operand, acc = s_j op acc (the fold a ring
+// schedule performs when every hop computes `local op incoming`).
+template <class Tr, int OP, int UNROLL, int BLOCK, bool REV>
 __global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
     typename Tr::Storage* dst, SrcList srcs, int k, size_t n, size_t head) {
   using S = typename Tr::Storage;
@@ -281,7 +283,10 @@ __global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
       const size_t i = pass == 0 ? t : tail0 + t;
       if ((pass == 0 && t < head) || (pass == 1 && i < n)) {
         S acc = static_cast<const S*>(srcs.p[0])[i];
-        for (int j = 1; j < k; j++) acc = apply<Tr, OP>(acc, static_cast<const S*>(srcs.p[j])[i]);
+        for (int j = 1; j < k; j++) {
+          const S v = static_cast<const S*>(srcs.p[j])[i];
+          acc = REV ? apply<Tr, OP>(v, acc) : apply<Tr, OP>(acc, v);
+        }
         dst[i] = acc;
       }
     }
@@ -305,7 +310,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) r[u] = bload<kAuxNT>(rj, lane_off + u * BLOCK * 16, sj.mis);
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) acc[u] = apply_packet<Tr, OP>(acc[u], r[u]);
+    for (int u = 0; u < UNROLL; u++) acc[u] = REV ? apply_packet<Tr, OP>(r[u], acc[u]) : apply_packet<Tr, OP>(acc[u], r[u]);
   }
   const auto rd = make_rsrc(reinterpret_cast<const char*>(dst + head) + base, bytes);
 #pragma unroll
@@ -388,28 +393,48 @@ int launch_fused(int op, void* dst, const void* src, size_t n, const uint64_t* w
 // peer's inbox (over xGMI when it is another GPU).  Completion: every wave
 // drains (vmcnt 0), the workgroup syncs, one lane releases at system scope
 // and takes a ticket; the workgroup holding the last ticket of this launch
-// publishes `*flag = seq` (MI355X_MICROARCH.md: counter fan-in + flag).
-// Tickets only grow; the host passes the launch's first ticket.
+// resets the counter and publishes `*flag = seq` (MI355X_MICROARCH.md:
+// counter fan-in + flag).
 // ---------------------------------------------------------------------------
 constexpr int kCopyBlock = 512;
 constexpr int kCopyUnroll = 2;
+constexpr int kMaxCopies = kMaxCopyEntries;
 
-__global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(
-    char* dst, const char* src, size_t bytes, uint64_t* flag, Seq seqv, unsigned* ticket, Seq ticketv,
-    const uint64_t* epoch) {
-  // dst head up to a 16-B boundary and the ragged tail: block 0, bytewise
+// Several copies in one launch (the mesh schedules send to every peer at
+// once, one xGMI link each): entry j owns blocks [first[j], first[j+1]),
+// grid-strides over its bytes and, through its own ticket counter, the
+// workgroup finishing last publishes its flag.
+struct CopyList {
+  int n;
+  unsigned first[kMaxCopies + 1];
+  char* dst[kMaxCopies];
+  const char* src[kMaxCopies];
+  uint64_t bytes[kMaxCopies];
+  uint64_t* flag[kMaxCopies];
+  Seq seq[kMaxCopies];
+  unsigned* ticket[kMaxCopies];
+};
+
+__global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(CopyList L, const uint64_t* epoch) {
+  int j = 0;
+  while (j + 1 < L.n && blockIdx.x >= L.first[j + 1]) j++;
+  const unsigned lb = blockIdx.x - L.first[j], nb = L.first[j + 1] - L.first[j];
+  char* dst = L.dst[j];
+  const char* src = L.src[j];
+  const size_t bytes = L.bytes[j];
+  // dst head up to a 16-B boundary and the ragged tail: the entry's block 0, bytewise
   const size_t head = ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) < bytes
                           ? ((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15) : bytes;
   const size_t nvec = (bytes - head) / 16;
   const size_t tail0 = head + nvec * 16;
-  if (blockIdx.x == 0) {
+  if (lb == 0) {
     for (size_t i = threadIdx.x; i < head; i += kCopyBlock) dst[i] = src[i];
     for (size_t i = tail0 + threadIdx.x; i < bytes; i += kCopyBlock) dst[i] = src[i];
   }
   constexpr uint32_t kTileBytes = kCopyBlock * kCopyUnroll * 16;
   const size_t body = nvec * 16;
   const Src ss = src_of(src + head);
-  for (size_t base = (size_t)blockIdx.x * kTileBytes; base < body; base += (size_t)gridDim.x * kTileBytes) {
+  for (size_t base = (size_t)lb * kTileBytes; base < body; base += (size_t)nb * kTileBytes) {
     const uint32_t n = (uint32_t)((body - base) < kTileBytes ? (body - base) : kTileBytes);
     const auto rs = make_rsrc(ss.base + base, n + ss.mis);
     const auto rd = make_rsrc(dst + head + base, n);
@@ -426,11 +451,14 @@ __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint64_t ep = epoch ? *epoch : 0;
-    const unsigned ticketBase = (unsigned)(ticketv.base + ep * ticketv.perRun);
-    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (t == ticketBase + gridDim.x - 1) {
+    const unsigned t = __hip_atomic_fetch_add(L.ticket[j], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == nb - 1) {
+      // last workgroup of this entry: reset the counter for the next launch
+      // (launches on one channel's counter are stream-ordered), publish
+      __hip_atomic_store(L.ticket[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      __hip_atomic_store(flag, seqv.base + ep * seqv.perRun, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(L.flag[j], L.seq[j].base + ep * L.seq[j].perRun, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -491,7 +519,7 @@ int launch3(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
   return launch_vec<Tr, OP, kUnroll, kVecBlock, kAuxNT, kAuxNT>(c, a, b, n, head, s);
 }
 
-template <class Tr, int OP>
+template <class Tr, int OP, bool REV = false>
 int launch_multi(void* dst, const void* const* srcs, int k, size_t n, hipStream_t s) {
   using S = typename Tr::Storage;
   if (n == 0) return GLOO_HIP_OK;
@@ -511,7 +539,7 @@ int launch_multi(void* dst, const void* const* srcs, int k, size_t n, hipStream_
   const size_t nvec = (n - head) / kV;
   size_t grid = ceil_div(nvec, (size_t)kVecBlock * kMultiUnroll);
   if (grid == 0) grid = 1;
-  reduce_multi_vec_kernel<Tr, OP, kMultiUnroll, kVecBlock><<<dim3((unsigned)grid), dim3(kVecBlock), 0, s>>>(
+  reduce_multi_vec_kernel<Tr, OP, kMultiUnroll, kVecBlock, REV><<<dim3((unsigned)grid), dim3(kVecBlock), 0, s>>>(
       static_cast<S*>(dst), list, k, n, head);
   return check_launch("reduce_multi_vec_kernel");
 }
@@ -527,13 +555,13 @@ int by_op3(int op, void* c, const void* a, const void* b, size_t n, hipStream_t 
   }
 }
 
-template <class Tr>
+template <class Tr, bool REV = false>
 int by_op_multi(int op, void* d, const void* const* srcs, int k, size_t n, hipStream_t s) {
   switch (op) {
-    case GLOO_HIP_SUM: return launch_multi<Tr, GLOO_HIP_SUM>(d, srcs, k, n, s);
-    case GLOO_HIP_PRODUCT: return launch_multi<Tr, GLOO_HIP_PRODUCT>(d, srcs, k, n, s);
-    case GLOO_HIP_MAX: return launch_multi<Tr, GLOO_HIP_MAX>(d, srcs, k, n, s);
-    case GLOO_HIP_MIN: return launch_multi<Tr, GLOO_HIP_MIN>(d, srcs, k, n, s);
+    case GLOO_HIP_SUM: return launch_multi<Tr, GLOO_HIP_SUM, REV>(d, srcs, k, n, s);
+    case GLOO_HIP_PRODUCT: return launch_multi<Tr, GLOO_HIP_PRODUCT, REV>(d, srcs, k, n, s);
+    case GLOO_HIP_MAX: return launch_multi<Tr, GLOO_HIP_MAX, REV>(d, srcs, k, n, s);
+    case GLOO_HIP_MIN: return launch_multi<Tr, GLOO_HIP_MIN, REV>(d, srcs, k, n, s);
     default: return set_error(GLOO_HIP_EINVAL_OP, "unknown reduction op");
   }
 }
@@ -555,19 +583,20 @@ int dispatch3(int op, int dtype, void* c, const void* a, const void* b, size_t n
   }
 }
 
+template <bool REV = false>
 int dispatch_multi(int op, int dtype, void* d, const void* const* srcs, int k, size_t n,
                    hipStream_t s) {
   switch (dtype) {
-    case GLOO_HIP_I8: return by_op_multi<TrI8>(op, d, srcs, k, n, s);
-    case GLOO_HIP_U8: return by_op_multi<TrU8>(op, d, srcs, k, n, s);
-    case GLOO_HIP_I32: return by_op_multi<TrI32>(op, d, srcs, k, n, s);
-    case GLOO_HIP_U32: return by_op_multi<TrU32>(op, d, srcs, k, n, s);
-    case GLOO_HIP_I64: return by_op_multi<TrI64>(op, d, srcs, k, n, s);
-    case GLOO_HIP_U64: return by_op_multi<TrU64>(op, d, srcs, k, n, s);
-    case GLOO_HIP_F16: return by_op_multi<TrF16>(op, d, srcs, k, n, s);
-    case GLOO_HIP_BF16: return by_op_multi<TrBF16>(op, d, srcs, k, n, s);
-    case GLOO_HIP_F32: return by_op_multi<TrF32>(op, d, srcs, k, n, s);
-    case GLOO_HIP_F64: return by_op_multi<TrF64>(op, d, srcs, k, n, s);
+    case GLOO_HIP_I8: return by_op_multi<TrI8, REV>(op, d, srcs, k, n, s);
+    case GLOO_HIP_U8: return by_op_multi<TrU8, REV>(op, d, srcs, k, n, s);
+    case GLOO_HIP_I32: return by_op_multi<TrI32, REV>(op, d, srcs, k, n, s);
+    case GLOO_HIP_U32: return by_op_multi<TrU32, REV>(op, d, srcs, k, n, s);
+    case GLOO_HIP_I64: return by_op_multi<TrI64, REV>(op, d, srcs, k, n, s);
+    case GLOO_HIP_U64: return by_op_multi<TrU64, REV>(op, d, srcs, k, n, s);
+    case GLOO_HIP_F16: return by_op_multi<TrF16, REV>(op, d, srcs, k, n, s);
+    case GLOO_HIP_BF16: return by_op_multi<TrBF16, REV>(op, d, srcs, k, n, s);
+    case GLOO_HIP_F32: return by_op_multi<TrF32, REV>(op, d, srcs, k, n, s);
+    case GLOO_HIP_F64: return by_op_multi<TrF64, REV>(op, d, srcs, k, n, s);
     default: return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
   }
 }
@@ -580,11 +609,40 @@ unsigned copySignalGrid(size_t bytes, unsigned maxBlocks) {
   return (unsigned)(g == 0 ? 1 : g);
 }
 
-int launchCopySignal(void* dst, const void* src, size_t bytes, uint64_t* flag, Seq seq, unsigned* ticket,
-                     Seq ticketv, const uint64_t* epoch, unsigned grid, hipStream_t s) {
-  copy_signal_kernel<<<grid, kCopyBlock, 0, s>>>(static_cast<char*>(dst), static_cast<const char*>(src), bytes,
-                                                 flag, seq, ticket, ticketv, epoch);
+int launchCopySignalMulti(const CopyDesc* d, int n, const uint64_t* epoch, hipStream_t s) {
+  if (n < 1 || n > kMaxCopies) return set_error(GLOO_HIP_EINVAL_ARG, "copy list size out of range");
+  CopyList L;
+  memset(&L, 0, sizeof(L));
+  L.n = n;
+  unsigned total = 0;
+  for (int j = 0; j < n; j++) {
+    if (!d[j].flag || !d[j].ticket || d[j].blocks == 0) return set_error(GLOO_HIP_EINVAL_ARG, "bad copy entry");
+    L.first[j] = total;
+    total += d[j].blocks;
+    L.dst[j] = static_cast<char*>(d[j].dst);
+    L.src[j] = static_cast<const char*>(d[j].src);
+    L.bytes[j] = d[j].bytes;
+    L.flag[j] = d[j].flag;
+    L.seq[j] = d[j].seq;
+    L.ticket[j] = d[j].ticket;
+  }
+  L.first[n] = total;
+  copy_signal_kernel<<<total, kCopyBlock, 0, s>>>(L, epoch);
   return check_launch("copy_signal_kernel");
+}
+
+int launchCopySignal(void* dst, const void* src, size_t bytes, uint64_t* flag, Seq seq, unsigned* ticket,
+                     const uint64_t* epoch, unsigned grid, hipStream_t s) {
+  CopyDesc d{dst, src, bytes, flag, seq, ticket, grid};
+  return launchCopySignalMulti(&d, 1, epoch, s);
+}
+
+int launchFold(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n, bool reverse,
+               hipStream_t s) {
+  if (k < 1 || k > GLOO_HIP_MAX_SRCS) return set_error(GLOO_HIP_EINVAL_ARG, "source count out of range");
+  if (n == 0) return GLOO_HIP_OK;
+  return reverse ? dispatch_multi<true>(op, dtype, dst, srcs, k, n, s)
+                 : dispatch_multi<false>(op, dtype, dst, srcs, k, n, s);
 }
 
 // Internal entry for the plan executor (see gloo_amd/signal.h).

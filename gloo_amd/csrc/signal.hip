@@ -43,7 +43,46 @@ __global__ __launch_bounds__(64) void wait_kernel(const uint64_t* flag, uint64_t
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
+struct WaitList {
+  int n;
+  const uint64_t* flag[kMaxWaitEntries];
+  Seq target[kMaxWaitEntries];
+};
+
+__global__ __launch_bounds__(64) void wait_multi_kernel(WaitList w, const uint64_t* epoch, uint64_t timeout_ticks,
+                                                        uint32_t* err) {
+  const int j = threadIdx.x;
+  if (j < w.n) {
+    const uint64_t target = seqValue(w.target[j].base, w.target[j].perRun, epoch);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(w.flag[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+      __builtin_amdgcn_s_sleep(8);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
 }  // namespace
+
+hipError_t launchWaitMulti(const uint64_t* const* flags, const Seq* targets, int n, const uint64_t* epoch,
+                           uint64_t timeoutTicks, uint32_t* err, hipStream_t stream) {
+  for (int i = 0; i < n; i += kMaxWaitEntries) {
+    WaitList w;
+    w.n = n - i < kMaxWaitEntries ? n - i : kMaxWaitEntries;
+    for (int j = 0; j < w.n; j++) {
+      w.flag[j] = flags[i + j];
+      w.target[j] = targets[i + j];
+    }
+    wait_multi_kernel<<<1, 64, 0, stream>>>(w, epoch, timeoutTicks, err);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
 
 hipError_t launchEpochBump(uint64_t* epoch, hipStream_t stream) {
   epoch_kernel<<<1, 64, 0, stream>>>(epoch, 0, 0);

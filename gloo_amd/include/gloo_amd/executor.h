@@ -81,6 +81,7 @@ class PlanExecutor {
   void run();
 
   const Plan& plan() const { return plan_; }
+  int planAlgorithm() const { return planAlgo_; }
   hipStream_t stream() const { return stream_; }
   bool deviceSignalling() const { return deviceSignal_; }
   bool fineGrainedArena() const { return fineArena_; }
@@ -113,11 +114,13 @@ class PlanExecutor {
   void tryCapture(uint64_t r);
   void dropGraph();
   Seq seqOf(size_t step, uint64_t r, bool graph) const;
-  Seq ticketOf(size_t step, uint64_t r, bool graph) const;
+  hipStream_t auxStream(size_t k);
+  hipEvent_t forkEvent(size_t k);
   char* userPtr(int j) const { return static_cast<char*>(ptrs_[j]); }
 
   std::shared_ptr<Context> ctx_;
   int algo_, op_, dtype_;
+  int planAlgo_;  // the plan executed (RING_CHUNKED may run as RING_CHUNKED_MESH)
   size_t es_;
   std::vector<void*> ptrs_;     // outputs (the reference's ptrs_ / out)
   std::vector<void*> inputs_;   // separate inputs (new-style allreduce), may be empty
@@ -149,10 +152,8 @@ class PlanExecutor {
   // with base = baseline + j + 1 - perRun precomputed per step (StepSeq).
   struct StepSeq {
     uint64_t base = 0, perRun = 0;
-    uint32_t ticket = 0;  // kernel-copy SEND: first ticket within the run
   };
   std::vector<StepSeq> stepSeq_;
-  uint32_t ticketsPerRun_ = 0;
   uint64_t runs_ = 0;          // runs enqueued so far
   uint64_t* epoch_ = nullptr;  // device: the run being executed (graph replay)
   hipGraphExec_t graphExec_ = nullptr;
@@ -163,7 +164,10 @@ class PlanExecutor {
   bool fineArena_ = false;     // inbox arena in fine-grained (cross-device coherent) memory
   bool kernelCopy_ = false;    // SEND = copy_signal_kernel instead of hipMemcpyAsync + signal
   unsigned copyBlocks_ = 64;
-  unsigned* ticket_ = nullptr; // completion tickets of copy_signal_kernel (device memory)
+  bool batchKernelCopy_ = true;  // a batch of SENDs = one multi-destination copy kernel
+  unsigned* ticket_ = nullptr;   // copy_signal_kernel tickets, one counter per (peer, slot)
+  std::vector<hipStream_t> aux_;        // forked SEND batches (memcpy engine)
+  std::vector<hipEvent_t> forkEvents_;
   double waitSeconds_ = 0;
   bool profiling_ = false;
   std::vector<hipEvent_t> events_;

@@ -46,12 +46,37 @@ int launchFusedSmall(int op, int dtype, void* dst, const void* src, size_t n, co
 
 // Peer copy + fused arrival signal (reduce.hip): `grid` workgroups copy
 // `bytes` from src (local) to dst (a peer's inbox); the workgroup that takes
-// the launch's last ticket publishes *flag = seq.  Tickets are 32-bit and
-// only grow: this launch's first ticket is ticket.value(epoch) (mod 2^32).
-// copySignalGrid() sizes the grid (capped at maxBlocks: a link, not HBM,
-// bounds a peer copy).
+// the launch's last ticket resets the counter (zero between launches; one
+// counter per channel, launches on it stream-ordered) and publishes *flag =
+// seq.  copySignalGrid() sizes the grid (capped at maxBlocks: a link, not
+// HBM, bounds a peer copy).
 unsigned copySignalGrid(size_t bytes, unsigned maxBlocks);
 int launchCopySignal(void* dst, const void* src, size_t bytes, uint64_t* flag, Seq seq, unsigned* ticketCounter,
-                     Seq ticket, const uint64_t* epoch, unsigned grid, hipStream_t stream);
+                     const uint64_t* epoch, unsigned grid, hipStream_t stream);
+
+// Up to kMaxCopyEntries such copies in ONE launch, all in flight together
+// (a mesh schedule's sends to every peer: one xGMI link each).
+constexpr int kMaxCopyEntries = 8;
+struct CopyDesc {
+  void* dst;
+  const void* src;
+  size_t bytes;
+  uint64_t* flag;
+  Seq seq;
+  unsigned* ticket;  // this entry's ticket counter (zero at launch)
+  unsigned blocks;   // copySignalGrid(bytes, ...)
+};
+int launchCopySignalMulti(const CopyDesc* d, int n, const uint64_t* epoch, hipStream_t stream);
+
+// Wait for several flags in one launch (one lane per flag), then ONE
+// system-scope acquire.  n <= kMaxWaitEntries.
+constexpr int kMaxWaitEntries = 16;
+hipError_t launchWaitMulti(const uint64_t* const* flags, const Seq* targets, int n, const uint64_t* epoch,
+                           uint64_t timeoutTicks, uint32_t* err, hipStream_t stream);
+
+// Multi-source fold dst = s0 op s1 op ... (left fold; reverse: acc = s_j op
+// acc), k <= GLOO_HIP_MAX_SRCS, one pass.  Returns a gloo_hip status.
+int launchFold(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n, bool reverse,
+               hipStream_t stream);
 
 }  // namespace gloo_amd

@@ -132,6 +132,13 @@ typedef enum {
   GLOO_HIP_ALGO_REDUCE_SCATTER = 4,   /* gloo/reduce_scatter.h (HD)           */
   GLOO_HIP_ALGO_ALLREDUCE_RING = 5,   /* new-style gloo::allreduce(opts), RING
                                          (gloo/allreduce.cc:147-392)          */
+  /* AllreduceRingChunked's RESULT with mesh data movement: each chunk pair
+   * goes straight from every rank to the rank where the ring finishes it,
+   * over all xGMI links at once, and is folded there in the ring's exact
+   * association and operand order (bit-identical), then sent to every rank.
+   * 2 <= size <= GLOO_HIP_MAX_SRCS.  RING_CHUNKED executes as this plan when
+   * GLOO_AMD_RING_MESH selects it. */
+  GLOO_HIP_ALGO_RING_CHUNKED_MESH = 6,
 } gloo_hip_algo_t;
 
 typedef enum {
@@ -145,6 +152,10 @@ typedef enum {
   GLOO_HIP_STEP_WAIT_SEND = 7,   /* wait until our last send to (peer, slot) has completed  */
   GLOO_HIP_STEP_LOCAL_REDUCE = 8,/* ptrs[0] = ((ptrs[0] op ptrs[1]) op ...), length elts    */
   GLOO_HIP_STEP_LOCAL_BCAST = 9, /* ptrs[i] = ptrs[0] for i >= 1, length elements           */
+  GLOO_HIP_STEP_FOLD_SRC = 10,   /* next source of the following FOLD: src[src_off..]        */
+  GLOO_HIP_STEP_FOLD = 11,       /* user[dst_off, +length) = fold of the pending FOLD_SRCs:
+                                    acc = s0; acc = acc op s_k (or s_k op acc with
+                                    GLOO_HIP_FOLD_REVERSE), k = 1.. in order             */
 } gloo_hip_step_kind_t;
 
 /* Message channels between a pair of ranks (the reference's slot roles). */
@@ -165,6 +176,8 @@ typedef enum {
  * output 0 (new-style allreduce; one input = copy), instead of folding the
  * outputs into output 0. */
 #define GLOO_HIP_FROM_INPUTS 4
+/* FOLD: each new source is the LEFT operand (acc = s_k op acc). */
+#define GLOO_HIP_FOLD_REVERSE 8
 
 typedef struct {
   int32_t kind;

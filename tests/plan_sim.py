@@ -17,9 +17,10 @@ import numpy as np
 import oracle
 
 KIND = dict(DECL_RECV=0, SEND=1, WAIT_RECV=2, REDUCE=3, COPY=4, NOTIFY=5, WAIT_NOTIFY=6,
-            WAIT_SEND=7, LOCAL_REDUCE=8, LOCAL_BCAST=9)
-ALGO = dict(ring_chunked=0, halving_doubling=1, ring=2, local=3, reduce_scatter=4, allreduce_new=5)
-SRC_ARENA, DST_ARENA, FROM_INPUTS = 1, 2, 4
+            WAIT_SEND=7, LOCAL_REDUCE=8, LOCAL_BCAST=9, FOLD_SRC=10, FOLD=11)
+ALGO = dict(ring_chunked=0, halving_doubling=1, ring=2, local=3, reduce_scatter=4, allreduce_new=5,
+            ring_chunked_mesh=6)
+SRC_ARENA, DST_ARENA, FROM_INPUTS, FOLD_REVERSE = 1, 2, 4, 8
 
 
 class Step(ctypes.Structure):
@@ -57,14 +58,19 @@ class ProtocolError(AssertionError):
     pass
 
 
-def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0):
+def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, runs=1):
     """inputs: [P][k][n] array of the dtype's storage type (the outputs'
     initial contents); ins: optional [P][kin][n] separate inputs (new-style
-    allreduce).  Returns the outputs [P][k][n]."""
+    allreduce).  runs > 1 executes the plan back to back that many times
+    (each run reduces the previous run's outputs), with no barrier between
+    runs, as repeated Algorithm::run() calls do.  Returns the outputs."""
     P, k, n = inputs.shape
     nin = 0 if ins is None else ins.shape[1]
     es = inputs.dtype.itemsize
     plans = [get_plan(algo, r, P, n, k, recv, nin=nin, elem_size=es, max_seg=max_seg) for r in range(P)]
+    if runs > 1:
+        plans = [([st for st in steps] + [st for _ in range(runs - 1) for st in steps
+                                          if st.kind != KIND["DECL_RECV"]], a) for steps, a in plans]
     user = [[inputs[r, j].copy() for j in range(k)] for r in range(P)]
     arena = [np.zeros(max(1, a), dtype=inputs.dtype) for _, a in plans]
     regions = {}
@@ -76,6 +82,7 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0):
                     raise ProtocolError(f"region {key} declared twice")
                 regions[key] = (s.dst_off, s.length)
     sent, consumed = {}, {}
+    pending = [[] for _ in range(P)]  # FOLD sources, read when the FOLD executes
     pc = [0] * P
     rng = random.Random(seed)
 
@@ -148,6 +155,16 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0):
             lo, hi = s.dst_off, s.dst_off + s.length
             for j in range(1, k):
                 user[r][j][lo:hi] = user[r][0][lo:hi]
+        elif K == KIND["FOLD_SRC"]:
+            pending[r].append((bool(s.flags & SRC_ARENA), s.src_off))
+        elif K == KIND["FOLD"]:
+            srcs = [space(r, a)[o:o + s.length].copy() for a, o in pending[r]]
+            pending[r] = []
+            acc = srcs[0]
+            for x in srcs[1:]:
+                acc = oracle.reduce3(op, dtype, x, acc) if s.flags & FOLD_REVERSE else \
+                    oracle.reduce3(op, dtype, acc, x)
+            user[r][0][s.dst_off:s.dst_off + s.length] = acc
         else:
             raise ProtocolError(f"unknown step kind {K}")
     for key in sent:

@@ -167,6 +167,9 @@ np.save(out, buf.cpu().numpy().view(np.float32))
 
 
 @pytest.mark.parametrize("algo,P,env", [
+    ("ring_chunked", 8, {"GLOO_AMD_TEST_N": "4194304"}),      # mesh, 16 MiB/rank: unfused, graph replay
+    ("ring_chunked", 8, {"GLOO_AMD_TEST_N": "4194304", "GLOO_AMD_COPY": "memcpy"}),
+    ("ring_chunked", 8, {"GLOO_AMD_TEST_N": "4194304", "GLOO_AMD_RING_MESH": "0"}),
     ("ring_chunked", 4, {}),                                  # auto: device-side signalling
     ("halving_doubling", 4, {}),
     ("halving_doubling", 5, {}),                              # non-power-of-2 binary blocks
@@ -177,7 +180,7 @@ np.save(out, buf.cpu().numpy().view(np.float32))
 def test_processes_ipc(torch, algo, P, env):
     """Ranks as processes: inbox arenas exchanged as HIP IPC handles through a
     FileStore; run twice (x2 of the sum, exact for these integers)."""
-    n = 100_003
+    n = int(env.get("GLOO_AMD_TEST_N", 100_003))
     x = np.array([np.arange(n, dtype=np.float32) * 0 + r + 1 for r in range(P)], dtype=np.float32)
     with tempfile.TemporaryDirectory() as d:
         inp = os.path.join(d, "in.npy")
@@ -197,10 +200,14 @@ def test_processes_ipc(torch, algo, P, env):
             assert (y == P * total).all(), (r, y[:5])
 
 
-def test_profiling_stats(torch):
+@pytest.mark.parametrize("mesh", ["0", "1"])
+def test_profiling_stats(torch, monkeypatch, mesh):
     """Measurement hook: every chunk reduction is timed with HIP events and
-    the algorithmic bytes add up to the reduce-scatter part of the schedule."""
+    the algorithmic bytes add up to the reduce-scatter part of the schedule
+    (ring: 2(P-1) two-operand reductions of n/2P; mesh: one P-source fold of
+    n/P, i.e. P-1 reductions and (P+1) n/P elements moved)."""
     import gloo_amd
+    monkeypatch.setenv("GLOO_AMD_RING_MESH", mesh)
     P, n = 4, 1 << 20
     url = "mem:" + uuid.uuid4().hex
     bufs = [torch.ones(n, device=f"cuda:{dev_of(torch, r)}") for r in range(P)]
@@ -224,9 +231,13 @@ def test_profiling_stats(torch):
         t.join()
     for r in range(P):
         st = out[r]
-        # 2(P-1) chunks of n/(2P) elements reduced per rank
-        assert st["reductions"] == 2 * (P - 1)
-        assert st["reduce_bytes"] == 3 * 4 * (n // (2 * P)) * 2 * (P - 1)
+        if mesh == "0":
+            # 2(P-1) chunks of n/(2P) elements reduced per rank
+            assert st["reductions"] == 2 * (P - 1)
+            assert st["reduce_bytes"] == 3 * 4 * (n // (2 * P)) * 2 * (P - 1)
+        else:
+            assert st["reductions"] == P - 1
+            assert st["reduce_bytes"] == (P + 1) * 4 * (n // P)
         assert st["reduce_s"] > 0
     assert float(bufs[0][0]) == P
 
@@ -473,6 +484,17 @@ print("MODES", json.dumps(modes))
     ("halving_doubling/sum/f32/P5/k1/n10007", {}, False),  # auto: every step fused -> eager is faster
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_FUSE_BYTES": "0"}, False),
     ("ring_chunked/sum/f32/P3/k1/n1000", {"GLOO_AMD_SIGNAL": "host", "GLOO_AMD_GRAPH": "1"}, False),
+    # ring-chunked runs as the mesh plan by default: batched sends (one
+    # multi-destination copy kernel, or forked hipMemcpyAsync streams),
+    # batched waits, one P-source fold
+    ("ring_chunked/sum/f32/P8/k1/n10007", {}, False),
+    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_COPY": "memcpy"}, False),
+    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, True),
+    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_COPY": "memcpy"}, True),
+    ("ring_chunked/max/f32/P5/k1/n999", {"GLOO_AMD_SIGNAL": "host"}, False),
+    ("ring_chunked/product/f32/P3/k1/n777", {"GLOO_AMD_COPY_BLOCKS": "1", "GLOO_AMD_FUSE_BYTES": "0"}, True),
+    ("ring_chunked/sum/f32/P2/k1/n1000", {}, False),
+    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_RING_MESH": "0", "GLOO_AMD_GRAPH": "1"}, True),
 ])
 def test_processes_graph_replay(torch, golden_sched, case, env, graph):
     """hipGraph replay: run 1 is enqueued eagerly, run 2 captures the plan and

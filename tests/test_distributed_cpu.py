@@ -23,8 +23,9 @@ import os, sys
 sys.path.insert(0, os.environ["GLOO_AMD_ROOT"]); sys.path.insert(0, os.path.join(os.environ["GLOO_AMD_ROOT"], "tests"))
 import numpy as np, torch, torch.distributed as dist
 import oracle
-from plan_sim import KIND, SRC_ARENA, DST_ARENA, get_plan
+from plan_sim import KIND, SRC_ARENA, DST_ARENA, FOLD_REVERSE, get_plan
 rank, size, port, case, outdir = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
+plan_algo = sys.argv[6] if len(sys.argv) > 6 else None
 dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=size)
 g = np.load(os.path.join(os.environ["GLOO_AMD_ROOT"], "tests", "golden", "sched_golden.npz"))
 algo, op, dtype = case.split("/")[:3]
@@ -33,7 +34,8 @@ recv = g[case + "/recv"] if algo == "reduce_scatter" else None
 if algo == "reduce_scatter":
     x = x[:, None, :]
 P, k, n = x.shape
-steps, arena_n = get_plan(algo, rank, P, n, k, recv)
+steps, arena_n = get_plan(plan_algo or algo, rank, P, n, k, recv)
+fold = []
 user = [x[rank, j].copy() for j in range(k)]
 arena = np.zeros(max(1, arena_n), dtype=x.dtype)
 regions = {(s.peer, s.slot): (s.dst_off, s.length) for s in steps if s.kind == KIND["DECL_RECV"]}
@@ -71,6 +73,14 @@ for s in steps:
     elif K == KIND["LOCAL_BCAST"]:
         for j in range(1, k):
             user[j][:s.length] = user[0][:s.length]
+    elif K == KIND["FOLD_SRC"]:
+        fold.append((arena if s.flags & SRC_ARENA else user[0])[s.src_off:s.src_off + s.length].copy())
+    elif K == KIND["FOLD"]:
+        acc = fold[0]
+        for v in fold[1:]:
+            acc = oracle.reduce3(op, dtype, v, acc) if s.flags & FOLD_REVERSE else oracle.reduce3(op, dtype, acc, v)
+        user[0][s.dst_off:s.dst_off + s.length] = acc
+        fold = []
 for p in pending:
     p.wait()
 dist.barrier()
@@ -87,14 +97,17 @@ def free_port():
     return p
 
 
-CASES = ["ring_chunked/sum/f32/P2/k1/n1000", "halving_doubling/sum/f32/P2/k1/n1000",
-         "halving_doubling/sum/f32/P3/k1/n1000", "ring_chunked/sum/f32/P3/k2/n1000",
-         "reduce_scatter/sum/f32/P2/n100", "reduce_scatter/sum/f32/P3/n10007",
-         "ring/sum/f32/P3/k1/n1000"]
+CASES = [("ring_chunked/sum/f32/P2/k1/n1000", None), ("halving_doubling/sum/f32/P2/k1/n1000", None),
+         ("halving_doubling/sum/f32/P3/k1/n1000", None), ("ring_chunked/sum/f32/P3/k2/n1000", None),
+         ("reduce_scatter/sum/f32/P2/n100", None), ("reduce_scatter/sum/f32/P3/n10007", None),
+         ("ring/sum/f32/P3/k1/n1000", None),
+         # the reference ring's bytes from the mesh plan (two all-to-all hops)
+         ("ring_chunked/sum/f32/P3/k2/n1000", "ring_chunked_mesh"),
+         ("ring_chunked/max/f32/P5/k1/n999", "ring_chunked_mesh")]
 
 
-@pytest.mark.parametrize("case", CASES)
-def test_plans_over_gloo_processes(golden_sched, case):
+@pytest.mark.parametrize("case,plan_algo", CASES)
+def test_plans_over_gloo_processes(golden_sched, case, plan_algo):
     algo = case.split("/")[0]
     P = int(case.split("/")[3][1:])
     with tempfile.TemporaryDirectory() as d:
@@ -102,7 +115,8 @@ def test_plans_over_gloo_processes(golden_sched, case):
         open(w, "w").write(PLAN_WORKER)
         env = dict(os.environ, GLOO_AMD_ROOT=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
         port = str(free_port())
-        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), port, case, d], env=env)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), port, case, d] +
+                                  ([plan_algo] if plan_algo else []), env=env)
                  for r in range(P)]
         assert [p.wait(timeout=240) for p in procs] == [0] * P
         outs = [np.load(os.path.join(d, f"out{r}.npy")) for r in range(P)]

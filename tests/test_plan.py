@@ -135,3 +135,64 @@ def test_new_style_allreduce_closed_form(P, n, seg):
     want = np.arange(n, dtype=np.float64) * P * P * 2 + 2 * P * (P - 1) / 2
     for r in range(P):
         assert (y[r, 0] == want).all() and (y[r, 1] == want).all()
+
+
+def _ring_chunked_keys():
+    return [k for k in _keys() if k.startswith("ring_chunked/") and int(k.split("/")[3][1:]) <= 8]
+
+
+@pytest.mark.parametrize("case", _ring_chunked_keys())
+def test_mesh_ring_chunked_matches_reference_golden(golden_sched, case):
+    """RING_CHUNKED_MESH (plan.cc planRingChunkedMesh) reproduces the
+    reference AllreduceRingChunked's bytes although the data moves in two
+    all-to-all hops instead of around the ring."""
+    op, dtype = case.split("/")[1:3]
+    x, want = golden_sched[case + "/in"], golden_sched[case + "/out"]
+    for seed in (0, 1, 2):
+        y = simulate("ring_chunked_mesh", op, dtype, x, seed=seed)
+        for r in range(y.shape[0]):
+            for j in range(y.shape[1]):
+                assert (y[r, j].view(np.uint8) == want.view(np.uint8)).all(), (seed, r, j)
+
+
+@pytest.mark.parametrize("op", ["sum", "product", "max", "min"])
+@pytest.mark.parametrize("dtype", ["f32", "f16", "bf16", "i32"])
+@pytest.mark.parametrize("P,n", [(2, 1000), (3, 5000), (5, 999), (7, 4099), (8, 100003), (8, 300), (6, 1)])
+def test_mesh_equals_ring_chunked_bitwise(op, dtype, P, n):
+    """Mesh vs ring plan on random data incl. NaN / signed zeros (max/min are
+    not commutative there, so operand order matters), over THREE back-to-back
+    runs under random interleavings: identical bytes, and no inbox is
+    overwritten before its fold has read it."""
+    rng = np.random.default_rng(P * 1000 + n)
+    if dtype == "i32":
+        x = rng.integers(-2**31, 2**31 - 1, size=(P, 1, n), dtype=np.int64).astype(np.int32)
+    else:
+        f = rng.standard_normal((P, 1, n)).astype(np.float32)
+        f[rng.random(f.shape) < 0.02] = np.nan
+        f[rng.random(f.shape) < 0.02] = -0.0
+        f[rng.random(f.shape) < 0.02] = 0.0
+        if dtype == "f32":
+            x = f
+        elif dtype == "f16":
+            x = f.astype(np.float16).view(np.uint16)
+        else:
+            x = (f.view(np.uint32) >> 16).astype(np.uint16)
+    want = simulate("ring_chunked", op, dtype, x, seed=7, runs=3)
+    for seed in (0, 1):
+        got = simulate("ring_chunked_mesh", op, dtype, x, seed=seed, runs=3)
+        assert (got.view(np.uint8) == want.view(np.uint8)).all(), seed
+
+
+@pytest.mark.parametrize("P,k", [(3, 2), (4, 3)])
+def test_mesh_multi_pointer(golden_sched, P, k):
+    """Several local pointers: local fold, mesh exchange, local broadcast."""
+    rng = np.random.default_rng(P + k)
+    x = rng.standard_normal((P, k, 2049)).astype(np.float32)
+    want = simulate("ring_chunked", "sum", "f32", x, seed=0)
+    got = simulate("ring_chunked_mesh", "sum", "f32", x, seed=1, runs=1)
+    assert (got.view(np.uint8) == want.view(np.uint8)).all()
+
+
+def test_mesh_rejects_more_than_8_ranks():
+    with pytest.raises(RuntimeError):
+        get_plan("ring_chunked_mesh", 0, 9, 1000)
