@@ -233,7 +233,8 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
     rank's time per allreduce, bus bandwidth, and the reduction kernels' own
     GiB/s measured with HIP events while the exchange runs (per-GPU
     efficiency vs the 1-GPU figure).
-    Config 4: halving-doubling at 1 KiB / 64 KiB / 1 MiB / 64 MiB per rank."""
+    Config 4: halving-doubling at 1 KiB / 64 KiB / 1 MiB / 64 MiB per rank,
+    derived mesh plan vs the reference's exchange route."""
     import tempfile
     obj = [tempfile.mkdtemp(prefix="gloo_amd_bench_")] if rank == 0 else [None]
     dist.broadcast_object_list(obj, src=0)
@@ -361,10 +362,14 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
                                                  3)})
         return summary
 
-    hd_variants = {"memcpy_graph": {"GLOO_AMD_COPY": "memcpy"},
-                   "kernel_graph": {"GLOO_AMD_COPY": "kernel"},
-                   "memcpy_eager": {"GLOO_AMD_COPY": "memcpy", "GLOO_AMD_GRAPH": "0"},
-                   "kernel_eager": {"GLOO_AMD_COPY": "kernel", "GLOO_AMD_GRAPH": "0"}}
+    # mesh = the derived mesh plan (default); reference_route = the
+    # reference's halving/doubling exchange (GLOO_AMD_MESH=0)
+    hd_variants = {"mesh": {},
+                   "mesh_memcpy_forked": {"GLOO_AMD_COPY": "memcpy"},
+                   "mesh_eager": {"GLOO_AMD_GRAPH": "0"},
+                   "reference_route": {"GLOO_AMD_MESH": "0"},
+                   "reference_route_kernel_copy": {"GLOO_AMD_MESH": "0", "GLOO_AMD_COPY": "kernel"},
+                   "reference_route_eager": {"GLOO_AMD_MESH": "0", "GLOO_AMD_GRAPH": "0"}}
     hd_summary = {k: hd_sweep(k, v) for k, v in hd_variants.items()}
     dist.barrier()
     if rank == 0:

@@ -222,11 +222,18 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   // planRingChunkedMesh): same bytes, two all-to-all hops over every xGMI
   // link instead of 2(P-1) hops around the ring.  Every rank must choose
   // alike, so the choice depends only on the environment and P.
+  // Halving-doubling and reduce-scatter likewise run as their derived mesh
+  // plans (mesh.cc).  GLOO_AMD_MESH=0 keeps the reference routes;
+  // GLOO_AMD_RING_MESH=0 only ring-chunked's.
   planAlgo_ = algo_;
-  if (algo_ == GLOO_HIP_ALGO_RING_CHUNKED && P >= 2 && P <= GLOO_HIP_MAX_SRCS) {
-    const char* m = std::getenv("GLOO_AMD_RING_MESH");
-    if (!(m && m[0] == '0')) planAlgo_ = GLOO_HIP_ALGO_RING_CHUNKED_MESH;
+  const char* m = std::getenv("GLOO_AMD_MESH");
+  const bool mesh = !(m && m[0] == '0') && P >= 2 && P <= GLOO_HIP_MAX_SRCS;
+  if (mesh && algo_ == GLOO_HIP_ALGO_RING_CHUNKED) {
+    const char* rm = std::getenv("GLOO_AMD_RING_MESH");
+    if (!(rm && rm[0] == '0')) planAlgo_ = GLOO_HIP_ALGO_RING_CHUNKED_MESH;
   }
+  if (mesh && (algo_ == GLOO_HIP_ALGO_HALVING_DOUBLING || algo_ == GLOO_HIP_ALGO_REDUCE_SCATTER))
+    planAlgo_ = algo_ | GLOO_HIP_ALGO_MESH;
   plan_ = planFor(planAlgo_, me, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_, maxSegmentBytes_,
                   recvElems_);
   GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
@@ -269,6 +276,8 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       const std::pair<int, int> key{isWait(s.kind) ? -1 - s.peer : s.peer, s.slot};
       const uint64_t j = seen[key]++;
       stepSeq_[i].base = base[key] + j + 1 - perRun[key];
+      // a previous-run credit: one run behind (met at once in run 1)
+      if (isWait(s.kind) && (s.flags & GLOO_HIP_PREV_RUN)) stepSeq_[i].base -= perRun[key];
       stepSeq_[i].perRun = perRun[key];
     }
   }
@@ -279,7 +288,10 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   // reads the records of every peer its plan talks to.
   std::set<int> planPeers, sendPeers, recvPeers;
   for (const Step& s : plan_.steps) {
-    if (s.peer >= 0) planPeers.insert(s.peer);
+    const bool talks = s.kind == GLOO_HIP_STEP_SEND || s.kind == GLOO_HIP_STEP_DECL_RECV ||
+                       s.kind == GLOO_HIP_STEP_WAIT_RECV || s.kind == GLOO_HIP_STEP_NOTIFY ||
+                       s.kind == GLOO_HIP_STEP_WAIT_NOTIFY || s.kind == GLOO_HIP_STEP_WAIT_SEND;
+    if (talks && s.peer >= 0 && s.peer != me) planPeers.insert(s.peer);
     if (s.kind == GLOO_HIP_STEP_SEND) sendPeers.insert(s.peer);
     if (s.kind == GLOO_HIP_STEP_DECL_RECV) recvPeers.insert(s.peer);
   }
@@ -399,7 +411,8 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     bool unfused = fuseBytes() == 0;
     for (const Step& s : plan_.steps)
       if ((s.kind == GLOO_HIP_STEP_SEND || s.kind == GLOO_HIP_STEP_REDUCE || s.kind == GLOO_HIP_STEP_COPY ||
-           s.kind == GLOO_HIP_STEP_LOCAL_REDUCE || s.kind == GLOO_HIP_STEP_LOCAL_BCAST) &&
+           s.kind == GLOO_HIP_STEP_LOCAL_REDUCE || s.kind == GLOO_HIP_STEP_LOCAL_BCAST ||
+           s.kind == GLOO_HIP_STEP_FOLD) &&
           s.length * es_ > fuseBytes())
         unfused = true;
     graphMode_ = gmode == "1" || (gmode == "auto" && unfused);
@@ -446,11 +459,14 @@ PlanExecutor::~PlanExecutor() {
 }
 
 void PlanExecutor::waitCounter(std::atomic<uint64_t>& c, uint64_t target, int peer, int slot) {
-  if (c.load(std::memory_order_acquire) >= target) return;
+  // signed difference: a target below the counter (a previous-run credit in
+  // the first run) is already met
+  auto met = [&] { return (int64_t)(c.load(std::memory_order_acquire) - target) >= 0; };
+  if (met()) return;
   const auto t0 = std::chrono::steady_clock::now();
   const auto deadline = t0 + ctx_->timeout();
   for (uint64_t i = 0;; i++) {
-    if (c.load(std::memory_order_acquire) >= target) break;
+    if (met()) break;
     if (i < 4096) {
       __builtin_ia32_pause();
     } else if (i < 8192) {
@@ -639,6 +655,38 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
       i = j - 1;
       continue;
     }
+    // A run of consecutive local COPYs with disjoint operands (a mesh
+    // schedule's results out of the inboxes): one multi-copy launch.
+    if (s.kind == GLOO_HIP_STEP_COPY && i + 1 < steps.size() && steps[i + 1].kind == GLOO_HIP_STEP_COPY &&
+        deviceSignal_) {
+      size_t j = i;
+      std::vector<std::pair<char*, const char*>> ops;
+      std::vector<size_t> lens;
+      for (; j < steps.size() && steps[j].kind == GLOO_HIP_STEP_COPY && ops.size() < (size_t)kMaxCopyEntries; j++) {
+        const Step& t = steps[j];
+        ops.push_back({userOrArena(t.flags & GLOO_HIP_DST_ARENA) + t.dst_off * es_,
+                       userOrArena(t.flags & GLOO_HIP_SRC_ARENA) + t.src_off * es_});
+        lens.push_back(t.length * es_);
+      }
+      bool disjoint = true;
+      for (size_t a = 0; a < ops.size(); a++)
+        for (size_t b = 0; b < ops.size(); b++) {
+          const char* d = ops[a].first;
+          const char* q = ops[b].second;
+          if (d < q + lens[b] && q < d + lens[a]) disjoint = false;
+          if (a != b && d < ops[b].first + lens[b] && ops[b].first < d + lens[a]) disjoint = false;
+        }
+      if (disjoint) {
+        CopyDesc d[kMaxCopyEntries];
+        int nd = 0;
+        for (size_t k = 0; k < ops.size(); k++)
+          if (lens[k]) d[nd++] = CopyDesc{ops[k].first, ops[k].second, lens[k], nullptr, Seq{}, nullptr,
+                                          copySignalGrid(lens[k], 256)};
+        if (nd) checkRc(launchCopySignalMulti(d, nd, epoch, stream_), "copy kernel (local batch)");
+        i = j - 1;
+        continue;
+      }
+    }
     // A run of consecutive waits: one launch polls them all.
     if (deviceSignal_ && isWaitKind(s.kind) && i + 1 < steps.size() && isWaitKind(steps[i + 1].kind)) {
       size_t j = i;
@@ -799,8 +847,9 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         // one pass over every source, in the plan's order (plan.cc FOLD)
         GLOO_AMD_ENFORCE(!foldSrcs.empty() && foldSrcs.size() <= GLOO_HIP_MAX_SRCS, "bad fold");
         if (profiling_) GLOO_AMD_HIP_CHECK(hipEventRecord(event(), stream_));
-        checkRc(launchFold(op_, dtype_, userPtr(0) + s.dst_off * es_, foldSrcs.data(), (int)foldSrcs.size(),
-                           s.length, (s.flags & GLOO_HIP_FOLD_REVERSE) != 0, stream_),
+        const int mode = s.flags & GLOO_HIP_FOLD_TREE ? 2 : s.flags & GLOO_HIP_FOLD_REVERSE ? 1 : 0;
+        checkRc(launchFold(op_, dtype_, userOrArena(s.flags & GLOO_HIP_DST_ARENA) + s.dst_off * es_,
+                           foldSrcs.data(), (int)foldSrcs.size(), s.length, mode, stream_),
                 "fold");
         if (profiling_) {
           GLOO_AMD_HIP_CHECK(hipEventRecord(event(), stream_));

@@ -22,6 +22,7 @@
 
 #include "gloo_amd.h"
 #include "gloo_amd/plan.h"
+#include "gloo_amd/mesh.h"
 
 namespace gloo_amd {
 
@@ -720,6 +721,12 @@ Plan makeAllreducePlan(int rank, int size, uint64_t count, const NewStyleOptions
 Plan makePlan(int algo, int rank, int size, uint64_t count, int nptrs, const std::vector<int>& recvElems) {
   if (size < 1 || rank < 0 || rank >= size) throw std::invalid_argument("bad rank/size");
   if (nptrs < 1) throw std::invalid_argument("need at least one pointer");
+  if (algo & GLOO_HIP_ALGO_MESH) {
+    const int base = algo & ~GLOO_HIP_ALGO_MESH;
+    if (base == GLOO_HIP_ALGO_REDUCE_SCATTER && (int)recvElems.size() != size)
+      throw std::invalid_argument("recvElems must have size entries");
+    return makeMeshPlan(base, rank, size, count, nptrs, recvElems);
+  }
   switch (algo) {
     case GLOO_HIP_ALGO_RING_CHUNKED: return planRingChunked(rank, size, count, nptrs);
     case GLOO_HIP_ALGO_RING_CHUNKED_MESH: return planRingChunkedMesh(rank, size, count, nptrs);
@@ -746,7 +753,7 @@ extern "C" int gloo_hip_plan_ex(int algo, int rank, int size, size_t count, int 
                                 gloo_hip_step_t* steps, size_t capacity, size_t* nsteps, size_t* arena_elems) {
   try {
     std::vector<int> re;
-    if (algo == GLOO_HIP_ALGO_REDUCE_SCATTER) {
+    if ((algo & ~GLOO_HIP_ALGO_MESH) == GLOO_HIP_ALGO_REDUCE_SCATTER) {
       if (!recv_elems) return GLOO_HIP_EINVAL_ARG;
       re.assign(recv_elems, recv_elems + size);
     }

@@ -267,9 +267,22 @@ struct SrcList {
   const void* p[GLOO_HIP_MAX_SRCS];
 };
 
-// REV: each new source is the left operand, acc = s_j op acc (the fold a ring
-// schedule performs when every hop computes `local op incoming`).
-template <class Tr, int OP, int UNROLL, int BLOCK, bool REV>
+// MODE 0: left fold acc = acc op s_j.  MODE 1 (reverse): acc = s_j op acc,
+// the fold a ring schedule performs when every hop computes `local op
+// incoming`.  MODE 2 (tree): balanced pairwise tree over the sources in order
+// (k a power of two), the fold of recursive halving.
+template <class Tr, int OP>
+__device__ __forceinline__ typename Tr::Storage tree_fold(typename Tr::Storage* v, int k) {
+#pragma unroll
+  for (int w = GLOO_HIP_MAX_SRCS; w > 1; w >>= 1)
+    if (w <= k) {
+#pragma unroll
+      for (int j = 0; j < w / 2; j++) v[j] = apply<Tr, OP>(v[2 * j], v[2 * j + 1]);
+    }
+  return v[0];
+}
+
+template <class Tr, int OP, int UNROLL, int BLOCK, int MODE>
 __global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
     typename Tr::Storage* dst, SrcList srcs, int k, size_t n, size_t head) {
   using S = typename Tr::Storage;
@@ -282,12 +295,20 @@ __global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
     for (int pass = 0; pass < 2; pass++) {
       const size_t i = pass == 0 ? t : tail0 + t;
       if ((pass == 0 && t < head) || (pass == 1 && i < n)) {
-        S acc = static_cast<const S*>(srcs.p[0])[i];
-        for (int j = 1; j < k; j++) {
-          const S v = static_cast<const S*>(srcs.p[j])[i];
-          acc = REV ? apply<Tr, OP>(v, acc) : apply<Tr, OP>(acc, v);
+        if (MODE == 2) {
+          S v[GLOO_HIP_MAX_SRCS];
+#pragma unroll
+          for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
+            if (j < k) v[j] = static_cast<const S*>(srcs.p[j])[i];
+          dst[i] = tree_fold<Tr, OP>(v, k);
+        } else {
+          S acc = static_cast<const S*>(srcs.p[0])[i];
+          for (int j = 1; j < k; j++) {
+            const S v = static_cast<const S*>(srcs.p[j])[i];
+            acc = MODE == 1 ? apply<Tr, OP>(v, acc) : apply<Tr, OP>(acc, v);
+          }
+          dst[i] = acc;
         }
-        dst[i] = acc;
       }
     }
   }
@@ -297,20 +318,44 @@ __global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
   const uint32_t bytes = (uint32_t)((body - base) < kTileBytes ? (body - base) : kTileBytes);
   const uint32_t lane_off = threadIdx.x * 16u;
   u32x4 acc[UNROLL];
-  {
-    const Src s0 = src_of(static_cast<const S*>(srcs.p[0]) + head);
-    const auto r0 = make_rsrc(s0.base + base, bytes + s0.mis);
+  if (MODE == 2) {
+    // all sources resident, then the tree level by level (k <= 8, uniform)
+    u32x4 v[GLOO_HIP_MAX_SRCS][UNROLL];
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) acc[u] = bload<kAuxNT>(r0, lane_off + u * BLOCK * 16, s0.mis);
-  }
-  for (int j = 1; j < k; j++) {
-    const Src sj = src_of(static_cast<const S*>(srcs.p[j]) + head);
-    const auto rj = make_rsrc(sj.base + base, bytes + sj.mis);
-    u32x4 r[UNROLL];
+    for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
+      if (j < k) {
+        const Src sj = src_of(static_cast<const S*>(srcs.p[j]) + head);
+        const auto rj = make_rsrc(sj.base + base, bytes + sj.mis);
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) r[u] = bload<kAuxNT>(rj, lane_off + u * BLOCK * 16, sj.mis);
+        for (int u = 0; u < UNROLL; u++) v[j][u] = bload<kAuxNT>(rj, lane_off + u * BLOCK * 16, sj.mis);
+      }
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) acc[u] = REV ? apply_packet<Tr, OP>(r[u], acc[u]) : apply_packet<Tr, OP>(acc[u], r[u]);
+    for (int w = GLOO_HIP_MAX_SRCS; w > 1; w >>= 1)
+      if (w <= k) {
+#pragma unroll
+        for (int j = 0; j < w / 2; j++)
+#pragma unroll
+          for (int u = 0; u < UNROLL; u++) v[j][u] = apply_packet<Tr, OP>(v[2 * j][u], v[2 * j + 1][u]);
+      }
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) acc[u] = v[0][u];
+  } else {
+    {
+      const Src s0 = src_of(static_cast<const S*>(srcs.p[0]) + head);
+      const auto r0 = make_rsrc(s0.base + base, bytes + s0.mis);
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) acc[u] = bload<kAuxNT>(r0, lane_off + u * BLOCK * 16, s0.mis);
+    }
+    for (int j = 1; j < k; j++) {
+      const Src sj = src_of(static_cast<const S*>(srcs.p[j]) + head);
+      const auto rj = make_rsrc(sj.base + base, bytes + sj.mis);
+      u32x4 r[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) r[u] = bload<kAuxNT>(rj, lane_off + u * BLOCK * 16, sj.mis);
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++)
+        acc[u] = MODE == 1 ? apply_packet<Tr, OP>(r[u], acc[u]) : apply_packet<Tr, OP>(acc[u], r[u]);
+    }
   }
   const auto rd = make_rsrc(reinterpret_cast<const char*>(dst + head) + base, bytes);
 #pragma unroll
@@ -338,8 +383,10 @@ __global__ __launch_bounds__(kFusedBlock) void fused_small_kernel(
     int good = 1;
     if (waitFlag) {
       const uint64_t waitTarget = epoch ? wait.base + *epoch * wait.perRun : wait.base;
+      // counters compare by signed difference: a target "below" the counter
+      // (a previous-run credit in the first run) is satisfied
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load(waitFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < waitTarget) {
+      while ((int64_t)(__hip_atomic_load(waitFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - waitTarget) < 0) {
         __builtin_amdgcn_s_sleep(4);
         if (__builtin_amdgcn_s_memrealtime() - t0 > timeoutTicks) {
           __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -445,6 +492,7 @@ __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(CopyList L, con
 #pragma unroll
     for (int u = 0; u < kCopyUnroll; u++) bstore<kAuxNT>(rd, lane_off + u * kCopyBlock * 16, v[u]);
   }
+  if (!L.flag[j]) return;  // a plain (local) copy: nobody to tell
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -519,7 +567,7 @@ int launch3(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
   return launch_vec<Tr, OP, kUnroll, kVecBlock, kAuxNT, kAuxNT>(c, a, b, n, head, s);
 }
 
-template <class Tr, int OP, bool REV = false>
+template <class Tr, int OP, int MODE = 0>
 int launch_multi(void* dst, const void* const* srcs, int k, size_t n, hipStream_t s) {
   using S = typename Tr::Storage;
   if (n == 0) return GLOO_HIP_OK;
@@ -539,7 +587,7 @@ int launch_multi(void* dst, const void* const* srcs, int k, size_t n, hipStream_
   const size_t nvec = (n - head) / kV;
   size_t grid = ceil_div(nvec, (size_t)kVecBlock * kMultiUnroll);
   if (grid == 0) grid = 1;
-  reduce_multi_vec_kernel<Tr, OP, kMultiUnroll, kVecBlock, REV><<<dim3((unsigned)grid), dim3(kVecBlock), 0, s>>>(
+  reduce_multi_vec_kernel<Tr, OP, kMultiUnroll, kVecBlock, MODE><<<dim3((unsigned)grid), dim3(kVecBlock), 0, s>>>(
       static_cast<S*>(dst), list, k, n, head);
   return check_launch("reduce_multi_vec_kernel");
 }
@@ -555,13 +603,13 @@ int by_op3(int op, void* c, const void* a, const void* b, size_t n, hipStream_t 
   }
 }
 
-template <class Tr, bool REV = false>
+template <class Tr, int MODE = 0>
 int by_op_multi(int op, void* d, const void* const* srcs, int k, size_t n, hipStream_t s) {
   switch (op) {
-    case GLOO_HIP_SUM: return launch_multi<Tr, GLOO_HIP_SUM, REV>(d, srcs, k, n, s);
-    case GLOO_HIP_PRODUCT: return launch_multi<Tr, GLOO_HIP_PRODUCT, REV>(d, srcs, k, n, s);
-    case GLOO_HIP_MAX: return launch_multi<Tr, GLOO_HIP_MAX, REV>(d, srcs, k, n, s);
-    case GLOO_HIP_MIN: return launch_multi<Tr, GLOO_HIP_MIN, REV>(d, srcs, k, n, s);
+    case GLOO_HIP_SUM: return launch_multi<Tr, GLOO_HIP_SUM, MODE>(d, srcs, k, n, s);
+    case GLOO_HIP_PRODUCT: return launch_multi<Tr, GLOO_HIP_PRODUCT, MODE>(d, srcs, k, n, s);
+    case GLOO_HIP_MAX: return launch_multi<Tr, GLOO_HIP_MAX, MODE>(d, srcs, k, n, s);
+    case GLOO_HIP_MIN: return launch_multi<Tr, GLOO_HIP_MIN, MODE>(d, srcs, k, n, s);
     default: return set_error(GLOO_HIP_EINVAL_OP, "unknown reduction op");
   }
 }
@@ -583,20 +631,20 @@ int dispatch3(int op, int dtype, void* c, const void* a, const void* b, size_t n
   }
 }
 
-template <bool REV = false>
+template <int MODE = 0>
 int dispatch_multi(int op, int dtype, void* d, const void* const* srcs, int k, size_t n,
                    hipStream_t s) {
   switch (dtype) {
-    case GLOO_HIP_I8: return by_op_multi<TrI8, REV>(op, d, srcs, k, n, s);
-    case GLOO_HIP_U8: return by_op_multi<TrU8, REV>(op, d, srcs, k, n, s);
-    case GLOO_HIP_I32: return by_op_multi<TrI32, REV>(op, d, srcs, k, n, s);
-    case GLOO_HIP_U32: return by_op_multi<TrU32, REV>(op, d, srcs, k, n, s);
-    case GLOO_HIP_I64: return by_op_multi<TrI64, REV>(op, d, srcs, k, n, s);
-    case GLOO_HIP_U64: return by_op_multi<TrU64, REV>(op, d, srcs, k, n, s);
-    case GLOO_HIP_F16: return by_op_multi<TrF16, REV>(op, d, srcs, k, n, s);
-    case GLOO_HIP_BF16: return by_op_multi<TrBF16, REV>(op, d, srcs, k, n, s);
-    case GLOO_HIP_F32: return by_op_multi<TrF32, REV>(op, d, srcs, k, n, s);
-    case GLOO_HIP_F64: return by_op_multi<TrF64, REV>(op, d, srcs, k, n, s);
+    case GLOO_HIP_I8: return by_op_multi<TrI8, MODE>(op, d, srcs, k, n, s);
+    case GLOO_HIP_U8: return by_op_multi<TrU8, MODE>(op, d, srcs, k, n, s);
+    case GLOO_HIP_I32: return by_op_multi<TrI32, MODE>(op, d, srcs, k, n, s);
+    case GLOO_HIP_U32: return by_op_multi<TrU32, MODE>(op, d, srcs, k, n, s);
+    case GLOO_HIP_I64: return by_op_multi<TrI64, MODE>(op, d, srcs, k, n, s);
+    case GLOO_HIP_U64: return by_op_multi<TrU64, MODE>(op, d, srcs, k, n, s);
+    case GLOO_HIP_F16: return by_op_multi<TrF16, MODE>(op, d, srcs, k, n, s);
+    case GLOO_HIP_BF16: return by_op_multi<TrBF16, MODE>(op, d, srcs, k, n, s);
+    case GLOO_HIP_F32: return by_op_multi<TrF32, MODE>(op, d, srcs, k, n, s);
+    case GLOO_HIP_F64: return by_op_multi<TrF64, MODE>(op, d, srcs, k, n, s);
     default: return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
   }
 }
@@ -616,7 +664,7 @@ int launchCopySignalMulti(const CopyDesc* d, int n, const uint64_t* epoch, hipSt
   L.n = n;
   unsigned total = 0;
   for (int j = 0; j < n; j++) {
-    if (!d[j].flag || !d[j].ticket || d[j].blocks == 0) return set_error(GLOO_HIP_EINVAL_ARG, "bad copy entry");
+    if ((d[j].flag && !d[j].ticket) || d[j].blocks == 0) return set_error(GLOO_HIP_EINVAL_ARG, "bad copy entry");
     L.first[j] = total;
     total += d[j].blocks;
     L.dst[j] = static_cast<char*>(d[j].dst);
@@ -637,12 +685,17 @@ int launchCopySignal(void* dst, const void* src, size_t bytes, uint64_t* flag, S
   return launchCopySignalMulti(&d, 1, epoch, s);
 }
 
-int launchFold(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n, bool reverse,
+int launchFold(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n, int mode,
                hipStream_t s) {
   if (k < 1 || k > GLOO_HIP_MAX_SRCS) return set_error(GLOO_HIP_EINVAL_ARG, "source count out of range");
+  if (mode == 2 && (k & (k - 1))) return set_error(GLOO_HIP_EINVAL_ARG, "tree fold needs a power-of-two count");
   if (n == 0) return GLOO_HIP_OK;
-  return reverse ? dispatch_multi<true>(op, dtype, dst, srcs, k, n, s)
-                 : dispatch_multi<false>(op, dtype, dst, srcs, k, n, s);
+  switch (mode) {
+    case 0: return dispatch_multi<0>(op, dtype, dst, srcs, k, n, s);
+    case 1: return dispatch_multi<1>(op, dtype, dst, srcs, k, n, s);
+    case 2: return dispatch_multi<2>(op, dtype, dst, srcs, k, n, s);
+    default: return set_error(GLOO_HIP_EINVAL_ARG, "unknown fold mode");
+  }
 }
 
 // Internal entry for the plan executor (see gloo_amd/signal.h).

@@ -33,7 +33,8 @@ __global__ __launch_bounds__(64) void wait_kernel(const uint64_t* flag, uint64_t
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   // relaxed polls, ONE acquire after the match (an acquire per poll would
   // invalidate the caches on every iteration)
-  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+  // signed difference: a target "below" the counter is already satisfied
+  while ((int64_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
     __builtin_amdgcn_s_sleep(8);
     if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
       __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(64) void wait_multi_kernel(WaitList w, const uint64
   if (j < w.n) {
     const uint64_t target = seqValue(w.target[j].base, w.target[j].perRun, epoch);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(w.flag[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+    while ((int64_t)(__hip_atomic_load(w.flag[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
       __builtin_amdgcn_s_sleep(8);
       if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
         __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

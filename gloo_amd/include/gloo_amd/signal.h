@@ -5,7 +5,8 @@
 // both ends stream-ordered, so a whole plan is enqueued — and captured into
 // a hipGraph — without host round trips:
 //   signal: system-scope release, then the flag word := value
-//   wait:   poll the flag (relaxed) until >= target, sleeping between polls;
+//   wait:   poll the flag (relaxed) until >= target (signed difference, so a
+//           target below the counter is met at once), sleeping between polls;
 //           ONE system-scope acquire after the match; give up after
 //           `timeoutTicks` of the 100 MHz realtime counter and set *err (the
 //           host raises IoException).
@@ -61,7 +62,7 @@ struct CopyDesc {
   void* dst;
   const void* src;
   size_t bytes;
-  uint64_t* flag;
+  uint64_t* flag;    // nullptr: a plain copy, no arrival signal
   Seq seq;
   unsigned* ticket;  // this entry's ticket counter (zero at launch)
   unsigned blocks;   // copySignalGrid(bytes, ...)
@@ -74,9 +75,10 @@ constexpr int kMaxWaitEntries = 16;
 hipError_t launchWaitMulti(const uint64_t* const* flags, const Seq* targets, int n, const uint64_t* epoch,
                            uint64_t timeoutTicks, uint32_t* err, hipStream_t stream);
 
-// Multi-source fold dst = s0 op s1 op ... (left fold; reverse: acc = s_j op
-// acc), k <= GLOO_HIP_MAX_SRCS, one pass.  Returns a gloo_hip status.
-int launchFold(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n, bool reverse,
+// Multi-source fold in one pass, k <= GLOO_HIP_MAX_SRCS.  mode 0: left fold
+// acc = acc op s_j; 1: reverse, acc = s_j op acc; 2: balanced pairwise tree
+// over the sources in order (k a power of two).  Returns a gloo_hip status.
+int launchFold(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n, int mode,
                hipStream_t stream);
 
 }  // namespace gloo_amd

@@ -141,6 +141,15 @@ typedef enum {
   GLOO_HIP_ALGO_RING_CHUNKED_MESH = 6,
 } gloo_hip_algo_t;
 
+/* algo | GLOO_HIP_ALGO_MESH: the algorithm's result with mesh data movement,
+ * derived mechanically (gloo_amd/csrc/mesh.cc): every rank's plan is run
+ * symbolically to find, per element range, the exact expression tree the
+ * reference evaluates and the rank that finishes it; raw pieces then go
+ * straight to that rank (all links at once), which evaluates the same tree,
+ * and (allreduce) sends the result to every rank.  Bit-identical results.
+ * For HALVING_DOUBLING and REDUCE_SCATTER (and RING_CHUNKED), 2 <= size <= 8. */
+#define GLOO_HIP_ALGO_MESH 0x100
+
 typedef enum {
   GLOO_HIP_STEP_DECL_RECV = 0,   /* inbox region for (peer, slot): arena[dst_off, +length) */
   GLOO_HIP_STEP_SEND = 1,        /* src[src_off, +length) -> peer's (me, slot) region       */
@@ -178,6 +187,13 @@ typedef enum {
 #define GLOO_HIP_FROM_INPUTS 4
 /* FOLD: each new source is the LEFT operand (acc = s_k op acc). */
 #define GLOO_HIP_FOLD_REVERSE 8
+/* FOLD: balanced pairwise tree over the sources in order (k a power of two):
+ * ((s0 op s1) op (s2 op s3)) op ((s4 op s5) op (s6 op s7)).  FOLD also takes
+ * GLOO_HIP_DST_ARENA (result into the arena). */
+#define GLOO_HIP_FOLD_TREE 16
+/* WAIT_NOTIFY: wait for the notification of the PREVIOUS run (a credit the
+ * receiver returns after consuming; satisfied at once in the first run). */
+#define GLOO_HIP_PREV_RUN 32
 
 typedef struct {
   int32_t kind;

@@ -20,7 +20,9 @@ KIND = dict(DECL_RECV=0, SEND=1, WAIT_RECV=2, REDUCE=3, COPY=4, NOTIFY=5, WAIT_N
             WAIT_SEND=7, LOCAL_REDUCE=8, LOCAL_BCAST=9, FOLD_SRC=10, FOLD=11)
 ALGO = dict(ring_chunked=0, halving_doubling=1, ring=2, local=3, reduce_scatter=4, allreduce_new=5,
             ring_chunked_mesh=6)
-SRC_ARENA, DST_ARENA, FROM_INPUTS, FOLD_REVERSE = 1, 2, 4, 8
+MESH = 0x100  # algo | MESH: the derived mesh plan (gloo_amd/csrc/mesh.cc)
+ALGO.update({"mesh_" + k: v | MESH for k, v in list(ALGO.items()) if v < 5})
+SRC_ARENA, DST_ARENA, FROM_INPUTS, FOLD_REVERSE, FOLD_TREE, PREV_RUN = 1, 2, 4, 8, 16, 32
 
 
 class Step(ctypes.Structure):
@@ -68,6 +70,13 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
     nin = 0 if ins is None else ins.shape[1]
     es = inputs.dtype.itemsize
     plans = [get_plan(algo, r, P, n, k, recv, nin=nin, elem_size=es, max_seg=max_seg) for r in range(P)]
+    # previous-run credits: per channel, how many per run
+    lag_per_run = {}
+    for r, (steps, _) in enumerate(plans):
+        for st in steps:
+            if st.kind == KIND["WAIT_NOTIFY"] and st.flags & PREV_RUN:
+                key = (st.peer, r, st.slot)
+                lag_per_run[key] = lag_per_run.get(key, 0) + 1
     if runs > 1:
         plans = [([st for st in steps] + [st for _ in range(runs - 1) for st in steps
                                           if st.kind != KIND["DECL_RECV"]], a) for steps, a in plans]
@@ -81,7 +90,7 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
                 if key in regions:
                     raise ProtocolError(f"region {key} declared twice")
                 regions[key] = (s.dst_off, s.length)
-    sent, consumed = {}, {}
+    sent, consumed, lagged = {}, {}, {}
     pending = [[] for _ in range(P)]  # FOLD sources, read when the FOLD executes
     pc = [0] * P
     rng = random.Random(seed)
@@ -94,6 +103,10 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
         if pc[r] >= len(steps):
             return False
         s = steps[pc[r]]
+        if s.kind == KIND["WAIT_NOTIFY"] and s.flags & PREV_RUN:
+            # the i-th such wait is met by the previous run's credits
+            key = (s.peer, r, s.slot)
+            return sent.get(key, 0) >= lagged.get(key, 0) + 1 - lag_per_run[key]
         if s.kind in (KIND["WAIT_RECV"], KIND["WAIT_NOTIFY"]):
             key = (s.peer, r, s.slot)
             return sent.get(key, 0) > consumed.get(key, 0)
@@ -110,6 +123,10 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
         pc[r] += 1
         K = s.kind
         if K == KIND["DECL_RECV"] or K == KIND["WAIT_SEND"]:
+            continue
+        if K == KIND["WAIT_NOTIFY"] and s.flags & PREV_RUN:
+            key = (s.peer, r, s.slot)
+            lagged[key] = lagged.get(key, 0) + 1
             continue
         if K == KIND["SEND"]:
             key = (r, s.peer, s.slot)
@@ -160,14 +177,23 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
         elif K == KIND["FOLD"]:
             srcs = [space(r, a)[o:o + s.length].copy() for a, o in pending[r]]
             pending[r] = []
-            acc = srcs[0]
-            for x in srcs[1:]:
-                acc = oracle.reduce3(op, dtype, x, acc) if s.flags & FOLD_REVERSE else \
-                    oracle.reduce3(op, dtype, acc, x)
-            user[r][0][s.dst_off:s.dst_off + s.length] = acc
+            if s.flags & FOLD_TREE:
+                while len(srcs) > 1:
+                    srcs = [oracle.reduce3(op, dtype, srcs[2 * j], srcs[2 * j + 1]) for j in range(len(srcs) // 2)]
+                acc = srcs[0]
+            else:
+                acc = srcs[0]
+                for x in srcs[1:]:
+                    acc = oracle.reduce3(op, dtype, x, acc) if s.flags & FOLD_REVERSE else \
+                        oracle.reduce3(op, dtype, acc, x)
+            space(r, s.flags & DST_ARENA)[s.dst_off:s.dst_off + s.length] = acc
         else:
             raise ProtocolError(f"unknown step kind {K}")
     for key in sent:
+        if key in lag_per_run:
+            if sent[key] != lagged.get(key, 0):
+                raise ProtocolError(f"{key}: {sent[key]} credits sent, {lagged.get(key, 0)} awaited")
+            continue
         if sent[key] != consumed.get(key, 0):
             raise ProtocolError(f"{key}: {sent[key]} sent, {consumed.get(key, 0)} consumed")
     return np.array([[user[r][j] for j in range(k)] for r in range(P)])

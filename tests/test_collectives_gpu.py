@@ -385,6 +385,15 @@ np.save(out, buf.cpu().numpy().view(xr.dtype))
                                                "GLOO_AMD_COPY_BLOCKS": "3"}),
     ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_COPY": "kernel"}),
     ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_FUSE_BYTES": "0", "GLOO_AMD_COPY": "kernel"}),
+    # the reference routes (GLOO_AMD_MESH=0) next to the derived mesh plans
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_MESH": "0"}),
+    ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_MESH": "0"}),
+    ("reduce_scatter/max/bf16/P8/n4096", {"GLOO_AMD_MESH": "0"}),
+    ("reduce_scatter/sum/f32/P5/n100", {"GLOO_AMD_MESH": "0", "GLOO_AMD_COPY": "kernel"}),
+    ("halving_doubling/sum/f64/P7/k1/n3001", {}),            # binary blocks: pairwise folds via temporaries
+    ("halving_doubling/min/f32/P5/k1/n1000", {"GLOO_AMD_COPY": "memcpy"}),
+    ("reduce_scatter/product/f16/P8/n4096", {"GLOO_AMD_COPY": "memcpy"}),
+    ("reduce_scatter/sum/f16/P4/n1024", {}),
 ])
 def test_processes_golden_device_signalling(torch, golden_sched, case, env):
     """Ranks as processes on the box's GPU(s): device-side signalling with the
@@ -495,6 +504,14 @@ print("MODES", json.dumps(modes))
     ("ring_chunked/product/f32/P3/k1/n777", {"GLOO_AMD_COPY_BLOCKS": "1", "GLOO_AMD_FUSE_BYTES": "0"}, True),
     ("ring_chunked/sum/f32/P2/k1/n1000", {}, False),
     ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_RING_MESH": "0", "GLOO_AMD_GRAPH": "1"}, True),
+    # derived mesh plans replayed: tree fold (P8), pairwise temporaries (P7),
+    # reduce-scatter with previous-run credits
+    ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, True),
+    ("halving_doubling/sum/f64/P7/k1/n3001", {"GLOO_AMD_GRAPH": "1"}, True),
+    ("halving_doubling/sum/f64/P7/k1/n3001", {}, False),
+    ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_GRAPH": "1"}, True),
+    ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_COPY": "memcpy"}, True),
+    ("reduce_scatter/sum/f32/P5/n100", {"GLOO_AMD_SIGNAL": "host"}, False),
 ])
 def test_processes_graph_replay(torch, golden_sched, case, env, graph):
     """hipGraph replay: run 1 is enqueued eagerly, run 2 captures the plan and

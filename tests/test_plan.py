@@ -196,3 +196,92 @@ def test_mesh_multi_pointer(golden_sched, P, k):
 def test_mesh_rejects_more_than_8_ranks():
     with pytest.raises(RuntimeError):
         get_plan("ring_chunked_mesh", 0, 9, 1000)
+
+
+def _mesh_golden_keys():
+    out = []
+    for k in _keys():
+        algo, P = k.split("/")[0], int(k.split("/")[3][1:])
+        if algo in ("ring_chunked", "halving_doubling", "reduce_scatter") and 2 <= P <= 8:
+            out.append(k)
+    return out
+
+
+@pytest.mark.parametrize("case", _mesh_golden_keys())
+def test_derived_mesh_plan_matches_reference_golden(golden_sched, case):
+    """algo | GLOO_HIP_ALGO_MESH (gloo_amd/csrc/mesh.cc): the plan derived by
+    running the reference schedule symbolically — raw pieces straight to the
+    rank that finishes them, the same expression tree evaluated there —
+    reproduces the reference's bytes for ring-chunked, halving-doubling
+    (balanced-tree fold for power-of-two P, pairwise for binary blocks) and
+    reduce-scatter."""
+    algo, op, dtype = case.split("/")[:3]
+    x, want = golden_sched[case + "/in"], golden_sched[case + "/out"]
+    for seed in (0, 1):
+        if algo == "reduce_scatter":
+            recv = golden_sched[case + "/recv"]
+            y = simulate("mesh_" + algo, op, dtype, x[:, None, :], recv=recv, seed=seed)
+            got = np.concatenate([y[r, 0, :recv[r]] for r in range(len(recv))])
+            assert (got.view(np.uint8) == want.view(np.uint8)).all(), seed
+        else:
+            y = simulate("mesh_" + algo, op, dtype, x, seed=seed)
+            for r in range(y.shape[0]):
+                for j in range(y.shape[1]):
+                    assert (y[r, j].view(np.uint8) == want.view(np.uint8)).all(), (seed, r, j)
+
+
+def _random(dtype, shape, seed):
+    rng = np.random.default_rng(seed)
+    if dtype == "i32":
+        return rng.integers(-2**31, 2**31 - 1, size=shape, dtype=np.int64).astype(np.int32)
+    f = rng.standard_normal(shape).astype(np.float32)
+    f[rng.random(shape) < 0.02] = np.nan
+    f[rng.random(shape) < 0.02] = -0.0
+    f[rng.random(shape) < 0.02] = 0.0
+    if dtype == "f32":
+        return f
+    if dtype == "f16":
+        return f.astype(np.float16).view(np.uint16)
+    return (f.view(np.uint32) >> 16).astype(np.uint16)
+
+
+@pytest.mark.parametrize("op", ["sum", "product", "max", "min"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "i32"])
+@pytest.mark.parametrize("P,n", [(2, 1000), (3, 999), (4, 4099), (5, 1000), (6, 777), (7, 3001), (8, 100003),
+                                 (8, 5)])
+def test_mesh_hd_equals_hd_bitwise(op, dtype, P, n):
+    """Derived mesh halving-doubling vs the reference schedule on random data
+    with NaN / signed zeros, three back-to-back runs, random interleavings."""
+    x = _random(dtype, (P, 1, n), P * 7 + n)
+    want = simulate("halving_doubling", op, dtype, x, seed=3, runs=3)
+    got = simulate("mesh_halving_doubling", op, dtype, x, seed=P, runs=3)
+    assert (got.view(np.uint8) == want.view(np.uint8)).all()
+
+
+@pytest.mark.parametrize("op", ["sum", "max"])
+@pytest.mark.parametrize("dtype", ["f16", "bf16", "f32"])
+@pytest.mark.parametrize("P,n", [(2, 100), (3, 1001), (5, 4099), (8, 4096), (8, 9)])
+def test_mesh_reduce_scatter_bitwise_and_credits(op, dtype, P, n):
+    """Derived mesh reduce-scatter: run 1 equals the reference's outputs;
+    three back-to-back runs (no return hop, so inbox reuse rests on the
+    previous-run credits) equal three single runs chained by hand."""
+    x = _random(dtype, (P, 1, n), P * 11 + n)
+    base = n // P
+    recv = np.array([base + (1 if r < n % P else 0) for r in range(P)], dtype=np.int32)
+    ref = simulate("reduce_scatter", op, dtype, x, recv=recv, seed=2)
+    once = simulate("mesh_reduce_scatter", op, dtype, x, recv=recv, seed=1)
+    for r in range(P):
+        assert (once[r, 0, :recv[r]].view(np.uint8) == ref[r, 0, :recv[r]].view(np.uint8)).all(), r
+    chained = x
+    for _ in range(3):
+        chained = simulate("mesh_reduce_scatter", op, dtype, chained, recv=recv, seed=5)
+    for seed in (0, 1, 2):
+        got = simulate("mesh_reduce_scatter", op, dtype, x, recv=recv, seed=seed, runs=3)
+        assert (got.view(np.uint8) == chained.view(np.uint8)).all(), seed
+
+
+def test_mesh_ring_has_no_mesh_form():
+    """AllreduceRing's ranks finish with different association orders, so no
+    single owner tree exists; the derivation refuses instead of guessing."""
+    with pytest.raises(RuntimeError):
+        get_plan("mesh_ring", 0, 4, 1000)
