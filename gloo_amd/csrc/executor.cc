@@ -400,7 +400,12 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     const std::string cmode = cp ? cp : "auto";
     kernelCopy_ = cmode == "kernel";
     batchKernelCopy_ = cmode != "memcpy";
-    if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS")) copyBlocks_ = (unsigned)std::max(1, std::atoi(cb));
+    // Workgroups per copy (executor.h): a few dozen saturate an xGMI link.
+    // GLOO_AMD_COPY_BLOCKS overrides both the remote and the same-GPU size.
+    if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS")) {
+      copyBlocks_ = (unsigned)std::max(1, std::atoi(cb));
+      copyBlocksLocal_ = copyBlocks_;
+    }
     const size_t tickets = std::max<size_t>(256, (size_t)P * GLOO_HIP_NUM_SLOTS * sizeof(unsigned));
     GLOO_AMD_HIP_CHECK(hipMalloc(&ticket_, tickets));
     GLOO_AMD_HIP_CHECK(hipMemset(ticket_, 0, tickets));
@@ -625,7 +630,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
             d[nd++] = CopyDesc{sendDst(t), userOrArena(t.flags & GLOO_HIP_SRC_ARENA) + t.src_off * es_, bytes,
                                ctx_->counterDevicePtr(inst_, me, t.peer, t.slot), seqOf(k, r, graph),
                                ticket_ + (size_t)t.peer * GLOO_HIP_NUM_SLOTS + t.slot,
-                               copySignalGrid(bytes, copyBlocks_)};
+                               copySignalGrid(bytes, copyBlocksFor(t.peer))};
           }
           checkRc(launchCopySignalMulti(d, nd, epoch, stream_), "copy_signal_kernel (batch)");
         }
@@ -757,7 +762,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         char* dst = peers_[s.peer].base + (remoteRegion_[{s.peer, s.slot}] + s.dst_off) * es_;
         const char* src = (s.flags & GLOO_HIP_SRC_ARENA ? arena_ : userPtr(0)) + s.src_off * es_;
         if (kernelCopy_) {
-          const unsigned grid = copySignalGrid(s.length * es_, copyBlocks_);
+          const unsigned grid = copySignalGrid(s.length * es_, copyBlocksFor(s.peer));
           checkRc(launchCopySignal(dst, src, s.length * es_, ctx_->counterDevicePtr(inst_, me, s.peer, s.slot),
                                    seqOf(i, r, graph), ticket_ + (size_t)s.peer * GLOO_HIP_NUM_SLOTS + s.slot, epoch,
                                    grid, stream_),
