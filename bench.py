@@ -233,8 +233,10 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
     rank's time per allreduce, bus bandwidth, and the reduction kernels' own
     GiB/s measured with HIP events while the exchange runs (per-GPU
     efficiency vs the 1-GPU figure).
-    Config 4: halving-doubling at 1 KiB / 64 KiB / 1 MiB / 64 MiB per rank,
-    derived mesh plan vs the reference's exchange route."""
+    Config 4: halving-doubling, 1 KiB .. 1 GiB per rank (x4 steps) for the
+    derived mesh plan and the reference's exchange route, 4 sizes for the
+    other variants.  Config 5: reduce-scatter of fp16 / bf16 buckets, all
+    four ops."""
     import tempfile
     obj = [tempfile.mkdtemp(prefix="gloo_amd_bench_")] if rank == 0 else [None]
     dist.broadcast_object_list(obj, src=0)
@@ -319,10 +321,11 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
                 "ring_kernel": ring_once("kernel", mesh="0"),
                 "mesh_host_workspace": ring_once("auto", "host")}
 
-    sizes = (1 << 10, 64 << 10, 1 << 20, 64 << 20)
+    short_sizes = (1 << 10, 64 << 10, 1 << 20, 64 << 20)
+    full_sizes = tuple(1 << lg for lg in range(10, 31, 2))  # config 4: 1 KiB .. 1 GiB per rank
     iters = 20
 
-    def hd_sweep(label, env):
+    def hd_sweep(label, env, sizes=short_sizes):
         def body():
             hd = []
             for nbytes in sizes:
@@ -370,7 +373,46 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
                    "reference_route": {"GLOO_AMD_MESH": "0"},
                    "reference_route_kernel_copy": {"GLOO_AMD_MESH": "0", "GLOO_AMD_COPY": "kernel"},
                    "reference_route_eager": {"GLOO_AMD_MESH": "0", "GLOO_AMD_GRAPH": "0"}}
-    hd_summary = {k: hd_sweep(k, v) for k, v in hd_variants.items()}
+    hd_summary = {k: hd_sweep(k, v, full_sizes if k in ("mesh", "reference_route") else short_sizes)
+                  for k, v in hd_variants.items()}
+
+    # Config 5: reduce-scatter (HD), fp16 / bf16 buckets, every op, 16 Mi
+    # elements per rank, recvElems = an even split.
+    def rs_once(dtype, op, env):
+        def body():
+            m = 16 << 20
+            recv = [m // world + (1 if r < m % world else 0) for r in range(world)]
+            b = torch.ones(m, dtype=torch.float16 if dtype == "f16" else torch.bfloat16, device=dev)
+            torch.cuda.synchronize(dev)
+            c = hip.Context(rank, world, "file:%s/rs_%s_%s_%s" % (obj[0], dtype, op, env.get("GLOO_AMD_MESH", "1")),
+                            device=dev.index, timeout_ms=60000)
+            a = hip.Algorithm(c, "reduce_scatter", op, dtype, [b.data_ptr()], m, recv_elems=recv)
+            a.run()
+            a.run()
+            ts = []
+            for _ in range(10):
+                dist.barrier()
+                t0 = time.perf_counter()
+                a.run()
+                ts.append(time.perf_counter() - t0)
+            a.close()
+            c.close()
+            return {"us": [round(t * 1e6, 1) for t in ts]}
+        try:
+            res = with_env(env, body)
+        except Exception as e:  # noqa: BLE001
+            res = {"error": repr(e)}
+        g = gather(res)
+        if any("error" in x for x in g):
+            return {"dtype": dtype, "op": op, "error": next(x["error"] for x in g if "error" in x)}
+        per = sorted(max(x["us"][k] for x in g) for k in range(10))
+        nbytes = (16 << 20) * 2
+        return {"dtype": dtype, "op": op, "route": "reference" if env.get("GLOO_AMD_MESH") == "0" else "mesh",
+                "elements_per_rank": 16 << 20, "us_p50": per[5], "us_max": per[-1],
+                "busbw_gib_s": round((world - 1) / world * nbytes / (per[5] / 1e6) / GIB, 2)}
+
+    rs_summary = [rs_once(dt, op, {}) for dt in ("f16", "bf16") for op in ("sum", "product", "min", "max")]
+    rs_summary += [rs_once(dt, "sum", {"GLOO_AMD_MESH": "0"}) for dt in ("f16", "bf16")]
     dist.barrier()
     if rank == 0:
         import shutil
@@ -381,6 +423,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
     out.update(ring)
     out["variants"] = variants
     out["halving_doubling"] = hd_summary
+    out["reduce_scatter"] = rs_summary
     return out
 
 
