@@ -329,14 +329,17 @@ lib.gloo_hip_allreduce.argtypes = [ctypes.c_void_p, ctypes.POINTER(AllreduceOpti
 EXPORTED = EXPORTED + ("gloo_hip_allreduce", "gloo_hip_plan_ex")
 
 
+ALLREDUCE_ALGORITHMS = {"ring": 1, "bcube": 2}  # AllreduceOptions::Algorithm (gloo/allreduce.h:38-42)
+
+
 def allreduce(ctx, outputs, elements, dtype, op="sum", inputs=None, max_segment_bytes=0, tag=0,
-              stream=0):
-    """gloo::allreduce(opts) with RING (gloo/allreduce.cc:147-392) on device
-    pointers; every output receives the reduction of all inputs (or of the
-    outputs when no inputs are given) over all ranks."""
+              stream=0, algorithm="ring"):
+    """gloo::allreduce(opts) on device pointers, RING (gloo/allreduce.cc:147-392)
+    or BCUBE (:397-669); every output receives the reduction of all inputs (or
+    of the outputs when no inputs are given) over all ranks."""
     inputs = list(inputs or [])
     o = AllreduceOptions()
-    o.algorithm = 1
+    o.algorithm = ALLREDUCE_ALGORITHMS[algorithm] if isinstance(algorithm, str) else int(algorithm)
     o.op = _as_op(op)
     o.dtype = _as_dtype(dtype)
     ins = (ctypes.c_void_p * max(1, len(inputs)))(*inputs)
@@ -350,3 +353,34 @@ def allreduce(ctx, outputs, elements, dtype, op="sum", inputs=None, max_segment_
     o.tag = tag
     o.stream = stream or None
     _check(lib.gloo_hip_allreduce(ctx._h, ctypes.byref(o)))
+
+
+# ---- new-style function API: gloo::reduce(opts) ----------------------------
+
+class ReduceOptions(ctypes.Structure):
+    """gloo_hip_reduce_options_t (mirrors gloo::ReduceOptions, gloo/reduce.h:19-110)."""
+    _fields_ = [("op", ctypes.c_int), ("dtype", ctypes.c_int), ("input", ctypes.c_void_p),
+                ("output", ctypes.c_void_p), ("elements", ctypes.c_size_t), ("root", ctypes.c_int),
+                ("max_segment_bytes", ctypes.c_size_t), ("tag", ctypes.c_uint32), ("stream", ctypes.c_void_p)]
+
+
+lib.gloo_hip_reduce_to_root.argtypes = [ctypes.c_void_p, ctypes.POINTER(ReduceOptions)]
+EXPORTED = EXPORTED + ("gloo_hip_reduce_to_root",)
+
+
+def reduce_to_root(ctx, output, elements, dtype, root, op="sum", input=None, max_segment_bytes=0, tag=0,
+                   stream=0):
+    """gloo::reduce(opts) (gloo/reduce.cc:21-247) on device pointers: the
+    root's output receives the reduction of every rank's input (or output,
+    when no input is given)."""
+    o = ReduceOptions()
+    o.op = _as_op(op)
+    o.dtype = _as_dtype(dtype)
+    o.input = input or None
+    o.output = output
+    o.elements = int(elements)
+    o.root = int(root)
+    o.max_segment_bytes = int(max_segment_bytes)
+    o.tag = tag
+    o.stream = stream or None
+    _check(lib.gloo_hip_reduce_to_root(ctx._h, ctypes.byref(o)))

@@ -34,6 +34,34 @@ int guarded(F&& f) {
     return gloo_amd::setError(GLOO_HIP_EINVAL_ARG, "unknown exception");
   }
 }
+
+// Function-style collectives: one executor per option set (the plan depends
+// on sizes, not pointers; every rank makes the same calls, so hits and
+// evictions agree), rebound to the call's buffers and run.
+void runCached(gloo_hip_context_t ctx, int algo, int op, int dtype, const std::vector<void*>& ins,
+               const std::vector<void*>& outs, size_t elements, size_t maxSeg, uint32_t tag,
+               gloo_hip_stream_t stream, const std::vector<int>& extra) {
+  std::string key = gloo_amd::strcat_(algo, "/", op, "/", dtype, "/", ins.size(), "/", outs.size(), "/", elements,
+                                      "/", maxSeg, "/", tag, "/", reinterpret_cast<uintptr_t>(stream));
+  for (int v : extra) key += gloo_amd::strcat_("/", v);
+  auto& cache = ctx->cache;
+  auto it = cache.begin();
+  for (; it != cache.end(); ++it)
+    if (it->first == key) break;
+  if (it == cache.end()) {
+    constexpr size_t kMaxCached = 16;
+    if (cache.size() == kMaxCached) cache.pop_back();
+    cache.emplace_front(key, std::make_unique<gloo_amd::PlanExecutor>(ctx->ctx, algo, op, dtype, outs, elements,
+                                                                      extra, static_cast<hipStream_t>(stream), ins,
+                                                                      maxSeg));
+    it = cache.begin();
+  } else if (it != cache.begin()) {
+    cache.splice(cache.begin(), cache, it);
+    it = cache.begin();
+  }
+  it->second->setBuffers(ins, outs);
+  it->second->run();
+}
 }  // namespace
 
 extern "C" {
@@ -97,32 +125,29 @@ int gloo_hip_algorithm_destroy(gloo_hip_algorithm_t a) {
 int gloo_hip_allreduce(gloo_hip_context_t ctx, const gloo_hip_allreduce_options_t* o) {
   return guarded([&] {
     GLOO_AMD_ENFORCE(ctx && o, "null argument");
-    GLOO_AMD_ENFORCE(o->algorithm == 0 || o->algorithm == GLOO_HIP_ALLREDUCE_RING, "only RING is implemented");
+    GLOO_AMD_ENFORCE(o->algorithm == 0 || o->algorithm == GLOO_HIP_ALLREDUCE_RING ||
+                         o->algorithm == GLOO_HIP_ALLREDUCE_BCUBE,
+                     "Algorithm not handled.");  // gloo/allreduce.cc:142-143
     GLOO_AMD_ENFORCE(o->noutputs >= 1 && o->outputs, "need at least one output");
     GLOO_AMD_ENFORCE(o->ninputs == 0 || o->inputs, "null inputs");
     if (o->elements == 0) return;  // gloo/allreduce.cc:98-100
     std::vector<void*> ins(o->inputs, o->inputs + o->ninputs), outs(o->outputs, o->outputs + o->noutputs);
-    const std::string key = gloo_amd::strcat_(o->op, "/", o->dtype, "/", o->ninputs, "/", o->noutputs, "/",
-                                              o->elements, "/", o->max_segment_bytes, "/", o->tag, "/",
-                                              reinterpret_cast<uintptr_t>(o->stream));
-    auto& cache = ctx->cache;
-    auto it = cache.begin();
-    for (; it != cache.end(); ++it)
-      if (it->first == key) break;
-    if (it == cache.end()) {
-      constexpr size_t kMaxCached = 16;
-      if (cache.size() == kMaxCached) cache.pop_back();
-      cache.emplace_front(key, std::make_unique<gloo_amd::PlanExecutor>(
-                                   ctx->ctx, GLOO_HIP_ALGO_ALLREDUCE_RING, o->op, o->dtype, outs, o->elements,
-                                   std::vector<int>{}, static_cast<hipStream_t>(o->stream), ins,
-                                   o->max_segment_bytes));
-      it = cache.begin();
-    } else if (it != cache.begin()) {
-      cache.splice(cache.begin(), cache, it);
-      it = cache.begin();
-    }
-    it->second->setBuffers(ins, outs);
-    it->second->run();
+    const int algo = o->algorithm == GLOO_HIP_ALLREDUCE_BCUBE ? GLOO_HIP_ALGO_ALLREDUCE_BCUBE
+                                                              : GLOO_HIP_ALGO_ALLREDUCE_RING;
+    runCached(ctx, algo, o->op, o->dtype, ins, outs, o->elements, o->max_segment_bytes, o->tag, o->stream, {});
+  });
+}
+
+int gloo_hip_reduce_to_root(gloo_hip_context_t ctx, const gloo_hip_reduce_options_t* o) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(ctx && o, "null argument");
+    if (o->elements == 0) return;  // gloo/reduce.cc:22-24
+    GLOO_AMD_ENFORCE(o->output, "null output");
+    GLOO_AMD_ENFORCE(o->root >= 0 && o->root < ctx->ctx->size, "root ", o->root, " out of range");  // :32
+    std::vector<void*> ins, outs{o->output};
+    if (o->input && o->input != o->output) ins.push_back(o->input);  // :46-48
+    runCached(ctx, GLOO_HIP_ALGO_REDUCE, o->op, o->dtype, ins, outs, o->elements, o->max_segment_bytes, o->tag,
+              o->stream, {o->root});
   });
 }
 

@@ -148,13 +148,14 @@ struct PlanExecutor::HostShm {
 namespace {
 Plan planFor(int algo, int rank, int size, size_t count, int nin, int nout, size_t es, size_t maxSeg,
              const std::vector<int>& recvElems) {
-  if (algo == GLOO_HIP_ALGO_ALLREDUCE_RING) {
+  if (isNewStyle(algo)) {
     NewStyleOptions o;
     o.ninputs = nin;
     o.noutputs = nout;
     o.elemSize = es;
     o.maxSegmentBytes = maxSeg;
-    return makeAllreducePlan(rank, size, count, o);
+    if (algo == GLOO_HIP_ALGO_REDUCE) o.root = recvElems.empty() ? 0 : recvElems[0];  // gloo::reduce: {root}
+    return makeNewStylePlan(algo, rank, size, count, o);
   }
   return makePlan(algo, rank, size, count, nout, recvElems);
 }
@@ -204,6 +205,10 @@ void PlanExecutor::classifyPointers() {
   };
   classify(ptrs_, outRemote_, outStage_, 1);   // output 0 is the rank's working buffer
   classify(inputs_, inRemote_, inStage_, 0);
+  // gloo::reduce reads its input in SEND / REDUCE steps, not only in the
+  // staged local fold
+  GLOO_AMD_ENFORCE(algo_ != GLOO_HIP_ALGO_REDUCE || inputs_.empty() || !inRemote_[0],
+                   "gloo::reduce: the input must live on the rank's own device");
 }
 
 PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int dtype,
@@ -607,6 +612,13 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
   const size_t kFuseBytes = fuseBytes();
   const bool fuse = deviceSignal_ && !profiling_ && kFuseBytes > 0;
   auto userOrArena = [&](bool arena) { return arena ? arena_ : userPtr(0); };
+  // a SEND's source: the arena, input 0 (gloo::reduce's first segments) or output 0
+  auto sendSrc = [&](const Step& t) -> const char* {
+    const char* base = t.flags & GLOO_HIP_SRC_ARENA ? arena_
+                       : t.flags & GLOO_HIP_FROM_INPUTS ? static_cast<const char*>(inputs_.at(0))
+                                                        : userPtr(0);
+    return base + t.src_off * es_;
+  };
   const std::vector<Step>& steps = plan_.steps;
   auto sendDst = [&](const Step& t) {
     return peers_[t.peer].base + (remoteRegion_[{t.peer, t.slot}] + t.dst_off) * es_;
@@ -627,7 +639,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
           for (size_t k = b; k < std::min(j, b + kMaxCopyEntries); k++) {
             const Step& t = steps[k];
             const size_t bytes = t.length * es_;
-            d[nd++] = CopyDesc{sendDst(t), userOrArena(t.flags & GLOO_HIP_SRC_ARENA) + t.src_off * es_, bytes,
+            d[nd++] = CopyDesc{sendDst(t), sendSrc(t), bytes,
                                ctx_->counterDevicePtr(inst_, me, t.peer, t.slot), seqOf(k, r, graph),
                                ticket_ + (size_t)t.peer * GLOO_HIP_NUM_SLOTS + t.slot,
                                copySignalGrid(bytes, copyBlocksFor(t.peer))};
@@ -644,8 +656,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
           hipStream_t a = auxStream(k - i);
           GLOO_AMD_HIP_CHECK(hipStreamWaitEvent(a, fork, 0));
           if (t.length)
-            GLOO_AMD_HIP_CHECK(hipMemcpyAsync(sendDst(t), userOrArena(t.flags & GLOO_HIP_SRC_ARENA) + t.src_off * es_,
-                                              t.length * es_, hipMemcpyDeviceToDevice, a));
+            GLOO_AMD_HIP_CHECK(hipMemcpyAsync(sendDst(t), sendSrc(t), t.length * es_, hipMemcpyDeviceToDevice, a));
           if (deviceSignal_) {
             GLOO_AMD_HIP_CHECK(launchSignal(ctx_->counterDevicePtr(inst_, me, t.peer, t.slot), seqOf(k, r, graph),
                                             epoch, a));
@@ -709,8 +720,9 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
     if (fuse) {
       const bool isWait = s.kind == GLOO_HIP_STEP_WAIT_RECV || s.kind == GLOO_HIP_STEP_WAIT_NOTIFY;
       const Step* t = isWait && i + 1 < steps.size() ? &steps[i + 1] : &s;
-      const bool body = t->kind == GLOO_HIP_STEP_REDUCE || t->kind == GLOO_HIP_STEP_COPY ||
-                        t->kind == GLOO_HIP_STEP_SEND;
+      // (a three-operand REDUCE, out = in op inbox, is not a fused shape)
+      const bool body = (t->kind == GLOO_HIP_STEP_REDUCE && !(t->flags & GLOO_HIP_FROM_INPUTS)) ||
+                        t->kind == GLOO_HIP_STEP_COPY || t->kind == GLOO_HIP_STEP_SEND;
       if (body && t->length * es_ <= kFuseBytes && (isWait || t->kind == GLOO_HIP_STEP_SEND)) {
         int op = 0;
         char* dst = nullptr;
@@ -724,7 +736,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
           src = userOrArena(t->flags & GLOO_HIP_SRC_ARENA) + t->src_off * es_;
         } else {
           dst = peers_[t->peer].base + (remoteRegion_[{t->peer, t->slot}] + t->dst_off) * es_;
-          src = userOrArena(t->flags & GLOO_HIP_SRC_ARENA) + t->src_off * es_;
+          src = sendSrc(*t);
         }
         const size_t bytes = t->length * es_;
         const bool overlap = dst < src + bytes && src < dst + bytes && dst != src;
@@ -760,7 +772,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         break;
       case GLOO_HIP_STEP_SEND: {
         char* dst = peers_[s.peer].base + (remoteRegion_[{s.peer, s.slot}] + s.dst_off) * es_;
-        const char* src = (s.flags & GLOO_HIP_SRC_ARENA ? arena_ : userPtr(0)) + s.src_off * es_;
+        const char* src = sendSrc(s);
         if (kernelCopy_) {
           const unsigned grid = copySignalGrid(s.length * es_, copyBlocksFor(s.peer));
           checkRc(launchCopySignal(dst, src, s.length * es_, ctx_->counterDevicePtr(inst_, me, s.peer, s.slot),
@@ -785,9 +797,16 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
       }
       case GLOO_HIP_STEP_REDUCE:
         if (profiling_) GLOO_AMD_HIP_CHECK(hipEventRecord(event(), stream_));
-        checkRc(gloo_hip_reduce(op_, dtype_, userPtr(0) + s.dst_off * es_, arena_ + s.src_off * es_, s.length,
-                                stream_),
-                "gloo_hip_reduce");
+        if (s.flags & GLOO_HIP_FROM_INPUTS) {  // out = in op inbox (gloo/reduce.cc:180-184)
+          checkRc(gloo_hip_reduce3(op_, dtype_, userPtr(0) + s.dst_off * es_,
+                                   static_cast<const char*>(inputs_.at(0)) + s.dst_off * es_,
+                                   arena_ + s.src_off * es_, s.length, stream_),
+                  "gloo_hip_reduce3");
+        } else {
+          checkRc(gloo_hip_reduce(op_, dtype_, userPtr(0) + s.dst_off * es_, arena_ + s.src_off * es_, s.length,
+                                  stream_),
+                  "gloo_hip_reduce");
+        }
         if (profiling_) {
           GLOO_AMD_HIP_CHECK(hipEventRecord(event(), stream_));
           reduceBytes_ += 3.0 * s.length * es_;

@@ -710,12 +710,258 @@ Plan planAllreduceRing(int rank, int size, uint64_t count, const NewStyleOptions
   return p;
 }
 
+// ---------------------------------------------------------------------------
+// New-style gloo::allreduce(opts), BCUBE (gloo/allreduce.cc:397-669).
+// The group of every step is computed exactly as the reference does
+// (:466-503).  Reduce-scatter receives land in `tmp` at i * chunkLength
+// (:529-533) and are folded into out[myChunk] in group order, out = out op
+// tmp_i (:580-592) — one FOLD pass over all of them when they fit in one
+// launch.  Allgather receives (the reference's in-place out->recv, :622-626)
+// land in a second arena region laid out like `out` and are copied there.
+// Posting a receive is a credit to the sender, as in the ring; messages of
+// length 0 are skipped on both sides (both compute the same length).
+// Arena = [tmp: bufferLength (:507-511) | allgather: count].
+// ---------------------------------------------------------------------------
+std::vector<uint64_t> groupSizePerStep(uint64_t size, uint64_t n) {  // :397-408
+  std::vector<uint64_t> out;
+  while (size % n == 0) {
+    out.push_back(n);
+    size /= n;
+  }
+  if (size > 1) out.push_back(size);
+  return out;
+}
+
+Plan planAllreduceBcube(int rank, int size, uint64_t count, const NewStyleOptions& o) {
+  Plan p;
+  if (count == 0) return p;                                             // :98-100
+  const bool localReduce = o.ninputs > 0 || o.noutputs > 1;
+  const int fromInputs = o.ninputs > 0 ? GLOO_HIP_FROM_INPUTS : 0;
+  auto reduceInputs = [&](uint64_t off, uint64_t len) {                 // :42-84
+    if (localReduce && len) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, fromInputs, off, 0, len));
+  };
+  auto broadcastOutputs = [&](uint64_t off, uint64_t len) {             // :89-98
+    if (o.noutputs > 1 && len) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, off, 0, len));
+  };
+  if (size == 1) {                                                      // :125-129
+    reduceInputs(0, count);
+    broadcastOutputs(0, count);
+    return p;
+  }
+  struct Group {
+    uint64_t bufferOffset = 0, bufferLength = 0, chunkLength = 0, myChunkOffset = 0, myChunkLength = 0;
+    std::vector<int> ranks;
+    // length of member i's chunk (:542-548, :615-621)
+    uint64_t lengthOf(size_t i) const {
+      const int64_t rest = (int64_t)bufferLength - (int64_t)(i * chunkLength);
+      return std::min<uint64_t>(chunkLength, (uint64_t)std::max<int64_t>(0, rest));
+    }
+    uint64_t offsetOf(size_t i) const { return bufferOffset + i * chunkLength; }
+  };
+  std::vector<Group> groups;
+  {
+    uint64_t peerDistance = 1, bufferOffset = 0, bufferLength = count;
+    for (const uint64_t groupSize : groupSizePerStep((uint64_t)size, 2)) {
+      Group g;
+      const uint64_t groupRank = ((uint64_t)rank / peerDistance) % groupSize;
+      const uint64_t baseRank = (uint64_t)rank - groupRank * peerDistance;
+      for (uint64_t i = 0; i < groupSize; i++) g.ranks.push_back((int)(baseRank + i * peerDistance));
+      g.bufferOffset = bufferOffset;
+      g.bufferLength = bufferLength;
+      g.chunkLength = (bufferLength + groupSize - 1) / groupSize;
+      g.myChunkOffset = bufferOffset + groupRank * g.chunkLength;
+      g.myChunkLength = g.lengthOf(groupRank);
+      groups.push_back(g);
+      peerDistance *= groupSize;
+      bufferOffset = g.myChunkOffset;
+      bufferLength = g.myChunkLength;
+    }
+  }
+  uint64_t tmpLength = count;                                            // :507-511
+  for (const Group& g : groups) tmpLength = std::max<uint64_t>(tmpLength, g.ranks.size() * g.chunkLength);
+  const uint64_t agBase = tmpLength;
+  p.arena = tmpLength + count;
+  // Every peer appears in exactly one step (members of a step's group differ
+  // from this rank in that step's mixed-radix digit only), so one region per
+  // (peer, slot) is enough.
+  for (const Group& g : groups)
+    for (size_t i = 0; i < g.ranks.size(); i++) {
+      const int peer = g.ranks[i];
+      if (peer == rank) continue;
+      if (g.myChunkLength)
+        p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, peer, GLOO_HIP_SLOT_DATA0, 0, i * g.chunkLength, 0,
+                             g.myChunkLength));
+      if (g.lengthOf(i))
+        p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, peer, GLOO_HIP_SLOT_AUX0, 0, agBase + g.offsetOf(i), 0,
+                             g.lengthOf(i)));
+    }
+  // Reduce/scatter (:519-593).
+  for (size_t step = 0; step < groups.size(); step++) {
+    const Group& g = groups[step];
+    for (int peer : g.ranks)                                             // tmp->recv (:524-534)
+      if (peer != rank && g.myChunkLength) p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, peer, GLOO_HIP_SLOT_NOTIFY));
+    if (step == 0)                                                       // :549-554
+      for (size_t i = 0; i < g.ranks.size(); i++)
+        if (g.ranks[i] != rank) reduceInputs(g.offsetOf(i), g.lengthOf(i));
+    // credits first, then every send in one batch (one launch, all links)
+    for (size_t i = 0; i < g.ranks.size(); i++)
+      if (g.ranks[i] != rank && g.lengthOf(i))
+        p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, g.ranks[i], GLOO_HIP_SLOT_NOTIFY));
+    for (size_t i = 0; i < g.ranks.size(); i++)                          // out->send (:555-559)
+      if (g.ranks[i] != rank && g.lengthOf(i))
+        p.steps.push_back(mk(GLOO_HIP_STEP_SEND, g.ranks[i], GLOO_HIP_SLOT_DATA0, 0, 0, g.offsetOf(i), g.lengthOf(i)));
+    if (g.myChunkLength)                                                 // :563-570
+      for (int peer : g.ranks)
+        if (peer != rank) p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, peer, GLOO_HIP_SLOT_DATA0));
+    if (step == 0) reduceInputs(g.myChunkOffset, g.myChunkLength);      // :574-577
+    if (g.myChunkLength == 0) continue;
+    // out = ((out op tmp_0) op tmp_1) ... over the peers in group order (:580-592)
+    if (g.ranks.size() <= (size_t)GLOO_HIP_MAX_SRCS) {
+      p.steps.push_back(mk(GLOO_HIP_STEP_FOLD_SRC, -1, 0, 0, 0, g.myChunkOffset, 0));
+      for (size_t i = 0; i < g.ranks.size(); i++)
+        if (g.ranks[i] != rank)
+          p.steps.push_back(mk(GLOO_HIP_STEP_FOLD_SRC, -1, 0, GLOO_HIP_SRC_ARENA, 0, i * g.chunkLength, 0));
+      p.steps.push_back(mk(GLOO_HIP_STEP_FOLD, -1, 0, 0, g.myChunkOffset, 0, g.myChunkLength));
+    } else {
+      for (size_t i = 0; i < g.ranks.size(); i++)
+        if (g.ranks[i] != rank)
+          p.steps.push_back(mk(GLOO_HIP_STEP_REDUCE, -1, 0, GLOO_HIP_SRC_ARENA, g.myChunkOffset, i * g.chunkLength,
+                               g.myChunkLength));
+    }
+  }
+  broadcastOutputs(groups.back().myChunkOffset, groups.back().myChunkLength);  // :599-603
+  // Allgather (:605-668).
+  for (auto it = groups.rbegin(); it != groups.rend(); ++it) {
+    const Group& g = *it;
+    for (size_t i = 0; i < g.ranks.size(); i++)                          // out->recv (:610-627)
+      if (g.ranks[i] != rank && g.lengthOf(i))
+        p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, g.ranks[i], GLOO_HIP_SLOT_AUX_NOTIFY));
+    if (g.myChunkLength) {                                               // out->send (:630-640)
+      for (int peer : g.ranks)
+        if (peer != rank) p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, peer, GLOO_HIP_SLOT_AUX_NOTIFY));
+      for (int peer : g.ranks)
+        if (peer != rank)
+          p.steps.push_back(mk(GLOO_HIP_STEP_SEND, peer, GLOO_HIP_SLOT_AUX0, 0, 0, g.myChunkOffset, g.myChunkLength));
+    }
+    for (size_t i = 0; i < g.ranks.size(); i++)                          // :643-650
+      if (g.ranks[i] != rank && g.lengthOf(i))
+        p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, g.ranks[i], GLOO_HIP_SLOT_AUX0));
+    for (size_t i = 0; i < g.ranks.size(); i++)
+      if (g.ranks[i] != rank && g.lengthOf(i))
+        p.steps.push_back(mk(GLOO_HIP_STEP_COPY, -1, 0, GLOO_HIP_SRC_ARENA, g.offsetOf(i), agBase + g.offsetOf(i),
+                             g.lengthOf(i)));
+    for (size_t i = 0; i < g.ranks.size(); i++)                          // :653-667
+      if (g.ranks[i] != rank) broadcastOutputs(g.offsetOf(i), g.lengthOf(i));
+  }
+  return p;
+}
+
+// ---------------------------------------------------------------------------
+// New-style gloo::reduce(opts) (gloo/reduce.cc:21-247).  A ring
+// reduce-scatter over two segment inboxes (tmp, :124-134) — out = in op tmp
+// (:180-184), the first numSegmentsPerRank sends read `in` (:206-210) — then
+// every rank's reduced chunk goes to the root (:221-246), landing in an arena
+// region laid out like `out` and copied there.  REDUCE / SEND carry
+// GLOO_HIP_FROM_INPUTS when a separate input exists.
+// Arena = [tmp0 | tmp1 | (root only) gather: numSegments segments].
+// ---------------------------------------------------------------------------
+Plan planReduce(int rank, int size, uint64_t count, const NewStyleOptions& o) {
+  Plan p;
+  if (count == 0) return p;                                             // :22-24
+  if (o.root < 0 || o.root >= size) throw std::invalid_argument("root out of range");  // :32
+  const int fromIn = o.ninputs > 0 ? GLOO_HIP_FROM_INPUTS : 0;
+  if (size == 1) {                                                      // :54-59
+    if (fromIn) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, GLOO_HIP_FROM_INPUTS, 0, 0, count));
+    return p;
+  }
+  auto roundUp = [](uint64_t v, uint64_t m) { return v % m == 0 ? v : v + m - v % m; };
+  const uint64_t es = o.elemSize;
+  const uint64_t totalBytes = count * es;
+  const uint64_t maxSegmentSize = es * ((o.maxSegmentBytes ? o.maxSegmentBytes : 1024 * 1024) / es);  // :90-91
+  if (maxSegmentSize == 0) throw std::invalid_argument("maxSegmentSize below one element");
+  const uint64_t P = (uint64_t)size;
+  const uint64_t segmentBytes =
+      roundUp(std::min<uint64_t>((totalBytes + (P * 2 - 1)) / (P * 2), maxSegmentSize), es);  // :95-101
+  const uint64_t numSegments =
+      roundUp(std::max<uint64_t>((totalBytes + (segmentBytes - 1)) / segmentBytes, P * 2), P);  // :113-117
+  const uint64_t nspr = numSegments / P;                                // :120
+  const uint64_t seg = segmentBytes / es;                               // elements
+  const uint64_t chunk = nspr * seg;                                    // :121
+  const int recvRank = (size + rank + 1) % size, sendRank = (size + rank - 1) % size;  // :34-43
+  const uint64_t gatherBase = 2 * seg;
+  p.arena = 2 * seg + (rank == o.root ? numSegments * seg : 0);
+  p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, recvRank, GLOO_HIP_SLOT_DATA0, 0, 0, 0, seg));
+  p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, recvRank, GLOO_HIP_SLOT_DATA1, 0, seg, 0, seg));
+  auto chunkLength = [&](int r) {                                       // :227-229, :239-241
+    return std::min<int64_t>((int64_t)chunk, (int64_t)count - (int64_t)((uint64_t)r * chunk));
+  };
+  if (rank == o.root)
+    for (int r = 0; r < size; r++)
+      if (r != rank && chunkLength(r) > 0)
+        p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, r, GLOO_HIP_SLOT_DIST, 0, gatherBase + (uint64_t)r * chunk, 0,
+                             (uint64_t)chunkLength(r)));
+  struct Off {
+    uint64_t sendOffset, recvOffset;
+    int64_t sendLength, recvLength;
+  };
+  auto offsets = [&](uint64_t i) {                                      // :138-169
+    Off r;
+    r.sendOffset = ((((uint64_t)rank + 1) * nspr + i) * seg) % (numSegments * seg);
+    r.recvOffset = ((((uint64_t)rank + 2) * nspr + i) * seg) % (numSegments * seg);
+    r.sendLength = std::min<int64_t>((int64_t)seg, (int64_t)count - (int64_t)r.sendOffset);
+    r.recvLength = std::min<int64_t>((int64_t)seg, (int64_t)count - (int64_t)r.recvOffset);
+    return r;
+  };
+  for (uint64_t i = 0; i < numSegments; i++) {                          // :171-213
+    const int buf = (int)(i & 1);
+    if (i >= 2) {
+      const Off prev = offsets(i - 2);
+      if (prev.recvLength > 0) {
+        p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, recvRank, GLOO_HIP_SLOT_DATA0 + buf));
+        p.steps.push_back(mk(GLOO_HIP_STEP_REDUCE, -1, 0, GLOO_HIP_SRC_ARENA | fromIn, prev.recvOffset, buf * seg,
+                             (uint64_t)prev.recvLength));
+      }
+    }
+    if (i + 2 < numSegments) {
+      const Off cur = offsets(i);
+      if (cur.recvLength > 0) p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, recvRank, GLOO_HIP_SLOT_NOTIFY));
+      if (cur.sendLength > 0) {
+        p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, sendRank, GLOO_HIP_SLOT_NOTIFY));
+        p.steps.push_back(mk(GLOO_HIP_STEP_SEND, sendRank, GLOO_HIP_SLOT_DATA0 + buf, i < nspr ? fromIn : 0, 0,
+                             cur.sendOffset, (uint64_t)cur.sendLength));
+      }
+    }
+  }
+  if (rank == o.root) {                                                 // :221-237
+    for (int r = 0; r < size; r++)
+      if (r != rank && chunkLength(r) > 0) p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, r, GLOO_HIP_SLOT_DIST_NOTIFY));
+    for (int r = 0; r < size; r++)
+      if (r != rank && chunkLength(r) > 0) p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, r, GLOO_HIP_SLOT_DIST));
+    for (int r = 0; r < size; r++)
+      if (r != rank && chunkLength(r) > 0)
+        p.steps.push_back(mk(GLOO_HIP_STEP_COPY, -1, 0, GLOO_HIP_SRC_ARENA, (uint64_t)r * chunk,
+                             gatherBase + (uint64_t)r * chunk, (uint64_t)chunkLength(r)));
+  } else if (chunkLength(rank) > 0) {                                   // :238-246
+    p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, o.root, GLOO_HIP_SLOT_DIST_NOTIFY));
+    p.steps.push_back(mk(GLOO_HIP_STEP_SEND, o.root, GLOO_HIP_SLOT_DIST, 0, 0, (uint64_t)rank * chunk,
+                         (uint64_t)chunkLength(rank)));
+  }
+  return p;
+}
+
 }  // namespace
 
-Plan makeAllreducePlan(int rank, int size, uint64_t count, const NewStyleOptions& o) {
+Plan makeNewStylePlan(int algo, int rank, int size, uint64_t count, const NewStyleOptions& o) {
   if (size < 1 || rank < 0 || rank >= size) throw std::invalid_argument("bad rank/size");
   if (o.noutputs < 1 || o.ninputs < 0 || o.elemSize == 0) throw std::invalid_argument("bad options");
-  return planAllreduceRing(rank, size, count, o);
+  switch (algo) {
+    case GLOO_HIP_ALGO_ALLREDUCE_RING: return planAllreduceRing(rank, size, count, o);
+    case GLOO_HIP_ALGO_ALLREDUCE_BCUBE: return planAllreduceBcube(rank, size, count, o);
+    case GLOO_HIP_ALGO_REDUCE:
+      if (o.ninputs > 1 || o.noutputs != 1) throw std::invalid_argument("gloo::reduce takes one input and one output");
+      return planReduce(rank, size, count, o);
+  }
+  throw std::invalid_argument("not a new-style algorithm");
 }
 
 Plan makePlan(int algo, int rank, int size, uint64_t count, int nptrs, const std::vector<int>& recvElems) {
@@ -758,13 +1004,17 @@ extern "C" int gloo_hip_plan_ex(int algo, int rank, int size, size_t count, int 
       re.assign(recv_elems, recv_elems + size);
     }
     gloo_amd::Plan p;
-    if (algo == GLOO_HIP_ALGO_ALLREDUCE_RING) {
+    if (gloo_amd::isNewStyle(algo)) {
       gloo_amd::NewStyleOptions o;
       o.ninputs = ninputs;
       o.noutputs = noutputs;
       o.elemSize = elem_size;
       o.maxSegmentBytes = max_segment_bytes;
-      p = gloo_amd::makeAllreducePlan(rank, size, count, o);
+      if (algo == GLOO_HIP_ALGO_REDUCE) {
+        if (!recv_elems) return GLOO_HIP_EINVAL_ARG;  // recv_elems[0] = root
+        o.root = recv_elems[0];
+      }
+      p = gloo_amd::makeNewStylePlan(algo, rank, size, count, o);
     } else {
       p = gloo_amd::makePlan(algo, rank, size, count, noutputs, re);
     }

@@ -200,6 +200,9 @@ class AllreduceOptions {
   void setTag(uint32_t tag) { tag_ = tag; }
   void setMaxSegmentSize(size_t bytes) { maxSegmentBytes_ = bytes; }
   void setStream(hipStream_t s) { stream_ = s; }
+  // AllreduceOptions::Algorithm (gloo/allreduce.h:38-42)
+  enum class Algorithm { UNSPECIFIED = 0, RING = 1, BCUBE = 2 };
+  void setAlgorithm(Algorithm a) { algorithm_ = a; }
 
   std::shared_ptr<Context> context_;
   std::vector<void*> inputs_, outputs_;
@@ -209,14 +212,62 @@ class AllreduceOptions {
   uint32_t tag_ = 0;
   size_t maxSegmentBytes_ = 0;
   hipStream_t stream_ = nullptr;
+  Algorithm algorithm_ = Algorithm::UNSPECIFIED;
 };
 
 // One call = one allreduce (builds a PlanExecutor each time; the C-ABI
 // gloo_hip_allreduce caches them per option set).
 inline void allreduce(const AllreduceOptions& o) {
   if (o.elements_ == 0) return;
-  PlanExecutor exec(o.context_, GLOO_HIP_ALGO_ALLREDUCE_RING, o.op_, o.dtype_, o.outputs_, o.elements_, {},
-                    o.stream_, o.inputs_, o.maxSegmentBytes_);
+  const int algo = o.algorithm_ == AllreduceOptions::Algorithm::BCUBE ? GLOO_HIP_ALGO_ALLREDUCE_BCUBE
+                                                                       : GLOO_HIP_ALGO_ALLREDUCE_RING;
+  PlanExecutor exec(o.context_, algo, o.op_, o.dtype_, o.outputs_, o.elements_, {}, o.stream_, o.inputs_,
+                    o.maxSegmentBytes_);
+  exec.run();
+}
+
+// gloo::ReduceOptions (gloo/reduce.h:19-110) over device pointers.
+class ReduceOptions {
+ public:
+  explicit ReduceOptions(const std::shared_ptr<Context>& context) : context_(context) {}
+  template <typename T>
+  void setInput(T* ptr, size_t elements) {
+    input_ = ptr;
+    elements_ = elements;
+    dtype_ = DType<T>::value;
+  }
+  template <typename T>
+  void setOutput(T* ptr, size_t elements) {
+    output_ = ptr;
+    elements_ = elements;
+    dtype_ = DType<T>::value;
+  }
+  void setRoot(int root) { root_ = root; }
+  void setReduceFunction(ReductionType op) { op_ = op; }
+  void setTag(uint32_t tag) { tag_ = tag; }
+  void setMaxSegmentSize(size_t bytes) { maxSegmentBytes_ = bytes; }
+  void setStream(hipStream_t s) { stream_ = s; }
+
+  std::shared_ptr<Context> context_;
+  void* input_ = nullptr;
+  void* output_ = nullptr;
+  size_t elements_ = 0;
+  int dtype_ = GLOO_HIP_F32;
+  int root_ = -1;
+  ReductionType op_ = SUM;
+  uint32_t tag_ = 0;
+  size_t maxSegmentBytes_ = 0;
+  hipStream_t stream_ = nullptr;
+};
+
+// gloo::reduce(opts) (gloo/reduce.cc:21-247).
+inline void reduce(const ReduceOptions& o) {
+  if (o.elements_ == 0) return;
+  GLOO_AMD_ENFORCE(o.root_ >= 0 && o.root_ < o.context_->size, "root ", o.root_, " out of range");
+  std::vector<void*> ins;
+  if (o.input_ && o.input_ != o.output_) ins.push_back(o.input_);
+  PlanExecutor exec(o.context_, GLOO_HIP_ALGO_REDUCE, o.op_, o.dtype_, {o.output_}, o.elements_, {o.root_},
+                    o.stream_, ins, o.maxSegmentBytes_);
   exec.run();
 }
 

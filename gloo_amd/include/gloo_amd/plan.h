@@ -19,13 +19,20 @@ struct Plan {
 Plan makePlan(int algo, int rank, int size, uint64_t count, int nptrs,
               const std::vector<int>& recvElems = {});
 
-// New-style allreduce parameters (gloo/allreduce.h:89-193).
+// New-style collective parameters (gloo/allreduce.h:89-193, gloo/reduce.h:19-110).
 struct NewStyleOptions {
   int ninputs = 0;
   int noutputs = 1;
   size_t elemSize = 4;
-  size_t maxSegmentBytes = 1024 * 1024;  // kMaxSegmentSize, gloo/allreduce.h:78
+  size_t maxSegmentBytes = 1024 * 1024;  // kMaxSegmentSize, gloo/allreduce.h:78, gloo/reduce.h:98
+  int root = 0;                          // gloo::reduce only (ReduceOptions::setRoot)
 };
-Plan makeAllreducePlan(int rank, int size, uint64_t count, const NewStyleOptions& o);
+// algo: GLOO_HIP_ALGO_ALLREDUCE_RING, GLOO_HIP_ALGO_ALLREDUCE_BCUBE or
+// GLOO_HIP_ALGO_REDUCE.
+Plan makeNewStylePlan(int algo, int rank, int size, uint64_t count, const NewStyleOptions& o);
+inline bool isNewStyle(int algo) {
+  return algo == GLOO_HIP_ALGO_ALLREDUCE_RING || algo == GLOO_HIP_ALGO_ALLREDUCE_BCUBE ||
+         algo == GLOO_HIP_ALGO_REDUCE;
+}
 
 }  // namespace gloo_amd

@@ -139,6 +139,11 @@ typedef enum {
    * 2 <= size <= GLOO_HIP_MAX_SRCS.  RING_CHUNKED executes as this plan when
    * GLOO_AMD_RING_MESH selects it. */
   GLOO_HIP_ALGO_RING_CHUNKED_MESH = 6,
+  GLOO_HIP_ALGO_ALLREDUCE_BCUBE = 7,  /* new-style gloo::allreduce(opts), BCUBE
+                                         (gloo/allreduce.cc:397-669)          */
+  GLOO_HIP_ALGO_REDUCE = 8,           /* new-style gloo::reduce(opts)
+                                         (gloo/reduce.cc:21-247); the root is
+                                         recv_elems[0] in gloo_hip_plan*      */
 } gloo_hip_algo_t;
 
 /* algo | GLOO_HIP_ALGO_MESH: the algorithm's result with mesh data movement,
@@ -183,7 +188,8 @@ typedef enum {
 #define GLOO_HIP_DST_ARENA 2
 /* LOCAL_REDUCE over [dst_off, +length) folds the separate INPUT buffers into
  * output 0 (new-style allreduce; one input = copy), instead of folding the
- * outputs into output 0. */
+ * outputs into output 0.  On REDUCE: user[dst] = input0[dst] op arena[src]
+ * (gloo::reduce's out = in op tmp); on SEND: the source is input 0. */
 #define GLOO_HIP_FROM_INPUTS 4
 /* FOLD: each new source is the LEFT operand (acc = s_k op acc). */
 #define GLOO_HIP_FOLD_REVERSE 8
@@ -297,9 +303,10 @@ int gloo_hip_algorithm_mode(gloo_hip_algorithm_t algo, int* mode4);
  * inbox arena (a store exchange); later calls reuse it with the buffers of
  * the call.
  * ---------------------------------------------------------------------- */
-#define GLOO_HIP_ALLREDUCE_RING 1 /* AllreduceOptions::Algorithm::RING */
+#define GLOO_HIP_ALLREDUCE_RING 1  /* AllreduceOptions::Algorithm::RING  */
+#define GLOO_HIP_ALLREDUCE_BCUBE 2 /* AllreduceOptions::Algorithm::BCUBE (gloo/allreduce.h:38-42) */
 typedef struct {
-  int algorithm;            /* 0 (unspecified) or GLOO_HIP_ALLREDUCE_RING */
+  int algorithm;            /* 0 (unspecified = RING), RING or BCUBE      */
   int op;                   /* gloo_hip_op_t: the reduce Func             */
   int dtype;                /* gloo_hip_dtype_t: setInputs<T>/setOutputs<T> */
   void* const* inputs;      /* device pointers, may be NULL               */
@@ -313,6 +320,29 @@ typedef struct {
 } gloo_hip_allreduce_options_t;
 
 int gloo_hip_allreduce(gloo_hip_context_t ctx, const gloo_hip_allreduce_options_t* opts);
+
+/* ------------------------------------------------------------------------
+ * New-style function API: gloo::reduce(ReduceOptions&) (gloo/reduce.h:19-112,
+ * gloo/reduce.cc:21-247): a ring reduce-scatter over <= max_segment_bytes
+ * segments, then every rank's reduced chunk is gathered at `root`.  `input`
+ * may be NULL (the output is the input).  Only the root's output holds the
+ * full result; the other ranks' outputs hold the same partial reductions the
+ * reference leaves there.  Collective, cached per option set like
+ * gloo_hip_allreduce.
+ * ---------------------------------------------------------------------- */
+typedef struct {
+  int op;                   /* gloo_hip_op_t: the reduce Func              */
+  int dtype;                /* gloo_hip_dtype_t: setInput<T>/setOutput<T>  */
+  void* input;              /* device pointer, may be NULL                 */
+  void* output;             /* device pointer                              */
+  size_t elements;
+  int root;                 /* setRoot                                     */
+  size_t max_segment_bytes; /* setMaxSegmentSize; 0 = 1 MiB (reduce.h:98)  */
+  uint32_t tag;             /* setTag                                      */
+  gloo_hip_stream_t stream; /* NULL: the output is complete on return      */
+} gloo_hip_reduce_options_t;
+
+int gloo_hip_reduce_to_root(gloo_hip_context_t ctx, const gloo_hip_reduce_options_t* opts);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -77,6 +77,11 @@ def ref():
         L.ref_allreduce_new.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
                                         ctypes.c_void_p, ctypes.c_void_p]
+        L.ref_allreduce_new_algo.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
+                                             ctypes.c_void_p, ctypes.c_void_p]
+        L.ref_reduce_new.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                                     ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.ref_last_error.restype = ctypes.c_char_p
         _ref = L
     return _ref

@@ -206,7 +206,76 @@ def gen_sched():
     print("sched_golden.npz:", len(out), "arrays")
 
 
+def _values(dtype, op, shape, rng):
+    if dtype in ("u64", "i32"):
+        npt = oracle.DTYPES[dtype][1]
+        hi = 1 << 40 if dtype == "u64" else 1 << 20
+        return rng.integers(0, hi, shape, dtype=np.int64).astype(npt)
+    return sched_inputs(dtype, op, shape, rng)
+
+
+def gen_newstyle():
+    """newstyle_golden.npz: gloo::allreduce(opts) with BCUBE
+    (gloo/allreduce.cc:397-669) and gloo::reduce(opts) (gloo/reduce.cc:21-247)."""
+    rng = np.random.default_rng(SEED + 2)
+    out = {}
+    bcube = []
+    for P in (2, 3, 4, 5, 6, 7, 8, 12):
+        for n in (1, 10, 1000, 4099):
+            bcube.append(("sum", "f32", P, 0, 1, n))
+    bcube += [("sum", "f32", 4, 2, 1, 1000), ("sum", "f32", 6, 3, 2, 999), ("sum", "f32", 8, 1, 3, 4099),
+              ("max", "f32", 6, 0, 1, 3000), ("min", "f32", 8, 0, 2, 777), ("product", "f64", 3, 2, 1, 999),
+              ("sum", "bf16", 8, 0, 1, 4096), ("sum", "f16", 4, 0, 1, 1024), ("sum", "u64", 7, 2, 2, 1000),
+              ("max", "bf16", 12, 0, 1, 5000)]
+    for op, dtype, P, nin, nout, n in bcube:
+        code, npt = oracle.DTYPES[dtype]
+        x = _values(dtype, op, (P, max(nin, 1), n), rng)
+        init = _values(dtype, op, (P, nout, n), rng)
+        y = np.ascontiguousarray(init.copy())
+        xin = np.ascontiguousarray(x[:, :nin]) if nin else np.zeros(1, dtype=npt)
+        rc = oracle.ref().ref_allreduce_new_algo(2, oracle.OPS[op], code, P, nin, nout, n, 0,
+                                                 xin.ctypes.data, y.ctypes.data)
+        if rc:
+            raise RuntimeError(f"bcube failed {rc}: {oracle.ref().ref_last_error()}")
+        key = f"bcube/{op}/{dtype}/P{P}/i{nin}/o{nout}/n{n}/s0"
+        assert all((y[r, j].view(np.uint8) == y[0, 0].view(np.uint8)).all()
+                   for r in range(P) for j in range(nout)), key
+        if nin:
+            out[key + "/in"] = x[:, :nin]
+        out[key + "/init"] = init
+        out[key + "/out"] = y[0, 0].copy()
+    red = []
+    for P in (2, 3, 4, 7):
+        for n in (1, 10, 1000, 10000):
+            red.append(("sum", "f32", P, 0, n, P - 1, 128 if n >= 1000 else 0))
+    red += [("sum", "f32", 4, 1, 1000, 0, 128), ("sum", "f32", 5, 1, 4099, 2, 0), ("max", "f32", 3, 0, 999, 1, 64),
+            ("product", "f64", 4, 1, 777, 3, 0), ("sum", "bf16", 8, 1, 4096, 5, 256), ("min", "f16", 6, 0, 2000, 0, 0),
+            ("sum", "u64", 7, 1, 1000, 6, 128), ("sum", "f32", 8, 0, 20011, 3, 0)]
+    for op, dtype, P, has_in, n, root, seg in red:
+        code, npt = oracle.DTYPES[dtype]
+        x = _values(dtype, op, (P, n), rng)
+        init = _values(dtype, op, (P, n), rng)
+        y = np.ascontiguousarray(init.copy())
+        xin = np.ascontiguousarray(x) if has_in else np.zeros(1, dtype=npt)
+        rc = oracle.ref().ref_reduce_new(oracle.OPS[op], code, P, has_in, n, seg, root,
+                                         xin.ctypes.data, y.ctypes.data)
+        if rc:
+            raise RuntimeError(f"reduce failed {rc}: {oracle.ref().ref_last_error()}")
+        key = f"reduce/{op}/{dtype}/P{P}/i{has_in}/n{n}/r{root}/s{seg}"
+        if has_in:
+            out[key + "/in"] = x[:, None, :]
+        out[key + "/init"] = init[:, None, :]
+        out[key + "/out"] = y  # every rank's output buffer, [P][n]
+    np.savez_compressed(os.path.join(OUT, "newstyle_golden.npz"), **out)
+    print("newstyle_golden.npz:", len(out), "arrays")
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    gen_math()
-    gen_sched()
+    which = sys.argv[1:] or ["math", "sched", "newstyle"]
+    if "math" in which:
+        gen_math()
+    if "sched" in which:
+        gen_sched()
+    if "newstyle" in which:
+        gen_newstyle()

@@ -38,6 +38,7 @@
 #include "gloo/allreduce_ring.h"
 #include "gloo/allreduce_ring_chunked.h"
 #include "gloo/math.h"
+#include "gloo/reduce.h"
 #include "gloo/reduce_scatter.h"
 #include "gloo/rendezvous/context.h"
 #include "gloo/rendezvous/hash_store.h"
@@ -213,10 +214,12 @@ int reduce_scatter(int op, int P, size_t n, const int* recvElems, const void* in
   });
 }
 
-// New-style gloo::allreduce(opts), ring algorithm (gloo/allreduce.cc:147-392).
+// New-style gloo::allreduce(opts), RING (gloo/allreduce.cc:147-392) or BCUBE
+// (:428-669), as `algorithm` (AllreduceOptions::Algorithm, gloo/allreduce.h:38-42).
 // in: [P][nin][n] (nin may be 0: outputs are the inputs); out: [P][nout][n].
 template <typename T>
-int allreduce_new(int op, int P, int nin, int nout, size_t n, size_t maxSeg, const void* in, void* out) {
+int allreduce_new(int algorithm, int op, int P, int nin, int nout, size_t n, size_t maxSeg, const void* in,
+                  void* out) {
   Fn3<T> fn = pick3<T>(op);
   if (!fn) return -1;
   std::vector<T> inputs((size_t)P * nin * n);
@@ -229,10 +232,31 @@ int allreduce_new(int op, int P, int nin, int nout, size_t n, size_t maxSeg, con
     for (int j = 0; j < nout; j++) op_.push_back(o + ((size_t)ctx->rank * nout + j) * n);
     if (nin) opts.setInputs(ip, n);
     opts.setOutputs(op_, n);
-    opts.setAlgorithm(gloo::AllreduceOptions::Algorithm::RING);
+    opts.setAlgorithm(algorithm == 2 ? gloo::AllreduceOptions::Algorithm::BCUBE
+                                     : gloo::AllreduceOptions::Algorithm::RING);
     opts.setReduceFunction(fn);
     if (maxSeg) opts.setMaxSegmentSize(maxSeg);
     gloo::allreduce(opts);
+  });
+}
+
+// New-style gloo::reduce(opts) (gloo/reduce.cc:21-247).  in: [P][n] (used
+// when has_input); out: [P][n] initial outputs, every rank's output after.
+template <typename T>
+int reduce_new(int op, int P, int has_input, size_t n, size_t maxSeg, int root, const void* in, void* out) {
+  Fn3<T> fn = pick3<T>(op);
+  if (!fn) return -1;
+  std::vector<T> inputs(has_input ? (size_t)P * n : 0);
+  if (has_input) std::memcpy(inputs.data(), in, inputs.size() * sizeof(T));
+  T* o = static_cast<T*>(out);
+  return spawn(P, [&](std::shared_ptr<gloo::Context> ctx) {
+    gloo::ReduceOptions opts(ctx);
+    if (has_input) opts.setInput(inputs.data() + (size_t)ctx->rank * n, n);
+    opts.setOutput(o + (size_t)ctx->rank * n, n);
+    opts.setRoot(root);
+    opts.setReduceFunction(fn);
+    if (maxSeg) opts.setMaxSegmentSize(maxSeg);
+    gloo::reduce(opts);
   });
 }
 
@@ -285,7 +309,19 @@ int ref_allreduce(int algo, int op, int dtype, int P, int k, size_t n, const voi
 // New-style allreduce; out holds the initial outputs and receives the result.
 int ref_allreduce_new(int op, int dtype, int P, int nin, int nout, size_t n, size_t maxSeg,
                       const void* in, void* out) {
-  DISPATCH(dtype, allreduce_new<T>(op, P, nin, nout, n, maxSeg, in, out));
+  DISPATCH(dtype, allreduce_new<T>(1, op, P, nin, nout, n, maxSeg, in, out));
+}
+
+// The same with the algorithm chosen: 1 = RING, 2 = BCUBE.
+int ref_allreduce_new_algo(int algorithm, int op, int dtype, int P, int nin, int nout, size_t n, size_t maxSeg,
+                           const void* in, void* out) {
+  DISPATCH(dtype, allreduce_new<T>(algorithm, op, P, nin, nout, n, maxSeg, in, out));
+}
+
+// New-style reduce; out holds the initial outputs and receives every rank's output.
+int ref_reduce_new(int op, int dtype, int P, int has_input, size_t n, size_t maxSeg, int root, const void* in,
+                   void* out) {
+  DISPATCH(dtype, reduce_new<T>(op, P, has_input, n, maxSeg, root, in, out));
 }
 
 // P ranks x n elements; rank r's reduced block lands at out[r][0:recvElems[r]].

@@ -19,7 +19,7 @@ import oracle
 KIND = dict(DECL_RECV=0, SEND=1, WAIT_RECV=2, REDUCE=3, COPY=4, NOTIFY=5, WAIT_NOTIFY=6,
             WAIT_SEND=7, LOCAL_REDUCE=8, LOCAL_BCAST=9, FOLD_SRC=10, FOLD=11)
 ALGO = dict(ring_chunked=0, halving_doubling=1, ring=2, local=3, reduce_scatter=4, allreduce_new=5,
-            ring_chunked_mesh=6)
+            ring_chunked_mesh=6, allreduce_bcube=7, reduce=8)
 MESH = 0x100  # algo | MESH: the derived mesh plan (gloo_amd/csrc/mesh.cc)
 ALGO.update({"mesh_" + k: v | MESH for k, v in list(ALGO.items()) if v < 5})
 SRC_ARENA, DST_ARENA, FROM_INPUTS, FOLD_REVERSE, FOLD_TREE, PREV_RUN = 1, 2, 4, 8, 16, 32
@@ -137,7 +137,7 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
             roff, cap = regions[key]
             if s.length > cap:
                 raise ProtocolError(f"send {key} of {s.length} exceeds region {cap}")
-            src = space(r, s.flags & SRC_ARENA)
+            src = ins[r, 0] if s.flags & FROM_INPUTS else space(r, s.flags & SRC_ARENA)
             arena[s.peer][roff:roff + s.length] = src[s.src_off:s.src_off + s.length]
             sent[key] = sent.get(key, 0) + 1
         elif K in (KIND["WAIT_RECV"], KIND["WAIT_NOTIFY"]):
@@ -148,7 +148,8 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
             sent[key] = sent.get(key, 0) + 1
         elif K == KIND["REDUCE"]:
             dst = user[r][0]
-            a = dst[s.dst_off:s.dst_off + s.length]
+            # FROM_INPUTS: out = in op inbox (gloo::reduce, gloo/reduce.cc:180-184)
+            a = (ins[r, 0] if s.flags & FROM_INPUTS else dst)[s.dst_off:s.dst_off + s.length]
             b = arena[r][s.src_off:s.src_off + s.length]
             dst[s.dst_off:s.dst_off + s.length] = oracle.reduce3(op, dtype, a, b)
         elif K == KIND["COPY"]:

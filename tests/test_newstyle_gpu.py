@@ -1,0 +1,185 @@
+"""GPU: gloo::allreduce(opts) with BCUBE and gloo::reduce(opts) through the
+C-ABI (gloo_hip_allreduce / gloo_hip_reduce_to_root), against the reference's
+own outputs (tests/golden/newstyle_golden.npz, oracle/gen_golden.py).
+
+Ranks as threads of one process (host-signalled, the pattern of
+gloo/test/base_test.h:107-152) and as processes (device-signalled, inboxes
+over HIP IPC, hipGraph replay of the cached schedule).
+"""
+import os
+import subprocess
+import sys
+import tempfile
+import threading
+import uuid
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden", "newstyle_golden.npz")
+
+
+@pytest.fixture(scope="module")
+def torch():
+    t = pytest.importorskip("torch")
+    if not t.cuda.is_available():
+        pytest.skip("no GPU")
+    return t
+
+
+@pytest.fixture(scope="module")
+def golden_new():
+    return np.load(GOLDEN)
+
+
+def _keys(prefix, max_p=8):
+    z = np.load(GOLDEN)
+    keys = sorted({k.rsplit("/", 1)[0] for k in z.files if k.startswith(prefix)})
+    return [k for k in keys if int(k.split("/")[3][1:]) <= max_p]
+
+
+def same_bytes(a, b):
+    return a.shape == b.shape and (a.view(np.uint8) == b.view(np.uint8)).all()
+
+
+def run_threads(P, body):
+    errors = []
+    ts = [threading.Thread(target=lambda r=r: _guard(body, r, errors)) for r in range(P)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+
+
+def _guard(body, r, errors):
+    try:
+        body(r)
+    except Exception as e:  # noqa: BLE001
+        errors.append((r, repr(e)))
+
+
+@pytest.mark.parametrize("case", _keys("bcube/"))
+def test_bcube_threads_golden(torch, golden_new, case):
+    """BCUBE allreduce, ranks as threads on the visible GPU(s); called twice
+    (the second call reuses the cached schedule with rebound buffers)."""
+    import gloo_amd
+    parts = case.split("/")
+    op, dtype, P = parts[1], parts[2], int(parts[3][1:])
+    nin, nout, n = int(parts[4][1:]), int(parts[5][1:]), int(parts[6][1:])
+    init = golden_new[case + "/init"]
+    ins = golden_new[case + "/in"] if nin else None
+    want = golden_new[case + "/out"]
+    url = "mem:" + uuid.uuid4().hex
+    ngpu = torch.cuda.device_count()
+    results = {}
+
+    def body(r):
+        d = torch.device("cuda", r % ngpu)
+        torch.cuda.set_device(d)
+        ctx = gloo_amd.Context(r, P, url, device=d.index, timeout_ms=60000)
+        for rep in range(2):
+            outs = [torch.from_numpy(init[r, j].view(np.uint8).copy()).to(d) for j in range(nout)]
+            inb = [torch.from_numpy(ins[r, j].view(np.uint8).copy()).to(d) for j in range(nin)]
+            torch.cuda.synchronize(d)
+            gloo_amd.allreduce(ctx, [t.data_ptr() for t in outs], n, dtype, op,
+                               inputs=[t.data_ptr() for t in inb], algorithm="bcube")
+            results[(r, rep)] = [t.cpu().numpy().view(init.dtype) for t in outs]
+        ctx.close()
+
+    run_threads(P, body)
+    for (r, rep), outs in results.items():
+        for j, y in enumerate(outs):
+            assert same_bytes(y, want), (r, rep, j)
+
+
+@pytest.mark.parametrize("case", _keys("reduce/"))
+def test_reduce_threads_golden(torch, golden_new, case):
+    """gloo::reduce: every rank's whole output equals the reference's (the
+    root holds the result, the others the partial sums the ring leaves)."""
+    import gloo_amd
+    parts = case.split("/")
+    op, dtype, P = parts[1], parts[2], int(parts[3][1:])
+    has_in, n, root, seg = int(parts[4][1:]), int(parts[5][1:]), int(parts[6][1:]), int(parts[7][1:])
+    init = golden_new[case + "/init"]
+    ins = golden_new[case + "/in"] if has_in else None
+    want = golden_new[case + "/out"]
+    url = "mem:" + uuid.uuid4().hex
+    ngpu = torch.cuda.device_count()
+    results = {}
+
+    def body(r):
+        d = torch.device("cuda", r % ngpu)
+        torch.cuda.set_device(d)
+        ctx = gloo_amd.Context(r, P, url, device=d.index, timeout_ms=60000)
+        for rep in range(2):
+            out = torch.from_numpy(init[r, 0].view(np.uint8).copy()).to(d)
+            inp = torch.from_numpy(ins[r, 0].view(np.uint8).copy()).to(d) if has_in else None
+            torch.cuda.synchronize(d)
+            gloo_amd.reduce_to_root(ctx, out.data_ptr(), n, dtype, root, op,
+                                    input=inp.data_ptr() if inp is not None else None, max_segment_bytes=seg)
+            results[(r, rep)] = out.cpu().numpy().view(init.dtype)
+        ctx.close()
+
+    run_threads(P, body)
+    for (r, rep), y in results.items():
+        assert same_bytes(y, want[r]), (r, rep)
+
+
+WORKER = r'''
+import os, sys, json, numpy as np
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, size, store, kind, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
+n = int(os.environ.get("GLOO_AMD_TEST_N", "300000"))
+dev = rank % torch.cuda.device_count()
+torch.cuda.set_device(dev)
+ctx = gloo_amd.Context(rank, size, store, device=dev, timeout_ms=60000)
+sets = [(torch.empty(n, device=dev), torch.empty(n, device=dev)) for _ in range(2)]
+res = []
+for it, s in enumerate([0, 0, 0, 1, 1, 0]):
+    inp, outp = sets[s]
+    inp.fill_((rank + 1) * (it + 1))
+    outp.fill_(-1)
+    torch.cuda.synchronize()
+    if kind == "bcube":
+        gloo_amd.allreduce(ctx, [outp.data_ptr()], n, "f32", "sum", inputs=[inp.data_ptr()], algorithm="bcube")
+    else:
+        gloo_amd.reduce_to_root(ctx, outp.data_ptr(), n, "f32", it % size, "sum", input=inp.data_ptr(),
+                                max_segment_bytes=256 << 10)
+    res.append(outp.cpu().numpy())
+ctx.close()
+np.save(out, np.array(res))
+'''
+
+
+@pytest.mark.parametrize("kind,P,env", [
+    ("bcube", 4, {}),                                   # 2 x 2: recursive halving shape
+    ("bcube", 6, {}),                                   # 2 x 3
+    ("bcube", 3, {"GLOO_AMD_SIGNAL": "host"}),
+    ("reduce", 4, {}),
+    ("reduce", 3, {"GLOO_AMD_COPY": "kernel"}),
+])
+def test_processes(torch, kind, P, env):
+    """Ranks as processes (device signalling unless overridden; inboxes over
+    HIP IPC), alternating buffer sets so the cached schedule is rebound and
+    re-captured; the root rotates for reduce.  Inputs (rank+1)*(it+1): exact
+    sums (it+1)*P(P+1)/2."""
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), kind,
+                                   os.path.join(d, f"o{r}.npy")], env=e) for r in range(P)]
+        assert [p.wait(timeout=300) for p in procs] == [0] * P
+        ys = [np.load(os.path.join(d, f"o{r}.npy")) for r in range(P)]
+    for it in range(ys[0].shape[0]):
+        want = (it + 1) * P * (P + 1) / 2
+        if kind == "bcube":
+            for r in range(P):
+                assert (ys[r][it] == want).all(), (r, it)
+        else:
+            assert (ys[it % P][it] == want).all(), it

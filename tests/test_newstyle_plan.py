@@ -1,0 +1,143 @@
+"""CPU: the new-style function collectives beyond the RING allreduce —
+gloo::allreduce(opts) with BCUBE (gloo/allreduce.cc:397-669) and
+gloo::reduce(opts) (gloo/reduce.cc:21-247) — restated as plans
+(gloo_amd/csrc/plan.cc) and executed by the all-rank CPU simulator.
+
+tests/golden/newstyle_golden.npz holds the reference's own outputs for these
+two functions (oracle/gen_golden.py, ranks as threads over the reference's TCP
+transport).  The closed-form grids mirror gloo/test/allreduce_test.cc:307-378
+(AllreduceNewBcube) and gloo/test/reduce_test.cc:24-89 (ReduceTest): uint64
+fixture src[j] = j*stride + id, maxSegmentSize 128, in place and not.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from plan_sim import simulate
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "newstyle_golden.npz")
+
+
+def _keys(prefix):
+    z = np.load(GOLDEN)
+    return sorted({k.rsplit("/", 1)[0] for k in z.files if k.startswith(prefix)})
+
+
+@pytest.fixture(scope="module")
+def golden_new():
+    return np.load(GOLDEN)
+
+
+def same_bytes(a, b):
+    return a.shape == b.shape and (a.view(np.uint8) == b.view(np.uint8)).all()
+
+
+@pytest.mark.parametrize("case", _keys("bcube/"))
+def test_bcube_matches_reference_golden(golden_new, case):
+    parts = case.split("/")
+    op, dtype = parts[1], parts[2]
+    nin, seg = int(parts[4][1:]), int(parts[7][1:])
+    init = golden_new[case + "/init"]
+    ins = golden_new[case + "/in"] if nin else None
+    want = golden_new[case + "/out"]
+    for seed in (0, 1, 2):
+        y = simulate("allreduce_bcube", op, dtype, init, seed=seed, ins=ins, max_seg=seg)
+        for r in range(y.shape[0]):
+            for j in range(y.shape[1]):
+                assert same_bytes(y[r, j], want), (seed, r, j)
+
+
+@pytest.mark.parametrize("case", _keys("reduce/"))
+def test_reduce_matches_reference_golden(golden_new, case):
+    """Every rank's whole output buffer (not only the root's) equals the
+    reference's: the ring part writes partial sums into every rank's output,
+    and the plan reproduces those writes too."""
+    parts = case.split("/")
+    op, dtype = parts[1], parts[2]
+    nin, root, seg = int(parts[4][1:]), int(parts[6][1:]), int(parts[7][1:])
+    init = golden_new[case + "/init"]
+    ins = golden_new[case + "/in"] if nin else None
+    want = golden_new[case + "/out"]
+    for seed in (0, 1, 2):
+        y = simulate("reduce", op, dtype, init, recv=np.array([root], np.int32), seed=seed, ins=ins,
+                     max_seg=seg)
+        assert same_bytes(y[:, 0], want), seed
+
+
+def _fixture(P, k, n):
+    """gloo/test/base_test.h:184-236 Fixture<uint64_t>::assignValues:
+    src[i][j] = j * stride + (rank * k + i), stride = P * k."""
+    stride = P * k
+    return np.array([[np.arange(n, dtype=np.uint64) * stride + (r * k + i) for i in range(k)]
+                     for r in range(P)], dtype=np.uint64)
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 6, 7, 8, 12])
+@pytest.mark.parametrize("k", [1, 2, 3])
+@pytest.mark.parametrize("n", [0, 1, 10, 100, 1000])
+@pytest.mark.parametrize("in_place", [True, False])
+def test_bcube_closed_form_grid(P, k, n, in_place):
+    """AllreduceNewBcube grid (gloo/test/allreduce_test.cc:369-378) widened to
+    P in {3, 6, 8, 12} (factorisations 3, 2*3, 2*2*2, 2*2*3)."""
+    x = _fixture(P, k, n)
+    if in_place:
+        y = simulate("allreduce_bcube", "sum", "u64", x, seed=P + n, max_seg=128)
+    else:
+        y = simulate("allreduce_bcube", "sum", "u64", np.zeros_like(x), seed=P + n, ins=x, max_seg=128)
+    stride = P * k
+    want = np.arange(n, dtype=np.uint64) * stride * stride + stride * (stride - 1) // 2
+    for r in range(P):
+        for j in range(k):
+            assert (y[r, j] == want).all(), (r, j)
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 7])
+@pytest.mark.parametrize("n", [0, 1, 10, 100, 1000, 10000])
+@pytest.mark.parametrize("in_place", [True, False])
+def test_reduce_closed_form_grid(P, n, in_place):
+    """ReduceTest grid (gloo/test/reduce_test.cc:82-89): every rank takes its
+    turn as root; the root's output is j*P*P + P*(P-1)/2."""
+    x = _fixture(P, 1, n)
+    want = np.arange(n, dtype=np.uint64) * P * P + P * (P - 1) // 2
+    for root in range(P):
+        if in_place:
+            y = simulate("reduce", "sum", "u64", x, recv=np.array([root], np.int32), seed=root, max_seg=128)
+        else:
+            y = simulate("reduce", "sum", "u64", np.zeros_like(x), recv=np.array([root], np.int32),
+                         seed=root, ins=x, max_seg=128)
+        assert (y[root, 0] == want).all(), root
+
+
+@pytest.mark.parametrize("P,n", [(2, 1000), (4, 4099), (7, 333), (8, 100003)])
+def test_reduce_repeated_runs(P, n):
+    """Three back-to-back runs with no barrier between them (the credits must
+    keep every inbox and the root's gather region safe): in place, run r
+    reduces run r-1's outputs, so three single runs chained by hand agree."""
+    rng = np.random.default_rng(P + n)
+    x = rng.integers(0, 1 << 20, size=(P, 1, n), dtype=np.uint64)
+    root = np.array([P - 1], np.int32)
+    chained = x
+    for _ in range(3):
+        chained = simulate("reduce", "sum", "u64", chained, recv=root, seed=9)
+    for seed in (0, 1):
+        got = simulate("reduce", "sum", "u64", x, recv=root, seed=seed, runs=3)
+        assert (got == chained).all(), seed
+
+
+@pytest.mark.parametrize("P,n", [(3, 1000), (6, 4099), (8, 100003)])
+def test_bcube_repeated_runs(P, n):
+    rng = np.random.default_rng(P * 3 + n)
+    x = rng.integers(0, 1 << 20, size=(P, 1, n), dtype=np.uint64)
+    chained = x
+    for _ in range(3):
+        chained = simulate("allreduce_bcube", "sum", "u64", chained, seed=4)
+    for seed in (0, 1):
+        got = simulate("allreduce_bcube", "sum", "u64", x, seed=seed, runs=3)
+        assert (got == chained).all(), seed
+
+
+def test_reduce_rejects_bad_root():
+    from plan_sim import get_plan
+    with pytest.raises(RuntimeError):
+        get_plan("reduce", 0, 4, 100, recv=np.array([4], np.int32), elem_size=8)
