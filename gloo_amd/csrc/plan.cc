@@ -817,10 +817,11 @@ Plan planAllreduceBcube(int rank, int size, uint64_t count, const NewStyleOption
     if (g.myChunkLength == 0) continue;
     // out = ((out op tmp_0) op tmp_1) ... over the peers in group order (:580-592)
     if (g.ranks.size() <= (size_t)GLOO_HIP_MAX_SRCS) {
-      p.steps.push_back(mk(GLOO_HIP_STEP_FOLD_SRC, -1, 0, 0, 0, g.myChunkOffset, 0));
+      p.steps.push_back(mk(GLOO_HIP_STEP_FOLD_SRC, -1, 0, 0, 0, g.myChunkOffset, g.myChunkLength));
       for (size_t i = 0; i < g.ranks.size(); i++)
         if (g.ranks[i] != rank)
-          p.steps.push_back(mk(GLOO_HIP_STEP_FOLD_SRC, -1, 0, GLOO_HIP_SRC_ARENA, 0, i * g.chunkLength, 0));
+          p.steps.push_back(mk(GLOO_HIP_STEP_FOLD_SRC, -1, 0, GLOO_HIP_SRC_ARENA, 0, i * g.chunkLength,
+                               g.myChunkLength));
       p.steps.push_back(mk(GLOO_HIP_STEP_FOLD, -1, 0, 0, g.myChunkOffset, 0, g.myChunkLength));
     } else {
       for (size_t i = 0; i < g.ranks.size(); i++)

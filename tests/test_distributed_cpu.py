@@ -27,16 +27,33 @@ from plan_sim import KIND, SRC_ARENA, DST_ARENA, FOLD_REVERSE, get_plan
 rank, size, port, case, outdir = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
 plan_algo = sys.argv[6] if len(sys.argv) > 6 else None
 dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=size)
-g = np.load(os.path.join(os.environ["GLOO_AMD_ROOT"], "tests", "golden", "sched_golden.npz"))
 algo, op, dtype = case.split("/")[:3]
-x = g[case + "/in"]
-recv = g[case + "/recv"] if algo == "reduce_scatter" else None
+newstyle = algo in ("bcube", "reduce")
+g = np.load(os.path.join(os.environ["GLOO_AMD_ROOT"], "tests", "golden",
+                         "newstyle_golden.npz" if newstyle else "sched_golden.npz"))
+ins = None
+if newstyle:
+    parts = case.split("/")
+    x = g[case + "/init"]
+    ins = g[case + "/in"][rank] if case + "/in" in g.files else None
+    if algo == "reduce":
+        recv = np.array([int(parts[6][1:])], np.int32)
+        seg = int(parts[7][1:])
+    else:
+        recv, seg = None, int(parts[7][1:])
+else:
+    x = g[case + "/in"]
+    recv = g[case + "/recv"] if algo == "reduce_scatter" else None
+    seg = 0
 if algo == "reduce_scatter":
     x = x[:, None, :]
 P, k, n = x.shape
-steps, arena_n = get_plan(plan_algo or algo, rank, P, n, k, recv)
+plan_name = plan_algo or {"bcube": "allreduce_bcube"}.get(algo, algo)
+steps, arena_n = get_plan(plan_name, rank, P, n, k, recv, nin=0 if ins is None else ins.shape[0],
+                          elem_size=x.dtype.itemsize, max_seg=seg)
 fold = []
 user = [x[rank, j].copy() for j in range(k)]
+FROM_INPUTS = 4
 arena = np.zeros(max(1, arena_n), dtype=x.dtype)
 regions = {(s.peer, s.slot): (s.dst_off, s.length) for s in steps if s.kind == KIND["DECL_RECV"]}
 as_t = lambda a: torch.from_numpy(a.view(np.uint8).copy())
@@ -44,7 +61,7 @@ pending = []
 for s in steps:
     K = s.kind
     if K == KIND["SEND"]:
-        src = arena if s.flags & SRC_ARENA else user[0]
+        src = ins[0] if s.flags & FROM_INPUTS else arena if s.flags & SRC_ARENA else user[0]
         payload = src[s.src_off:s.src_off + s.length]
         pending.append(dist.isend(torch.tensor([s.length], dtype=torch.int64), s.peer, tag=10 * s.slot))
         pending.append(dist.isend(as_t(payload), s.peer, tag=10 * s.slot + 1))
@@ -61,18 +78,25 @@ for s in steps:
     elif K == KIND["WAIT_NOTIFY"]:
         dist.recv(torch.zeros(1), s.peer, tag=10 * s.slot + 5)
     elif K == KIND["REDUCE"]:
-        d = user[0][s.dst_off:s.dst_off + s.length]
+        d = (ins[0] if s.flags & FROM_INPUTS else user[0])[s.dst_off:s.dst_off + s.length]
         user[0][s.dst_off:s.dst_off + s.length] = oracle.reduce3(op, dtype, d, arena[s.src_off:s.src_off + s.length])
     elif K == KIND["COPY"]:
         src = arena if s.flags & SRC_ARENA else user[0]
         dst = arena if s.flags & DST_ARENA else user[0]
         dst[s.dst_off:s.dst_off + s.length] = src[s.src_off:s.src_off + s.length].copy()
     elif K == KIND["LOCAL_REDUCE"]:
-        for j in range(1, k):
-            user[0][:s.length] = oracle.reduce3(op, dtype, user[0][:s.length], user[j][:s.length])
+        lo, hi = s.dst_off, s.dst_off + s.length
+        if s.flags & FROM_INPUTS:
+            acc = ins[0][lo:hi].copy()
+            for j in range(1, ins.shape[0]):
+                acc = oracle.reduce3(op, dtype, acc, ins[j][lo:hi])
+            user[0][lo:hi] = acc
+        else:
+            for j in range(1, k):
+                user[0][lo:hi] = oracle.reduce3(op, dtype, user[0][lo:hi], user[j][lo:hi])
     elif K == KIND["LOCAL_BCAST"]:
         for j in range(1, k):
-            user[j][:s.length] = user[0][:s.length]
+            user[j][s.dst_off:s.dst_off + s.length] = user[0][s.dst_off:s.dst_off + s.length]
     elif K == KIND["FOLD_SRC"]:
         fold.append((arena if s.flags & SRC_ARENA else user[0])[s.src_off:s.src_off + s.length].copy())
     elif K == KIND["FOLD"]:
@@ -103,12 +127,17 @@ CASES = [("ring_chunked/sum/f32/P2/k1/n1000", None), ("halving_doubling/sum/f32/
          ("ring/sum/f32/P3/k1/n1000", None),
          # the reference ring's bytes from the mesh plan (two all-to-all hops)
          ("ring_chunked/sum/f32/P3/k2/n1000", "ring_chunked_mesh"),
-         ("ring_chunked/max/f32/P5/k1/n999", "ring_chunked_mesh")]
+         ("ring_chunked/max/f32/P5/k1/n999", "ring_chunked_mesh"),
+         # new-style gloo::allreduce BCUBE and gloo::reduce (tests/golden/newstyle_golden.npz)
+         ("bcube/sum/f32/P2/i0/o1/n1000/s0", None), ("bcube/sum/f32/P6/i3/o2/n999/s0", None),
+         ("reduce/sum/f32/P3/i0/n1000/r2/s128", None), ("reduce/sum/f32/P5/i1/n4099/r2/s0", None)]
 
 
 @pytest.mark.parametrize("case,plan_algo", CASES)
 def test_plans_over_gloo_processes(golden_sched, case, plan_algo):
     algo = case.split("/")[0]
+    if algo in ("bcube", "reduce"):
+        golden_sched = np.load(os.path.join(ROOT, "tests", "golden", "newstyle_golden.npz"))
     P = int(case.split("/")[3][1:])
     with tempfile.TemporaryDirectory() as d:
         w = os.path.join(d, "w.py")
@@ -125,9 +154,9 @@ def test_plans_over_gloo_processes(golden_sched, case, plan_algo):
         recv = golden_sched[case + "/recv"]
         got = np.concatenate([outs[r][0, :recv[r]] for r in range(P)])
         assert (got.view(np.uint8) == want.view(np.uint8)).all()
-    elif algo == "ring":
+    elif algo in ("ring", "reduce"):  # rank-specific outputs
         for r in range(P):
-            assert (outs[r][0].view(np.uint8) == want[r].view(np.uint8)).all()
+            assert (outs[r][0].view(np.uint8) == want[r].view(np.uint8)).all(), r
     else:
         for r in range(P):
             for j in range(outs[r].shape[0]):
