@@ -222,7 +222,7 @@ def copy_ceiling(torch, dev, nbytes=1 << 30, iters=10):
     return round(2.0 * nbytes / t / 1e9, 1)
 
 
-def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
+def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     """BASELINE config 3 (+ a config-4 sweep) at N > 1 ranks, one per GPU.
 
     Config 3: AllreduceRingChunked fp32 sum, 256 MiB per rank.  Chunks move
@@ -236,7 +236,9 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
     Config 4: halving-doubling, 1 KiB .. 1 GiB per rank (x4 steps) for the
     derived mesh plan and the reference's exchange route, 4 sizes for the
     other variants.  Config 5: reduce-scatter of fp16 / bf16 buckets, all
-    four ops."""
+    four ops.  New style: BCUBE allreduce and gloo::reduce, four sizes.
+    `partial` collects each finished subsection, so a watchdog firing late
+    still reports everything measured before it."""
     import tempfile
     obj = [tempfile.mkdtemp(prefix="gloo_amd_bench_")] if rank == 0 else [None]
     dist.broadcast_object_list(obj, src=0)
@@ -314,12 +316,18 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
 
     # default: the mesh plan (batched sends = one multi-destination copy kernel)
     ring = ring_once("auto")
+    ngpu = torch.cuda.device_count()
+    partial["config"] = "allreduce_ring_chunked fp32 sum, %d ranks, %d MiB/rank" % (world, args.allreduce_mib)
+    partial["data_path"] = "xGMI peer copies" if ngpu >= world else f"{world} ranks on {ngpu} GPU(s)"
+    partial.update(ring)
     if "error" in ring:
-        return ring
-    variants = {"mesh_memcpy_forked": ring_once("memcpy"),
-                "ring_memcpy": ring_once("memcpy", mesh="0"),
-                "ring_kernel": ring_once("kernel", mesh="0"),
-                "mesh_host_workspace": ring_once("auto", "host")}
+        return dict(partial)
+    variants = {}
+    partial["variants"] = variants
+    variants["mesh_memcpy_forked"] = ring_once("memcpy")
+    variants["ring_memcpy"] = ring_once("memcpy", mesh="0")
+    variants["ring_kernel"] = ring_once("kernel", mesh="0")
+    variants["mesh_host_workspace"] = ring_once("auto", "host")
 
     short_sizes = (1 << 10, 64 << 10, 1 << 20, 64 << 20)
     full_sizes = tuple(1 << lg for lg in range(10, 31, 2))  # config 4: 1 KiB .. 1 GiB per rank
@@ -373,8 +381,10 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
                    "reference_route": {"GLOO_AMD_MESH": "0"},
                    "reference_route_kernel_copy": {"GLOO_AMD_MESH": "0", "GLOO_AMD_COPY": "kernel"},
                    "reference_route_eager": {"GLOO_AMD_MESH": "0", "GLOO_AMD_GRAPH": "0"}}
-    hd_summary = {k: hd_sweep(k, v, full_sizes if k in ("mesh", "reference_route") else short_sizes)
-                  for k, v in hd_variants.items()}
+    hd_summary = {}
+    partial["halving_doubling"] = hd_summary
+    for k, v in hd_variants.items():
+        hd_summary[k] = hd_sweep(k, v, full_sizes if k in ("mesh", "reference_route") else short_sizes)
 
     # Config 5: reduce-scatter (HD), fp16 / bf16 buckets, every op, 16 Mi
     # elements per rank, recvElems = an even split.
@@ -413,18 +423,53 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args):
 
     rs_summary = [rs_once(dt, op, {}) for dt in ("f16", "bf16") for op in ("sum", "product", "min", "max")]
     rs_summary += [rs_once(dt, "sum", {"GLOO_AMD_MESH": "0"}) for dt in ("f16", "bf16")]
+    partial["reduce_scatter"] = rs_summary
+
+    # New-style function API: gloo::allreduce BCUBE and
+    # gloo::reduce to rank 0, fp32 sum, separate input and output.
+    def newstyle(kind, nbytes):
+        def body():
+            m = max(1, nbytes // 4)
+            inp = torch.ones(m, device=dev)
+            outp = torch.zeros(m, device=dev)
+            torch.cuda.synchronize(dev)
+            c = hip.Context(rank, world, "file:%s/ns_%s_%d" % (obj[0], kind, nbytes), device=dev.index,
+                            timeout_ms=60000)
+
+            def call():
+                if kind == "bcube":
+                    hip.allreduce(c, [outp.data_ptr()], m, "f32", "sum", inputs=[inp.data_ptr()], algorithm="bcube")
+                else:
+                    hip.reduce_to_root(c, outp.data_ptr(), m, "f32", 0, "sum", input=inp.data_ptr())
+            call()
+            call()
+            ts = []
+            for _ in range(10):
+                dist.barrier()
+                t0 = time.perf_counter()
+                call()
+                ts.append(time.perf_counter() - t0)
+            ok = bool((outp[:: max(1, m // 1024)] == world).all()) if (kind == "bcube" or rank == 0) else True
+            c.close()
+            return {"us": [round(t * 1e6, 1) for t in ts], "ok": ok}
+        try:
+            res = body()
+        except Exception as e:  # noqa: BLE001
+            res = {"error": repr(e)}
+        g = gather(res)
+        if any("error" in x for x in g):
+            return {"bytes": nbytes, "error": next(x["error"] for x in g if "error" in x)}
+        per = sorted(max(x["us"][k] for x in g) for k in range(10))
+        return {"bytes": nbytes, "us_p50": per[5], "us_max": per[-1], "verified": all(x["ok"] for x in g)}
+
+    ns_sizes = (64 << 10, 1 << 20, 16 << 20, 256 << 20)
+    partial["new_style"] = {"bcube_allreduce": [newstyle("bcube", b) for b in ns_sizes]}
+    partial["new_style"]["reduce_to_root0"] = [newstyle("reduce", b) for b in ns_sizes]
     dist.barrier()
     if rank == 0:
         import shutil
         shutil.rmtree(obj[0], ignore_errors=True)
-    ngpu = torch.cuda.device_count()
-    out = {"config": "allreduce_ring_chunked fp32 sum, %d ranks, %d MiB/rank" % (world, args.allreduce_mib),
-           "data_path": "xGMI peer copies" if ngpu >= world else f"{world} ranks on {ngpu} GPU(s)"}
-    out.update(ring)
-    out["variants"] = variants
-    out["halving_doubling"] = hd_summary
-    out["reduce_scatter"] = rs_summary
-    return out
+    return dict(partial)
 
 
 def arm_watchdog(seconds, on_fire):
@@ -551,14 +596,16 @@ def main():
         # A failure in the collective must never cost the headline line: every
         # rank arms a watchdog; if it fires, rank 0 prints the headline with
         # the section marked as timed out, and the process exits.
+        partial = {}
+
         def fire():
             if rank == 0:
-                out["xgmi_allreduce"] = {"error": "watchdog: section exceeded 240 s"}
+                out["xgmi_allreduce"] = dict(partial, error="watchdog: section exceeded 300 s")
                 print(json.dumps(out), flush=True)
             os._exit(0)
 
-        wd = arm_watchdog(240, fire)
-        xr = xgmi_allreduce(torch, dist, hip, rank, world, dev, args)
+        wd = arm_watchdog(300, fire)
+        xr = xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial)
         wd.cancel()
         if rank == 0:
             out["xgmi_allreduce"] = xr

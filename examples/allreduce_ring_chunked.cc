@@ -2,7 +2,9 @@
 // (gloo/examples/example_allreduce.cc, gloo/benchmark/cuda_main.cc:173-214)
 // on the MI355X-native surface: N ranks as threads, one GPU each (wrapping
 // around the visible GPUs), fp32 sum over device buffers, checked against the
-// closed form of gloo/test/base_test.h:184-236.
+// closed form of gloo/test/base_test.h:184-236.  After the ring-chunked
+// allreduce the same check runs for halving-doubling (the reference's
+// constructor signature) and the new-style BCUBE allreduce and reduce.
 //
 // With "host" as the third argument the inboxes live in pinned host memory
 // (HipHostWorkspace, the reference's CudaHostWorkspace placement).
@@ -37,11 +39,21 @@ int main(int argc, char** argv) {
       (void)hipSetDevice(dev);
       auto ctx = std::make_shared<gloo_amd::Context>(r, P);
       ctx->connect(store, dev);
-      std::vector<float> host(count);
-      for (int j = 0; j < count; j++) host[j] = float(j % 1000) * P + r;
+      std::vector<float> init(count), host(count);
+      for (int j = 0; j < count; j++) init[j] = float(j % 1000) * P + r;
       float* d = nullptr;
+      float* o = nullptr;
       (void)hipMalloc(&d, count * sizeof(float));
-      (void)hipMemcpy(d, host.data(), count * sizeof(float), hipMemcpyHostToDevice);
+      (void)hipMalloc(&o, count * sizeof(float));
+      auto load = [&] { (void)hipMemcpy(d, init.data(), count * sizeof(float), hipMemcpyHostToDevice); };
+      auto verify = [&](const float* p) {
+        (void)hipMemcpy(host.data(), p, count * sizeof(float), hipMemcpyDeviceToHost);
+        for (int j = 0; j < count; j++) {
+          const float want = float(j % 1000) * P * P + P * (P - 1) / 2.0f;
+          if (host[j] != want) bad[r]++;
+        }
+      };
+      load();
       if (hostWs) {
         gloo_amd::HipAllreduceRingChunked<float, gloo_amd::HipHostWorkspace<float>> algo(ctx, {d}, count);
         algo.run();
@@ -49,18 +61,43 @@ int main(int argc, char** argv) {
         gloo_amd::HipAllreduceRingChunked<float> algo(ctx, {d}, count);
         algo.run();
       }
-      (void)hipMemcpy(host.data(), d, count * sizeof(float), hipMemcpyDeviceToHost);
-      for (int j = 0; j < count; j++) {
-        const float want = float(j % 1000) * P * P + P * (P - 1) / 2.0f;
-        if (host[j] != want) bad[r]++;
+      verify(d);
+      // the reference's HD signature (streams, pipelineBroadcastAndReduce)
+      load();
+      {
+        gloo_amd::HipAllreduceHalvingDoubling<float> hd(ctx, {d}, count, {}, true);
+        hd.run();
       }
+      verify(d);
+      // new-style gloo::allreduce(opts) with BCUBE, separate input and output
+      load();
+      {
+        gloo_amd::AllreduceOptions opts(ctx);
+        opts.setInput(d, count);
+        opts.setOutput(o, count);
+        opts.setAlgorithm(gloo_amd::AllreduceOptions::Algorithm::BCUBE);
+        opts.setReduceFunction(gloo_amd::SUM);
+        gloo_amd::allreduce(opts);
+      }
+      verify(o);
+      // new-style gloo::reduce(opts) to rank P-1
+      {
+        gloo_amd::ReduceOptions opts(ctx);
+        opts.setInput(d, count);
+        opts.setOutput(o, count);
+        opts.setRoot(P - 1);
+        opts.setReduceFunction(gloo_amd::SUM);
+        gloo_amd::reduce(opts);
+      }
+      if (r == P - 1) verify(o);
+      (void)hipFree(o);
       (void)hipFree(d);
     });
   }
   for (auto& t : ts) t.join();
   int total = 0;
   for (int r = 0; r < P; r++) total += bad[r];
-  std::printf("allreduce_ring_chunked: %d ranks x %d floats (%s workspace): %s\n", P, count,
+  std::printf("ring_chunked, halving_doubling, bcube, reduce: %d ranks x %d floats (%s workspace): %s\n", P, count,
               hostWs ? "host" : "device", total ? "MISMATCH" : "ok");
   return total ? 1 : 0;
 }

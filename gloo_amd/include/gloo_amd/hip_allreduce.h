@@ -11,7 +11,9 @@
 //   gloo::ReduceScatterHalvingDoubling  -> gloo_amd::HipReduceScatterHalvingDoubling<T>
 //                                          (gloo/reduce_scatter.h:112-117)
 //   gloo::allreduce(AllreduceOptions)   -> gloo_amd::allreduce(AllreduceOptions)
-//                                          (gloo/allreduce.h:89-193), RING
+//                                          (gloo/allreduce.h:89-193), RING / BCUBE
+//   gloo::reduce(ReduceOptions)         -> gloo_amd::reduce(ReduceOptions)
+//                                          (gloo/reduce.h:19-112)
 // Same constructor shapes (context, ptrs, count[, recvElems][, streams][, fn])
 // and run().  Differences, by design: one rank drives one GPU (all `ptrs` of
 // a rank live on that rank's device — ranks are processes or threads), the
@@ -145,6 +147,16 @@ class HipAllreduceHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_HAL
                               const std::vector<hipStream_t>& streams = {},
                               const HipReductionFunction<T>* fn = HipReductionFunction<T>::sum)
       : HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING, W>(context, ptrs, count, {}, streams, fn) {}
+  // The reference's exact signature (gloo/cuda_allreduce_halving_doubling.h:25-30).
+  // pipelineBroadcastAndReduce overlaps the reference's per-chunk local
+  // reduce / broadcast LocalOps with the exchange; here the local fold of a
+  // rank's pointers is one fused pass before the exchange and the broadcast
+  // one copy after it, so the flag changes no byte and no step and is accepted
+  // for source compatibility.
+  HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
+                              const std::vector<hipStream_t>& streams, bool /*pipelineBroadcastAndReduce*/)
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING, W>(context, ptrs, count, {}, streams,
+                                                               HipReductionFunction<T>::sum) {}
 };
 
 template <typename T, typename W = HipDeviceWorkspace<T>>
