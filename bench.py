@@ -425,20 +425,21 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     rs_summary += [rs_once(dt, "sum", {"GLOO_AMD_MESH": "0"}) for dt in ("f16", "bf16")]
     partial["reduce_scatter"] = rs_summary
 
-    # New-style function API: gloo::allreduce BCUBE and
-    # gloo::reduce to rank 0, fp32 sum, separate input and output.
-    def newstyle(kind, nbytes):
+    # New-style function API: gloo::allreduce RING / BCUBE
+    # and gloo::reduce to rank 0, fp32 sum, separate input and output; the
+    # derived mesh route (default) and the reference's exchange route.
+    def newstyle(kind, nbytes, env=None):
         def body():
             m = max(1, nbytes // 4)
             inp = torch.ones(m, device=dev)
             outp = torch.zeros(m, device=dev)
             torch.cuda.synchronize(dev)
-            c = hip.Context(rank, world, "file:%s/ns_%s_%d" % (obj[0], kind, nbytes), device=dev.index,
-                            timeout_ms=60000)
+            c = hip.Context(rank, world, "file:%s/ns_%s_%d_%s" % (obj[0], kind, nbytes, bool(env)),
+                            device=dev.index, timeout_ms=60000)
 
             def call():
-                if kind == "bcube":
-                    hip.allreduce(c, [outp.data_ptr()], m, "f32", "sum", inputs=[inp.data_ptr()], algorithm="bcube")
+                if kind in ("ring", "bcube"):
+                    hip.allreduce(c, [outp.data_ptr()], m, "f32", "sum", inputs=[inp.data_ptr()], algorithm=kind)
                 else:
                     hip.reduce_to_root(c, outp.data_ptr(), m, "f32", 0, "sum", input=inp.data_ptr())
             call()
@@ -449,11 +450,11 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                 t0 = time.perf_counter()
                 call()
                 ts.append(time.perf_counter() - t0)
-            ok = bool((outp[:: max(1, m // 1024)] == world).all()) if (kind == "bcube" or rank == 0) else True
+            ok = bool((outp[:: max(1, m // 1024)] == world).all()) if (kind != "reduce" or rank == 0) else True
             c.close()
             return {"us": [round(t * 1e6, 1) for t in ts], "ok": ok}
         try:
-            res = body()
+            res = with_env(env or {}, body)
         except Exception as e:  # noqa: BLE001
             res = {"error": repr(e)}
         g = gather(res)
@@ -463,8 +464,12 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         return {"bytes": nbytes, "us_p50": per[5], "us_max": per[-1], "verified": all(x["ok"] for x in g)}
 
     ns_sizes = (64 << 10, 1 << 20, 16 << 20, 256 << 20)
-    partial["new_style"] = {"bcube_allreduce": [newstyle("bcube", b) for b in ns_sizes]}
-    partial["new_style"]["reduce_to_root0"] = [newstyle("reduce", b) for b in ns_sizes]
+    ns = {}
+    partial["new_style"] = ns
+    ref_route = {"GLOO_AMD_MESH": "0"}
+    for kind, label in (("ring", "ring_allreduce"), ("bcube", "bcube_allreduce"), ("reduce", "reduce_to_root0")):
+        ns[label] = [newstyle(kind, b) for b in ns_sizes]
+        ns[label + "_reference_route"] = [newstyle(kind, b, ref_route) for b in ns_sizes[2:]]
     dist.barrier()
     if rank == 0:
         import shutil

@@ -154,7 +154,7 @@ Plan planFor(int algo, int rank, int size, size_t count, int nin, int nout, size
     o.noutputs = nout;
     o.elemSize = es;
     o.maxSegmentBytes = maxSeg;
-    if (algo == GLOO_HIP_ALGO_REDUCE) o.root = recvElems.empty() ? 0 : recvElems[0];  // gloo::reduce: {root}
+    if ((algo & ~GLOO_HIP_ALGO_MESH) == GLOO_HIP_ALGO_REDUCE) o.root = recvElems.empty() ? 0 : recvElems[0];  // {root}
     return makeNewStylePlan(algo, rank, size, count, o);
   }
   return makePlan(algo, rank, size, count, nout, recvElems);
@@ -237,7 +237,8 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     const char* rm = std::getenv("GLOO_AMD_RING_MESH");
     if (!(rm && rm[0] == '0')) planAlgo_ = GLOO_HIP_ALGO_RING_CHUNKED_MESH;
   }
-  if (mesh && (algo_ == GLOO_HIP_ALGO_HALVING_DOUBLING || algo_ == GLOO_HIP_ALGO_REDUCE_SCATTER))
+  if (mesh && (algo_ == GLOO_HIP_ALGO_HALVING_DOUBLING || algo_ == GLOO_HIP_ALGO_REDUCE_SCATTER ||
+               isNewStyle(algo_)))
     planAlgo_ = algo_ | GLOO_HIP_ALGO_MESH;
   plan_ = planFor(planAlgo_, me, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_, maxSegmentBytes_,
                   recvElems_);
@@ -864,8 +865,8 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         }
         break;
       }
-      case GLOO_HIP_STEP_FOLD_SRC:
-        foldSrcs.push_back(userOrArena(s.flags & GLOO_HIP_SRC_ARENA) + s.src_off * es_);
+      case GLOO_HIP_STEP_FOLD_SRC:  // the arena, input 0 (gloo::reduce's contribution) or output 0
+        foldSrcs.push_back(sendSrc(s));
         break;
       case GLOO_HIP_STEP_FOLD: {
         // one pass over every source, in the plan's order (plan.cc FOLD)

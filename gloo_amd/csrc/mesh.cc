@@ -131,13 +131,43 @@ struct Job {
 };
 
 bool isAllreduce(int algo) {
-  return algo == GLOO_HIP_ALGO_RING_CHUNKED || algo == GLOO_HIP_ALGO_HALVING_DOUBLING || algo == GLOO_HIP_ALGO_RING;
+  return algo == GLOO_HIP_ALGO_RING_CHUNKED || algo == GLOO_HIP_ALGO_HALVING_DOUBLING || algo == GLOO_HIP_ALGO_RING ||
+         algo == GLOO_HIP_ALGO_ALLREDUCE_RING || algo == GLOO_HIP_ALGO_ALLREDUCE_BCUBE;
+}
+
+// Combine aligned piece lists of several operands position by position.
+template <typename F>
+void zipPieces(const std::vector<std::vector<Piece>>& ops, const std::vector<uint64_t>& offs, uint64_t len, F&& emit) {
+  std::vector<size_t> idx(ops.size(), 0);
+  for (uint64_t t = 0; t < len;) {
+    uint64_t e = len;
+    std::vector<const Value*> vs;
+    for (size_t k = 0; k < ops.size(); k++) {
+      while (ops[k][idx[k]].hi <= offs[k] + t) idx[k]++;
+      e = std::min(e, ops[k][idx[k]].hi - offs[k]);
+      vs.push_back(&ops[k][idx[k]].v);
+    }
+    emit(t, e, vs);
+    t = e;
+  }
 }
 
 // Run every rank's plan symbolically; returns the final user buffers.
-std::vector<Buffer> dataflow(int algo, int size, uint64_t count, const std::vector<int>& recvElems, Forest& F) {
+// New-style algorithms are modelled with one output and no separate input:
+// a rank's leaf is its contribution (the local reduction of its inputs,
+// which the reference computes range by range before using it).
+std::vector<Buffer> dataflow(int algo, int size, uint64_t count, const std::vector<int>& recvElems, Forest& F,
+                             const NewStyleOptions* ns) {
   std::vector<Plan> plans;
-  for (int r = 0; r < size; r++) plans.push_back(makePlan(algo, r, size, count, 1, recvElems));
+  NewStyleOptions model;
+  if (ns) {
+    model = *ns;
+    model.ninputs = 0;
+    model.noutputs = 1;
+  }
+  for (int r = 0; r < size; r++)
+    plans.push_back(ns ? makeNewStylePlan(algo, r, size, count, model) : makePlan(algo, r, size, count, 1, recvElems));
+  std::vector<std::pair<bool, uint64_t>> foldSrcs;  // pending FOLD sources: (arena?, offset)
   std::vector<Buffer> user(size), arena(size);
   for (int r = 0; r < size; r++) {
     std::vector<Piece> init{{0, count, Value{F.leaf(r), 0, r}}};
@@ -189,6 +219,48 @@ std::vector<Buffer> dataflow(int algo, int size, uint64_t count, const std::vect
             t = e;
           }
           user[r].write(out, s.dst_off, s.dst_off);
+        } else if (s.kind == GLOO_HIP_STEP_FOLD_SRC) {
+          foldSrcs.push_back({(s.flags & GLOO_HIP_SRC_ARENA) != 0, s.src_off});
+        } else if (s.kind == GLOO_HIP_STEP_FOLD) {
+          // acc = s0; acc = acc op s_k (REVERSE: s_k op acc; TREE: pairwise)
+          std::vector<std::vector<Piece>> ops;
+          std::vector<uint64_t> offs;
+          for (const auto& fs : foldSrcs) {
+            ops.push_back(space(r, fs.first).read(fs.second, fs.second + s.length));
+            offs.push_back(fs.second);
+          }
+          foldSrcs.clear();
+          std::vector<Piece> out;
+          zipPieces(ops, offs, s.length, [&](uint64_t t, uint64_t e, const std::vector<const Value*>& vs) {
+            bool known = true;
+            for (size_t k = 0; k < vs.size(); k++) {
+              if (vs[k]->tree < 0) known = false;
+              else if ((int64_t)(offs[k] + t) + vs[k]->delta != (int64_t)(offs[0] + t) + vs[0]->delta)
+                throw std::runtime_error("fold of different elements");
+            }
+            Value v;
+            if (known) {
+              std::vector<int> level;
+              for (const Value* x : vs) level.push_back(x->tree);
+              int acc;
+              if (s.flags & GLOO_HIP_FOLD_TREE) {
+                while (level.size() > 1) {
+                  std::vector<int> next;
+                  for (size_t k = 0; k + 1 < level.size(); k += 2) next.push_back(F.node(level[k], level[k + 1]));
+                  level = next;
+                }
+                acc = level[0];
+              } else {
+                acc = level[0];
+                for (size_t k = 1; k < level.size(); k++)
+                  acc = s.flags & GLOO_HIP_FOLD_REVERSE ? F.node(level[k], acc) : F.node(acc, level[k]);
+              }
+              // element index as seen from the destination position
+              v = Value{acc, (int64_t)(offs[0] + t) + vs[0]->delta - (int64_t)(s.dst_off + t), r};
+            }
+            out.push_back({s.dst_off + t, s.dst_off + e, v});
+          });
+          space(r, s.flags & GLOO_HIP_DST_ARENA).write(out, s.dst_off, s.dst_off);
         } else if (s.kind == GLOO_HIP_STEP_COPY) {
           const auto pieces = space(r, s.flags & GLOO_HIP_SRC_ARENA).read(s.src_off, s.src_off + s.length);
           space(r, s.flags & GLOO_HIP_DST_ARENA).write(pieces, s.src_off, s.dst_off);
@@ -212,8 +284,9 @@ int countLeaves(const Forest& F, int t) {
   return n.leaf >= 0 ? 1 : countLeaves(F, n.lhs) + countLeaves(F, n.rhs);
 }
 
-std::vector<Job> findJobs(int algo, int size, uint64_t count, const std::vector<int>& recvElems, Forest& F) {
-  const auto user = dataflow(algo, size, count, recvElems, F);
+std::vector<Job> findJobs(int algo, int size, uint64_t count, const std::vector<int>& recvElems, Forest& F,
+                          const NewStyleOptions* ns) {
+  const auto user = dataflow(algo, size, count, recvElems, F, ns);
   std::vector<Job> jobs;
   auto add = [&](int owner, const Piece& p) {
     if (p.v.tree < 0) throw std::runtime_error("output element with unknown contents");
@@ -248,6 +321,13 @@ std::vector<Job> findJobs(int algo, int size, uint64_t count, const std::vector<
   } else if (algo == GLOO_HIP_ALGO_REDUCE_SCATTER) {
     for (int r = 0; r < size; r++)
       for (const Piece& p : user[r].read(0, (uint64_t)recvElems[r])) add(r, p);
+  } else if (algo == GLOO_HIP_ALGO_REDUCE && ns) {
+    // gloo::reduce: the root's output; each range is owned by the rank that
+    // finished its tree (the reference then gathers it at the root)
+    for (const Piece& p : user[ns->root].read(0, count)) {
+      if (p.v.delta != 0) throw std::runtime_error("reduce output misplaced");
+      add(p.v.producer, p);
+    }
   } else {
     throw std::runtime_error("no mesh form for this algorithm");
   }
@@ -303,15 +383,25 @@ Step mkStep(int kind, int peer = -1, int slot = 0, int flags = 0, uint64_t dst =
 
 }  // namespace
 
-Plan makeMeshPlan(int algo, int rank, int size, uint64_t count, int nptrs, const std::vector<int>& recvElems) {
+Plan makeMeshPlan(int algo, int rank, int size, uint64_t count, int nptrs, const std::vector<int>& recvElems,
+                  const NewStyleOptions* ns) {
   if (size < 2 || size > GLOO_HIP_MAX_SRCS) throw std::invalid_argument("mesh plans need 2 <= size <= 8");
   if (rank < 0 || rank >= size) throw std::invalid_argument("bad rank");
   Plan p;
   const bool allreduce = isAllreduce(algo);
+  const bool toRoot = algo == GLOO_HIP_ALGO_REDUCE;  // gloo::reduce: results go to the root only
+  if (toRoot && !ns) throw std::invalid_argument("gloo::reduce needs its options");
   if (count == 0) return p;
-  if (nptrs > 1) p.steps.push_back(mkStep(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, 0, 0, 0, count));
+  // A rank's contribution: the local reduction of its inputs (new-style,
+  // the reference's reduceInputs over the whole range), or of its pointers.
+  // gloo::reduce reads its single input in place (leafFlags).
+  const int leafFlags = toRoot && ns->ninputs > 0 ? GLOO_HIP_FROM_INPUTS : 0;
+  if (ns && !toRoot && ns->ninputs > 0)
+    p.steps.push_back(mkStep(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, GLOO_HIP_FROM_INPUTS, 0, 0, count));
+  else if (nptrs > 1)
+    p.steps.push_back(mkStep(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, 0, 0, 0, count));
   Forest F;
-  const std::vector<Job> jobs = findJobs(algo, size, count, recvElems, F);
+  const std::vector<Job> jobs = findJobs(algo, size, count, recvElems, F, ns);
   // per owner: its jobs (<= 2: two data slots per direction)
   std::vector<std::vector<int>> byOwner(size);
   for (int j = 0; j < (int)jobs.size(); j++) byOwner[jobs[j].owner].push_back(j);
@@ -347,6 +437,14 @@ Plan makeMeshPlan(int algo, int rank, int size, uint64_t count, int nptrs, const
         p.steps.push_back(mkStep(GLOO_HIP_STEP_DECL_RECV, o, slotOf(j, GLOO_HIP_SLOT_AUX0), 0, agRegion[j], 0,
                                  jobs[j].hi - jobs[j].lo));
       }
+  std::map<int, uint64_t> rootRegion;  // job -> root's arena offset (gloo::reduce)
+  if (toRoot && rank == ns->root)
+    for (int o : peersFrom(rank))
+      for (int j : byOwner[o]) {
+        rootRegion[j] = alloc(jobs[j].hi - jobs[j].lo);
+        p.steps.push_back(mkStep(GLOO_HIP_STEP_DECL_RECV, o, slotOf(j, GLOO_HIP_SLOT_AUX0), 0, rootRegion[j], 0,
+                                 jobs[j].hi - jobs[j].lo));
+      }
   // Reduce-scatter has no return hop, so an owner hands back a credit once
   // its folds have read the inboxes; a sender's next-run send waits for it.
   if (!allreduce)
@@ -356,7 +454,7 @@ Plan makeMeshPlan(int algo, int rank, int size, uint64_t count, int nptrs, const
   // my raw piece of every other owner's jobs, all at once
   for (int o : peersFrom(rank))
     for (int j : byOwner[o])
-      p.steps.push_back(mkStep(GLOO_HIP_STEP_SEND, o, slotOf(j, GLOO_HIP_SLOT_DATA0), 0, 0, jobs[j].elem,
+      p.steps.push_back(mkStep(GLOO_HIP_STEP_SEND, o, slotOf(j, GLOO_HIP_SLOT_DATA0), leafFlags, 0, jobs[j].elem,
                                jobs[j].hi - jobs[j].lo));
   if (!byOwner[rank].empty()) {
     for (int j : byOwner[rank])
@@ -366,19 +464,19 @@ Plan makeMeshPlan(int algo, int rank, int size, uint64_t count, int nptrs, const
       const uint64_t len = J.hi - J.lo;
       // where each leaf lives: peers' inboxes, or my own input in place —
       // staged to the arena if it overlaps the output at another offset
-      std::map<int, std::pair<bool, uint64_t>> leafAt;  // rank -> (arena?, offset)
-      for (int s : peersFrom(rank)) leafAt[s] = {true, rsRegion[{j, s}]};
+      std::map<int, std::pair<int, uint64_t>> leafAt;  // rank -> (FOLD_SRC flags, offset)
+      for (int s : peersFrom(rank)) leafAt[s] = {GLOO_HIP_SRC_ARENA, rsRegion[{j, s}]};
       const bool overlap = J.elem != J.lo && J.elem < J.hi && J.lo < J.elem + len;
       if (overlap) {
         const uint64_t t = alloc(len);
         p.steps.push_back(mkStep(GLOO_HIP_STEP_COPY, -1, 0, GLOO_HIP_DST_ARENA, t, J.elem, len));
-        leafAt[rank] = {true, t};
+        leafAt[rank] = {GLOO_HIP_SRC_ARENA, t};
       } else {
-        leafAt[rank] = {false, J.elem};
+        leafAt[rank] = {leafFlags, J.elem};
       }
       auto src = [&](int leaf) {
         const auto& l = leafAt.at(leaf);
-        return mkStep(GLOO_HIP_STEP_FOLD_SRC, -1, 0, l.first ? GLOO_HIP_SRC_ARENA : 0, 0, l.second, len);
+        return mkStep(GLOO_HIP_STEP_FOLD_SRC, -1, 0, l.first, 0, l.second, len);
       };
       std::vector<int> order;
       if (leftChain(F, J.tree, order)) {
@@ -393,31 +491,48 @@ Plan makeMeshPlan(int algo, int rank, int size, uint64_t count, int nptrs, const
       } else {
         // any other shape: post-order, one pairwise fold per node, inner
         // nodes into arena temporaries
-        std::function<std::pair<bool, uint64_t>(int, bool)> eval = [&](int t, bool root) {
+        std::function<std::pair<int, uint64_t>(int, bool)> eval = [&](int t, bool root) {
           const TreeNode& n = F.at(t);
           if (n.leaf >= 0) return leafAt.at(n.leaf);
           const auto a = eval(n.lhs, false);
           const auto b = eval(n.rhs, false);
-          p.steps.push_back(mkStep(GLOO_HIP_STEP_FOLD_SRC, -1, 0, a.first ? GLOO_HIP_SRC_ARENA : 0, 0, a.second, len));
-          p.steps.push_back(mkStep(GLOO_HIP_STEP_FOLD_SRC, -1, 0, b.first ? GLOO_HIP_SRC_ARENA : 0, 0, b.second, len));
+          p.steps.push_back(mkStep(GLOO_HIP_STEP_FOLD_SRC, -1, 0, a.first, 0, a.second, len));
+          p.steps.push_back(mkStep(GLOO_HIP_STEP_FOLD_SRC, -1, 0, b.first, 0, b.second, len));
           if (root) {
             p.steps.push_back(mkStep(GLOO_HIP_STEP_FOLD, -1, 0, 0, J.lo, 0, len));
-            return std::make_pair(false, J.lo);
+            return std::make_pair(0, J.lo);
           }
           const uint64_t tmp = alloc(len);
           p.steps.push_back(mkStep(GLOO_HIP_STEP_FOLD, -1, 0, GLOO_HIP_DST_ARENA, tmp, 0, len));
-          return std::make_pair(true, tmp);
+          return std::make_pair((int)GLOO_HIP_SRC_ARENA, tmp);
         };
         eval(J.tree, true);
       }
     }
     if (!allreduce)
       for (int s : peersFrom(rank)) p.steps.push_back(mkStep(GLOO_HIP_STEP_NOTIFY, s, GLOO_HIP_SLOT_NOTIFY));
+    if (toRoot && rank != ns->root) {
+      // results to the root; its previous-run copy-out must be done
+      p.steps.push_back(mkStep(GLOO_HIP_STEP_WAIT_NOTIFY, ns->root, GLOO_HIP_SLOT_DIST_NOTIFY, GLOO_HIP_PREV_RUN));
+      for (int j : byOwner[rank])
+        p.steps.push_back(mkStep(GLOO_HIP_STEP_SEND, ns->root, slotOf(j, GLOO_HIP_SLOT_AUX0), 0, 0, jobs[j].lo,
+                                 jobs[j].hi - jobs[j].lo));
+    }
     if (allreduce)
       for (int j : byOwner[rank])
         for (int s : peersFrom(rank))
           p.steps.push_back(mkStep(GLOO_HIP_STEP_SEND, s, slotOf(j, GLOO_HIP_SLOT_AUX0), 0, 0, jobs[j].lo,
                                    jobs[j].hi - jobs[j].lo));
+  }
+  if (toRoot && rank == ns->root) {
+    for (int o : peersFrom(rank))
+      for (int j : byOwner[o]) p.steps.push_back(mkStep(GLOO_HIP_STEP_WAIT_RECV, o, slotOf(j, GLOO_HIP_SLOT_AUX0)));
+    for (int o : peersFrom(rank))
+      for (int j : byOwner[o])
+        p.steps.push_back(mkStep(GLOO_HIP_STEP_COPY, -1, 0, GLOO_HIP_SRC_ARENA, jobs[j].lo, rootRegion[j],
+                                 jobs[j].hi - jobs[j].lo));
+    for (int o : peersFrom(rank))
+      if (!byOwner[o].empty()) p.steps.push_back(mkStep(GLOO_HIP_STEP_NOTIFY, o, GLOO_HIP_SLOT_DIST_NOTIFY));
   }
   if (allreduce) {
     for (int o : peersFrom(rank))

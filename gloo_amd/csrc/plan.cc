@@ -955,12 +955,17 @@ Plan planReduce(int rank, int size, uint64_t count, const NewStyleOptions& o) {
 Plan makeNewStylePlan(int algo, int rank, int size, uint64_t count, const NewStyleOptions& o) {
   if (size < 1 || rank < 0 || rank >= size) throw std::invalid_argument("bad rank/size");
   if (o.noutputs < 1 || o.ninputs < 0 || o.elemSize == 0) throw std::invalid_argument("bad options");
+  if ((algo & ~GLOO_HIP_ALGO_MESH) == GLOO_HIP_ALGO_REDUCE && (o.ninputs > 1 || o.noutputs != 1))
+    throw std::invalid_argument("gloo::reduce takes one input and one output");
+  if (algo & GLOO_HIP_ALGO_MESH) {
+    const int base = algo & ~GLOO_HIP_ALGO_MESH;
+    if (base == GLOO_HIP_ALGO_REDUCE && (o.root < 0 || o.root >= size)) throw std::invalid_argument("root out of range");
+    return makeMeshPlan(base, rank, size, count, o.noutputs, {}, &o);
+  }
   switch (algo) {
     case GLOO_HIP_ALGO_ALLREDUCE_RING: return planAllreduceRing(rank, size, count, o);
     case GLOO_HIP_ALGO_ALLREDUCE_BCUBE: return planAllreduceBcube(rank, size, count, o);
-    case GLOO_HIP_ALGO_REDUCE:
-      if (o.ninputs > 1 || o.noutputs != 1) throw std::invalid_argument("gloo::reduce takes one input and one output");
-      return planReduce(rank, size, count, o);
+    case GLOO_HIP_ALGO_REDUCE: return planReduce(rank, size, count, o);
   }
   throw std::invalid_argument("not a new-style algorithm");
 }
@@ -1011,7 +1016,7 @@ extern "C" int gloo_hip_plan_ex(int algo, int rank, int size, size_t count, int 
       o.noutputs = noutputs;
       o.elemSize = elem_size;
       o.maxSegmentBytes = max_segment_bytes;
-      if (algo == GLOO_HIP_ALGO_REDUCE) {
+      if ((algo & ~GLOO_HIP_ALGO_MESH) == GLOO_HIP_ALGO_REDUCE) {
         if (!recv_elems) return GLOO_HIP_EINVAL_ARG;  // recv_elems[0] = root
         o.root = recv_elems[0];
       }

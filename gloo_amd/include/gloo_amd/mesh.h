@@ -15,6 +15,9 @@
 
 namespace gloo_amd {
 
-Plan makeMeshPlan(int algo, int rank, int size, uint64_t count, int nptrs, const std::vector<int>& recvElems);
+// ns: the options of a new-style algorithm (ALLREDUCE_RING, ALLREDUCE_BCUBE,
+// REDUCE), nullptr for the class-style ones.
+Plan makeMeshPlan(int algo, int rank, int size, uint64_t count, int nptrs, const std::vector<int>& recvElems,
+                  const NewStyleOptions* ns = nullptr);
 
 }  // namespace gloo_amd

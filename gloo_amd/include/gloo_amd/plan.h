@@ -28,9 +28,10 @@ struct NewStyleOptions {
   int root = 0;                          // gloo::reduce only (ReduceOptions::setRoot)
 };
 // algo: GLOO_HIP_ALGO_ALLREDUCE_RING, GLOO_HIP_ALGO_ALLREDUCE_BCUBE or
-// GLOO_HIP_ALGO_REDUCE.
+// GLOO_HIP_ALGO_REDUCE, optionally | GLOO_HIP_ALGO_MESH (mesh.h).
 Plan makeNewStylePlan(int algo, int rank, int size, uint64_t count, const NewStyleOptions& o);
 inline bool isNewStyle(int algo) {
+  algo &= ~GLOO_HIP_ALGO_MESH;
   return algo == GLOO_HIP_ALGO_ALLREDUCE_RING || algo == GLOO_HIP_ALGO_ALLREDUCE_BCUBE ||
          algo == GLOO_HIP_ALGO_REDUCE;
 }

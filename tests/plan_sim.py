@@ -21,7 +21,7 @@ KIND = dict(DECL_RECV=0, SEND=1, WAIT_RECV=2, REDUCE=3, COPY=4, NOTIFY=5, WAIT_N
 ALGO = dict(ring_chunked=0, halving_doubling=1, ring=2, local=3, reduce_scatter=4, allreduce_new=5,
             ring_chunked_mesh=6, allreduce_bcube=7, reduce=8)
 MESH = 0x100  # algo | MESH: the derived mesh plan (gloo_amd/csrc/mesh.cc)
-ALGO.update({"mesh_" + k: v | MESH for k, v in list(ALGO.items()) if v < 5})
+ALGO.update({"mesh_" + k: v | MESH for k, v in list(ALGO.items()) if v < 5 or v in (5, 7, 8)})
 SRC_ARENA, DST_ARENA, FROM_INPUTS, FOLD_REVERSE, FOLD_TREE, PREV_RUN = 1, 2, 4, 8, 16, 32
 
 
@@ -174,9 +174,10 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
             for j in range(1, k):
                 user[r][j][lo:hi] = user[r][0][lo:hi]
         elif K == KIND["FOLD_SRC"]:
-            pending[r].append((bool(s.flags & SRC_ARENA), s.src_off))
+            pending[r].append((s.flags, s.src_off))
         elif K == KIND["FOLD"]:
-            srcs = [space(r, a)[o:o + s.length].copy() for a, o in pending[r]]
+            srcs = [(ins[r, 0] if f & FROM_INPUTS else space(r, f & SRC_ARENA))[o:o + s.length].copy()
+                    for f, o in pending[r]]
             pending[r] = []
             if s.flags & FOLD_TREE:
                 while len(srcs) > 1:

@@ -62,11 +62,14 @@ def _guard(body, r, errors):
         errors.append((r, repr(e)))
 
 
+@pytest.mark.parametrize("mesh", ["1", "0"])
 @pytest.mark.parametrize("case", _keys("bcube/"))
-def test_bcube_threads_golden(torch, golden_new, case):
+def test_bcube_threads_golden(torch, golden_new, case, mesh, monkeypatch):
     """BCUBE allreduce, ranks as threads on the visible GPU(s); called twice
-    (the second call reuses the cached schedule with rebound buffers)."""
+    (the second call reuses the cached schedule with rebound buffers).  Both
+    routes: the derived mesh plan (default, 2 <= P <= 8) and the reference's."""
     import gloo_amd
+    monkeypatch.setenv("GLOO_AMD_MESH", mesh)
     parts = case.split("/")
     op, dtype, P = parts[1], parts[2], int(parts[3][1:])
     nin, nout, n = int(parts[4][1:]), int(parts[5][1:]), int(parts[6][1:])
@@ -96,11 +99,14 @@ def test_bcube_threads_golden(torch, golden_new, case):
             assert same_bytes(y, want), (r, rep, j)
 
 
+@pytest.mark.parametrize("mesh", ["1", "0"])
 @pytest.mark.parametrize("case", _keys("reduce/"))
-def test_reduce_threads_golden(torch, golden_new, case):
-    """gloo::reduce: every rank's whole output equals the reference's (the
-    root holds the result, the others the partial sums the ring leaves)."""
+def test_reduce_threads_golden(torch, golden_new, case, mesh, monkeypatch):
+    """gloo::reduce: the root's output equals the reference's on both routes;
+    on the reference route every rank's whole output does (the others hold
+    the partial sums the ring leaves; the mesh route leaves other scratch)."""
     import gloo_amd
+    monkeypatch.setenv("GLOO_AMD_MESH", mesh)
     parts = case.split("/")
     op, dtype, P = parts[1], parts[2], int(parts[3][1:])
     has_in, n, root, seg = int(parts[4][1:]), int(parts[5][1:]), int(parts[6][1:]), int(parts[7][1:])
@@ -126,7 +132,8 @@ def test_reduce_threads_golden(torch, golden_new, case):
 
     run_threads(P, body)
     for (r, rep), y in results.items():
-        assert same_bytes(y, want[r]), (r, rep)
+        if mesh == "0" or r == root:
+            assert same_bytes(y, want[r]), (r, rep)
 
 
 WORKER = r'''
@@ -145,8 +152,9 @@ for it, s in enumerate([0, 0, 0, 1, 1, 0]):
     inp.fill_((rank + 1) * (it + 1))
     outp.fill_(-1)
     torch.cuda.synchronize()
-    if kind == "bcube":
-        gloo_amd.allreduce(ctx, [outp.data_ptr()], n, "f32", "sum", inputs=[inp.data_ptr()], algorithm="bcube")
+    if kind in ("bcube", "ring"):
+        gloo_amd.allreduce(ctx, [outp.data_ptr()], n, "f32", "sum", inputs=[inp.data_ptr()], algorithm=kind,
+                           max_segment_bytes=128 << 10)
     else:
         gloo_amd.reduce_to_root(ctx, outp.data_ptr(), n, "f32", it % size, "sum", input=inp.data_ptr(),
                                 max_segment_bytes=256 << 10)
@@ -157,11 +165,15 @@ np.save(out, np.array(res))
 
 
 @pytest.mark.parametrize("kind,P,env", [
-    ("bcube", 4, {}),                                   # 2 x 2: recursive halving shape
-    ("bcube", 6, {}),                                   # 2 x 3
+    ("bcube", 4, {}),                                   # 2 x 2: recursive halving shape (mesh: tree fold)
+    ("bcube", 6, {}),                                   # 2 x 3 (mesh: pairwise folds)
+    ("bcube", 4, {"GLOO_AMD_MESH": "0"}),               # the reference's exchange route
     ("bcube", 3, {"GLOO_AMD_SIGNAL": "host"}),
     ("reduce", 4, {}),
+    ("reduce", 5, {"GLOO_AMD_MESH": "0"}),
     ("reduce", 3, {"GLOO_AMD_COPY": "kernel"}),
+    ("ring", 4, {}),                                    # new-style RING, mesh route
+    ("ring", 3, {"GLOO_AMD_MESH": "0"}),
 ])
 def test_processes(torch, kind, P, env):
     """Ranks as processes (device signalling unless overridden; inboxes over
@@ -178,7 +190,7 @@ def test_processes(torch, kind, P, env):
         ys = [np.load(os.path.join(d, f"o{r}.npy")) for r in range(P)]
     for it in range(ys[0].shape[0]):
         want = (it + 1) * P * (P + 1) / 2
-        if kind == "bcube":
+        if kind in ("bcube", "ring"):
             for r in range(P):
                 assert (ys[r][it] == want).all(), (r, it)
         else:

@@ -141,3 +141,96 @@ def test_reduce_rejects_bad_root():
     from plan_sim import get_plan
     with pytest.raises(RuntimeError):
         get_plan("reduce", 0, 4, 100, recv=np.array([4], np.int32), elem_size=8)
+
+
+# ---- derived mesh plans of the new-style collectives (gloo_amd/csrc/mesh.cc) ----
+
+def _random(dtype, shape, seed):
+    rng = np.random.default_rng(seed)
+    if dtype in ("i32", "u64"):
+        return rng.integers(0, 1 << 30, size=shape, dtype=np.int64).astype(np.int32 if dtype == "i32" else np.uint64)
+    f = rng.standard_normal(shape).astype(np.float32)
+    f[rng.random(shape) < 0.02] = np.nan
+    f[rng.random(shape) < 0.02] = -0.0
+    f[rng.random(shape) < 0.02] = 0.0
+    if dtype == "f32":
+        return f
+    if dtype == "f16":
+        return f.astype(np.float16).view(np.uint16)
+    return (f.view(np.uint32) >> 16).astype(np.uint16)
+
+
+def _mesh_keys(prefix):
+    return [k for k in _keys(prefix) if 2 <= int(k.split("/")[3][1:]) <= 8]
+
+
+@pytest.mark.parametrize("case", _mesh_keys("bcube/"))
+def test_mesh_bcube_matches_reference_golden(golden_new, case):
+    """BCUBE's result with mesh data movement: the trees the reference builds
+    (balanced for P = 2^k, pairwise otherwise) evaluated at their owners."""
+    parts = case.split("/")
+    op, dtype, nin = parts[1], parts[2], int(parts[4][1:])
+    init = golden_new[case + "/init"]
+    ins = golden_new[case + "/in"] if nin else None
+    want = golden_new[case + "/out"]
+    for seed in (0, 1):
+        y = simulate("mesh_allreduce_bcube", op, dtype, init, seed=seed, ins=ins)
+        for r in range(y.shape[0]):
+            for j in range(y.shape[1]):
+                assert same_bytes(y[r, j], want), (seed, r, j)
+
+
+def _ring_new_keys():
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "sched_golden.npz"))
+    keys = sorted({k.rsplit("/", 1)[0] for k in z.files if k.startswith("allreduce_new/")})
+    return [k for k in keys if 2 <= int(k.split("/")[3][1:]) <= 8]
+
+
+@pytest.mark.parametrize("case", _ring_new_keys())
+def test_mesh_new_style_ring_matches_reference_golden(golden_sched, case):
+    """gloo::allreduce RING (<= 1 MiB segments around the ring in the
+    reference) as two all-to-all hops, same bytes."""
+    parts = case.split("/")
+    op, dtype, nin, seg = parts[1], parts[2], int(parts[4][1:]), int(parts[7][1:])
+    init = golden_sched[case + "/init"]
+    ins = golden_sched[case + "/in"] if nin else None
+    want = golden_sched[case + "/out"]
+    y = simulate("mesh_allreduce_new", op, dtype, init, seed=3, ins=ins, max_seg=seg)
+    for r in range(y.shape[0]):
+        for j in range(y.shape[1]):
+            assert same_bytes(y[r, j], want), (r, j)
+
+
+@pytest.mark.parametrize("case", _mesh_keys("reduce/"))
+def test_mesh_reduce_root_matches_reference_golden(golden_new, case):
+    """gloo::reduce with mesh data movement: the ROOT's output equals the
+    reference's (the other ranks' outputs are scratch in both)."""
+    parts = case.split("/")
+    op, dtype = parts[1], parts[2]
+    nin, root, seg = int(parts[4][1:]), int(parts[6][1:]), int(parts[7][1:])
+    init = golden_new[case + "/init"]
+    ins = golden_new[case + "/in"] if nin else None
+    want = golden_new[case + "/out"]
+    for seed in (0, 1):
+        y = simulate("mesh_reduce", op, dtype, init, recv=np.array([root], np.int32), seed=seed, ins=ins,
+                     max_seg=seg)
+        assert same_bytes(y[root, 0], want[root]), seed
+
+
+@pytest.mark.parametrize("op", ["sum", "product", "max", "min"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "i32"])
+@pytest.mark.parametrize("P,n,seg", [(2, 1000, 0), (3, 999, 128), (5, 4099, 256), (6, 777, 64), (8, 20011, 0)])
+def test_mesh_new_style_bitwise_random(op, dtype, P, n, seg):
+    """Mesh vs reference route on random data with NaN / signed zeros, for
+    RING and BCUBE allreduce (three chained in-place runs) and reduce to a
+    rotating root (separate inputs, three runs)."""
+    x = _random(dtype, (P, 1, n), P * 13 + n)
+    for algo in ("allreduce_new", "allreduce_bcube"):
+        want = simulate(algo, op, dtype, x, seed=1, runs=3, max_seg=seg)
+        got = simulate("mesh_" + algo, op, dtype, x, seed=P, runs=3, max_seg=seg)
+        assert same_bytes(got, want), algo
+    root = np.array([n % P], np.int32)
+    init = _random(dtype, (P, 1, n), n)
+    want = simulate("reduce", op, dtype, init, recv=root, seed=2, ins=x, max_seg=seg)
+    got = simulate("mesh_reduce", op, dtype, init, recv=root, seed=P, ins=x, runs=3, max_seg=seg)
+    assert same_bytes(got[root[0], 0], want[root[0], 0])
