@@ -1028,7 +1028,7 @@ extern "C" int gloo_hip_plan_ex(int algo, int rank, int size, size_t count, int 
     if (arena_elems) *arena_elems = p.arena;
     if (steps) {
       if (capacity < p.steps.size()) return GLOO_HIP_EINVAL_ARG;
-      std::memcpy(steps, p.steps.data(), p.steps.size() * sizeof(gloo_hip_step_t));
+      if (!p.steps.empty()) std::memcpy(steps, p.steps.data(), p.steps.size() * sizeof(gloo_hip_step_t));
     }
     return GLOO_HIP_OK;
   } catch (const std::exception&) {

@@ -31,9 +31,26 @@ class Step(ctypes.Structure):
                 ("length", ctypes.c_uint64)]
 
 
+_plan_lib = None
+
+
+def plan_lib():
+    """The planners' C-ABI: the product library, or (GLOO_AMD_PLAN_LIB) a
+    host-only build of plan.cc + mesh.cc, e.g. under AddressSanitizer."""
+    global _plan_lib
+    if _plan_lib is None:
+        import os
+        path = os.environ.get("GLOO_AMD_PLAN_LIB")
+        if path:
+            _plan_lib = ctypes.CDLL(path)
+        else:
+            import gloo_amd
+            _plan_lib = gloo_amd.lib
+    return _plan_lib
+
+
 def get_plan(algo, rank, size, count, nptrs=1, recv=None, nin=0, elem_size=4, max_seg=0):
-    import gloo_amd
-    L = gloo_amd.lib
+    L = plan_lib()
     n = ctypes.c_size_t()
     arena = ctypes.c_size_t()
     rp = None
