@@ -388,14 +388,13 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
 
     # Config 5: reduce-scatter (HD), fp16 / bf16 buckets, every op, 16 Mi
     # elements per rank, recvElems = an even split.
-    def rs_once(dtype, op, env):
+    def rs_once(dtype, op, env, m=16 << 20):
         def body():
-            m = 16 << 20
             recv = [m // world + (1 if r < m % world else 0) for r in range(world)]
             b = torch.ones(m, dtype=torch.float16 if dtype == "f16" else torch.bfloat16, device=dev)
             torch.cuda.synchronize(dev)
-            c = hip.Context(rank, world, "file:%s/rs_%s_%s_%s" % (obj[0], dtype, op, env.get("GLOO_AMD_MESH", "1")),
-                            device=dev.index, timeout_ms=60000)
+            c = hip.Context(rank, world, "file:%s/rs_%s_%s_%s_%d" % (obj[0], dtype, op, env.get("GLOO_AMD_MESH", "1"),
+                                                                     m), device=dev.index, timeout_ms=60000)
             a = hip.Algorithm(c, "reduce_scatter", op, dtype, [b.data_ptr()], m, recv_elems=recv)
             a.run()
             a.run()
@@ -416,14 +415,17 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         if any("error" in x for x in g):
             return {"dtype": dtype, "op": op, "error": next(x["error"] for x in g if "error" in x)}
         per = sorted(max(x["us"][k] for x in g) for k in range(10))
-        nbytes = (16 << 20) * 2
+        nbytes = m * 2
         return {"dtype": dtype, "op": op, "route": "reference" if env.get("GLOO_AMD_MESH") == "0" else "mesh",
-                "elements_per_rank": 16 << 20, "us_p50": per[5], "us_max": per[-1],
+                "elements_per_rank": m, "us_p50": per[5], "us_max": per[-1],
                 "busbw_gib_s": round((world - 1) / world * nbytes / (per[5] / 1e6) / GIB, 2)}
 
     rs_summary = [rs_once(dt, op, {}) for dt in ("f16", "bf16") for op in ("sum", "product", "min", "max")]
     rs_summary += [rs_once(dt, "sum", {"GLOO_AMD_MESH": "0"}) for dt in ("f16", "bf16")]
     partial["reduce_scatter"] = rs_summary
+    # the other two bucket sizes of SURVEY 8(d) config 5: 1 Mi and 64 Mi elements per rank
+    for m in (1 << 20, 64 << 20):
+        rs_summary += [rs_once(dt, "sum", env, m) for dt in ("f16", "bf16") for env in ({}, {"GLOO_AMD_MESH": "0"})]
 
     # New-style function API: gloo::allreduce RING / BCUBE
     # and gloo::reduce to rank 0, fp32 sum, separate input and output; the
