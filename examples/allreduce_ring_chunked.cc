@@ -14,6 +14,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -30,6 +31,9 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "no GPU\n");
     return 2;
   }
+  // the framework's allocation mutex (gloo::CudaShared::setMutex, gloo/cuda.h:40-54)
+  static std::mutex frameworkAllocMutex;
+  gloo_amd::HipShared::setMutex(&frameworkAllocMutex);
   auto store = gloo_amd::openStore("mem:example");
   std::vector<int> bad(P, 0);
   std::vector<std::thread> ts;

@@ -34,7 +34,7 @@ Context::Context(int r, int s, std::chrono::milliseconds timeout)
 }
 
 Context::~Context() {
-  if (shmDev_) (void)hipHostUnregister(shm_);
+  if (shmDev_) GLOO_AMD_HIP_RELEASE(hipHostUnregister(shm_));
   if (shm_) ::munmap(shm_, shmBytes_);
 }
 
@@ -83,7 +83,7 @@ std::atomic<uint64_t>& Context::counter(uint64_t inst, int src, int dst, int slo
 
 void Context::ensureDeviceMapped() {
   if (shmDev_) return;
-  GLOO_AMD_HIP_CHECK(hipHostRegister(shm_, shmBytes_, hipHostRegisterMapped | hipHostRegisterPortable));
+  GLOO_AMD_HIP_ALLOC(hipHostRegister(shm_, shmBytes_, hipHostRegisterMapped | hipHostRegisterPortable));
   void* d = nullptr;
   GLOO_AMD_HIP_CHECK(hipHostGetDevicePointer(&d, shm_, 0));
   shmDev_ = d;

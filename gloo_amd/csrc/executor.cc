@@ -129,7 +129,7 @@ struct PlanExecutor::HostShm {
     return h;
   }
   void map() {
-    GLOO_AMD_HIP_CHECK(hipHostRegister(host, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    GLOO_AMD_HIP_ALLOC(hipHostRegister(host, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
     GLOO_AMD_HIP_CHECK(hipHostGetDevicePointer(&dev, host, 0));
   }
   void unlink() {
@@ -138,7 +138,7 @@ struct PlanExecutor::HostShm {
   }
   ~HostShm() {
     if (host) {
-      (void)hipHostUnregister(host);
+      GLOO_AMD_HIP_RELEASE(hipHostUnregister(host));
       ::munmap(host, bytes);
     }
     unlink();
@@ -199,7 +199,7 @@ void PlanExecutor::classifyPointers() {
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
         (void)hipGetLastError();
       }
-      if (remote[j] && !stage[j]) GLOO_AMD_HIP_CHECK(hipMalloc(&stage[j], std::max<size_t>(256, count_ * es_)));
+      if (remote[j] && !stage[j]) GLOO_AMD_HIP_ALLOC(hipMalloc(&stage[j], std::max<size_t>(256, count_ * es_)));
       anyRemote_ = anyRemote_ || remote[j];
     }
   };
@@ -337,10 +337,10 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     arenaShm_ = HostShm::create(arenaBytes);
     arena_ = static_cast<char*>(arenaShm_->dev);
   } else if (fineArena_) {
-    GLOO_AMD_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), arenaBytes,
+    GLOO_AMD_HIP_ALLOC(hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), arenaBytes,
                                              hipDeviceMallocFinegrained));
   } else {
-    GLOO_AMD_HIP_CHECK(hipMalloc(&arena_, arenaBytes));
+    GLOO_AMD_HIP_ALLOC(hipMalloc(&arena_, arenaBytes));
   }
   ArenaRecord rec;
   std::memset(&rec, 0, sizeof(rec));
@@ -353,7 +353,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     GLOO_AMD_ENFORCE(arenaShm_->name.size() < sizeof(rec.shm), "shm name too long");
     std::memcpy(rec.shm, arenaShm_->name.c_str(), arenaShm_->name.size() + 1);
   } else {
-    GLOO_AMD_HIP_CHECK(hipIpcGetMemHandle(&rec.handle, arena_));
+    GLOO_AMD_HIP_ALLOC(hipIpcGetMemHandle(&rec.handle, arena_));
   }
   std::vector<char> blob(sizeof(rec));
   std::memcpy(blob.data(), &rec, sizeof(rec));
@@ -380,7 +380,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       }
     } else {
       void* p = nullptr;
-      GLOO_AMD_HIP_CHECK(hipIpcOpenMemHandle(&p, pr.handle, hipIpcMemLazyEnablePeerAccess));
+      GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&p, pr.handle, hipIpcMemLazyEnablePeerAccess));
       peers_[peer].base = static_cast<char*>(p);
       peers_[peer].ipc = true;
     }
@@ -413,7 +413,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       copyBlocksLocal_ = copyBlocks_;
     }
     const size_t tickets = std::max<size_t>(256, (size_t)P * GLOO_HIP_NUM_SLOTS * sizeof(unsigned));
-    GLOO_AMD_HIP_CHECK(hipMalloc(&ticket_, tickets));
+    GLOO_AMD_HIP_ALLOC(hipMalloc(&ticket_, tickets));
     GLOO_AMD_HIP_CHECK(hipMemset(ticket_, 0, tickets));
     // Graph replay pays off once a plan has steps that are not fused
     // one-workgroup launches (measured); "1" / "0" force it.
@@ -428,7 +428,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
         unfused = true;
     graphMode_ = gmode == "1" || (gmode == "auto" && unfused);
     if (graphMode_) {
-      GLOO_AMD_HIP_CHECK(hipMalloc(&epoch_, sizeof(uint64_t)));
+      GLOO_AMD_HIP_ALLOC(hipMalloc(&epoch_, sizeof(uint64_t)));
       GLOO_AMD_HIP_CHECK(hipMemset(epoch_, 0, sizeof(uint64_t)));
     }
   }
@@ -441,26 +441,26 @@ PlanExecutor::~PlanExecutor() {
     if (stream_) (void)hipStreamSynchronize(stream_);
     if (ctx_->size > 1) {
       for (auto& p : peers_)
-        if (p.ipc && p.base) (void)hipIpcCloseMemHandle(p.base);
+        if (p.ipc && p.base) GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(p.base));
       // nobody may free an arena a peer still maps
       ctx_->barrier(strcat_("inst", inst_, "/closed"));
       peerShm_.clear();
       if (arenaShm_) {
         arenaShm_.reset();
       } else if (arena_) {
-        (void)hipFree(arena_);
+        GLOO_AMD_HIP_RELEASE(hipFree(arena_));
       }
     }
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
     for (hipEvent_t e : forkEvents_) (void)hipEventDestroy(e);
     for (hipStream_t a : aux_) (void)hipStreamDestroy(a);
     if (graphExec_) (void)hipGraphExecDestroy(graphExec_);
-    if (epoch_) (void)hipFree(epoch_);
-    if (ticket_) (void)hipFree(ticket_);
+    if (epoch_) GLOO_AMD_HIP_RELEASE(hipFree(epoch_));
+    if (ticket_) GLOO_AMD_HIP_RELEASE(hipFree(ticket_));
     for (char* p : outStage_)
-      if (p) (void)hipFree(p);
+      if (p) GLOO_AMD_HIP_RELEASE(hipFree(p));
     for (char* p : inStage_)
-      if (p) (void)hipFree(p);
+      if (p) GLOO_AMD_HIP_RELEASE(hipFree(p));
     if (ownStream_ && stream_) (void)hipStreamDestroy(stream_);
   } catch (...) {
     // teardown is best effort; never throw from a destructor

@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <mutex>
 #include <sstream>
 #include <stdexcept>
 #include <string>
@@ -23,6 +24,16 @@ struct IoException : Exception {
   explicit IoException(const std::string& m) : Exception(m) {}
 };
 
+// gloo::CudaShared (gloo/cuda.h:40-54): the mutex that serialises this
+// library's device allocations, frees and IPC mappings with those of the
+// host framework (which may install its own allocator's mutex).  Held only
+// around the individual HIP calls, never across a rendezvous.
+class HipShared {
+ public:
+  static std::mutex& getMutex();
+  static void setMutex(std::mutex* m);
+};
+
 template <typename... Args>
 std::string strcat_(Args&&... args) {
   std::ostringstream ss;
@@ -37,6 +48,18 @@ std::string strcat_(Args&&... args) {
     if (!(cond))                                                                       \
       throw ::gloo_amd::EnforceNotMet(::gloo_amd::strcat_(__FILE__, ":", __LINE__,     \
                                                           ": ", #cond, " ", ##__VA_ARGS__)); \
+  } while (0)
+
+// A HIP allocation / free / mapping call under HipShared's mutex.
+#define GLOO_AMD_HIP_ALLOC(expr)                                                       \
+  do {                                                                                 \
+    std::lock_guard<std::mutex> allocLock_(::gloo_amd::HipShared::getMutex());         \
+    GLOO_AMD_HIP_CHECK(expr);                                                          \
+  } while (0)
+#define GLOO_AMD_HIP_RELEASE(expr)                                                     \
+  do {                                                                                 \
+    std::lock_guard<std::mutex> allocLock_(::gloo_amd::HipShared::getMutex());         \
+    (void)(expr);                                                                      \
   } while (0)
 
 #define GLOO_AMD_HIP_CHECK(expr)                                                       \
