@@ -378,6 +378,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     hd_variants = {"mesh": {},
                    "mesh_memcpy_forked": {"GLOO_AMD_COPY": "memcpy"},
                    "mesh_eager": {"GLOO_AMD_GRAPH": "0"},
+                   "mesh_host_block_flags": {"GLOO_AMD_MAILBOX": "0"},
                    "reference_route": {"GLOO_AMD_MESH": "0"},
                    "reference_route_kernel_copy": {"GLOO_AMD_MESH": "0", "GLOO_AMD_COPY": "kernel"},
                    "reference_route_eager": {"GLOO_AMD_MESH": "0", "GLOO_AMD_GRAPH": "0"}}

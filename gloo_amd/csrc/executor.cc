@@ -31,7 +31,16 @@ struct ArenaRecord {
   hipIpcMemHandle_t handle;  // DEVICE workspace
   int32_t host;              // HOST workspace: the arena is the shm segment `shm`
   char shm[60];
+  int32_t deviceSignal;      // this rank signals with stream-ordered kernels
+  int32_t hasMailbox;        // ... into device-resident mailboxes
+  uint64_t mailboxPtr;
+  hipIpcMemHandle_t mailboxHandle;
 };
+
+bool mailboxesEnabled() {
+  const char* e = std::getenv("GLOO_AMD_MAILBOX");
+  return !(e && e[0] == '0');
+}
 
 void bumpCounter(void* p) { static_cast<std::atomic<uint64_t>*>(p)->fetch_add(1, std::memory_order_acq_rel); }
 
@@ -259,9 +268,11 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     ownStream_ = true;
   }
   // Baseline every channel before anyone can signal this instance (instance
-  // slots are recycled modulo kMaxLiveInstances), count its messages per
-  // run, and give every step its sequence number (StepSeq).
-  {
+  // slots of the host control block are recycled modulo kMaxLiveInstances;
+  // a device mailbox is fresh, so its channels start at 0), count its
+  // messages per run, and give every step its sequence number (StepSeq).
+  // Runs before the ready barrier, i.e. before any peer can signal.
+  auto assignSeqs = [&] {
     std::map<std::pair<int, int>, uint64_t> base, perRun, seen;
     auto isWait = [](int k) { return k == GLOO_HIP_STEP_WAIT_RECV || k == GLOO_HIP_STEP_WAIT_NOTIFY; };
     auto isSend = [](int k) { return k == GLOO_HIP_STEP_SEND || k == GLOO_HIP_STEP_NOTIFY; };
@@ -271,8 +282,9 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       // two apart in the maps by the sign of the key
       const std::pair<int, int> key{isWait(s.kind) ? -1 - s.peer : s.peer, s.slot};
       if (!base.count(key))
-        base[key] = isWait(s.kind) ? ctx_->counter(inst_, s.peer, me, s.slot).load(std::memory_order_acquire)
-                                   : ctx_->counter(inst_, me, s.peer, s.slot).load(std::memory_order_acquire);
+        base[key] = mailboxWith(s.peer) ? 0
+                    : isWait(s.kind)   ? ctx_->counter(inst_, s.peer, me, s.slot).load(std::memory_order_acquire)
+                                       : ctx_->counter(inst_, me, s.peer, s.slot).load(std::memory_order_acquire);
       perRun[key]++;
     }
     stepSeq_.resize(plan_.steps.size());
@@ -286,9 +298,12 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       if (isWait(s.kind) && (s.flags & GLOO_HIP_PREV_RUN)) stepSeq_[i].base -= perRun[key];
       stepSeq_[i].perRun = perRun[key];
     }
-  }
+  };
 
-  if (P == 1) return;  // no transport: local reduce / broadcast only
+  if (P == 1) {  // no transport: local reduce / broadcast only
+    assignSeqs();
+    return;
+  }
 
   // Phase 1: who is where.  Every rank publishes (pid, device); each rank
   // reads the records of every peer its plan talks to.
@@ -342,12 +357,29 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   } else {
     GLOO_AMD_HIP_ALLOC(hipMalloc(&arena_, arenaBytes));
   }
+  // Device-side signalling polls a mailbox in this GPU's own (fine-grained)
+  // memory that the peers write over xGMI: one 64-bit counter per
+  // (sender, slot).  Measured on MI355X: a cross-rank hop costs about 1 us
+  // this way against about 2.4 us through the host control block
+  // (tools/pingpong.cc, profiles/round1/r1q_pingpong.jsonl).
+  if (deviceSignal_ && mailboxesEnabled()) {
+    const size_t mbBytes = ((size_t)P * GLOO_HIP_NUM_SLOTS * sizeof(uint64_t) + 4095) / 4096 * 4096;
+    GLOO_AMD_HIP_ALLOC(hipExtMallocWithFlags(reinterpret_cast<void**>(&mailbox_), mbBytes, hipDeviceMallocFinegrained));
+    GLOO_AMD_HIP_CHECK(hipMemsetAsync(mailbox_, 0, mbBytes, stream_));
+    GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
   ArenaRecord rec;
   std::memset(&rec, 0, sizeof(rec));
   rec.pid = ctx_->pid();
   rec.device = ctx_->device();
   rec.ptr = reinterpret_cast<uint64_t>(arena_);
   rec.bytes = arenaBytes;
+  rec.deviceSignal = deviceSignal_ ? 1 : 0;
+  if (mailbox_) {
+    rec.hasMailbox = 1;
+    rec.mailboxPtr = reinterpret_cast<uint64_t>(mailbox_);
+    GLOO_AMD_HIP_ALLOC(hipIpcGetMemHandle(&rec.mailboxHandle, mailbox_));
+  }
   if (hostArena_) {
     rec.host = 1;
     GLOO_AMD_ENFORCE(arenaShm_->name.size() < sizeof(rec.shm), "shm name too long");
@@ -359,13 +391,33 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   std::memcpy(blob.data(), &rec, sizeof(rec));
   ctx_->store().set(strcat_("gloo_amd/inst", inst_, "/arena/", me), blob);
 
-  // Map the inbox arena of every peer this rank sends to, and find where in
-  // it the peer declared the region for our messages (its own plan).
-  for (int peer : sendPeers) {
+  // Every plan peer's record: its mailbox (a channel uses mailboxes when
+  // both ends signal from the device and have one — both ends decide alike),
+  // and, for a peer this rank sends to, its inbox arena and the region the
+  // peer declared there for our messages (its own plan).
+  peerMailbox_.assign(P, nullptr);
+  peerMailboxIpc_.assign(P, false);
+  for (int peer : planPeers) {
     auto v = ctx_->store().get(strcat_("gloo_amd/inst", inst_, "/arena/", peer), ctx_->timeout());
     GLOO_AMD_ENFORCE(v.size() == sizeof(ArenaRecord), "bad arena record from rank ", peer);
     ArenaRecord pr;
     std::memcpy(&pr, v.data(), sizeof(pr));
+    if (mailbox_ && pr.deviceSignal && pr.hasMailbox) {
+      if (pr.pid == ctx_->pid()) {
+        peerMailbox_[peer] = reinterpret_cast<uint64_t*>(pr.mailboxPtr);
+        if (pr.device != ctx_->device()) {
+          hipError_t e = hipDeviceEnablePeerAccess(pr.device, 0);
+          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
+          (void)hipGetLastError();
+        }
+      } else {
+        void* p = nullptr;
+        GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&p, pr.mailboxHandle, hipIpcMemLazyEnablePeerAccess));
+        peerMailbox_[peer] = static_cast<uint64_t*>(p);
+        peerMailboxIpc_[peer] = true;
+      }
+    }
+    if (!sendPeers.count(peer)) continue;
     if (pr.host && pr.pid != ctx_->pid()) {
       // another process's host workspace: map the same pages here
       peerShm_.push_back(HostShm::open(std::string(pr.shm), pr.bytes));
@@ -395,6 +447,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     if (s.kind == GLOO_HIP_STEP_SEND)
       GLOO_AMD_ENFORCE(remoteRegion_.count({s.peer, s.slot}), "rank ", s.peer, " declared no region for rank ",
                        me, " slot ", s.slot);
+  assignSeqs();
   if (deviceSignal_) {
     (void)ctx_->counterDevicePtr(inst_, 0, 0, 0);  // register the control block now
     ctx_->errorWord(me).store(0);
@@ -442,6 +495,8 @@ PlanExecutor::~PlanExecutor() {
     if (ctx_->size > 1) {
       for (auto& p : peers_)
         if (p.ipc && p.base) GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(p.base));
+      for (size_t q = 0; q < peerMailbox_.size(); q++)
+        if (peerMailboxIpc_[q] && peerMailbox_[q]) GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(peerMailbox_[q]));
       // nobody may free an arena a peer still maps
       ctx_->barrier(strcat_("inst", inst_, "/closed"));
       peerShm_.clear();
@@ -450,6 +505,7 @@ PlanExecutor::~PlanExecutor() {
       } else if (arena_) {
         GLOO_AMD_HIP_RELEASE(hipFree(arena_));
       }
+      if (mailbox_) GLOO_AMD_HIP_RELEASE(hipFree(mailbox_));
     }
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
     for (hipEvent_t e : forkEvents_) (void)hipEventDestroy(e);
@@ -510,6 +566,20 @@ hipEvent_t PlanExecutor::forkEvent(size_t k) {
     forkEvents_.push_back(e);
   }
   return forkEvents_[k];
+}
+
+bool PlanExecutor::mailboxWith(int peer) const {
+  return mailbox_ && peer >= 0 && peer < (int)peerMailbox_.size() && peerMailbox_[peer] != nullptr;
+}
+
+uint64_t* PlanExecutor::sigFlag(int peer, int slot) {
+  if (mailboxWith(peer)) return peerMailbox_[peer] + (size_t)ctx_->rank * GLOO_HIP_NUM_SLOTS + slot;
+  return ctx_->counterDevicePtr(inst_, ctx_->rank, peer, slot);
+}
+
+uint64_t* PlanExecutor::waitFlag(int peer, int slot) {
+  if (mailboxWith(peer)) return mailbox_ + (size_t)peer * GLOO_HIP_NUM_SLOTS + slot;
+  return ctx_->counterDevicePtr(inst_, peer, ctx_->rank, slot);
 }
 
 Seq PlanExecutor::seqOf(size_t i, uint64_t r, bool graph) const {
@@ -591,7 +661,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
   auto signal = [&](size_t i) {
     const Step& s = plan_.steps[i];
     if (deviceSignal_) {
-      GLOO_AMD_HIP_CHECK(launchSignal(ctx_->counterDevicePtr(inst_, me, s.peer, s.slot), seqOf(i, r, graph), epoch,
+      GLOO_AMD_HIP_CHECK(launchSignal(sigFlag(s.peer, s.slot), seqOf(i, r, graph), epoch,
                                       stream_));
     } else {
       enqueueBump(stream_, ctx_->counter(inst_, me, s.peer, s.slot));
@@ -641,7 +711,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
             const Step& t = steps[k];
             const size_t bytes = t.length * es_;
             d[nd++] = CopyDesc{sendDst(t), sendSrc(t), bytes,
-                               ctx_->counterDevicePtr(inst_, me, t.peer, t.slot), seqOf(k, r, graph),
+                               sigFlag(t.peer, t.slot), seqOf(k, r, graph),
                                ticket_ + (size_t)t.peer * GLOO_HIP_NUM_SLOTS + t.slot,
                                copySignalGrid(bytes, copyBlocksFor(t.peer))};
           }
@@ -659,7 +729,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
           if (t.length)
             GLOO_AMD_HIP_CHECK(hipMemcpyAsync(sendDst(t), sendSrc(t), t.length * es_, hipMemcpyDeviceToDevice, a));
           if (deviceSignal_) {
-            GLOO_AMD_HIP_CHECK(launchSignal(ctx_->counterDevicePtr(inst_, me, t.peer, t.slot), seqOf(k, r, graph),
+            GLOO_AMD_HIP_CHECK(launchSignal(sigFlag(t.peer, t.slot), seqOf(k, r, graph),
                                             epoch, a));
           } else {
             enqueueBump(a, ctx_->counter(inst_, me, t.peer, t.slot));
@@ -710,7 +780,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
       std::vector<const uint64_t*> flags;
       std::vector<Seq> targets;
       for (; j < steps.size() && isWaitKind(steps[j].kind); j++) {
-        flags.push_back(ctx_->counterDevicePtr(inst_, steps[j].peer, me, steps[j].slot));
+        flags.push_back(waitFlag(steps[j].peer, steps[j].slot));
         targets.push_back(seqOf(j, r, graph));
       }
       GLOO_AMD_HIP_CHECK(launchWaitMulti(flags.data(), targets.data(), (int)flags.size(), epoch, timeoutTicks,
@@ -746,18 +816,18 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
           Seq wt;
           if (isWait) {
             wt = seqOf(i, r, graph);
-            wf = ctx_->counterDevicePtr(inst_, s.peer, me, s.slot);
+            wf = waitFlag(s.peer, s.slot);
           }
           uint64_t* sf = nullptr;
           Seq sv;
           size_t consumed = isWait ? 2 : 1;
           if (t->kind == GLOO_HIP_STEP_SEND) {
             sv = seqOf(isWait ? i + 1 : i, r, graph);
-            sf = ctx_->counterDevicePtr(inst_, me, t->peer, t->slot);
+            sf = sigFlag(t->peer, t->slot);
           } else if (isWait && i + 2 < steps.size() && steps[i + 2].kind == GLOO_HIP_STEP_NOTIFY) {
             const Step& nt = steps[i + 2];
             sv = seqOf(i + 2, r, graph);
-            sf = ctx_->counterDevicePtr(inst_, me, nt.peer, nt.slot);
+            sf = sigFlag(nt.peer, nt.slot);
             consumed = 3;
           }
           checkRc(launchFusedSmall(op, dtype_, dst, src, t->length, wf, wt, timeoutTicks, ctx_->errorWordDevicePtr(me),
@@ -776,7 +846,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         const char* src = sendSrc(s);
         if (kernelCopy_) {
           const unsigned grid = copySignalGrid(s.length * es_, copyBlocksFor(s.peer));
-          checkRc(launchCopySignal(dst, src, s.length * es_, ctx_->counterDevicePtr(inst_, me, s.peer, s.slot),
+          checkRc(launchCopySignal(dst, src, s.length * es_, sigFlag(s.peer, s.slot),
                                    seqOf(i, r, graph), ticket_ + (size_t)s.peer * GLOO_HIP_NUM_SLOTS + s.slot, epoch,
                                    grid, stream_),
                   "copy_signal_kernel");
@@ -789,7 +859,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
       case GLOO_HIP_STEP_WAIT_RECV:
       case GLOO_HIP_STEP_WAIT_NOTIFY: {
         if (deviceSignal_) {
-          GLOO_AMD_HIP_CHECK(launchWait(ctx_->counterDevicePtr(inst_, s.peer, me, s.slot), seqOf(i, r, graph), epoch,
+          GLOO_AMD_HIP_CHECK(launchWait(waitFlag(s.peer, s.slot), seqOf(i, r, graph), epoch,
                                         timeoutTicks, ctx_->errorWordDevicePtr(me), stream_));
         } else {
           waitCounter(ctx_->counter(inst_, s.peer, me, s.slot), seqOf(i, r, false).base, s.peer, s.slot);

@@ -114,6 +114,12 @@ class PlanExecutor {
   void tryCapture(uint64_t r);
   void dropGraph();
   Seq seqOf(size_t step, uint64_t r, bool graph) const;
+  // Where a device-side signal to `peer` lands / a device-side wait for
+  // `peer` polls: the receiver's device mailbox when both ends have one,
+  // else the counter in the node's host control block.
+  bool mailboxWith(int peer) const;
+  uint64_t* sigFlag(int peer, int slot);
+  uint64_t* waitFlag(int peer, int slot);
   hipStream_t auxStream(size_t k);
   hipEvent_t forkEvent(size_t k);
   char* userPtr(int j) const { return static_cast<char*>(ptrs_[j]); }
@@ -161,6 +167,9 @@ class PlanExecutor {
   uint64_t stableRuns_ = 0;    // runs since the buffers last changed
   std::string graphError_;
   bool deviceSignal_ = false;  // stream-ordered signal/wait kernels instead of host waits
+  uint64_t* mailbox_ = nullptr;           // this rank's incoming counters, (sender, slot), fine-grained HBM
+  std::vector<uint64_t*> peerMailbox_;    // peers' mailboxes (nullptr: that channel uses the host block)
+  std::vector<bool> peerMailboxIpc_;
   bool fineArena_ = false;     // inbox arena in fine-grained (cross-device coherent) memory
   bool kernelCopy_ = false;    // SEND = copy_signal_kernel instead of hipMemcpyAsync + signal
   unsigned copyBlocks_ = 64;        // per copy to a peer on another GPU (xGMI)

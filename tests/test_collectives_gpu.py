@@ -176,6 +176,8 @@ np.save(out, buf.cpu().numpy().view(np.float32))
     ("ring_chunked", 3, {"GLOO_AMD_SIGNAL": "host"}),         # host waits across processes
     ("halving_doubling", 4, {"GLOO_AMD_ARENA": "fine"}),      # fine-grained inboxes over IPC
     ("ring_chunked", 8, {"GLOO_AMD_ARENA": "fine"}),
+    ("ring_chunked", 4, {"GLOO_AMD_MAILBOX": "0"}),            # device signals through the host control block
+    ("halving_doubling", 5, {"GLOO_AMD_MAILBOX": "0", "GLOO_AMD_MESH": "0"}),
 ])
 def test_processes_ipc(torch, algo, P, env):
     """Ranks as processes: inbox arenas exchanged as HIP IPC handles through a
