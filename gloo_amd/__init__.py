@@ -289,15 +289,15 @@ class Algorithm:
 
     def mode(self):
         """How run() executes: device-side signalling, fine-grained inboxes,
-        kernel copy engine, hipGraph replay; 'graph_error' says why capture
-        was abandoned (empty if it was not)."""
+        kernel copy engine, hipGraph replay, one-launch plan interpreter;
+        'graph_error' says why capture was abandoned (empty if it was not)."""
         out = (ctypes.c_int * 4)()
         _check(lib.gloo_hip_algorithm_mode(self._h, out))
         err = lib.gloo_hip_last_error()
         err = err.decode() if isinstance(err, bytes) else (err or "")
         return {"device_signal": bool(out[0]), "fine_arena": out[1] == 1,
                 "host_arena": out[1] == 2, "kernel_copy": bool(out[2]),
-                "graph": bool(out[3]),
+                "graph": out[3] == 1, "interp": out[3] == 2,
                 "graph_error": err[len("graph capture abandoned: "):]
                 if err.startswith("graph capture abandoned: ") else ""}
 

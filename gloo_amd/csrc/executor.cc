@@ -84,6 +84,15 @@ size_t fuseBytes() {
   return v;
 }
 
+// Largest message of a plan the one-launch interpreter runs (0: never).
+size_t interpBytes() {
+  static const size_t v = [] {
+    const char* e = std::getenv("GLOO_AMD_INTERP_BYTES");
+    return e ? (size_t)std::strtoull(e, nullptr, 10) : fuseBytes();
+  }();
+  return v;
+}
+
 std::set<std::pair<const Context*, uint64_t>>& liveInstances() {
   static std::set<std::pair<const Context*, uint64_t>> s;
   return s;
@@ -176,6 +185,7 @@ void PlanExecutor::setBuffers(const std::vector<void*>& inputs, const std::vecto
   if (inputs != inputs_ || outputs != ptrs_) {
     dropGraph();
     stableRuns_ = 0;
+    interpDirty_ = true;
   }
   inputs_ = inputs;
   ptrs_ = outputs;
@@ -480,6 +490,9 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
           s.length * es_ > fuseBytes())
         unfused = true;
     graphMode_ = gmode == "1" || (gmode == "auto" && unfused);
+    const char* im = std::getenv("GLOO_AMD_INTERP");
+    interpMode_ = !(im && std::string(im) == "0") && gmode != "1" && interpBytes() > 0;
+    if (interpMode_) GLOO_AMD_HIP_ALLOC(hipMalloc(&interpSteps_, kInterpMaxSteps * sizeof(InterpStep)));
     if (graphMode_) {
       GLOO_AMD_HIP_ALLOC(hipMalloc(&epoch_, sizeof(uint64_t)));
       GLOO_AMD_HIP_CHECK(hipMemset(epoch_, 0, sizeof(uint64_t)));
@@ -512,6 +525,7 @@ PlanExecutor::~PlanExecutor() {
     for (hipStream_t a : aux_) (void)hipStreamDestroy(a);
     if (graphExec_) (void)hipGraphExecDestroy(graphExec_);
     if (epoch_) GLOO_AMD_HIP_RELEASE(hipFree(epoch_));
+    if (interpSteps_) GLOO_AMD_HIP_RELEASE(hipFree(interpSteps_));
     if (ticket_) GLOO_AMD_HIP_RELEASE(hipFree(ticket_));
     for (char* p : outStage_)
       if (p) GLOO_AMD_HIP_RELEASE(hipFree(p));
@@ -600,10 +614,24 @@ void PlanExecutor::run() {
   reduceSeconds_ = reduceBytes_ = 0;
   reduceCount_ = 0;
   const uint64_t r = runs_ + 1;
+  const bool interp = deviceSignal_ && interpMode_ && !profiling_;
+  if (interp && interpDirty_) buildInterp();
   const bool graphable = deviceSignal_ && graphMode_ && !profiling_;
-  if (graphable && !graphExec_ && stableRuns_ >= 1) tryCapture(r);
-  if (graphable && graphExec_) {
-    GLOO_AMD_HIP_CHECK(hipGraphLaunch(graphExec_, stream_));
+  if (interp && interpCount_ > 0) {
+    const uint64_t timeoutTicks = (uint64_t)ctx_->timeout().count() * 100000ull;  // 100 MHz realtime clock
+    checkRc(launchPlanInterp(op_, dtype_, interpSteps_, interpCount_, r, timeoutTicks, ctx_->errorWordDevicePtr(me),
+                             stream_),
+            "plan interpreter");
+  } else if (graphable && (graphExec_ || stableRuns_ >= 1)) {
+    if (!graphExec_) tryCapture(r);  // sets the device epoch to r - 1
+    if (graphExec_) {
+      // a run enqueued eagerly since the last replay left the epoch behind
+      if (epochRuns_ != r - 1) GLOO_AMD_HIP_CHECK(launchEpochSet(epoch_, r - 1, stream_));
+      GLOO_AMD_HIP_CHECK(hipGraphLaunch(graphExec_, stream_));
+      epochRuns_ = r;
+    } else {
+      enqueue(r, false);
+    }
   } else {
     enqueue(r, false);
   }
@@ -630,6 +658,7 @@ void PlanExecutor::tryCapture(uint64_t r) {
   // from it.  Capture failures are not fatal: the plan keeps being enqueued
   // eagerly (graphError() says why).
   GLOO_AMD_HIP_CHECK(launchEpochSet(epoch_, r - 1, stream_));
+  epochRuns_ = r - 1;
   GLOO_AMD_HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   hipGraph_t g = nullptr;
   try {
@@ -652,6 +681,133 @@ void PlanExecutor::tryCapture(uint64_t r) {
     graphError_ = hipGetErrorString(e);
     (void)hipGetLastError();
   }
+}
+
+void PlanExecutor::buildInterp() {
+  interpDirty_ = false;
+  interpCount_ = 0;
+  if (anyRemote_) return;
+  const size_t limit = interpBytes();
+  auto userOrArena = [&](bool arena) { return arena ? arena_ : userPtr(0); };
+  auto sendSrc = [&](const Step& t) -> const char* {
+    const char* base = t.flags & GLOO_HIP_SRC_ARENA ? arena_
+                       : t.flags & GLOO_HIP_FROM_INPUTS ? static_cast<const char*>(inputs_.at(0))
+                                                        : userPtr(0);
+    return base + t.src_off * es_;
+  };
+  std::vector<InterpStep> v;
+  auto push = [&](int kind) -> InterpStep& {
+    v.emplace_back();
+    InterpStep& t = v.back();
+    std::memset(&t, 0, sizeof t);
+    t.kind = kind;
+    return t;
+  };
+  auto withSeq = [&](InterpStep& t, size_t i, uint64_t* flag) {
+    t.flag = flag;
+    t.base = stepSeq_[i].base;
+    t.perRun = stepSeq_[i].perRun;
+  };
+  // dst = src[0] op src[1] ... (left fold); a copy for one source
+  auto fold = [&](char* dst, const std::vector<const char*>& srcs, size_t n, int mode) {
+    InterpStep& t = push(kInterpFold);
+    t.dst = dst;
+    t.nsrc = (int)srcs.size();
+    t.mode = mode;
+    for (size_t k = 0; k < srcs.size(); k++) t.src[k] = srcs[k];
+    t.n = n;
+  };
+  // false: overlapping operands (a memmove), not an interpreter shape
+  auto copy = [&](char* dst, const char* src, size_t bytes) {
+    if (dst == src || bytes == 0) return true;
+    if (dst < src + bytes && src < dst + bytes) return false;
+    InterpStep& t = push(kInterpCopy);
+    t.dst = dst;
+    t.src[0] = src;
+    t.n = bytes;
+    return true;
+  };
+  std::vector<const char*> foldSrcs;
+  const std::vector<Step>& steps = plan_.steps;
+  for (size_t i = 0; i < steps.size(); i++) {
+    const Step& s = steps[i];
+    const size_t bytes = s.length * es_;
+    if (bytes > limit) return;
+    switch (s.kind) {
+      case GLOO_HIP_STEP_DECL_RECV:
+      case GLOO_HIP_STEP_WAIT_SEND:
+        break;
+      case GLOO_HIP_STEP_SEND: {
+        InterpStep& t = push(kInterpSend);
+        t.dst = peers_[s.peer].base + (remoteRegion_.at({s.peer, s.slot}) + s.dst_off) * es_;
+        t.src[0] = sendSrc(s);
+        t.n = bytes;
+        withSeq(t, i, sigFlag(s.peer, s.slot));
+        break;
+      }
+      case GLOO_HIP_STEP_NOTIFY:
+        withSeq(push(kInterpSignal), i, sigFlag(s.peer, s.slot));
+        break;
+      case GLOO_HIP_STEP_WAIT_RECV:
+      case GLOO_HIP_STEP_WAIT_NOTIFY:
+        withSeq(push(kInterpWait), i, waitFlag(s.peer, s.slot));
+        break;
+      case GLOO_HIP_STEP_REDUCE: {  // out = (in | out) op inbox
+        const char* a = (s.flags & GLOO_HIP_FROM_INPUTS ? static_cast<const char*>(inputs_.at(0))
+                                                         : static_cast<const char*>(userPtr(0))) +
+                        s.dst_off * es_;
+        fold(userPtr(0) + s.dst_off * es_, {a, arena_ + s.src_off * es_}, s.length, 0);
+        break;
+      }
+      case GLOO_HIP_STEP_COPY:
+        if (!copy(userOrArena(s.flags & GLOO_HIP_DST_ARENA) + s.dst_off * es_,
+                  userOrArena(s.flags & GLOO_HIP_SRC_ARENA) + s.src_off * es_, bytes))
+          return;
+        break;
+      case GLOO_HIP_STEP_LOCAL_REDUCE: {  // as enqueue(): chained folds of <= GLOO_HIP_MAX_SRCS sources
+        const size_t off = s.dst_off * es_;
+        const std::vector<void*>& from = s.flags & GLOO_HIP_FROM_INPUTS ? inputs_ : ptrs_;
+        char* out0 = userPtr(0) + off;
+        if (from.size() == 1) {
+          if (!copy(out0, static_cast<const char*>(from[0]) + off, bytes)) return;
+          break;
+        }
+        std::vector<const char*> srcs;
+        size_t j = 0;
+        for (; j < from.size() && srcs.size() < GLOO_HIP_MAX_SRCS; j++)
+          srcs.push_back(static_cast<const char*>(from[j]) + off);
+        fold(out0, srcs, s.length, 0);
+        while (j < from.size()) {
+          srcs.assign(1, out0);
+          for (; j < from.size() && srcs.size() < GLOO_HIP_MAX_SRCS; j++)
+            srcs.push_back(static_cast<const char*>(from[j]) + off);
+          fold(out0, srcs, s.length, 0);
+        }
+        break;
+      }
+      case GLOO_HIP_STEP_LOCAL_BCAST:
+        for (size_t j = 1; j < ptrs_.size(); j++)
+          if (!copy(userPtr(j) + s.dst_off * es_, userPtr(0) + s.dst_off * es_, bytes)) return;
+        break;
+      case GLOO_HIP_STEP_FOLD_SRC:
+        foldSrcs.push_back(sendSrc(s));
+        break;
+      case GLOO_HIP_STEP_FOLD:
+        GLOO_AMD_ENFORCE(!foldSrcs.empty() && foldSrcs.size() <= GLOO_HIP_MAX_SRCS, "bad fold");
+        fold(userOrArena(s.flags & GLOO_HIP_DST_ARENA) + s.dst_off * es_, foldSrcs, s.length,
+             s.flags & GLOO_HIP_FOLD_TREE ? 2 : s.flags & GLOO_HIP_FOLD_REVERSE ? 1 : 0);
+        foldSrcs.clear();
+        break;
+      default:
+        return;
+    }
+    if (v.size() > (size_t)kInterpMaxSteps) return;
+  }
+  if (v.empty()) return;
+  // an earlier launch may still read the list
+  GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+  GLOO_AMD_HIP_CHECK(hipMemcpy(interpSteps_, v.data(), v.size() * sizeof(InterpStep), hipMemcpyHostToDevice));
+  interpCount_ = (int)v.size();
 }
 
 void PlanExecutor::enqueue(uint64_t r, bool graph) {

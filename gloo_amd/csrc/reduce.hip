@@ -434,6 +434,175 @@ int launch_fused(int op, void* dst, const void* src, size_t n, const uint64_t* w
 }
 
 // ---------------------------------------------------------------------------
+// One-launch plan interpreter (signal.h InterpStep): one workgroup walks the
+// whole step list of a small plan.  Visibility follows the fused step's
+// protocol: every data step ends with each wave draining its memory
+// operations (vmcnt 0) and a workgroup barrier, so a following send / signal
+// can publish them with ONE lane's system-scope release + flag store; a wait
+// has ONE lane poll relaxed, then ONE system-scope acquire, then a barrier
+// before any lane reads the inbox.
+// ---------------------------------------------------------------------------
+constexpr int kInterpBlock = 512;
+// Packets per lane in flight per pass: a pass costs ONE memory latency (all
+// of its loads issue before the first use), so a 32 KiB copy is one pass.
+constexpr int kInterpCopyUnroll = 4;
+constexpr int kInterpFoldUnroll = 2;
+
+__device__ __forceinline__ void interp_copy(char* dst, const char* src, uint64_t n) {
+  const uint64_t t = threadIdx.x;
+  uint64_t done = 0;
+  if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
+    const uint64_t nv = n / 16;
+    const u32x4* s = reinterpret_cast<const u32x4*>(src);
+    u32x4* d = reinterpret_cast<u32x4*>(dst);
+    for (uint64_t b = 0; b < nv; b += (uint64_t)kInterpBlock * kInterpCopyUnroll) {
+      u32x4 v[kInterpCopyUnroll];
+#pragma unroll
+      for (int u = 0; u < kInterpCopyUnroll; u++) {
+        const uint64_t i = b + (uint64_t)u * kInterpBlock + t;
+        if (i < nv) v[u] = s[i];
+      }
+#pragma unroll
+      for (int u = 0; u < kInterpCopyUnroll; u++) {
+        const uint64_t i = b + (uint64_t)u * kInterpBlock + t;
+        if (i < nv) d[i] = v[u];
+      }
+    }
+    done = nv * 16;
+  }
+  for (uint64_t i = done + t; i < n; i += kInterpBlock) dst[i] = src[i];
+}
+
+// dst[i] = fold over the step's sources (mode as launchFold) for n elements:
+// 16-byte packets when every operand is 16-byte aligned, elements after.
+template <class Tr, int OP>
+__device__ __forceinline__ void interp_fold(const InterpStep& st) {
+  using S = typename Tr::Storage;
+  constexpr int kV = 16 / sizeof(S);
+  // byte lanes unpack 16 per packet: one packet per lane keeps them in VGPRs
+  constexpr int kU = sizeof(S) == 1 ? 1 : kInterpFoldUnroll;
+  const int ns = st.nsrc, mode = st.mode;
+  const uint64_t n = st.n;
+  const uint64_t t = threadIdx.x;
+  const char* src[GLOO_HIP_MAX_SRCS];
+  uintptr_t align = (uintptr_t)st.dst;
+#pragma unroll
+  for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++) {
+    src[j] = j < ns ? st.src[j] : nullptr;
+    align |= (uintptr_t)src[j];
+  }
+  const uint64_t nv = (align & 15) ? 0 : n / kV;
+  u32x4* dv = reinterpret_cast<u32x4*>(st.dst);
+  for (uint64_t b = 0; b < nv; b += (uint64_t)kInterpBlock * kU) {
+    u32x4 v[GLOO_HIP_MAX_SRCS][kU];
+#pragma unroll
+    for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
+      if (j < ns) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+          const uint64_t i = b + (uint64_t)u * kInterpBlock + t;
+          v[j][u] = i < nv ? reinterpret_cast<const u32x4*>(src[j])[i] : u32x4{0, 0, 0, 0};
+        }
+      }
+    if (mode == 2) {
+#pragma unroll
+      for (int w = GLOO_HIP_MAX_SRCS; w > 1; w >>= 1)
+        if (w <= ns) {
+#pragma unroll
+          for (int j = 0; j < w / 2; j++)
+#pragma unroll
+            for (int u = 0; u < kU; u++) v[j][u] = apply_packet<Tr, OP>(v[2 * j][u], v[2 * j + 1][u]);
+        }
+    } else {
+#pragma unroll
+      for (int j = 1; j < GLOO_HIP_MAX_SRCS; j++)
+        if (j < ns) {
+#pragma unroll
+          for (int u = 0; u < kU; u++)
+            v[0][u] = mode == 1 ? apply_packet<Tr, OP>(v[j][u], v[0][u]) : apply_packet<Tr, OP>(v[0][u], v[j][u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const uint64_t i = b + (uint64_t)u * kInterpBlock + t;
+      if (i < nv) dv[i] = v[0][u];
+    }
+  }
+  S* dst = reinterpret_cast<S*>(st.dst);
+  for (uint64_t i = nv * kV + t; i < n; i += kInterpBlock) {
+    S e[GLOO_HIP_MAX_SRCS];
+#pragma unroll
+    for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
+      if (j < ns) e[j] = reinterpret_cast<const S*>(src[j])[i];
+    if (mode == 2) {
+      dst[i] = tree_fold<Tr, OP>(e, ns);
+    } else {
+      S acc = e[0];
+#pragma unroll
+      for (int j = 1; j < GLOO_HIP_MAX_SRCS; j++)
+        if (j < ns) acc = mode == 1 ? apply<Tr, OP>(e[j], acc) : apply<Tr, OP>(acc, e[j]);
+      dst[i] = acc;
+    }
+  }
+}
+
+template <class Tr, int OP>
+__global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpStep* steps, int nsteps, uint64_t run,
+                                                                   uint64_t timeoutTicks, uint32_t* err) {
+  __shared__ int ok;
+  for (int k = 0; k < nsteps; k++) {
+    const InterpStep& st = steps[k];
+    const int kind = st.kind;
+    const uint64_t value = st.base + run * st.perRun;
+    if (kind == kInterpWait) {
+      if (threadIdx.x == 0) {
+        int good = 1;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        // signed difference: a target below the counter is already met
+        while ((int64_t)(__hip_atomic_load(st.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - value) < 0) {
+          __builtin_amdgcn_s_sleep(2);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > timeoutTicks) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            good = 0;
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        ok = good;
+      }
+      __syncthreads();
+      if (!ok) return;  // timed out: no further work, no further signal
+      continue;
+    }
+    if (kind == kInterpCopy || kind == kInterpSend) {
+      interp_copy(st.dst, st.src[0], st.n);
+    } else if (kind == kInterpFold) {
+      interp_fold<Tr, OP>(st);
+    }
+    // every wave's writes of this step are performed before the barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if ((kind == kInterpSend || kind == kInterpSignal) && threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __hip_atomic_store(st.flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+template <class Tr>
+int launch_interp(int op, const InterpStep* steps, int nsteps, uint64_t run, uint64_t tt, uint32_t* err,
+                  hipStream_t s) {
+  switch (op) {
+    case GLOO_HIP_SUM: plan_interp_kernel<Tr, GLOO_HIP_SUM><<<1, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
+    case GLOO_HIP_PRODUCT: plan_interp_kernel<Tr, GLOO_HIP_PRODUCT><<<1, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
+    case GLOO_HIP_MAX: plan_interp_kernel<Tr, GLOO_HIP_MAX><<<1, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
+    case GLOO_HIP_MIN: plan_interp_kernel<Tr, GLOO_HIP_MIN><<<1, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
+    default: return GLOO_HIP_EINVAL_OP;
+  }
+  return GLOO_HIP_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Peer copy with the arrival signal fused in: the SEND of a plan as one
 // launch.  A capped grid walks 16 KiB tiles (512 lanes x 2 x 16 B): loads
 // from local HBM (`nt`, any misalignment via soffset), 16-B stores into the
@@ -718,6 +887,28 @@ int launchFusedSmall(int op, int dtype, void* dst, const void* src, size_t n, co
   }
   if (rc != GLOO_HIP_OK) return set_error(rc, "fused step: bad op");
   return check_launch("fused_small_kernel");
+}
+
+int launchPlanInterp(int op, int dtype, const InterpStep* steps, int nsteps, uint64_t run, uint64_t tt,
+                     uint32_t* err, hipStream_t s) {
+  static_assert(GLOO_HIP_MAX_SRCS <= 8, "InterpStep holds 8 sources");
+  if (nsteps < 0 || nsteps > kInterpMaxSteps) return set_error(GLOO_HIP_EINVAL_ARG, "interpreter: bad step count");
+  int rc;
+  switch (dtype) {
+    case GLOO_HIP_I8: rc = launch_interp<TrI8>(op, steps, nsteps, run, tt, err, s); break;
+    case GLOO_HIP_U8: rc = launch_interp<TrU8>(op, steps, nsteps, run, tt, err, s); break;
+    case GLOO_HIP_I32: rc = launch_interp<TrI32>(op, steps, nsteps, run, tt, err, s); break;
+    case GLOO_HIP_U32: rc = launch_interp<TrU32>(op, steps, nsteps, run, tt, err, s); break;
+    case GLOO_HIP_I64: rc = launch_interp<TrI64>(op, steps, nsteps, run, tt, err, s); break;
+    case GLOO_HIP_U64: rc = launch_interp<TrU64>(op, steps, nsteps, run, tt, err, s); break;
+    case GLOO_HIP_F16: rc = launch_interp<TrF16>(op, steps, nsteps, run, tt, err, s); break;
+    case GLOO_HIP_BF16: rc = launch_interp<TrBF16>(op, steps, nsteps, run, tt, err, s); break;
+    case GLOO_HIP_F32: rc = launch_interp<TrF32>(op, steps, nsteps, run, tt, err, s); break;
+    case GLOO_HIP_F64: rc = launch_interp<TrF64>(op, steps, nsteps, run, tt, err, s); break;
+    default: return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
+  }
+  if (rc != GLOO_HIP_OK) return set_error(rc, "interpreter: bad op");
+  return check_launch("plan_interp_kernel");
 }
 
 }  // namespace gloo_amd

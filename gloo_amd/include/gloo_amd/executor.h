@@ -44,6 +44,13 @@
 // (default), or GLOO_AMD_COPY=kernel: copy_signal_kernel, one launch that
 // copies with GLOO_AMD_COPY_BLOCKS workgroups (default 64) and publishes the
 // arrival itself.
+//
+// One-launch interpreter (device signalling, GLOO_AMD_INTERP, default on):
+// when every message of the plan is at most GLOO_AMD_INTERP_BYTES (default
+// the fuse limit, 64 KiB) and no operand lives on another GPU of this
+// process, the steps are resolved once into a device-resident InterpStep
+// list (signal.h) and every run() is ONE one-workgroup launch walking it —
+// a small allreduce costs its cross-rank hops, not a kernel boundary each.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -89,6 +96,8 @@ class PlanExecutor {
   bool kernelCopy() const { return kernelCopy_; }
   // True once run() replays a captured hipGraph.
   bool graphed() const { return graphExec_ != nullptr; }
+  // True once run() executes the plan as one interpreter launch.
+  bool interpreted() const { return interpMode_ && interpCount_ > 0; }
   // Why graph capture was abandoned (empty if it was not).
   const std::string& graphError() const { return graphError_; }
   // Host time spent blocked in WAIT steps during the last run(), seconds.
@@ -113,6 +122,9 @@ class PlanExecutor {
   void enqueue(uint64_t r, bool graph);
   void tryCapture(uint64_t r);
   void dropGraph();
+  // Resolve the plan into interpSteps_ for the current buffers; interpCount_
+  // = 0 if some step is not an interpreter shape (the plan runs enqueued).
+  void buildInterp();
   Seq seqOf(size_t step, uint64_t r, bool graph) const;
   // Where a device-side signal to `peer` lands / a device-side wait for
   // `peer` polls: the receiver's device mailbox when both ends have one,
@@ -164,9 +176,14 @@ class PlanExecutor {
   uint64_t* epoch_ = nullptr;  // device: the run being executed (graph replay)
   hipGraphExec_t graphExec_ = nullptr;
   bool graphMode_ = false;
+  uint64_t epochRuns_ = 0;     // the device epoch once the work queued so far has run
   uint64_t stableRuns_ = 0;    // runs since the buffers last changed
   std::string graphError_;
   bool deviceSignal_ = false;  // stream-ordered signal/wait kernels instead of host waits
+  bool interpMode_ = false;            // the interpreter may run this plan
+  bool interpDirty_ = true;            // interpSteps_ predates the current buffers
+  InterpStep* interpSteps_ = nullptr;  // device copy of the resolved steps
+  int interpCount_ = 0;
   uint64_t* mailbox_ = nullptr;           // this rank's incoming counters, (sender, slot), fine-grained HBM
   std::vector<uint64_t*> peerMailbox_;    // peers' mailboxes (nullptr: that channel uses the host block)
   std::vector<bool> peerMailboxIpc_;

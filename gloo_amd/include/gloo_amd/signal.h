@@ -75,6 +75,30 @@ constexpr int kMaxWaitEntries = 16;
 hipError_t launchWaitMulti(const uint64_t* const* flags, const Seq* targets, int n, const uint64_t* epoch,
                            uint64_t timeoutTicks, uint32_t* err, hipStream_t stream);
 
+// One-launch plan interpreter (reduce.hip) for plans whose every message is
+// small: ONE workgroup walks a precompiled step list — copies, sends (copy,
+// drain, one system-scope release, flag store), signals, waits (one lane
+// polls, one acquire, barrier) and folds — with a workgroup barrier between
+// steps.  A small allreduce becomes a single kernel: its device time is the
+// cross-rank hops, not the kernel boundaries between them.  Sequence values
+// are base + run * perRun (the eager numbering).  A wait that times out sets
+// *err and ends the launch.
+enum { kInterpCopy = 0, kInterpSend = 1, kInterpSignal = 2, kInterpWait = 3, kInterpFold = 4 };
+struct InterpStep {
+  int32_t kind;       // kInterp*
+  int32_t mode;       // FOLD: 0 left fold, 1 reverse (acc = s op acc), 2 balanced tree
+  int32_t nsrc;       // FOLD: sources
+  int32_t pad;
+  uint64_t* flag;     // SEND / SIGNAL: the flag written; WAIT: the flag polled
+  uint64_t base, perRun;
+  char* dst;
+  const char* src[8]; // COPY / SEND: src[0]; FOLD: the sources in order
+  uint64_t n;         // COPY / SEND: bytes; FOLD: elements
+};
+constexpr int kInterpMaxSteps = 512;
+int launchPlanInterp(int op, int dtype, const InterpStep* steps, int nsteps, uint64_t run, uint64_t timeoutTicks,
+                     uint32_t* err, hipStream_t stream);
+
 // Multi-source fold in one pass, k <= GLOO_HIP_MAX_SRCS.  mode 0: left fold
 // acc = acc op s_j; 1: reverse, acc = s_j op acc; 2: balanced pairwise tree
 // over the sources in order (k a power of two).  Returns a gloo_hip status.

@@ -548,6 +548,56 @@ def test_processes_graph_replay(torch, golden_sched, case, env, graph):
         assert modes[-1]["graph_error"] == "", modes[-1]
 
 
+@pytest.mark.parametrize("case,env,interp", [
+    ("halving_doubling/sum/f32/P5/k1/n10007", {}, True),
+    ("halving_doubling/sum/f32/P8/k1/n1000", {}, True),             # tree fold
+    ("halving_doubling/sum/f64/P7/k1/n3001", {}, True),             # pairwise temporaries
+    ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_MAILBOX": "0"}, True),  # host-block flags
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_MESH": "0"}, True),     # the reference's step list
+    ("ring_chunked/sum/f32/P8/k1/n10007", {}, True),
+    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_RING_MESH": "0"}, True),    # chunked ring: many hops
+    ("ring_chunked/max/f32/P5/k1/n999", {}, True),
+    ("ring_chunked/product/f32/P3/k1/n777", {}, True),
+    ("reduce_scatter/max/bf16/P8/n4096", {}, True),
+    ("reduce_scatter/sum/f32/P8/n10007", {}, True),                 # previous-run credits
+    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_INTERP_BYTES": "1000000000"}, True),
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_INTERP": "0"}, False),
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_INTERP_BYTES": "1024"}, False),
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, False),
+    ("reduce_scatter/sum/f32/P5/n100", {"GLOO_AMD_SIGNAL": "host"}, False),
+])
+def test_processes_interp(torch, golden_sched, case, env, interp):
+    """One-launch plan interpreter: every run() of a small plan is ONE
+    one-workgroup kernel walking the resolved step list (waits, sends,
+    signals, folds, copies).  Five runs with the buffer reset to the input
+    each time, every one byte for byte the reference's output; interp=False
+    cases check the knobs and shapes that keep the enqueued path."""
+    algo = case.split("/")[0]
+    P = int(case.split("/")[3][1:])
+    runs = 5
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(GRAPH_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), case,
+                                   os.path.join(d, f"o{r}"), str(runs)], env=e, stdout=subprocess.PIPE, text=True)
+                 for r in range(P)]
+        outs = [p.communicate(timeout=300)[0] for p in procs]
+        assert [p.returncode for p in procs] == [0] * P
+        ys = [[np.load(os.path.join(d, f"o{r}.{it}.npy")) for it in range(runs)] for r in range(P)]
+    want = golden_sched[case + "/out"]
+    for it in range(runs):
+        if algo == "reduce_scatter":
+            recv = golden_sched[case + "/recv"]
+            assert same_bytes(np.concatenate([ys[r][it][:recv[r]] for r in range(P)]), want), it
+        else:
+            for r in range(P):
+                assert same_bytes(ys[r][it], want), (r, it)
+    for r in range(P):
+        modes = json.loads(outs[r].split("MODES", 1)[1])
+        assert [m["interp"] for m in modes] == [interp] * runs, modes
+
+
 NEW_STYLE_GRAPH_WORKER = r'''
 import os, sys, numpy as np
 sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
@@ -570,16 +620,18 @@ np.save(out, np.array(res))
 '''
 
 
-def test_processes_new_style_rebinding_graph(torch):
+@pytest.mark.parametrize("env", [{}, {"GLOO_AMD_INTERP_BYTES": str(1 << 24)}])
+def test_processes_new_style_rebinding_graph(torch, env):
     """Function-style allreduce (1.6 MB per rank: unfused steps, so the plan
     is captured) called with alternating buffer sets: every rebinding drops
-    the captured graph, the next steady call re-captures it.
+    the captured graph, the next steady call re-captures it.  With the
+    interpreter limit raised, every rebinding re-resolves its step list.
     Each call sums (rank + 1) * (it + 1) over the ranks exactly."""
     P = 4
     with tempfile.TemporaryDirectory() as d:
         w = os.path.join(d, "w.py")
         open(w, "w").write(NEW_STYLE_GRAPH_WORKER)
-        e = dict(os.environ, GLOO_AMD_ROOT=ROOT)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
         procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"),
                                    os.path.join(d, f"o{r}.npy")], env=e) for r in range(P)]
         assert [p.wait(timeout=300) for p in procs] == [0] * P
