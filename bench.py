@@ -352,10 +352,11 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                         t0 = time.perf_counter()
                         a2.run()
                         ts.append(time.perf_counter() - t0)
-                    g = a2.mode()["graph"]
+                    md = a2.mode()
                     a2.close()
                     ctx2.close()
-                    hd.append({"bytes": nbytes, "us": [round(t * 1e6, 1) for t in ts], "graph": g})
+                    hd.append({"bytes": nbytes, "us": [round(t * 1e6, 1) for t in ts], "graph": md["graph"],
+                               "interp": md["interp"]})
                 except Exception as e:  # noqa: BLE001
                     hd.append({"bytes": nbytes, "error": repr(e)})
             return hd
@@ -368,7 +369,8 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                 continue
             per = sorted(max(h[i]["us"][k] for h in hd_all) for k in range(iters))
             summary.append({"bytes": nbytes, "us_p50": per[iters // 2], "us_max": per[-1],
-                            "graph": all(h[i]["graph"] for h in hd_all),
+                            "launch": "interp" if all(h[i]["interp"] for h in hd_all)
+                            else "graph" if all(h[i]["graph"] for h in hd_all) else "eager",
                             "busbw_gib_s": round(2 * (world - 1) / world * nbytes / (per[iters // 2] / 1e6) / GIB,
                                                  3)})
         return summary
@@ -377,11 +379,12 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     # reference's halving/doubling exchange (GLOO_AMD_MESH=0)
     hd_variants = {"mesh": {},
                    "mesh_memcpy_forked": {"GLOO_AMD_COPY": "memcpy"},
-                   "mesh_eager": {"GLOO_AMD_GRAPH": "0"},
+                   "mesh_eager": {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_INTERP": "0"},
+                   "mesh_no_interp": {"GLOO_AMD_INTERP": "0"},
                    "mesh_host_block_flags": {"GLOO_AMD_MAILBOX": "0"},
                    "reference_route": {"GLOO_AMD_MESH": "0"},
                    "reference_route_kernel_copy": {"GLOO_AMD_MESH": "0", "GLOO_AMD_COPY": "kernel"},
-                   "reference_route_eager": {"GLOO_AMD_MESH": "0", "GLOO_AMD_GRAPH": "0"}}
+                   "reference_route_eager": {"GLOO_AMD_MESH": "0", "GLOO_AMD_GRAPH": "0", "GLOO_AMD_INTERP": "0"}}
     hd_summary = {}
     partial["halving_doubling"] = hd_summary
     for k, v in hd_variants.items():
