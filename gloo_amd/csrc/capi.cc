@@ -176,7 +176,7 @@ int gloo_hip_algorithm_mode(gloo_hip_algorithm_t a, int* mode) {
     mode[0] = a->exec->deviceSignalling() ? 1 : 0;
     mode[1] = a->exec->hostArena() ? 2 : a->exec->fineGrainedArena() ? 1 : 0;
     mode[2] = a->exec->kernelCopy() ? 1 : 0;
-    mode[3] = a->exec->graphed() ? 1 : a->exec->interpreted() ? 2 : 0;
+    mode[3] = a->exec->graphed() ? 1 : a->exec->interpreted() ? 1 + a->exec->interpSlices() : 0;
     gloo_amd::setError(0, a->exec->graphError().empty() ? "" : "graph capture abandoned: " + a->exec->graphError());
   });
 }

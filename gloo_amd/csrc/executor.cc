@@ -35,6 +35,7 @@ struct ArenaRecord {
   int32_t hasMailbox;        // ... into device-resident mailboxes
   uint64_t mailboxPtr;
   hipIpcMemHandle_t mailboxHandle;
+  int32_t interpSlices;      // slices this rank could run its plan in (0: no sliced interpreter)
 };
 
 bool mailboxesEnabled() {
@@ -91,6 +92,95 @@ size_t interpBytes() {
     return e ? (size_t)std::strtoull(e, nullptr, 10) : fuseBytes();
   }();
   return v;
+}
+
+// Workgroups per sliced interpreter launch: about one per this many bytes of
+// the plan's largest message.
+size_t sliceBytes() {
+  static const size_t v = [] {
+    const char* e = std::getenv("GLOO_AMD_INTERP_SLICE_BYTES");
+    return e ? std::max<size_t>(1, std::strtoull(e, nullptr, 10)) : (size_t)(32 << 10);
+  }();
+  return v;
+}
+
+// A range of one of a rank's buffers, symbolically: output j = j, input j =
+// kIn + j, the inbox arena = kArena.
+struct Access {
+  int buf;
+  size_t off, len;
+};
+constexpr int kIn = 1 << 20, kArena = -1;
+
+// Can the plan run as slices (signal.h, sliced interpreter)?  Workgroup g
+// handles slice g of every step and never meets the others, so every step
+// must read exactly the ranges earlier steps wrote: a read overlapping an
+// earlier write (a peer's message into the arena counts as one, written
+// before anything) must be that same range, and a write overlapping any
+// earlier access must be that same range.  Reads of data nobody wrote this
+// run (the user's buffers) may overlap freely.
+bool sliceable(const Plan& plan, int nin, int nout, const std::vector<Access>& remoteWrites) {
+  std::map<int, std::vector<Access>> reads, writes;
+  auto clash = [](const Access& a, const Access& b) {
+    const bool overlap = a.off < b.off + b.len && b.off < a.off + a.len;
+    return overlap && !(a.off == b.off && a.len == b.len);
+  };
+  auto write = [&](const Access& w) {
+    if (!w.len) return true;
+    for (const Access& x : reads[w.buf])
+      if (clash(x, w)) return false;
+    for (const Access& x : writes[w.buf])
+      if (clash(x, w)) return false;
+    writes[w.buf].push_back(w);
+    return true;
+  };
+  auto read = [&](const Access& r) {
+    if (!r.len) return true;
+    for (const Access& x : writes[r.buf])
+      if (clash(x, r)) return false;
+    reads[r.buf].push_back(r);
+    return true;
+  };
+  for (const Access& w : remoteWrites)
+    if (!write(w)) return false;
+  auto sendBuf = [](const Step& t) {
+    return t.flags & GLOO_HIP_SRC_ARENA ? kArena : t.flags & GLOO_HIP_FROM_INPUTS ? kIn : 0;
+  };
+  for (const Step& t : plan.steps) {
+    const size_t L = t.length;
+    bool ok = true;
+    switch (t.kind) {
+      case GLOO_HIP_STEP_SEND:
+      case GLOO_HIP_STEP_FOLD_SRC:
+        ok = read({sendBuf(t), t.src_off, L});
+        break;
+      case GLOO_HIP_STEP_REDUCE:
+        ok = read({t.flags & GLOO_HIP_FROM_INPUTS ? kIn : 0, t.dst_off, L}) && read({kArena, t.src_off, L}) &&
+             write({0, t.dst_off, L});
+        break;
+      case GLOO_HIP_STEP_COPY:
+        ok = read({t.flags & GLOO_HIP_SRC_ARENA ? kArena : 0, t.src_off, L}) &&
+             write({t.flags & GLOO_HIP_DST_ARENA ? kArena : 0, t.dst_off, L});
+        break;
+      case GLOO_HIP_STEP_FOLD:
+        ok = write({t.flags & GLOO_HIP_DST_ARENA ? kArena : 0, t.dst_off, L});
+        break;
+      case GLOO_HIP_STEP_LOCAL_REDUCE: {
+        const bool fromIn = t.flags & GLOO_HIP_FROM_INPUTS;
+        for (int j = 0; j < (fromIn ? nin : nout) && ok; j++) ok = read({(fromIn ? kIn : 0) + j, t.dst_off, L});
+        ok = ok && write({0, t.dst_off, L});
+        break;
+      }
+      case GLOO_HIP_STEP_LOCAL_BCAST:
+        ok = read({0, t.dst_off, L});
+        for (int j = 1; j < nout && ok; j++) ok = write({j, t.dst_off, L});
+        break;
+      default:
+        break;
+    }
+    if (!ok) return false;
+  }
+  return true;
 }
 
 std::set<std::pair<const Context*, uint64_t>>& liveInstances() {
@@ -373,13 +463,51 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   // this way against about 2.4 us through the host control block
   // (tools/pingpong.cc, profiles/round1/r1q_pingpong.jsonl).
   if (deviceSignal_ && mailboxesEnabled()) {
-    const size_t mbBytes = ((size_t)P * GLOO_HIP_NUM_SLOTS * sizeof(uint64_t) + 4095) / 4096 * 4096;
+    // one word per (sender, slot, slice): slices of the sliced interpreter
+    const size_t mbBytes = ((size_t)P * GLOO_HIP_NUM_SLOTS * kMaxSlices * sizeof(uint64_t) + 4095) / 4096 * 4096;
     GLOO_AMD_HIP_ALLOC(hipExtMallocWithFlags(reinterpret_cast<void**>(&mailbox_), mbBytes, hipDeviceMallocFinegrained));
     GLOO_AMD_HIP_CHECK(hipMemsetAsync(mailbox_, 0, mbBytes, stream_));
     GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
   }
+  // Interpreter (executor.h): the knobs every rank reads alike, and this
+  // rank's proposal for the sliced form — one workgroup per sliceBytes() of
+  // its largest message, if its own plan and the messages its peers write
+  // into its arena slice consistently (sliceable).  All ranks then take the
+  // smallest proposal, so they agree.
+  {
+    const char* im = std::getenv("GLOO_AMD_INTERP");
+    const char* gm = std::getenv("GLOO_AMD_GRAPH");
+    interpMode_ = deviceSignal_ && !(im && std::string(im) == "0") && !(gm && std::string(gm) == "1") &&
+                  interpBytes() > 0;
+  }
+  int32_t proposal = 0;
+  if (interpMode_ && mailbox_ && !anyRemote_ && !hostArena_) {
+    size_t maxMsg = 0;
+    for (const Step& s : plan_.steps) maxMsg = std::max(maxMsg, (size_t)s.length * es_);
+    const size_t want = std::min<size_t>(kMaxSlices, std::max<size_t>(1, (maxMsg + sliceBytes() - 1) / sliceBytes()));
+    // above kMaxSlices slices of sliceBytes() graph replay is as fast
+    // (measured: 2 MiB messages, 32 slices 41.5 us vs graph 39.5 us)
+    if (maxMsg <= (size_t)kMaxSlices * sliceBytes()) {
+      std::map<std::pair<int, int>, size_t> decl;  // (sender, slot) -> arena offset
+      for (const Step& d : plan_.steps)
+        if (d.kind == GLOO_HIP_STEP_DECL_RECV) decl[{d.peer, d.slot}] = d.dst_off;
+      std::vector<Access> remote;
+      bool ok = true;
+      for (int peer : recvPeers) {
+        const Plan theirs = planFor(planAlgo_, peer, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
+        for (const Step& t : theirs.steps)
+          if (t.kind == GLOO_HIP_STEP_SEND && t.peer == me) {
+            auto it = decl.find({peer, t.slot});
+            if (it == decl.end()) ok = false;
+            else remote.push_back({kArena, it->second + t.dst_off, t.length});
+          }
+      }
+      if (ok && sliceable(plan_, (int)inputs_.size(), (int)ptrs_.size(), remote)) proposal = (int32_t)want;
+    }
+  }
   ArenaRecord rec;
   std::memset(&rec, 0, sizeof(rec));
+  rec.interpSlices = proposal;
   rec.pid = ctx_->pid();
   rec.device = ctx_->device();
   rec.ptr = reinterpret_cast<uint64_t>(arena_);
@@ -457,6 +585,17 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     if (s.kind == GLOO_HIP_STEP_SEND)
       GLOO_AMD_ENFORCE(remoteRegion_.count({s.peer, s.slot}), "rank ", s.peer, " declared no region for rank ",
                        me, " slot ", s.slot);
+  // the sliced interpreter runs on every rank or on none
+  int32_t agreed = proposal;
+  for (int r = 0; r < P && agreed > 1; r++) {
+    if (r == me) continue;
+    auto v = ctx_->store().get(strcat_("gloo_amd/inst", inst_, "/arena/", r), ctx_->timeout());
+    GLOO_AMD_ENFORCE(v.size() == sizeof(ArenaRecord), "bad arena record from rank ", r);
+    ArenaRecord pr;
+    std::memcpy(&pr, v.data(), sizeof(pr));
+    agreed = std::min(agreed, pr.interpSlices);
+  }
+  slices_ = agreed > 1 ? agreed : 1;
   assignSeqs();
   if (deviceSignal_) {
     (void)ctx_->counterDevicePtr(inst_, 0, 0, 0);  // register the control block now
@@ -490,8 +629,6 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
           s.length * es_ > fuseBytes())
         unfused = true;
     graphMode_ = gmode == "1" || (gmode == "auto" && unfused);
-    const char* im = std::getenv("GLOO_AMD_INTERP");
-    interpMode_ = !(im && std::string(im) == "0") && gmode != "1" && interpBytes() > 0;
     if (interpMode_) GLOO_AMD_HIP_ALLOC(hipMalloc(&interpSteps_, kInterpMaxSteps * sizeof(InterpStep)));
     if (graphMode_) {
       GLOO_AMD_HIP_ALLOC(hipMalloc(&epoch_, sizeof(uint64_t)));
@@ -587,12 +724,12 @@ bool PlanExecutor::mailboxWith(int peer) const {
 }
 
 uint64_t* PlanExecutor::sigFlag(int peer, int slot) {
-  if (mailboxWith(peer)) return peerMailbox_[peer] + (size_t)ctx_->rank * GLOO_HIP_NUM_SLOTS + slot;
+  if (mailboxWith(peer)) return peerMailbox_[peer] + ((size_t)ctx_->rank * GLOO_HIP_NUM_SLOTS + slot) * kMaxSlices;
   return ctx_->counterDevicePtr(inst_, ctx_->rank, peer, slot);
 }
 
 uint64_t* PlanExecutor::waitFlag(int peer, int slot) {
-  if (mailboxWith(peer)) return mailbox_ + (size_t)peer * GLOO_HIP_NUM_SLOTS + slot;
+  if (mailboxWith(peer)) return mailbox_ + ((size_t)peer * GLOO_HIP_NUM_SLOTS + slot) * kMaxSlices;
   return ctx_->counterDevicePtr(inst_, peer, ctx_->rank, slot);
 }
 
@@ -614,13 +751,15 @@ void PlanExecutor::run() {
   reduceSeconds_ = reduceBytes_ = 0;
   reduceCount_ = 0;
   const uint64_t r = runs_ + 1;
-  const bool interp = deviceSignal_ && interpMode_ && !profiling_;
+  // sliced plans must run sliced on every rank (their flags are per slice);
+  // profiling then reports no reduce events
+  const bool interp = deviceSignal_ && interpMode_ && (!profiling_ || slices_ > 1);
   if (interp && interpDirty_) buildInterp();
   const bool graphable = deviceSignal_ && graphMode_ && !profiling_;
   if (interp && interpCount_ > 0) {
     const uint64_t timeoutTicks = (uint64_t)ctx_->timeout().count() * 100000ull;  // 100 MHz realtime clock
     checkRc(launchPlanInterp(op_, dtype_, interpSteps_, interpCount_, r, timeoutTicks, ctx_->errorWordDevicePtr(me),
-                             stream_),
+                             slices_, stream_),
             "plan interpreter");
   } else if (graphable && (graphExec_ || stableRuns_ >= 1)) {
     if (!graphExec_) tryCapture(r);  // sets the device epoch to r - 1
@@ -686,8 +825,11 @@ void PlanExecutor::tryCapture(uint64_t r) {
 void PlanExecutor::buildInterp() {
   interpDirty_ = false;
   interpCount_ = 0;
+  // a sliced plan has no other route: every rank's flags are per slice
+  GLOO_AMD_ENFORCE(slices_ == 1 || !anyRemote_,
+                   "buffers on another GPU of the process with a sliced interpreter plan");
   if (anyRemote_) return;
-  const size_t limit = interpBytes();
+  const size_t limit = interpBytes() * slices_;
   auto userOrArena = [&](bool arena) { return arena ? arena_ : userPtr(0); };
   auto sendSrc = [&](const Step& t) -> const char* {
     const char* base = t.flags & GLOO_HIP_SRC_ARENA ? arena_
@@ -718,21 +860,26 @@ void PlanExecutor::buildInterp() {
     t.n = n;
   };
   // false: overlapping operands (a memmove), not an interpreter shape
-  auto copy = [&](char* dst, const char* src, size_t bytes) {
+  auto copy = [&](char* dst, const char* src, size_t elems) {
+    const size_t bytes = elems * es_;
     if (dst == src || bytes == 0) return true;
     if (dst < src + bytes && src < dst + bytes) return false;
     InterpStep& t = push(kInterpCopy);
     t.dst = dst;
     t.src[0] = src;
-    t.n = bytes;
+    t.n = elems;
     return true;
+  };
+  auto fail = [&] {
+    GLOO_AMD_ENFORCE(slices_ == 1, "a sliced interpreter plan with a step the interpreter cannot run");
+    v.clear();
   };
   std::vector<const char*> foldSrcs;
   const std::vector<Step>& steps = plan_.steps;
   for (size_t i = 0; i < steps.size(); i++) {
     const Step& s = steps[i];
     const size_t bytes = s.length * es_;
-    if (bytes > limit) return;
+    if (bytes > limit) return fail();
     switch (s.kind) {
       case GLOO_HIP_STEP_DECL_RECV:
       case GLOO_HIP_STEP_WAIT_SEND:
@@ -741,7 +888,7 @@ void PlanExecutor::buildInterp() {
         InterpStep& t = push(kInterpSend);
         t.dst = peers_[s.peer].base + (remoteRegion_.at({s.peer, s.slot}) + s.dst_off) * es_;
         t.src[0] = sendSrc(s);
-        t.n = bytes;
+        t.n = s.length;
         withSeq(t, i, sigFlag(s.peer, s.slot));
         break;
       }
@@ -761,15 +908,15 @@ void PlanExecutor::buildInterp() {
       }
       case GLOO_HIP_STEP_COPY:
         if (!copy(userOrArena(s.flags & GLOO_HIP_DST_ARENA) + s.dst_off * es_,
-                  userOrArena(s.flags & GLOO_HIP_SRC_ARENA) + s.src_off * es_, bytes))
-          return;
+                  userOrArena(s.flags & GLOO_HIP_SRC_ARENA) + s.src_off * es_, s.length))
+          return fail();
         break;
       case GLOO_HIP_STEP_LOCAL_REDUCE: {  // as enqueue(): chained folds of <= GLOO_HIP_MAX_SRCS sources
         const size_t off = s.dst_off * es_;
         const std::vector<void*>& from = s.flags & GLOO_HIP_FROM_INPUTS ? inputs_ : ptrs_;
         char* out0 = userPtr(0) + off;
         if (from.size() == 1) {
-          if (!copy(out0, static_cast<const char*>(from[0]) + off, bytes)) return;
+          if (!copy(out0, static_cast<const char*>(from[0]) + off, s.length)) return fail();
           break;
         }
         std::vector<const char*> srcs;
@@ -787,7 +934,7 @@ void PlanExecutor::buildInterp() {
       }
       case GLOO_HIP_STEP_LOCAL_BCAST:
         for (size_t j = 1; j < ptrs_.size(); j++)
-          if (!copy(userPtr(j) + s.dst_off * es_, userPtr(0) + s.dst_off * es_, bytes)) return;
+          if (!copy(userPtr(j) + s.dst_off * es_, userPtr(0) + s.dst_off * es_, s.length)) return fail();
         break;
       case GLOO_HIP_STEP_FOLD_SRC:
         foldSrcs.push_back(sendSrc(s));
@@ -799,9 +946,9 @@ void PlanExecutor::buildInterp() {
         foldSrcs.clear();
         break;
       default:
-        return;
+        return fail();
     }
-    if (v.size() > (size_t)kInterpMaxSteps) return;
+    if (v.size() > (size_t)kInterpMaxSteps) return fail();
   }
   if (v.empty()) return;
   // an earlier launch may still read the list

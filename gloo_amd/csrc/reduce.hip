@@ -476,23 +476,24 @@ __device__ __forceinline__ void interp_copy(char* dst, const char* src, uint64_t
 // dst[i] = fold over the step's sources (mode as launchFold) for n elements:
 // 16-byte packets when every operand is 16-byte aligned, elements after.
 template <class Tr, int OP>
-__device__ __forceinline__ void interp_fold(const InterpStep& st) {
+__device__ __forceinline__ void interp_fold(const InterpStep& st, uint64_t lo, uint64_t hi) {
   using S = typename Tr::Storage;
   constexpr int kV = 16 / sizeof(S);
   // byte lanes unpack 16 per packet: one packet per lane keeps them in VGPRs
   constexpr int kU = sizeof(S) == 1 ? 1 : kInterpFoldUnroll;
   const int ns = st.nsrc, mode = st.mode;
-  const uint64_t n = st.n;
+  const uint64_t n = hi - lo;
   const uint64_t t = threadIdx.x;
   const char* src[GLOO_HIP_MAX_SRCS];
-  uintptr_t align = (uintptr_t)st.dst;
+  char* dstp = st.dst + lo * sizeof(S);
+  uintptr_t align = (uintptr_t)dstp;
 #pragma unroll
   for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++) {
-    src[j] = j < ns ? st.src[j] : nullptr;
+    src[j] = j < ns ? st.src[j] + lo * sizeof(S) : nullptr;
     align |= (uintptr_t)src[j];
   }
   const uint64_t nv = (align & 15) ? 0 : n / kV;
-  u32x4* dv = reinterpret_cast<u32x4*>(st.dst);
+  u32x4* dv = reinterpret_cast<u32x4*>(dstp);
   for (uint64_t b = 0; b < nv; b += (uint64_t)kInterpBlock * kU) {
     u32x4 v[GLOO_HIP_MAX_SRCS][kU];
 #pragma unroll
@@ -528,7 +529,7 @@ __device__ __forceinline__ void interp_fold(const InterpStep& st) {
       if (i < nv) dv[i] = v[0][u];
     }
   }
-  S* dst = reinterpret_cast<S*>(st.dst);
+  S* dst = reinterpret_cast<S*>(dstp);
   for (uint64_t i = nv * kV + t; i < n; i += kInterpBlock) {
     S e[GLOO_HIP_MAX_SRCS];
 #pragma unroll
@@ -549,17 +550,21 @@ __device__ __forceinline__ void interp_fold(const InterpStep& st) {
 template <class Tr, int OP>
 __global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpStep* steps, int nsteps, uint64_t run,
                                                                    uint64_t timeoutTicks, uint32_t* err) {
+  using S = typename Tr::Storage;
+  constexpr uint64_t kV = 16 / sizeof(S);
   __shared__ int ok;
+  const uint64_t g = blockIdx.x, G = gridDim.x;
   for (int k = 0; k < nsteps; k++) {
     const InterpStep& st = steps[k];
     const int kind = st.kind;
     const uint64_t value = st.base + run * st.perRun;
     if (kind == kInterpWait) {
       if (threadIdx.x == 0) {
+        const uint64_t* flag = st.flag + g;
         int good = 1;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         // signed difference: a target below the counter is already met
-        while ((int64_t)(__hip_atomic_load(st.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - value) < 0) {
+        while ((int64_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - value) < 0) {
           __builtin_amdgcn_s_sleep(2);
           if (__builtin_amdgcn_s_memrealtime() - t0 > timeoutTicks) {
             __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -574,29 +579,34 @@ __global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpS
       if (!ok) return;  // timed out: no further work, no further signal
       continue;
     }
+    // this workgroup's slice of the step (signal.h): 16-byte granular
+    const uint64_t n = st.n;
+    const uint64_t q = ((n + G - 1) / G + kV - 1) / kV * kV;
+    const uint64_t lo = g * q < n ? g * q : n;
+    const uint64_t hi = lo + q < n ? lo + q : n;
     if (kind == kInterpCopy || kind == kInterpSend) {
-      interp_copy(st.dst, st.src[0], st.n);
+      interp_copy(st.dst + lo * sizeof(S), st.src[0] + lo * sizeof(S), (hi - lo) * sizeof(S));
     } else if (kind == kInterpFold) {
-      interp_fold<Tr, OP>(st);
+      interp_fold<Tr, OP>(st, lo, hi);
     }
     // every wave's writes of this step are performed before the barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if ((kind == kInterpSend || kind == kInterpSignal) && threadIdx.x == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      __hip_atomic_store(st.flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(st.flag + g, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
 
 template <class Tr>
 int launch_interp(int op, const InterpStep* steps, int nsteps, uint64_t run, uint64_t tt, uint32_t* err,
-                  hipStream_t s) {
+                  int G, hipStream_t s) {
   switch (op) {
-    case GLOO_HIP_SUM: plan_interp_kernel<Tr, GLOO_HIP_SUM><<<1, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
-    case GLOO_HIP_PRODUCT: plan_interp_kernel<Tr, GLOO_HIP_PRODUCT><<<1, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
-    case GLOO_HIP_MAX: plan_interp_kernel<Tr, GLOO_HIP_MAX><<<1, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
-    case GLOO_HIP_MIN: plan_interp_kernel<Tr, GLOO_HIP_MIN><<<1, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
+    case GLOO_HIP_SUM: plan_interp_kernel<Tr, GLOO_HIP_SUM><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
+    case GLOO_HIP_PRODUCT: plan_interp_kernel<Tr, GLOO_HIP_PRODUCT><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
+    case GLOO_HIP_MAX: plan_interp_kernel<Tr, GLOO_HIP_MAX><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
+    case GLOO_HIP_MIN: plan_interp_kernel<Tr, GLOO_HIP_MIN><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
     default: return GLOO_HIP_EINVAL_OP;
   }
   return GLOO_HIP_OK;
@@ -890,21 +900,22 @@ int launchFusedSmall(int op, int dtype, void* dst, const void* src, size_t n, co
 }
 
 int launchPlanInterp(int op, int dtype, const InterpStep* steps, int nsteps, uint64_t run, uint64_t tt,
-                     uint32_t* err, hipStream_t s) {
+                     uint32_t* err, int G, hipStream_t s) {
   static_assert(GLOO_HIP_MAX_SRCS <= 8, "InterpStep holds 8 sources");
   if (nsteps < 0 || nsteps > kInterpMaxSteps) return set_error(GLOO_HIP_EINVAL_ARG, "interpreter: bad step count");
+  if (G < 1 || G > kMaxSlices) return set_error(GLOO_HIP_EINVAL_ARG, "interpreter: bad slice count");
   int rc;
   switch (dtype) {
-    case GLOO_HIP_I8: rc = launch_interp<TrI8>(op, steps, nsteps, run, tt, err, s); break;
-    case GLOO_HIP_U8: rc = launch_interp<TrU8>(op, steps, nsteps, run, tt, err, s); break;
-    case GLOO_HIP_I32: rc = launch_interp<TrI32>(op, steps, nsteps, run, tt, err, s); break;
-    case GLOO_HIP_U32: rc = launch_interp<TrU32>(op, steps, nsteps, run, tt, err, s); break;
-    case GLOO_HIP_I64: rc = launch_interp<TrI64>(op, steps, nsteps, run, tt, err, s); break;
-    case GLOO_HIP_U64: rc = launch_interp<TrU64>(op, steps, nsteps, run, tt, err, s); break;
-    case GLOO_HIP_F16: rc = launch_interp<TrF16>(op, steps, nsteps, run, tt, err, s); break;
-    case GLOO_HIP_BF16: rc = launch_interp<TrBF16>(op, steps, nsteps, run, tt, err, s); break;
-    case GLOO_HIP_F32: rc = launch_interp<TrF32>(op, steps, nsteps, run, tt, err, s); break;
-    case GLOO_HIP_F64: rc = launch_interp<TrF64>(op, steps, nsteps, run, tt, err, s); break;
+    case GLOO_HIP_I8: rc = launch_interp<TrI8>(op, steps, nsteps, run, tt, err, G, s); break;
+    case GLOO_HIP_U8: rc = launch_interp<TrU8>(op, steps, nsteps, run, tt, err, G, s); break;
+    case GLOO_HIP_I32: rc = launch_interp<TrI32>(op, steps, nsteps, run, tt, err, G, s); break;
+    case GLOO_HIP_U32: rc = launch_interp<TrU32>(op, steps, nsteps, run, tt, err, G, s); break;
+    case GLOO_HIP_I64: rc = launch_interp<TrI64>(op, steps, nsteps, run, tt, err, G, s); break;
+    case GLOO_HIP_U64: rc = launch_interp<TrU64>(op, steps, nsteps, run, tt, err, G, s); break;
+    case GLOO_HIP_F16: rc = launch_interp<TrF16>(op, steps, nsteps, run, tt, err, G, s); break;
+    case GLOO_HIP_BF16: rc = launch_interp<TrBF16>(op, steps, nsteps, run, tt, err, G, s); break;
+    case GLOO_HIP_F32: rc = launch_interp<TrF32>(op, steps, nsteps, run, tt, err, G, s); break;
+    case GLOO_HIP_F64: rc = launch_interp<TrF64>(op, steps, nsteps, run, tt, err, G, s); break;
     default: return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
   }
   if (rc != GLOO_HIP_OK) return set_error(rc, "interpreter: bad op");

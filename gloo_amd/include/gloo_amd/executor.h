@@ -51,6 +51,10 @@
 // process, the steps are resolved once into a device-resident InterpStep
 // list (signal.h) and every run() is ONE one-workgroup launch walking it —
 // a small allreduce costs its cross-rank hops, not a kernel boundary each.
+// Larger plans (messages up to kMaxSlices x GLOO_AMD_INTERP_SLICE_BYTES) run
+// SLICED when every rank's plan allows it: one workgroup per
+// GLOO_AMD_INTERP_SLICE_BYTES of the largest message, each running the whole
+// plan on its slice of every step with its own flag words (signal.h).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -98,6 +102,8 @@ class PlanExecutor {
   bool graphed() const { return graphExec_ != nullptr; }
   // True once run() executes the plan as one interpreter launch.
   bool interpreted() const { return interpMode_ && interpCount_ > 0; }
+  // Workgroups of that launch: > 1 when every rank runs the plan sliced.
+  int interpSlices() const { return slices_; }
   // Why graph capture was abandoned (empty if it was not).
   const std::string& graphError() const { return graphError_; }
   // Host time spent blocked in WAIT steps during the last run(), seconds.
@@ -184,6 +190,7 @@ class PlanExecutor {
   bool interpDirty_ = true;            // interpSteps_ predates the current buffers
   InterpStep* interpSteps_ = nullptr;  // device copy of the resolved steps
   int interpCount_ = 0;
+  int slices_ = 1;                     // workgroups of the (sliced) interpreter, agreed by all ranks
   uint64_t* mailbox_ = nullptr;           // this rank's incoming counters, (sender, slot), fine-grained HBM
   std::vector<uint64_t*> peerMailbox_;    // peers' mailboxes (nullptr: that channel uses the host block)
   std::vector<bool> peerMailboxIpc_;

@@ -76,28 +76,39 @@ hipError_t launchWaitMulti(const uint64_t* const* flags, const Seq* targets, int
                            uint64_t timeoutTicks, uint32_t* err, hipStream_t stream);
 
 // One-launch plan interpreter (reduce.hip) for plans whose every message is
-// small: ONE workgroup walks a precompiled step list — copies, sends (copy,
+// small: a workgroup walks a precompiled step list — copies, sends (copy,
 // drain, one system-scope release, flag store), signals, waits (one lane
 // polls, one acquire, barrier) and folds — with a workgroup barrier between
 // steps.  A small allreduce becomes a single kernel: its device time is the
 // cross-rank hops, not the kernel boundaries between them.  Sequence values
 // are base + run * perRun (the eager numbering).  A wait that times out sets
-// *err and ends the launch.
+// *err and ends the workgroup.
+//
+// Sliced form (`slices` > 1 workgroups): workgroup g runs the WHOLE list on
+// slice g of every step — elements [lo, hi) with q = ceil(n / slices) rounded
+// up to 16 bytes, lo = min(n, g q), hi = min(n, lo + q) — and signals / waits
+// on its own flag word `flag + g`.  The slices never meet inside the launch
+// (no grid barrier): every rank slices every message alike, so slice g of a
+// message is produced, sent, received and consumed by workgroups g alone.  The
+// executor proves per plan that each step reads exactly the ranges earlier
+// steps or peers wrote (executor.cc sliceable) before choosing it.
 enum { kInterpCopy = 0, kInterpSend = 1, kInterpSignal = 2, kInterpWait = 3, kInterpFold = 4 };
 struct InterpStep {
   int32_t kind;       // kInterp*
   int32_t mode;       // FOLD: 0 left fold, 1 reverse (acc = s op acc), 2 balanced tree
   int32_t nsrc;       // FOLD: sources
   int32_t pad;
-  uint64_t* flag;     // SEND / SIGNAL: the flag written; WAIT: the flag polled
+  uint64_t* flag;     // SEND / SIGNAL: the flag written; WAIT: the flag polled (slice 0's)
   uint64_t base, perRun;
   char* dst;
   const char* src[8]; // COPY / SEND: src[0]; FOLD: the sources in order
-  uint64_t n;         // COPY / SEND: bytes; FOLD: elements
+  uint64_t n;         // elements
 };
 constexpr int kInterpMaxSteps = 512;
+// Flag words per (sender, slot) in a device mailbox: one per slice.
+constexpr int kMaxSlices = 32;
 int launchPlanInterp(int op, int dtype, const InterpStep* steps, int nsteps, uint64_t run, uint64_t timeoutTicks,
-                     uint32_t* err, hipStream_t stream);
+                     uint32_t* err, int slices, hipStream_t stream);
 
 // Multi-source fold in one pass, k <= GLOO_HIP_MAX_SRCS.  mode 0: left fold
 // acc = acc op s_j; 1: reverse, acc = s_j op acc; 2: balanced pairwise tree

@@ -291,9 +291,9 @@ int gloo_hip_algorithm_stats(gloo_hip_algorithm_t algo, double* stats4);
  * tools): mode4[0] = device-side signalling, [1] = inbox arena (0 device
  * coarse-grained, 1 device fine-grained, 2 pinned host),
  * [2] = kernel copy engine, [3] = how run() launches the plan: 0 enqueued
- * step by step, 1 a captured hipGraph replayed, 2 the one-launch plan
- * interpreter (small plans).  If graph capture was abandoned,
- * gloo_hip_last_error() says why. */
+ * step by step, 1 a captured hipGraph replayed, k >= 2 the one-launch plan
+ * interpreter with k - 1 workgroups (> 1: sliced).  If graph capture was
+ * abandoned, gloo_hip_last_error() says why. */
 int gloo_hip_algorithm_mode(gloo_hip_algorithm_t algo, int* mode4);
 
 /* ------------------------------------------------------------------------

@@ -77,12 +77,92 @@ class ProtocolError(AssertionError):
     pass
 
 
-def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, runs=1):
+def slice_range(length, g, slices, elem_size):
+    """Slice g of a step of `length` elements in the sliced interpreter
+    (gloo_amd/include/gloo_amd/signal.h): q = ceil(length / slices) rounded
+    up to 16 bytes, [min(length, g q), min(length, g q + q))."""
+    kv = max(1, 16 // elem_size)
+    q = -(-(-(-length // slices)) // kv) * kv
+    lo = min(length, g * q)
+    return lo, min(length, lo + q)
+
+
+def sliceable(algo, P, n, rank, k=1, nin=0, recv=None, elem_size=4, max_seg=0):
+    """Python statement of the executor's rule (gloo_amd/csrc/executor.cc
+    sliceable): may `rank` run its plan sliced?  Every read overlapping an
+    earlier write (peers' messages into the arena count as written first)
+    must be exactly that range; every write overlapping an earlier access
+    must be exactly that range."""
+    steps, _ = get_plan(algo, rank, P, n, k, recv, nin=nin, elem_size=elem_size, max_seg=max_seg)
+    decl = {(s.peer, s.slot): s.dst_off for s in steps if s.kind == KIND["DECL_RECV"]}
+    reads, writes = {}, {}
+
+    def clash(a, b):
+        return a[0] < b[0] + b[1] and b[0] < a[0] + a[1] and a != b
+
+    def write(buf, off, ln):
+        if not ln:
+            return True
+        if any(clash(x, (off, ln)) for x in reads.get(buf, []) + writes.get(buf, [])):
+            return False
+        writes.setdefault(buf, []).append((off, ln))
+        return True
+
+    def read(buf, off, ln):
+        if not ln:
+            return True
+        if any(clash(x, (off, ln)) for x in writes.get(buf, [])):
+            return False
+        reads.setdefault(buf, []).append((off, ln))
+        return True
+
+    ARENA, IN = -1, 1 << 20
+    for peer in range(P):
+        if peer == rank:
+            continue
+        theirs, _ = get_plan(algo, peer, P, n, 1, recv, nin=0, elem_size=elem_size, max_seg=max_seg)
+        for t in theirs:
+            if t.kind == KIND["SEND"] and t.peer == rank:
+                if (peer, t.slot) not in decl or not write(ARENA, decl[(peer, t.slot)] + t.dst_off, t.length):
+                    return False
+
+    def send_buf(t):
+        return ARENA if t.flags & SRC_ARENA else IN if t.flags & FROM_INPUTS else 0
+
+    for t in steps:
+        K, L = t.kind, t.length
+        if K in (KIND["SEND"], KIND["FOLD_SRC"]):
+            ok = read(send_buf(t), t.src_off, L)
+        elif K == KIND["REDUCE"]:
+            ok = read(IN if t.flags & FROM_INPUTS else 0, t.dst_off, L) and read(ARENA, t.src_off, L) and \
+                write(0, t.dst_off, L)
+        elif K == KIND["COPY"]:
+            ok = read(ARENA if t.flags & SRC_ARENA else 0, t.src_off, L) and \
+                write(ARENA if t.flags & DST_ARENA else 0, t.dst_off, L)
+        elif K == KIND["FOLD"]:
+            ok = write(ARENA if t.flags & DST_ARENA else 0, t.dst_off, L)
+        elif K == KIND["LOCAL_REDUCE"]:
+            from_in = t.flags & FROM_INPUTS
+            ok = all(read((IN if from_in else 0) + j, t.dst_off, L) for j in range(nin if from_in else k)) and \
+                write(0, t.dst_off, L)
+        elif K == KIND["LOCAL_BCAST"]:
+            ok = read(0, t.dst_off, L) and all(write(j, t.dst_off, L) for j in range(1, k))
+        else:
+            ok = True
+        if not ok:
+            return False
+    return True
+
+
+def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, runs=1, slices=1):
     """inputs: [P][k][n] array of the dtype's storage type (the outputs'
     initial contents); ins: optional [P][kin][n] separate inputs (new-style
     allreduce).  runs > 1 executes the plan back to back that many times
     (each run reduces the previous run's outputs), with no barrier between
-    runs, as repeated Algorithm::run() calls do.  Returns the outputs."""
+    runs, as repeated Algorithm::run() calls do.  slices > 1 executes it as
+    the sliced interpreter does: every (rank, slice) is its own process
+    applying each step to its slice only, with its own channel counters,
+    interleaved at random with all the others.  Returns the outputs."""
     P, k, n = inputs.shape
     nin = 0 if ins is None else ins.shape[1]
     es = inputs.dtype.itemsize
@@ -108,73 +188,76 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
                     raise ProtocolError(f"region {key} declared twice")
                 regions[key] = (s.dst_off, s.length)
     sent, consumed, lagged = {}, {}, {}
-    pending = [[] for _ in range(P)]  # FOLD sources, read when the FOLD executes
-    pc = [0] * P
+    procs = [(r, g) for r in range(P) for g in range(slices)]
+    pending = {p: [] for p in procs}  # FOLD sources, read when the FOLD executes
+    pc = {p: 0 for p in procs}
     rng = random.Random(seed)
 
     def space(r, is_arena):
         return arena[r] if is_arena else user[r][0]
 
-    def runnable(r):
+    def runnable(p):
+        r, g = p
         steps = plans[r][0]
-        if pc[r] >= len(steps):
+        if pc[p] >= len(steps):
             return False
-        s = steps[pc[r]]
+        s = steps[pc[p]]
         if s.kind == KIND["WAIT_NOTIFY"] and s.flags & PREV_RUN:
             # the i-th such wait is met by the previous run's credits
-            key = (s.peer, r, s.slot)
-            return sent.get(key, 0) >= lagged.get(key, 0) + 1 - lag_per_run[key]
+            key = (s.peer, r, s.slot, g)
+            return sent.get(key, 0) >= lagged.get(key, 0) + 1 - lag_per_run[key[:3]]
         if s.kind in (KIND["WAIT_RECV"], KIND["WAIT_NOTIFY"]):
-            key = (s.peer, r, s.slot)
+            key = (s.peer, r, s.slot, g)
             return sent.get(key, 0) > consumed.get(key, 0)
         return True
 
     while True:
-        ready = [r for r in range(P) if runnable(r)]
+        ready = [p for p in procs if runnable(p)]
         if not ready:
-            if all(pc[r] >= len(plans[r][0]) for r in range(P)):
+            if all(pc[p] >= len(plans[p[0]][0]) for p in procs):
                 break
             raise ProtocolError(f"deadlock at pcs {pc}")
-        r = rng.choice(ready)
-        s = plans[r][0][pc[r]]
-        pc[r] += 1
+        r, g = rng.choice(ready)
+        s = plans[r][0][pc[(r, g)]]
+        pc[(r, g)] += 1
         K = s.kind
+        a0, a1 = slice_range(s.length, g, slices, es)  # this process's part of the step
         if K == KIND["DECL_RECV"] or K == KIND["WAIT_SEND"]:
             continue
         if K == KIND["WAIT_NOTIFY"] and s.flags & PREV_RUN:
-            key = (s.peer, r, s.slot)
+            key = (s.peer, r, s.slot, g)
             lagged[key] = lagged.get(key, 0) + 1
             continue
         if K == KIND["SEND"]:
-            key = (r, s.peer, s.slot)
-            if key not in regions:
+            key = (r, s.peer, s.slot, g)
+            if key[:3] not in regions:
                 raise ProtocolError(f"send to undeclared region {key}")
             if sent.get(key, 0) > consumed.get(key, 0):
                 raise ProtocolError(f"send {key} overwrites an unconsumed message")
-            roff, cap = regions[key]
+            roff, cap = regions[key[:3]]
             if s.length > cap:
                 raise ProtocolError(f"send {key} of {s.length} exceeds region {cap}")
             src = ins[r, 0] if s.flags & FROM_INPUTS else space(r, s.flags & SRC_ARENA)
-            arena[s.peer][roff:roff + s.length] = src[s.src_off:s.src_off + s.length]
+            arena[s.peer][roff + a0:roff + a1] = src[s.src_off + a0:s.src_off + a1]
             sent[key] = sent.get(key, 0) + 1
         elif K in (KIND["WAIT_RECV"], KIND["WAIT_NOTIFY"]):
-            key = (s.peer, r, s.slot)
+            key = (s.peer, r, s.slot, g)
             consumed[key] = consumed.get(key, 0) + 1
         elif K == KIND["NOTIFY"]:
-            key = (r, s.peer, s.slot)
+            key = (r, s.peer, s.slot, g)
             sent[key] = sent.get(key, 0) + 1
         elif K == KIND["REDUCE"]:
             dst = user[r][0]
             # FROM_INPUTS: out = in op inbox (gloo::reduce, gloo/reduce.cc:180-184)
-            a = (ins[r, 0] if s.flags & FROM_INPUTS else dst)[s.dst_off:s.dst_off + s.length]
-            b = arena[r][s.src_off:s.src_off + s.length]
-            dst[s.dst_off:s.dst_off + s.length] = oracle.reduce3(op, dtype, a, b)
+            a = (ins[r, 0] if s.flags & FROM_INPUTS else dst)[s.dst_off + a0:s.dst_off + a1]
+            b = arena[r][s.src_off + a0:s.src_off + a1]
+            dst[s.dst_off + a0:s.dst_off + a1] = oracle.reduce3(op, dtype, a, b)
         elif K == KIND["COPY"]:
             src = space(r, s.flags & SRC_ARENA)
             dst = space(r, s.flags & DST_ARENA)
-            dst[s.dst_off:s.dst_off + s.length] = src[s.src_off:s.src_off + s.length].copy()
+            dst[s.dst_off + a0:s.dst_off + a1] = src[s.src_off + a0:s.src_off + a1].copy()
         elif K == KIND["LOCAL_REDUCE"]:
-            lo, hi = s.dst_off, s.dst_off + s.length
+            lo, hi = s.dst_off + a0, s.dst_off + a1
             out0 = user[r][0]
             if s.flags & FROM_INPUTS:
                 if nin == 1:
@@ -187,15 +270,15 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
                 for j in range(1, k):
                     out0[lo:hi] = oracle.reduce3(op, dtype, out0[lo:hi], user[r][j][lo:hi])
         elif K == KIND["LOCAL_BCAST"]:
-            lo, hi = s.dst_off, s.dst_off + s.length
+            lo, hi = s.dst_off + a0, s.dst_off + a1
             for j in range(1, k):
                 user[r][j][lo:hi] = user[r][0][lo:hi]
         elif K == KIND["FOLD_SRC"]:
-            pending[r].append((s.flags, s.src_off))
+            pending[(r, g)].append((s.flags, s.src_off))
         elif K == KIND["FOLD"]:
-            srcs = [(ins[r, 0] if f & FROM_INPUTS else space(r, f & SRC_ARENA))[o:o + s.length].copy()
-                    for f, o in pending[r]]
-            pending[r] = []
+            srcs = [(ins[r, 0] if f & FROM_INPUTS else space(r, f & SRC_ARENA))[o + a0:o + a1].copy()
+                    for f, o in pending[(r, g)]]
+            pending[(r, g)] = []
             if s.flags & FOLD_TREE:
                 while len(srcs) > 1:
                     srcs = [oracle.reduce3(op, dtype, srcs[2 * j], srcs[2 * j + 1]) for j in range(len(srcs) // 2)]
@@ -205,11 +288,11 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
                 for x in srcs[1:]:
                     acc = oracle.reduce3(op, dtype, x, acc) if s.flags & FOLD_REVERSE else \
                         oracle.reduce3(op, dtype, acc, x)
-            space(r, s.flags & DST_ARENA)[s.dst_off:s.dst_off + s.length] = acc
+            space(r, s.flags & DST_ARENA)[s.dst_off + a0:s.dst_off + a1] = acc
         else:
             raise ProtocolError(f"unknown step kind {K}")
     for key in sent:
-        if key in lag_per_run:
+        if key[:3] in lag_per_run:
             if sent[key] != lagged.get(key, 0):
                 raise ProtocolError(f"{key}: {sent[key]} credits sent, {lagged.get(key, 0)} awaited")
             continue

@@ -334,23 +334,26 @@ try:
     print("NO-ERROR")
 except gloo_amd.GlooHipError as e:
     print("RAISED", round(time.time() - t0, 1), str(e)[:200])
+print("INTERP", a.mode()["interp"])
 '''
 
 
-@pytest.mark.parametrize("mode", ["device", "host"])
-def test_dead_peer_times_out(torch, mode):
+@pytest.mark.parametrize("mode,interp", [("device", "1"), ("device", "0"), ("host", "1")])
+def test_dead_peer_times_out(torch, mode, interp):
     """Failure detection (SURVEY §5: context timeout -> IoException): a peer
     that disappears makes run() raise after the timeout instead of hanging —
-    through the device-side wait kernel's bounded spin, or the host wait."""
+    through the interpreter's bounded spin (it ends the launch), the
+    device-side wait kernel's, or the host wait."""
     with tempfile.TemporaryDirectory() as d:
         w = os.path.join(d, "w.py")
         open(w, "w").write(DEAD_PEER_WORKER)
-        env = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_SIGNAL=mode)
+        env = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_SIGNAL=mode, GLOO_AMD_INTERP=interp)
         procs = [subprocess.Popen([sys.executable, w, str(r), "2", "file:" + os.path.join(d, "s")], env=env,
                                   stdout=subprocess.PIPE, text=True) for r in range(2)]
         outs = [p.communicate(timeout=120)[0] for p in procs]
     assert "RAISED" in outs[0], outs[0]
     assert "timed out" in outs[0].lower()
+    assert ("INTERP True" in outs[0]) == (mode == "device" and interp == "1"), outs[0]
 
 
 GOLDEN_PROC_WORKER = r'''
@@ -596,6 +599,84 @@ def test_processes_interp(torch, golden_sched, case, env, interp):
     for r in range(P):
         modes = json.loads(outs[r].split("MODES", 1)[1])
         assert [m["interp"] for m in modes] == [interp] * runs, modes
+
+
+def _expected_slices(case, env):
+    """The slice count the executor must agree on (executor.cc): per rank
+    ceil(largest message / GLOO_AMD_INTERP_SLICE_BYTES) if that is at most
+    32 and its plan is sliceable (plan_sim.sliceable, the rule restated), the
+    minimum over ranks, 1 if that is not above 1."""
+    from plan_sim import get_plan, sliceable
+    algo, P = case.split("/")[0], int(case.split("/")[3][1:])
+    n = int(case.split("/")[-1][1:])
+    es = {"f16": 2, "bf16": 2, "f32": 4, "f64": 8}[case.split("/")[2]]
+    if env.get("GLOO_AMD_MAILBOX") == "0":
+        return 1  # slices need every channel's flags in device mailboxes
+    mesh = env.get("GLOO_AMD_MESH", "1") != "0"
+    route = algo
+    if mesh and algo == "ring_chunked" and env.get("GLOO_AMD_RING_MESH", "1") != "0":
+        route = "ring_chunked_mesh"
+    elif mesh and algo in ("halving_doubling", "reduce_scatter"):
+        route = "mesh_" + algo
+    recv = None
+    if algo == "reduce_scatter":
+        recv = np.array([n // P + (1 if r < n % P else 0) for r in range(P)], np.int32)
+    sb = int(env.get("GLOO_AMD_INTERP_SLICE_BYTES", 32768))
+    props = []
+    for r in range(P):
+        steps, _ = get_plan(route, r, P, n, 1, recv, elem_size=es)
+        biggest = max(s.length for s in steps) * es
+        ok = biggest <= 32 * sb and sliceable(route, P, n, r, recv=recv, elem_size=es)
+        props.append(min(32, max(1, -(-biggest // sb))) if ok else 0)
+    g = min(props)
+    return g if g > 1 else 1
+
+
+@pytest.mark.parametrize("case,env", [
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "4096"}),
+    ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024"}),
+    ("halving_doubling/sum/f64/P7/k1/n3001", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024"}),
+    ("halving_doubling/sum/f32/P8/k1/n1000", {"GLOO_AMD_INTERP_SLICE_BYTES": "64"}),
+    ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024", "GLOO_AMD_MAILBOX": "0"}),
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024", "GLOO_AMD_MESH": "0"}),
+    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024"}),
+    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_INTERP_SLICE_BYTES": "512"}),
+    ("ring_chunked/max/f32/P5/k1/n999", {"GLOO_AMD_INTERP_SLICE_BYTES": "256"}),
+    ("ring_chunked/product/f32/P3/k1/n777", {"GLOO_AMD_INTERP_SLICE_BYTES": "100"}),   # ragged slices
+    ("reduce_scatter/max/bf16/P8/n4096", {"GLOO_AMD_INTERP_SLICE_BYTES": "256"}),
+    ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024"}),    # refused: uneven pieces
+])
+def test_processes_sliced_interp(torch, golden_sched, case, env):
+    """Sliced interpreter: every rank runs its plan in several workgroups,
+    workgroup g on slice g of every step with its own flag words.  The ranks
+    must agree on the slice count the rule predicts (1 where a plan is
+    refused), and five back-to-back runs must give the reference's bytes."""
+    algo = case.split("/")[0]
+    P = int(case.split("/")[3][1:])
+    want_slices = _expected_slices(case, env)
+    runs = 5
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(GRAPH_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), case,
+                                   os.path.join(d, f"o{r}"), str(runs)], env=e, stdout=subprocess.PIPE, text=True)
+                 for r in range(P)]
+        outs = [p.communicate(timeout=300)[0] for p in procs]
+        assert [p.returncode for p in procs] == [0] * P
+        ys = [[np.load(os.path.join(d, f"o{r}.{it}.npy")) for it in range(runs)] for r in range(P)]
+    want = golden_sched[case + "/out"]
+    for it in range(runs):
+        if algo == "reduce_scatter":
+            recv = golden_sched[case + "/recv"]
+            assert same_bytes(np.concatenate([ys[r][it][:recv[r]] for r in range(P)]), want), it
+        else:
+            for r in range(P):
+                assert same_bytes(ys[r][it], want), (r, it)
+    for r in range(P):
+        modes = json.loads(outs[r].split("MODES", 1)[1])
+        assert all(m["interp"] for m in modes), modes
+        assert [m["interp_slices"] for m in modes] == [want_slices] * runs, (want_slices, modes)
 
 
 NEW_STYLE_GRAPH_WORKER = r'''

@@ -1,7 +1,8 @@
 #!/bin/bash
-# tools/latency for 2 rank processes: HD allreduce of 1 KiB .. 1 MiB under
-# each launch mode (executor.h): the one-launch interpreter (default for
-# small plans), hipGraph replay, step-by-step enqueue.  JSON lines into
+# tools/latency for 2 rank processes: HD allreduce of 1 KiB .. 16 MiB under
+# each launch mode (executor.h): the defaults (sliced interpreter up to
+# 32 x 64 KiB messages, graph replay above), the interpreter held to one
+# workgroup, hipGraph replay, step-by-step enqueue.  JSON lines into
 # gpurun_out/latency.jsonl.
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
@@ -17,8 +18,9 @@ run_pair() {  # label count env...
   wait $p1 || return 1
   rm -rf "$d"
 }
-for count in 256 4096 16384 262144; do
-  run_pair interp $count GLOO_AMD_INTERP_BYTES=1048576 || exit 1
+for count in 256 16384 65536 262144 1048576 4194304; do
+  run_pair default $count || exit 1
+  run_pair one_workgroup $count GLOO_AMD_INTERP_SLICE_BYTES=1000000000 || exit 1
   run_pair graph $count GLOO_AMD_GRAPH=1 || exit 1
   run_pair eager $count GLOO_AMD_GRAPH=0 GLOO_AMD_INTERP=0 || exit 1
 done
