@@ -183,6 +183,17 @@ bool sliceable(const Plan& plan, int nin, int nout, const std::vector<Access>& r
   return true;
 }
 
+// Most workgroups of a sliced launch (<= kMaxSlices).  Ranks that share a
+// GPU each bring this many, and a slice spins until its peer slice runs, so
+// the default keeps 8 ranks on one GPU co-resident.
+int maxSlices() {
+  static const int v = [] {
+    const char* e = std::getenv("GLOO_AMD_INTERP_MAX_SLICES");
+    return e ? std::min(kMaxSlices, std::max(1, std::atoi(e))) : 32;
+  }();
+  return v;
+}
+
 std::set<std::pair<const Context*, uint64_t>>& liveInstances() {
   static std::set<std::pair<const Context*, uint64_t>> s;
   return s;
@@ -484,10 +495,10 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   if (interpMode_ && mailbox_ && !anyRemote_ && !hostArena_) {
     size_t maxMsg = 0;
     for (const Step& s : plan_.steps) maxMsg = std::max(maxMsg, (size_t)s.length * es_);
-    const size_t want = std::min<size_t>(kMaxSlices, std::max<size_t>(1, (maxMsg + sliceBytes() - 1) / sliceBytes()));
-    // above kMaxSlices slices of sliceBytes() graph replay is as fast
+    const size_t want = std::min<size_t>(maxSlices(), std::max<size_t>(1, (maxMsg + sliceBytes() - 1) / sliceBytes()));
+    // above maxSlices() slices of sliceBytes() graph replay is as fast
     // (measured: 2 MiB messages, 32 slices 41.5 us vs graph 39.5 us)
-    if (maxMsg <= (size_t)kMaxSlices * sliceBytes()) {
+    if (maxMsg <= (size_t)maxSlices() * sliceBytes()) {
       std::map<std::pair<int, int>, size_t> decl;  // (sender, slot) -> arena offset
       for (const Step& d : plan_.steps)
         if (d.kind == GLOO_HIP_STEP_DECL_RECV) decl[{d.peer, d.slot}] = d.dst_off;
@@ -829,7 +840,8 @@ void PlanExecutor::buildInterp() {
   GLOO_AMD_ENFORCE(slices_ == 1 || !anyRemote_,
                    "buffers on another GPU of the process with a sliced interpreter plan");
   if (anyRemote_) return;
-  const size_t limit = interpBytes() * slices_;
+  // a sliced plan's message sizes were vetted when the ranks agreed on it
+  const size_t limit = slices_ > 1 ? SIZE_MAX : interpBytes();
   auto userOrArena = [&](bool arena) { return arena ? arena_ : userPtr(0); };
   auto sendSrc = [&](const Step& t) -> const char* {
     const char* base = t.flags & GLOO_HIP_SRC_ARENA ? arena_

@@ -106,7 +106,7 @@ struct InterpStep {
 };
 constexpr int kInterpMaxSteps = 512;
 // Flag words per (sender, slot) in a device mailbox: one per slice.
-constexpr int kMaxSlices = 32;
+constexpr int kMaxSlices = 256;
 int launchPlanInterp(int op, int dtype, const InterpStep* steps, int nsteps, uint64_t run, uint64_t timeoutTicks,
                      uint32_t* err, int slices, hipStream_t stream);
 
