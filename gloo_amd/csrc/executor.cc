@@ -112,6 +112,52 @@ struct Access {
 };
 constexpr int kIn = 1 << 20, kArena = -1;
 
+// The sliced form splits a plan's whole-range local steps (LOCAL_REDUCE /
+// LOCAL_BCAST over [0, n)) at every boundary the other steps use in the
+// user buffers, so that the pieces later steps read are exactly pieces that
+// were written.  Element-wise, so the bytes are the same.
+std::vector<size_t> userCuts(const Plan& plan) {
+  std::set<size_t> c;
+  auto add = [&](size_t off, size_t len) {
+    c.insert(off);
+    c.insert(off + len);
+  };
+  for (const Step& t : plan.steps) {
+    switch (t.kind) {
+      case GLOO_HIP_STEP_SEND:
+      case GLOO_HIP_STEP_FOLD_SRC:
+        if (!(t.flags & GLOO_HIP_SRC_ARENA)) add(t.src_off, t.length);
+        break;
+      case GLOO_HIP_STEP_REDUCE:
+        add(t.dst_off, t.length);
+        break;
+      case GLOO_HIP_STEP_COPY:
+        if (!(t.flags & GLOO_HIP_SRC_ARENA)) add(t.src_off, t.length);
+        if (!(t.flags & GLOO_HIP_DST_ARENA)) add(t.dst_off, t.length);
+        break;
+      case GLOO_HIP_STEP_FOLD:
+        if (!(t.flags & GLOO_HIP_DST_ARENA)) add(t.dst_off, t.length);
+        break;
+      default:
+        break;
+    }
+  }
+  return std::vector<size_t>(c.begin(), c.end());
+}
+
+// [off, off + len) cut at `cuts` (sorted): the (offset, length) pieces.
+std::vector<std::pair<size_t, size_t>> cutRange(const std::vector<size_t>& cuts, size_t off, size_t len) {
+  std::vector<std::pair<size_t, size_t>> out;
+  size_t at = off;
+  for (size_t c : cuts)
+    if (c > at && c < off + len) {
+      out.push_back({at, c - at});
+      at = c;
+    }
+  if (off + len > at) out.push_back({at, off + len - at});
+  return out;
+}
+
 // Can the plan run as slices (signal.h, sliced interpreter)?  Workgroup g
 // handles slice g of every step and never meets the others, so every step
 // must read exactly the ranges earlier steps wrote: a read overlapping an
@@ -120,6 +166,7 @@ constexpr int kIn = 1 << 20, kArena = -1;
 // earlier access must be that same range.  Reads of data nobody wrote this
 // run (the user's buffers) may overlap freely.
 bool sliceable(const Plan& plan, int nin, int nout, const std::vector<Access>& remoteWrites) {
+  const std::vector<size_t> cuts = userCuts(plan);
   std::map<int, std::vector<Access>> reads, writes;
   auto clash = [](const Access& a, const Access& b) {
     const bool overlap = a.off < b.off + b.len && b.off < a.off + a.len;
@@ -167,13 +214,18 @@ bool sliceable(const Plan& plan, int nin, int nout, const std::vector<Access>& r
         break;
       case GLOO_HIP_STEP_LOCAL_REDUCE: {
         const bool fromIn = t.flags & GLOO_HIP_FROM_INPUTS;
-        for (int j = 0; j < (fromIn ? nin : nout) && ok; j++) ok = read({(fromIn ? kIn : 0) + j, t.dst_off, L});
-        ok = ok && write({0, t.dst_off, L});
+        for (const auto& pc : cutRange(cuts, t.dst_off, L)) {
+          for (int j = 0; j < (fromIn ? nin : nout) && ok; j++)
+            ok = read({(fromIn ? kIn : 0) + j, pc.first, pc.second});
+          ok = ok && write({0, pc.first, pc.second});
+        }
         break;
       }
       case GLOO_HIP_STEP_LOCAL_BCAST:
-        ok = read({0, t.dst_off, L});
-        for (int j = 1; j < nout && ok; j++) ok = write({j, t.dst_off, L});
+        for (const auto& pc : cutRange(cuts, t.dst_off, L)) {
+          ok = ok && read({0, pc.first, pc.second});
+          for (int j = 1; j < nout && ok; j++) ok = write({j, pc.first, pc.second});
+        }
         break;
       default:
         break;
@@ -886,6 +938,8 @@ void PlanExecutor::buildInterp() {
     GLOO_AMD_ENFORCE(slices_ == 1, "a sliced interpreter plan with a step the interpreter cannot run");
     v.clear();
   };
+  const std::vector<size_t> cuts = slices_ > 1 ? userCuts(plan_) : std::vector<size_t>();
+  auto pieces = [&](const Step& t) { return cutRange(cuts, t.dst_off, t.length); };
   std::vector<const char*> foldSrcs;
   const std::vector<Step>& steps = plan_.steps;
   for (size_t i = 0; i < steps.size(); i++) {
@@ -923,30 +977,33 @@ void PlanExecutor::buildInterp() {
                   userOrArena(s.flags & GLOO_HIP_SRC_ARENA) + s.src_off * es_, s.length))
           return fail();
         break;
-      case GLOO_HIP_STEP_LOCAL_REDUCE: {  // as enqueue(): chained folds of <= GLOO_HIP_MAX_SRCS sources
-        const size_t off = s.dst_off * es_;
-        const std::vector<void*>& from = s.flags & GLOO_HIP_FROM_INPUTS ? inputs_ : ptrs_;
-        char* out0 = userPtr(0) + off;
-        if (from.size() == 1) {
-          if (!copy(out0, static_cast<const char*>(from[0]) + off, s.length)) return fail();
-          break;
-        }
-        std::vector<const char*> srcs;
-        size_t j = 0;
-        for (; j < from.size() && srcs.size() < GLOO_HIP_MAX_SRCS; j++)
-          srcs.push_back(static_cast<const char*>(from[j]) + off);
-        fold(out0, srcs, s.length, 0);
-        while (j < from.size()) {
-          srcs.assign(1, out0);
+      case GLOO_HIP_STEP_LOCAL_REDUCE:  // as enqueue(): chained folds of <= GLOO_HIP_MAX_SRCS sources
+        // sliced: one piece per range the other steps use (userCuts)
+        for (const auto& pc : pieces(s)) {
+          const size_t off = pc.first * es_, len = pc.second;
+          const std::vector<void*>& from = s.flags & GLOO_HIP_FROM_INPUTS ? inputs_ : ptrs_;
+          char* out0 = userPtr(0) + off;
+          if (from.size() == 1) {
+            if (!copy(out0, static_cast<const char*>(from[0]) + off, len)) return fail();
+            continue;
+          }
+          std::vector<const char*> srcs;
+          size_t j = 0;
           for (; j < from.size() && srcs.size() < GLOO_HIP_MAX_SRCS; j++)
             srcs.push_back(static_cast<const char*>(from[j]) + off);
-          fold(out0, srcs, s.length, 0);
+          fold(out0, srcs, len, 0);
+          while (j < from.size()) {
+            srcs.assign(1, out0);
+            for (; j < from.size() && srcs.size() < GLOO_HIP_MAX_SRCS; j++)
+              srcs.push_back(static_cast<const char*>(from[j]) + off);
+            fold(out0, srcs, len, 0);
+          }
         }
         break;
-      }
       case GLOO_HIP_STEP_LOCAL_BCAST:
-        for (size_t j = 1; j < ptrs_.size(); j++)
-          if (!copy(userPtr(j) + s.dst_off * es_, userPtr(0) + s.dst_off * es_, s.length)) return fail();
+        for (const auto& pc : pieces(s))
+          for (size_t j = 1; j < ptrs_.size(); j++)
+            if (!copy(userPtr(j) + pc.first * es_, userPtr(0) + pc.first * es_, pc.second)) return fail();
         break;
       case GLOO_HIP_STEP_FOLD_SRC:
         foldSrcs.push_back(sendSrc(s));

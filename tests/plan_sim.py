@@ -87,6 +87,37 @@ def slice_range(length, g, slices, elem_size):
     return lo, min(length, lo + q)
 
 
+def user_cuts(steps):
+    """Boundaries the non-local steps use in the user buffers (executor.cc
+    userCuts): the sliced form splits whole-range local steps there."""
+    c = set()
+    for t in steps:
+        K = t.kind
+        if K in (KIND["SEND"], KIND["FOLD_SRC"]) and not t.flags & SRC_ARENA:
+            c |= {t.src_off, t.src_off + t.length}
+        elif K == KIND["REDUCE"]:
+            c |= {t.dst_off, t.dst_off + t.length}
+        elif K == KIND["COPY"]:
+            if not t.flags & SRC_ARENA:
+                c |= {t.src_off, t.src_off + t.length}
+            if not t.flags & DST_ARENA:
+                c |= {t.dst_off, t.dst_off + t.length}
+        elif K == KIND["FOLD"] and not t.flags & DST_ARENA:
+            c |= {t.dst_off, t.dst_off + t.length}
+    return sorted(c)
+
+
+def cut_range(cuts, off, length):
+    out, at = [], off
+    for c in cuts:
+        if at < c < off + length:
+            out.append((at, c - at))
+            at = c
+    if off + length > at:
+        out.append((at, off + length - at))
+    return out
+
+
 def sliceable(algo, P, n, rank, k=1, nin=0, recv=None, elem_size=4, max_seg=0):
     """Python statement of the executor's rule (gloo_amd/csrc/executor.cc
     sliceable): may `rank` run its plan sliced?  Every read overlapping an
@@ -95,6 +126,7 @@ def sliceable(algo, P, n, rank, k=1, nin=0, recv=None, elem_size=4, max_seg=0):
     must be exactly that range."""
     steps, _ = get_plan(algo, rank, P, n, k, recv, nin=nin, elem_size=elem_size, max_seg=max_seg)
     decl = {(s.peer, s.slot): s.dst_off for s in steps if s.kind == KIND["DECL_RECV"]}
+    cuts = user_cuts(steps)
     reads, writes = {}, {}
 
     def clash(a, b):
@@ -143,10 +175,11 @@ def sliceable(algo, P, n, rank, k=1, nin=0, recv=None, elem_size=4, max_seg=0):
             ok = write(ARENA if t.flags & DST_ARENA else 0, t.dst_off, L)
         elif K == KIND["LOCAL_REDUCE"]:
             from_in = t.flags & FROM_INPUTS
-            ok = all(read((IN if from_in else 0) + j, t.dst_off, L) for j in range(nin if from_in else k)) and \
-                write(0, t.dst_off, L)
+            ok = all(all(read((IN if from_in else 0) + j, o, ln) for j in range(nin if from_in else k)) and
+                     write(0, o, ln) for o, ln in cut_range(cuts, t.dst_off, L))
         elif K == KIND["LOCAL_BCAST"]:
-            ok = read(0, t.dst_off, L) and all(write(j, t.dst_off, L) for j in range(1, k))
+            ok = all(read(0, o, ln) and all(write(j, o, ln) for j in range(1, k))
+                     for o, ln in cut_range(cuts, t.dst_off, L))
         else:
             ok = True
         if not ok:
@@ -211,6 +244,24 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
             return sent.get(key, 0) > consumed.get(key, 0)
         return True
 
+    cuts = [user_cuts(steps) for steps, _ in plans]
+
+    def local_step(r, s, lo, hi):
+        out0 = user[r][0]
+        if s.kind == KIND["LOCAL_BCAST"]:
+            for j in range(1, k):
+                user[r][j][lo:hi] = out0[lo:hi]
+        elif s.flags & FROM_INPUTS:
+            if nin == 1:
+                out0[lo:hi] = ins[r, 0, lo:hi]
+            else:
+                out0[lo:hi] = oracle.reduce3(op, dtype, ins[r, 0, lo:hi], ins[r, 1, lo:hi])
+                for j in range(2, nin):
+                    out0[lo:hi] = oracle.reduce3(op, dtype, out0[lo:hi], ins[r, j, lo:hi])
+        else:
+            for j in range(1, k):
+                out0[lo:hi] = oracle.reduce3(op, dtype, out0[lo:hi], user[r][j][lo:hi])
+
     while True:
         ready = [p for p in procs if runnable(p)]
         if not ready:
@@ -256,23 +307,13 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
             src = space(r, s.flags & SRC_ARENA)
             dst = space(r, s.flags & DST_ARENA)
             dst[s.dst_off + a0:s.dst_off + a1] = src[s.src_off + a0:s.src_off + a1].copy()
-        elif K == KIND["LOCAL_REDUCE"]:
-            lo, hi = s.dst_off + a0, s.dst_off + a1
-            out0 = user[r][0]
-            if s.flags & FROM_INPUTS:
-                if nin == 1:
-                    out0[lo:hi] = ins[r, 0, lo:hi]
-                else:
-                    out0[lo:hi] = oracle.reduce3(op, dtype, ins[r, 0, lo:hi], ins[r, 1, lo:hi])
-                    for j in range(2, nin):
-                        out0[lo:hi] = oracle.reduce3(op, dtype, out0[lo:hi], ins[r, j, lo:hi])
-            else:
-                for j in range(1, k):
-                    out0[lo:hi] = oracle.reduce3(op, dtype, out0[lo:hi], user[r][j][lo:hi])
-        elif K == KIND["LOCAL_BCAST"]:
-            lo, hi = s.dst_off + a0, s.dst_off + a1
-            for j in range(1, k):
-                user[r][j][lo:hi] = user[r][0][lo:hi]
+        elif K in (KIND["LOCAL_REDUCE"], KIND["LOCAL_BCAST"]):
+            # sliced: the executor first splits whole-range local steps at the
+            # user-buffer boundaries the other steps use (executor.cc userCuts)
+            pieces = cut_range(cuts[r], s.dst_off, s.length) if slices > 1 else [(s.dst_off, s.length)]
+            for o, ln in pieces:
+                b0, b1 = slice_range(ln, g, slices, es)
+                local_step(r, s, o + b0, o + b1)
         elif K == KIND["FOLD_SRC"]:
             pending[(r, g)].append((s.flags, s.src_off))
         elif K == KIND["FOLD"]:

@@ -174,6 +174,11 @@ np.save(out, np.array(res))
     ("reduce", 3, {"GLOO_AMD_COPY": "kernel"}),
     ("ring", 4, {}),                                    # new-style RING, mesh route
     ("ring", 3, {"GLOO_AMD_MESH": "0"}),
+    # the sliced interpreter (executor.h), ragged slices, local steps split
+    ("ring", 4, {"GLOO_AMD_TEST_N": "1001", "GLOO_AMD_INTERP_SLICE_BYTES": "128"}),
+    ("bcube", 6, {"GLOO_AMD_TEST_N": "999", "GLOO_AMD_INTERP_SLICE_BYTES": "64"}),
+    ("reduce", 4, {"GLOO_AMD_TEST_N": "4097", "GLOO_AMD_INTERP_SLICE_BYTES": "256"}),
+    ("ring", 4, {"GLOO_AMD_INTERP": "0"}),              # graph replay / eager route at the default size
 ])
 def test_processes(torch, kind, P, env):
     """Ranks as processes (device signalling unless overridden; inboxes over

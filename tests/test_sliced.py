@@ -107,3 +107,53 @@ def test_refused_plans_would_be_wrong_sliced(algo):
             wrong = True
             break
     assert wrong
+
+
+def _new_style_cases():
+    d = os.path.join(os.path.dirname(__file__), "golden")
+    out = []
+    z = np.load(os.path.join(d, "newstyle_golden.npz"))
+    for case in sorted({k.rsplit("/", 1)[0] for k in z.files}):
+        if 2 <= int(case.split("/")[3][1:]) <= 8:
+            out.append(("new", case))
+    z = np.load(os.path.join(d, "sched_golden.npz"))
+    for case in sorted({k.rsplit("/", 1)[0] for k in z.files if k.startswith("allreduce_new/")}):
+        if 2 <= int(case.split("/")[3][1:]) <= 8:
+            out.append(("sched", case))
+    return out
+
+
+@pytest.fixture(scope="module")
+def golden_new():
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", "newstyle_golden.npz"))
+
+
+@pytest.mark.parametrize("src,case", _new_style_cases())
+def test_sliced_new_style_matches_reference(golden_sched, golden_new, src, case):
+    """The new-style collectives' mesh plans (gloo::allreduce RING / BCUBE,
+    gloo::reduce) sliced: their whole-range local steps (reduceInputs /
+    broadcastOutputs) are split at the boundaries the exchange uses, after
+    which every (rank, slice) runs alone and the bytes are the reference's
+    (the root's output for reduce)."""
+    g = golden_new if src == "new" else golden_sched
+    parts = case.split("/")
+    kind, op, dtype, P, nin = parts[0], parts[1], parts[2], int(parts[3][1:]), int(parts[4][1:])
+    algo = {"bcube": "mesh_allreduce_bcube", "allreduce_new": "mesh_allreduce_new", "reduce": "mesh_reduce"}[kind]
+    seg = int(parts[7][1:])
+    init = g[case + "/init"]
+    ins = g[case + "/in"] if nin else None
+    want = g[case + "/out"]
+    root = int(parts[6][1:]) if kind == "reduce" else None
+    recv = np.array([root], np.int32) if kind == "reduce" else None
+    n, k = init.shape[2], init.shape[1]
+    es = ES[dtype] if dtype in ES else init.dtype.itemsize
+    if not all(sliceable(algo, P, n, r, k=k, nin=nin, recv=recv, elem_size=es, max_seg=seg) for r in range(P)):
+        pytest.skip("not sliceable")
+    for slices, seed in ((2, 0), (5, 1)):
+        y = simulate(algo, op, dtype, init, recv=recv, seed=seed, ins=ins, max_seg=seg, slices=slices)
+        if kind == "reduce":  # only the root's output is defined on the mesh route
+            assert (y[root, 0].view(np.uint8) == want[root].view(np.uint8)).all(), slices
+            continue
+        for r in range(P):
+            for j in range(k):
+                assert (y[r, j].view(np.uint8) == want.view(np.uint8)).all(), (slices, r, j)
