@@ -244,3 +244,51 @@ def test_stream_ordering(hip):
             hip.reduce("sum", a, b)             # uses the current (side) stream
     s.synchronize()
     assert float(a[0]) == 11.0 and float(a[-1]) == 11.0
+
+
+@pytest.mark.parametrize("dtype,inplace", [("u8", True), ("u8", False), ("i8", True)])
+def test_beyond_4gi_elements(hip, dtype, inplace):
+    """Maximum sizes: n = 2^32 + 4099 one-byte elements at a misaligned start.
+
+    The reference's kernels index with `int n` (gloo/cuda.cu:274-401) and its
+    ring-chunked `count`/`bytes_` are `int` (gloo/cuda_allreduce_ring_chunked.h:54-55),
+    so nothing past 2^31 elements is reachable there; the C-ABI takes size_t.
+    A constant fill catches any 32-bit offset wrap both ways: a wrapped in-place
+    kernel would leave the high region at `x` and fold the low one twice.  Spot
+    values near 2^31, 2^32 and the ragged tail are checked against the oracle.
+    """
+    import torch
+    code, npt = oracle.DTYPES[dtype]
+    n = (1 << 32) + 4099
+    off = 3
+    x, y = (7, 250) if dtype == "u8" else (-100, -90)
+    ta = torch.full((n + off + 64,), x, dtype=torch.uint8 if dtype == "u8" else torch.int8, device="cuda")
+    tb = torch.full_like(ta, y)
+    spots = np.array([0, 1, (1 << 31) - 1, 1 << 31, (1 << 32) - 1, 1 << 32, n - 2, n - 1], dtype=np.int64)
+    rng = np.random.default_rng(11)
+    sa = rng.integers(-128 if dtype == "i8" else 0, 128 if dtype == "i8" else 256, spots.size).astype(npt)
+    sb = rng.integers(-128 if dtype == "i8" else 0, 128 if dtype == "i8" else 256, spots.size).astype(npt)
+    idx = torch.from_numpy(spots + off).cuda()
+    ta[idx] = torch.from_numpy(sa).cuda()
+    tb[idx] = torch.from_numpy(sb).cuda()
+    pa, pb = ta.data_ptr() + off, tb.data_ptr() + off
+    if inplace:
+        hip.reduce_ptr("sum", dtype, pa, pb, n)
+        out = ta
+    else:
+        out = torch.zeros_like(ta)
+        hip.reduce3_ptr("sum", dtype, out.data_ptr() + off, pa, pb, n)
+    torch.cuda.synchronize()
+    body = out[off:off + n]
+    want_fill = oracle.reduce3("sum", dtype, np.array([x], npt), np.array([y], npt))[0]
+    eq = body == int(want_fill)
+    eq[torch.from_numpy(spots).cuda()] = True
+    assert bool(eq.all()), "32-bit offset wrap or missed region"
+    del eq
+    got = out[idx].cpu().numpy().view(npt)
+    assert (got == oracle.reduce3("sum", dtype, sa, sb)).all()
+    # guard bytes either side untouched
+    if not inplace:
+        assert bool((out[:off] == 0).all()) and bool((out[off + n:] == 0).all())
+    else:
+        assert bool((out[:off] == x).all()) and bool((out[off + n:] == x).all())
