@@ -235,6 +235,38 @@ bool sliceable(const Plan& plan, int nin, int nout, const std::vector<Access>& r
   return true;
 }
 
+// Upper bound on the interpreter steps buildInterp() emits for the sliced
+// form of `plan`: it mirrors buildInterp's pushes, with the whole-range local
+// steps counted once per piece.  A plan over the device list's capacity
+// (kInterpMaxSteps) must not be proposed for slicing, because a sliced plan
+// has no other route (many small segments of a large new-style call).
+size_t slicedInterpSteps(const Plan& plan, int nin, int nout) {
+  const std::vector<size_t> cuts = userCuts(plan);
+  size_t k = 0;
+  for (const Step& t : plan.steps) {
+    switch (t.kind) {
+      case GLOO_HIP_STEP_DECL_RECV:
+      case GLOO_HIP_STEP_WAIT_SEND:
+      case GLOO_HIP_STEP_FOLD_SRC:
+        break;
+      case GLOO_HIP_STEP_LOCAL_REDUCE: {
+        const size_t srcs = (size_t)std::max(1, t.flags & GLOO_HIP_FROM_INPUTS ? nin : nout);
+        const size_t per =
+            srcs <= GLOO_HIP_MAX_SRCS ? 1 : 1 + (srcs - GLOO_HIP_MAX_SRCS + GLOO_HIP_MAX_SRCS - 2) / (GLOO_HIP_MAX_SRCS - 1);
+        k += cutRange(cuts, t.dst_off, t.length).size() * per;
+        break;
+      }
+      case GLOO_HIP_STEP_LOCAL_BCAST:
+        k += cutRange(cuts, t.dst_off, t.length).size() * (size_t)std::max(0, nout - 1);
+        break;
+      default:
+        k += 1;
+        break;
+    }
+  }
+  return k;
+}
+
 // Most workgroups of a sliced launch (<= kMaxSlices).  Ranks that share a
 // GPU each bring this many, and a slice spins until its peer slice runs, so
 // the default keeps 8 ranks on one GPU co-resident.
@@ -565,7 +597,9 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
             else remote.push_back({kArena, it->second + t.dst_off, t.length});
           }
       }
-      if (ok && sliceable(plan_, (int)inputs_.size(), (int)ptrs_.size(), remote)) proposal = (int32_t)want;
+      if (ok && slicedInterpSteps(plan_, (int)inputs_.size(), (int)ptrs_.size()) <= (size_t)kInterpMaxSteps &&
+          sliceable(plan_, (int)inputs_.size(), (int)ptrs_.size(), remote))
+        proposal = (int32_t)want;
     }
   }
   ArenaRecord rec;

@@ -179,6 +179,10 @@ np.save(out, np.array(res))
     ("bcube", 6, {"GLOO_AMD_TEST_N": "999", "GLOO_AMD_INTERP_SLICE_BYTES": "64"}),
     ("reduce", 4, {"GLOO_AMD_TEST_N": "4097", "GLOO_AMD_INTERP_SLICE_BYTES": "256"}),
     ("ring", 4, {"GLOO_AMD_INTERP": "0"}),              # graph replay / eager route at the default size
+    # many segments: more interpreter steps than the device list holds, so no
+    # rank may propose the sliced form (it has no fallback route)
+    ("reduce", 4, {"GLOO_AMD_MESH": "0", "GLOO_AMD_TEST_N": "8000000"}),
+    ("ring", 4, {"GLOO_AMD_MESH": "0", "GLOO_AMD_TEST_N": "8000000"}),
 ])
 def test_processes(torch, kind, P, env):
     """Ranks as processes (device signalling unless overridden; inboxes over
