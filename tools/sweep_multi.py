@@ -28,7 +28,10 @@ def main():
     g = torch.Generator(device=dev).manual_seed(3)
     sets = [[torch.rand(N, device=dev, generator=g) * 2 - 1 for _ in range(8)] for _ in range(2)]
     dsts = [torch.empty(N, device=dev) for _ in range(2)]
-    for k in range(2, 9):
+    ks = range(2, 9)
+    if "--k" in sys.argv:  # one k only (PMC passes)
+        ks = [int(sys.argv[sys.argv.index("--k") + 1])]
+    for k in ks:
         # bits first: the fused left fold equals the reference's pairwise loop
         ref = sets[0][0].clone()
         for j in range(1, k):
