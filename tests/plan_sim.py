@@ -340,3 +340,29 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
         if sent[key] != consumed.get(key, 0):
             raise ProtocolError(f"{key}: {sent[key]} sent, {consumed.get(key, 0)} consumed")
     return np.array([[user[r][j] for j in range(k)] for r in range(P)])
+
+
+INTERP_MAX_STEPS = 512  # gloo_amd/include/gloo_amd/signal.h kInterpMaxSteps
+MAX_SRCS = 8            # include/gloo_amd.h GLOO_HIP_MAX_SRCS
+
+
+def sliced_interp_steps(algo, P, n, rank, k=1, nin=0, recv=None, elem_size=4, max_seg=0):
+    """Python statement of executor.cc slicedInterpSteps: an upper bound on the
+    device step list buildInterp() emits for `rank`'s sliced plan.  A rank
+    proposes slicing only when this is <= INTERP_MAX_STEPS."""
+    steps, _ = get_plan(algo, rank, P, n, k, recv, nin=nin, elem_size=elem_size, max_seg=max_seg)
+    cuts = user_cuts(steps)
+    total = 0
+    for t in steps:
+        K = t.kind
+        if K in (KIND["DECL_RECV"], KIND["WAIT_SEND"], KIND["FOLD_SRC"]):
+            continue
+        if K == KIND["LOCAL_REDUCE"]:
+            srcs = max(1, nin if t.flags & FROM_INPUTS else k)
+            per = 1 if srcs <= MAX_SRCS else 1 + (srcs - MAX_SRCS + MAX_SRCS - 2) // (MAX_SRCS - 1)
+            total += len(cut_range(cuts, t.dst_off, t.length)) * per
+        elif K == KIND["LOCAL_BCAST"]:
+            total += len(cut_range(cuts, t.dst_off, t.length)) * max(0, k - 1)
+        else:
+            total += 1
+    return total

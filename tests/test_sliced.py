@@ -157,3 +157,20 @@ def test_sliced_new_style_matches_reference(golden_sched, golden_new, src, case)
         for r in range(P):
             for j in range(k):
                 assert (y[r, j].view(np.uint8) == want.view(np.uint8)).all(), (slices, r, j)
+
+
+def test_many_segment_plans_are_not_proposed_for_slicing():
+    """A sliced plan has no fallback route, so a rank proposes slicing only if
+    its device step list fits (executor.cc slicedInterpSteps).  The new-style
+    gloo::reduce on the reference route at 256 MiB with 1 MiB segments, 4 ranks
+    (the 4-rank bench rehearsal that failed before the bound existed), needs
+    far more than the 512 entries; the small default test plans fit."""
+    from plan_sim import INTERP_MAX_STEPS, sliced_interp_steps
+    n = (256 << 20) // 4
+    recv = np.array([0], np.int32)
+    big = [sliced_interp_steps("reduce", 4, n, r, nin=1, recv=recv, max_seg=1 << 20) for r in range(4)]
+    assert max(big) > INTERP_MAX_STEPS, big
+    small = [sliced_interp_steps("reduce", 4, 4097, r, nin=1, recv=recv, max_seg=256 << 10) for r in range(4)]
+    assert max(small) <= INTERP_MAX_STEPS, small
+    ring = [sliced_interp_steps("mesh_allreduce_new", 4, 1001, r, nin=1, max_seg=128 << 10) for r in range(4)]
+    assert 0 < max(ring) <= INTERP_MAX_STEPS, ring
