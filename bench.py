@@ -47,9 +47,10 @@ def parse():
     p.add_argument("--pairs", type=int, default=6, help="rotated (dst, src) pairs")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline sample (seconds of CPU work)")
-    p.add_argument("--cpu-threads", type=int, default=16,
-                   help="threads for the all-cores CPU figure (the box's CPU share)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-config1", action="store_true", help="skip the config-1 CPU allreduce in cpu_baseline")
+    p.add_argument("--config1-seconds", type=float, default=2.0,
+                   help="config 1: minimum seconds per batch (gloo/benchmark default 2 s)")
     p.add_argument("--no-host-staged", action="store_true")
     p.add_argument("--variant", type=int, default=0, help="kernel variant (tuning)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -57,6 +58,8 @@ def parse():
                    help="N>1: skip the config-3 xGMI ring-chunked allreduce section")
     p.add_argument("--allreduce-mib", type=int, default=256, help="config 3: MiB per rank")
     p.add_argument("--allreduce-iters", type=int, default=5)
+    p.add_argument("--quick", action="store_true",
+                   help="N>1: config 3 + one variant, short HD sweep, RS at 16 Mi (rehearsals)")
     return p.parse_args()
 
 
@@ -69,53 +72,122 @@ def relaunch_distributed(args):
     return subprocess.call(cmd)
 
 
+def progress(msg):
+    """One progress line on stderr (every rank): a long multi-rank run keeps
+    writing, and a stuck section names itself."""
+    print(f"[bench r{os.environ.get('RANK', '0')} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def host_cores():
+    """(cores, how): the CPU share this process may use — the cgroup quota
+    (/sys/fs/cgroup/cpu.max) when one is set, else the affinity mask."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) / int(period))), f"cgroup quota {quota}/{period} (/sys/fs/cgroup/cpu.max)"
+    except (OSError, ValueError):
+        pass
+    try:
+        n = len(os.sched_getaffinity(0))
+        return n, "sched_getaffinity (no cgroup CPU quota)"
+    except AttributeError:
+        return os.cpu_count() or 1, "os.cpu_count"
+
+
 def cpu_baseline(args, n):
-    """The reference's gloo::sum<float> on host memory, same in-place form and
-    rotation as the GPU leg; bounded to ~args.cpu_seconds of CPU work."""
+    """The reference's gloo::sum<float> on host memory (64 MiB chunks, the
+    same rotation as the GPU leg), bounded to ~args.cpu_seconds of CPU work:
+    the 2-operand in-place form (how ReductionFunction<T>::sum calls it) and
+    the 3-operand form, on 1 thread (how Gloo calls it) and split over the
+    box's CPU share; plus BASELINE config 1 — the reference's own
+    AllreduceRingChunked<float>, 2 ranks over TCP loopback — with the
+    reference benchmark's methodology (gloo/benchmark/runner.cc:311-363)."""
     import numpy as np
     import oracle
     if oracle.ref_available():
-        fn = oracle.ref_baseline().ref_base_sum_f32
+        L = oracle.ref_baseline()
+        f3 = L.ref_base_sum_f32
+        f2 = L.ref_base_sum2_f32
         kind = "reference"
     else:
-        fn = oracle.lib().oracle_sum_f32_mt
+        f3 = oracle.lib().oracle_sum_f32_mt
+        f2 = lambda a, b, m, t: f3(a, a, b, m, t)  # noqa: E731
         kind = "port"
     pairs = max(2, args.pairs // 2)
     rng = np.random.default_rng(1)
     bufs = [(rng.uniform(-1, 1, n).astype(np.float32), rng.uniform(-1, 1, n).astype(np.float32))
             for _ in range(pairs)]
+    outs = [np.empty(n, np.float32) for _ in range(pairs)]
 
-    def timed(threads, budget):
+    def timed(form, threads, budget):
         done, t0 = 0, time.perf_counter()
         while True:
             d, s = bufs[done % pairs]
-            fn(d.ctypes.data, d.ctypes.data, s.ctypes.data, n, threads)
+            if form == 2:
+                f2(d.ctypes.data, s.ctypes.data, n, threads)
+            else:
+                f3(outs[done % pairs].ctypes.data, d.ctypes.data, s.ctypes.data, n, threads)
             done += 1
             el = time.perf_counter() - t0
             if el >= budget and done >= 3:
                 return done, el
 
-    d, s = bufs[0]
-    fn(d.ctypes.data, d.ctypes.data, s.ctypes.data, n, 1)  # page in
-    calls1, t1 = timed(1, args.cpu_seconds)
-    nt = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    callsn, tn = timed(nt, max(1.0, args.cpu_seconds / 4))
+    for i in range(pairs):  # page in
+        d, s = bufs[i]
+        f3(outs[i].ctypes.data, d.ctypes.data, s.ctypes.data, n, 1)
     alg = 3.0 * n * 4
+    nt, how = host_cores()
+    nt = max(1, min(nt, os.cpu_count() or 1))
+    res = {}
+    for form, budget1 in ((2, args.cpu_seconds * 0.6), (3, args.cpu_seconds * 0.4)):
+        c1, t1 = timed(form, 1, budget1)
+        cn, tn = timed(form, nt, max(1.0, args.cpu_seconds / 5))
+        res[form] = (round(alg * c1 / t1 / GIB, 3), c1, t1, round(alg * cn / tn / GIB, 3), cn, tn)
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
             model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
     except OSError:
         pass
-    return {
-        "value": round(alg * calls1 / t1 / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": kind,
-        "sample": (f"{calls1} calls of gloo::sum<float>(a,a,b,n) in place, n={n} "
-                   f"(64 MiB), {pairs} rotated pairs, {t1:.1f} s, 1 thread as Gloo calls it; "
-                   f"algorithmic bytes 3*n*4"),
-        "all_cores": {"value": round(alg * callsn / tn / GIB, 3), "threads": nt,
-                      "sample": f"{callsn} calls, range split over {nt} std::threads, {tn:.1f} s"},
+    v2, v3 = res[2], res[3]
+    out = {
+        "value": v2[0], "unit": "GiB/s", "cores": 1, "kind": kind,
+        "sample": (f"{v2[1]} calls of gloo::sum<float>(a,b,n) (the in-place 2-operand form, "
+                   f"gloo/math.h:25-28), n={n} (64 MiB), {pairs} rotated pairs, {v2[2]:.1f} s, 1 thread as "
+                   f"Gloo calls it; algorithmic bytes 3*n*4"),
+        "three_operand": {"value": v3[0], "sample": f"{v3[1]} calls of gloo::sum<float>(c,a,b,n), c distinct, "
+                                                    f"1 thread, {v3[2]:.1f} s"},
+        "all_cores": {"value": v2[3], "threads": nt, "threads_from": how,
+                      "three_operand_value": v3[3],
+                      "sample": (f"{v2[4]} (2-operand) + {v3[4]} (3-operand) calls, range split over {nt} "
+                                 f"std::threads, {v2[5]:.1f} + {v3[5]:.1f} s")},
         "cpu_model": model, "host_cpus_visible": os.cpu_count(),
     }
+    if kind == "reference" and not args.no_config1:
+        out["config1_allreduce_ring_chunked"] = config1(oracle, args)
+    return out
+
+
+def config1(oracle, args, n=1 << 24):
+    """BASELINE config 1: the reference's AllreduceRingChunked<float>, size=2,
+    2 ranks (threads) over TCP loopback, n = 16 Mi fp32; 5 warmup runs, then
+    batches of runs until one lasts >= args.config1_seconds; p50 / p99 of the
+    per-iteration latencies and the payload GiB/s n*4/p50
+    (gloo/benchmark/runner.cc:311-363, :497-506)."""
+    import numpy as np
+    cap = 100000
+    buf = (ctypes.c_double * cap)()
+    cnt = ctypes.c_int(0)
+    t0 = time.perf_counter()
+    rc = oracle.ref().ref_allreduce_samples(0, 2, n, 5, args.config1_seconds, buf, cap, ctypes.byref(cnt))
+    if rc:
+        return {"error": oracle.ref().ref_last_error().decode()}
+    s = np.sort(np.array(buf[:cnt.value]))
+    p50, p99 = float(s[len(s) // 2]), float(s[min(len(s) - 1, int(len(s) * 0.99))])
+    return {"elements": n, "ranks": 2, "transport": "tcp loopback (reference)", "samples": int(cnt.value),
+            "p50_ms": round(p50 * 1e3, 3), "p99_ms": round(p99 * 1e3, 3),
+            "payload_gib_s_p50": round(n * 4 / p50 / GIB, 3), "wall_s": round(time.perf_counter() - t0, 1)}
 
 
 def host_staged(torch, hip, n, dev, iters=20):
@@ -261,14 +333,42 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                 else:
                     os.environ[k] = v
 
+    # Result check of config 3 at every world size: rank r's input is
+    # N(0,1) from seed (7, r); after run 1 the values at 4096 sampled
+    # positions must equal the reference schedule's fold at those positions
+    # (gloo/allreduce_ring_chunked.h:102-158: chunk pair q starts on rank q,
+    # every later rank computes `local + incoming`), bit for bit; after the
+    # last run every rank must hold the same bytes.
+    import numpy as np
+    sample = np.unique(np.random.default_rng(11).integers(0, n, 4096))
+    x_np = np.random.default_rng([7, rank]).standard_normal(n, dtype=np.float32)
+    x_all = gather(x_np[sample].tolist())
+    chunks = 2 * world
+    cs = max(256, (n + chunks - 1) // chunks)
+
+    def expected_at_sample():
+        xs = np.array(x_all, dtype=np.float32)  # [world][len(sample)]
+        q = (sample // cs) // 2
+        acc = xs[q, np.arange(len(sample))].copy()
+        for j in range(1, world):
+            acc = xs[(q + j) % world, np.arange(len(sample))] + acc
+        return acc
+
+    want_sample = expected_at_sample()
+
     def ring_once(engine, workspace="device", mesh="1"):
+        progress(f"config 3: ring_chunked engine={engine} workspace={workspace} mesh={mesh}")
+
         def body():
-            buf = torch.ones(n, device=dev)
+            import hashlib
+            buf = torch.from_numpy(x_np).to(dev)
             torch.cuda.synchronize(dev)
             ctx = hip.Context(rank, world, "file:%s/ring_%s_%s_%s" % (obj[0], engine, workspace, mesh),
                               device=dev.index, timeout_ms=60000)
             a = hip.Algorithm(ctx, "ring_chunked", "sum", "f32", [buf.data_ptr()], n, workspace=workspace)
             a.run()
+            got = buf[torch.from_numpy(sample).to(dev)].cpu().numpy()
+            ok_first = bool((got.view(np.uint32) == want_sample.view(np.uint32)).all())
             # timed: steady state (the plan replays as a hipGraph from run 3 on)
             times = []
             for _ in range(args.allreduce_iters):
@@ -287,13 +387,13 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                 red_s += st["reduce_s"]
                 red_b += st["reduce_bytes"]
                 wait_s += st["wait_s"]
-            runs = 1 + args.allreduce_iters + 3
-            want = float(world) ** runs
-            ok = bool((buf[:: max(1, n // 4096)] == want).all()) if want < 2 ** 24 else None
+            torch.cuda.synchronize(dev)
+            dig = hashlib.sha256(buf.cpu().numpy().view(np.uint8).tobytes()).hexdigest()
             a.close()
             ctx.close()
             return {"ms": [round(t * 1e3, 3) for t in times], "reduce_s": red_s, "reduce_b": red_b,
-                    "wait_ms_per_run": round(wait_s / 3 * 1e3, 3), "verified": ok, "graph": graphed}
+                    "wait_ms_per_run": round(wait_s / 3 * 1e3, 3), "first_run_ok": ok_first, "digest": dig,
+                    "graph": graphed}
         try:
             res = with_env({"GLOO_AMD_COPY": engine, "GLOO_AMD_RING_MESH": mesh}, body)
         except Exception as e:  # noqa: BLE001
@@ -312,7 +412,10 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                 "reduce_kernel_gib_s_per_gpu": [round(x, 1) for x in per_gpu],
                 "reduce_kernel_gib_s_min": round(min(per_gpu), 1) if per_gpu else None,
                 "host_wait_ms_per_run_max_profiled": max(g["wait_ms_per_run"] for g in gathered),
-                "verified": all(g["verified"] is not False for g in gathered)}
+                "verified": bool(all(g["first_run_ok"] for g in gathered) and
+                                 len({g["digest"] for g in gathered}) == 1),
+                "verify": "run 1 vs the reference ring fold at 4096 sampled positions on every rank, "
+                          "bit-exact; after the last run every rank's 256 MiB digest equal"}
 
     # default: the mesh plan (batched sends = one multi-destination copy kernel)
     ring = ring_once("auto")
@@ -324,10 +427,11 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         return dict(partial)
     variants = {}
     partial["variants"] = variants
-    variants["mesh_memcpy_forked"] = ring_once("memcpy")
     variants["ring_memcpy"] = ring_once("memcpy", mesh="0")
-    variants["ring_kernel"] = ring_once("kernel", mesh="0")
-    variants["mesh_host_workspace"] = ring_once("auto", "host")
+    if not args.quick:
+        variants["mesh_memcpy_forked"] = ring_once("memcpy")
+        variants["ring_kernel"] = ring_once("kernel", mesh="0")
+        variants["mesh_host_workspace"] = ring_once("auto", "host")
 
     short_sizes = (1 << 10, 64 << 10, 1 << 20, 64 << 20)
     full_sizes = tuple(1 << lg for lg in range(10, 31, 2))  # config 4: 1 KiB .. 1 GiB per rank
@@ -337,14 +441,19 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         def body():
             hd = []
             for nbytes in sizes:
+                progress(f"halving_doubling {label} {nbytes} B")
                 m = max(1, nbytes // 4)
                 try:
-                    b2 = torch.ones(m, device=dev)
+                    # rank r contributes r + 1: run 1 must give P(P+1)/2 in
+                    # every element (exact in fp32), whatever the fold order
+                    b2 = torch.full((m,), float(rank + 1), device=dev)
                     torch.cuda.synchronize(dev)
                     ctx2 = hip.Context(rank, world, "file:%s/hd_%s_%d" % (obj[0], label, nbytes),
                                        device=dev.index, timeout_ms=60000)
                     a2 = hip.Algorithm(ctx2, "halving_doubling", "sum", "f32", [b2.data_ptr()], m)
                     a2.run()
+                    ok = bool((b2 == world * (world + 1) / 2).all())
+                    b2.fill_(1.0)
                     a2.run()
                     ts = []
                     for _ in range(iters):
@@ -356,7 +465,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                     a2.close()
                     ctx2.close()
                     hd.append({"bytes": nbytes, "us": [round(t * 1e6, 1) for t in ts], "graph": md["graph"],
-                               "interp": md["interp"]})
+                               "interp": md["interp"], "ok": ok})
                 except Exception as e:  # noqa: BLE001
                     hd.append({"bytes": nbytes, "error": repr(e)})
             return hd
@@ -369,6 +478,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                 continue
             per = sorted(max(h[i]["us"][k] for h in hd_all) for k in range(iters))
             summary.append({"bytes": nbytes, "us_p50": per[iters // 2], "us_max": per[-1],
+                            "verified": all(h[i]["ok"] for h in hd_all),
                             "launch": "interp" if all(h[i]["interp"] for h in hd_all)
                             else "graph" if all(h[i]["graph"] for h in hd_all) else "eager",
                             "busbw_gib_s": round(2 * (world - 1) / world * nbytes / (per[iters // 2] / 1e6) / GIB,
@@ -388,19 +498,29 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     hd_summary = {}
     partial["halving_doubling"] = hd_summary
     for k, v in hd_variants.items():
-        hd_summary[k] = hd_sweep(k, v, full_sizes if k in ("mesh", "reference_route") else short_sizes)
+        if args.quick and k not in ("mesh", "reference_route"):
+            continue
+        big = k in ("mesh", "reference_route") and not args.quick
+        hd_summary[k] = hd_sweep(k, v, full_sizes if big else short_sizes)
 
     # Config 5: reduce-scatter (HD), fp16 / bf16 buckets, every op, 16 Mi
     # elements per rank, recvElems = an even split.
     def rs_once(dtype, op, env, m=16 << 20):
+        progress(f"reduce_scatter {dtype} {op} {env} {m}")
+
         def body():
             recv = [m // world + (1 if r < m % world else 0) for r in range(world)]
-            b = torch.ones(m, dtype=torch.float16 if dtype == "f16" else torch.bfloat16, device=dev)
+            # rank r contributes 1 + r % 2: every op's result is exact in
+            # fp16 / bf16 for P <= 8, so run 1's block is checked whole
+            vals = [1.0 + r % 2 for r in range(world)]
+            want = {"sum": sum(vals), "product": float(np.prod(vals)), "max": max(vals), "min": min(vals)}[op]
+            b = torch.full((m,), vals[rank], dtype=torch.float16 if dtype == "f16" else torch.bfloat16, device=dev)
             torch.cuda.synchronize(dev)
             c = hip.Context(rank, world, "file:%s/rs_%s_%s_%s_%d" % (obj[0], dtype, op, env.get("GLOO_AMD_MESH", "1"),
                                                                      m), device=dev.index, timeout_ms=60000)
             a = hip.Algorithm(c, "reduce_scatter", op, dtype, [b.data_ptr()], m, recv_elems=recv)
             a.run()
+            ok = bool((b[:recv[rank]].float() == want).all())
             a.run()
             ts = []
             for _ in range(10):
@@ -410,7 +530,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                 ts.append(time.perf_counter() - t0)
             a.close()
             c.close()
-            return {"us": [round(t * 1e6, 1) for t in ts]}
+            return {"us": [round(t * 1e6, 1) for t in ts], "ok": ok}
         try:
             res = with_env(env, body)
         except Exception as e:  # noqa: BLE001
@@ -422,9 +542,13 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         nbytes = m * 2
         return {"dtype": dtype, "op": op, "route": "reference" if env.get("GLOO_AMD_MESH") == "0" else "mesh",
                 "elements_per_rank": m, "us_p50": per[5], "us_max": per[-1],
+                "verified": all(x["ok"] for x in g),
                 "busbw_gib_s": round((world - 1) / world * nbytes / (per[5] / 1e6) / GIB, 2)}
 
     rs_summary = [rs_once(dt, op, {}) for dt in ("f16", "bf16") for op in ("sum", "product", "min", "max")]
+    if args.quick:
+        partial["reduce_scatter"] = rs_summary
+        return dict(partial)
     rs_summary += [rs_once(dt, "sum", {"GLOO_AMD_MESH": "0"}) for dt in ("f16", "bf16")]
     partial["reduce_scatter"] = rs_summary
     # the other two bucket sizes of SURVEY 8(d) config 5: 1 Mi and 64 Mi elements per rank
@@ -435,6 +559,8 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     # and gloo::reduce to rank 0, fp32 sum, separate input and output; the
     # derived mesh route (default) and the reference's exchange route.
     def newstyle(kind, nbytes, env=None):
+        progress(f"new style {kind} {nbytes} B {env}")
+
         def body():
             m = max(1, nbytes // 4)
             inp = torch.ones(m, device=dev)
@@ -522,6 +648,7 @@ def main():
         d, s = pairs[i % len(pairs)]
         hip.reduce_ptr("sum", "f32", d.data_ptr(), s.data_ptr(), n, sh)
 
+    progress(f"config 2: {args.warmup} warmup + {args.steps} timed steps")
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
@@ -615,6 +742,7 @@ def main():
                 print(json.dumps(out), flush=True)
             os._exit(0)
 
+        progress("N>1 sections")
         wd = arm_watchdog(300, fire)
         xr = xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial)
         wd.cancel()

@@ -146,7 +146,7 @@ __device__ __forceinline__ typename Tr::Storage apply(typename Tr::Storage a,
 
 // Apply the op lane-wise to one 16-byte packet.
 template <class Tr, int OP>
-__device__ __forceinline__ u32x4 apply_packet(u32x4 a, u32x4 b) {
+__device__ __forceinline__ u32x4 generic_packet(u32x4 a, u32x4 b) {
   using S = typename Tr::Storage;
   constexpr int kV = 16 / sizeof(S);
   union P {
@@ -159,6 +159,10 @@ __device__ __forceinline__ u32x4 apply_packet(u32x4 a, u32x4 b) {
 #pragma unroll
   for (int i = 0; i < kV; i++) pc.e[i] = apply<Tr, OP>(pa.e[i], pb.e[i]);
   return pc.v;
+}
+template <class Tr, int OP>
+__device__ __forceinline__ u32x4 apply_packet(u32x4 a, u32x4 b) {
+  return generic_packet<Tr, OP>(a, b);
 }
 
 // Byte-lane SWAR specialisations: 16 int8/uint8 adds in 4 dword ops each
@@ -260,6 +264,62 @@ __global__ __launch_bounds__(BLOCK) void reduce_vec_kernel(
 #pragma unroll
   for (int u = 0; u < UNROLL; u++)
     bstore<SAUX>(rc, lane_off + u * BLOCK * 16, apply_packet<Tr, OP>(x[u], y[u]));
+}
+
+// Software-pipelined persistent form (measurement variants 9-12): a grid of
+// G workgroups walks tiles g, g + G, ...; the loads of the next tile are in
+// flight while the current one is combined and stored, so a workgroup keeps
+// two tiles outstanding and the grid pays one dispatch ramp for many tiles.
+template <class Tr, int OP, int UNROLL, int BLOCK, int LAUX, int SAUX>
+__global__ __launch_bounds__(BLOCK) void reduce_vec_pipe_kernel(
+    typename Tr::Storage* c, const typename Tr::Storage* a,
+    const typename Tr::Storage* b, size_t n, size_t head) {
+  using S = typename Tr::Storage;
+  constexpr int kV = 16 / sizeof(S);
+  constexpr uint32_t kTileBytes = (uint32_t)BLOCK * UNROLL * 16;
+  const size_t nvec = (n - head) / kV;
+  if (blockIdx.x == 0) edges<Tr, OP>(c, a, b, head, head + nvec * kV, n);
+  const size_t body = nvec * 16;
+  const Src sa = src_of(a + head), sb = src_of(b + head);
+  const char* cbase = reinterpret_cast<const char*>(c + head);
+  const uint32_t lane_off = threadIdx.x * 16u;
+  const size_t stride = (size_t)gridDim.x * kTileBytes;
+  size_t base = (size_t)blockIdx.x * kTileBytes;
+  if (base >= body) return;
+  u32x4 x[UNROLL], y[UNROLL], nx[UNROLL], ny[UNROLL];
+  {
+    const uint32_t bytes = (uint32_t)((body - base) < kTileBytes ? (body - base) : kTileBytes);
+    const auto ra = make_rsrc(sa.base + base, bytes + sa.mis);
+    const auto rb = make_rsrc(sb.base + base, bytes + sb.mis);
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) x[u] = bload<LAUX>(ra, lane_off + u * BLOCK * 16, sa.mis);
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) y[u] = bload<LAUX>(rb, lane_off + u * BLOCK * 16, sb.mis);
+  }
+  for (;;) {
+    const size_t next = base + stride;
+    const bool more = next < body;
+    if (more) {
+      const uint32_t nbytes = (uint32_t)((body - next) < kTileBytes ? (body - next) : kTileBytes);
+      const auto ra = make_rsrc(sa.base + next, nbytes + sa.mis);
+      const auto rb = make_rsrc(sb.base + next, nbytes + sb.mis);
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) nx[u] = bload<LAUX>(ra, lane_off + u * BLOCK * 16, sa.mis);
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) ny[u] = bload<LAUX>(rb, lane_off + u * BLOCK * 16, sb.mis);
+    }
+    const uint32_t bytes = (uint32_t)((body - base) < kTileBytes ? (body - base) : kTileBytes);
+    const auto rc = make_rsrc(cbase + base, bytes);
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) bstore<SAUX>(rc, lane_off + u * BLOCK * 16, apply_packet<Tr, OP>(x[u], y[u]));
+    if (!more) break;
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      x[u] = nx[u];
+      y[u] = ny[u];
+    }
+    base = next;
+  }
 }
 
 // Multi-source left fold dst = ((s0 op s1) op s2) ... in one pass.
@@ -448,33 +508,40 @@ constexpr int kInterpBlock = 512;
 constexpr int kInterpCopyUnroll = 4;
 constexpr int kInterpFoldUnroll = 2;
 
+// Bytes [0, n) of src to dst.  The destination is brought to a 16-byte
+// boundary element-wise (head); the body then moves in 16-byte packets
+// whatever the source's misalignment (Src: aligned-down descriptor base, the
+// byte offset in the buffer instruction's soffset, as reduce_vec_kernel);
+// the ragged tail goes byte-wise.  Per pass the descriptors are rebuilt at
+// the pass base, so 32-bit lane offsets suffice, and the range check drops
+// the packets past the body.
 __device__ __forceinline__ void interp_copy(char* dst, const char* src, uint64_t n) {
   const uint64_t t = threadIdx.x;
-  uint64_t done = 0;
-  if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
-    const uint64_t nv = n / 16;
-    const u32x4* s = reinterpret_cast<const u32x4*>(src);
-    u32x4* d = reinterpret_cast<u32x4*>(dst);
-    for (uint64_t b = 0; b < nv; b += (uint64_t)kInterpBlock * kInterpCopyUnroll) {
-      u32x4 v[kInterpCopyUnroll];
+  uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+  if (head > n) head = n;
+  if (t < head) dst[t] = src[t];
+  const uint64_t body = (n - head) / 16 * 16;
+  char* d = dst + head;
+  const Src ss = src_of(src + head);
+  constexpr uint64_t kPass = (uint64_t)kInterpBlock * kInterpCopyUnroll * 16;
+  const uint32_t lane_off = (uint32_t)t * 16u;
+  for (uint64_t b = 0; b < body; b += kPass) {
+    const uint32_t bytes = (uint32_t)(body - b < kPass ? body - b : kPass);
+    const auto rs = make_rsrc(ss.base + b, bytes + ss.mis);
+    const auto rd = make_rsrc(d + b, bytes);
+    u32x4 v[kInterpCopyUnroll];
 #pragma unroll
-      for (int u = 0; u < kInterpCopyUnroll; u++) {
-        const uint64_t i = b + (uint64_t)u * kInterpBlock + t;
-        if (i < nv) v[u] = s[i];
-      }
+    for (int u = 0; u < kInterpCopyUnroll; u++) v[u] = bload<0>(rs, lane_off + u * kInterpBlock * 16, ss.mis);
 #pragma unroll
-      for (int u = 0; u < kInterpCopyUnroll; u++) {
-        const uint64_t i = b + (uint64_t)u * kInterpBlock + t;
-        if (i < nv) d[i] = v[u];
-      }
-    }
-    done = nv * 16;
+    for (int u = 0; u < kInterpCopyUnroll; u++) bstore<0>(rd, lane_off + u * kInterpBlock * 16, v[u]);
   }
-  for (uint64_t i = done + t; i < n; i += kInterpBlock) dst[i] = src[i];
+  for (uint64_t i = head + body + t; i < n; i += kInterpBlock) dst[i] = src[i];
 }
 
 // dst[i] = fold over the step's sources (mode as launchFold) for n elements:
-// 16-byte packets when every operand is 16-byte aligned, elements after.
+// the destination's head element-wise up to a 16-byte boundary, then
+// 16-byte packets with every source at its own misalignment (soffset, as
+// interp_copy), then the ragged tail element-wise.
 template <class Tr, int OP>
 __device__ __forceinline__ void interp_fold(const InterpStep& st, uint64_t lo, uint64_t hi) {
   using S = typename Tr::Storage;
@@ -486,24 +553,40 @@ __device__ __forceinline__ void interp_fold(const InterpStep& st, uint64_t lo, u
   const uint64_t t = threadIdx.x;
   const char* src[GLOO_HIP_MAX_SRCS];
   char* dstp = st.dst + lo * sizeof(S);
-  uintptr_t align = (uintptr_t)dstp;
 #pragma unroll
-  for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++) {
-    src[j] = j < ns ? st.src[j] + lo * sizeof(S) : nullptr;
-    align |= (uintptr_t)src[j];
-  }
-  const uint64_t nv = (align & 15) ? 0 : n / kV;
-  u32x4* dv = reinterpret_cast<u32x4*>(dstp);
-  for (uint64_t b = 0; b < nv; b += (uint64_t)kInterpBlock * kU) {
+  for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++) src[j] = j < ns ? st.src[j] + lo * sizeof(S) : nullptr;
+  auto one = [&](uint64_t i) {
+    S e[GLOO_HIP_MAX_SRCS];
+#pragma unroll
+    for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
+      if (j < ns) e[j] = reinterpret_cast<const S*>(src[j])[i];
+    if (mode == 2) {
+      reinterpret_cast<S*>(dstp)[i] = tree_fold<Tr, OP>(e, ns);
+    } else {
+      S acc = e[0];
+#pragma unroll
+      for (int j = 1; j < GLOO_HIP_MAX_SRCS; j++)
+        if (j < ns) acc = mode == 1 ? apply<Tr, OP>(e[j], acc) : apply<Tr, OP>(acc, e[j]);
+      reinterpret_cast<S*>(dstp)[i] = acc;
+    }
+  };
+  uint64_t head = ((16 - ((uintptr_t)dstp & 15)) & 15) / sizeof(S);
+  if (head > n) head = n;
+  const uint64_t nv = (n - head) / kV;
+  const uint64_t body = nv * 16;
+  char* dbody = dstp + head * sizeof(S);
+  constexpr uint64_t kPass = (uint64_t)kInterpBlock * kU * 16;
+  const uint32_t lane_off = (uint32_t)t * 16u;
+  for (uint64_t b = 0; b < body; b += kPass) {
+    const uint32_t bytes = (uint32_t)(body - b < kPass ? body - b : kPass);
     u32x4 v[GLOO_HIP_MAX_SRCS][kU];
 #pragma unroll
     for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
       if (j < ns) {
+        const Src sj = src_of(src[j] + head * sizeof(S));
+        const auto rj = make_rsrc(sj.base + b, bytes + sj.mis);
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
-          const uint64_t i = b + (uint64_t)u * kInterpBlock + t;
-          v[j][u] = i < nv ? reinterpret_cast<const u32x4*>(src[j])[i] : u32x4{0, 0, 0, 0};
-        }
+        for (int u = 0; u < kU; u++) v[j][u] = bload<0>(rj, lane_off + u * kInterpBlock * 16, sj.mis);
       }
     if (mode == 2) {
 #pragma unroll
@@ -512,7 +595,7 @@ __device__ __forceinline__ void interp_fold(const InterpStep& st, uint64_t lo, u
 #pragma unroll
           for (int j = 0; j < w / 2; j++)
 #pragma unroll
-            for (int u = 0; u < kU; u++) v[j][u] = apply_packet<Tr, OP>(v[2 * j][u], v[2 * j + 1][u]);
+            for (int u = 0; u < kU; u++) v[j][u] = generic_packet<Tr, OP>(v[2 * j][u], v[2 * j + 1][u]);
         }
     } else {
 #pragma unroll
@@ -520,31 +603,16 @@ __device__ __forceinline__ void interp_fold(const InterpStep& st, uint64_t lo, u
         if (j < ns) {
 #pragma unroll
           for (int u = 0; u < kU; u++)
-            v[0][u] = mode == 1 ? apply_packet<Tr, OP>(v[j][u], v[0][u]) : apply_packet<Tr, OP>(v[0][u], v[j][u]);
+            v[0][u] = mode == 1 ? generic_packet<Tr, OP>(v[j][u], v[0][u]) : generic_packet<Tr, OP>(v[0][u], v[j][u]);
         }
     }
+    const auto rd = make_rsrc(dbody + b, bytes);
 #pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const uint64_t i = b + (uint64_t)u * kInterpBlock + t;
-      if (i < nv) dv[i] = v[0][u];
-    }
+    for (int u = 0; u < kU; u++) bstore<0>(rd, lane_off + u * kInterpBlock * 16, v[0][u]);
   }
-  S* dst = reinterpret_cast<S*>(dstp);
-  for (uint64_t i = nv * kV + t; i < n; i += kInterpBlock) {
-    S e[GLOO_HIP_MAX_SRCS];
-#pragma unroll
-    for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
-      if (j < ns) e[j] = reinterpret_cast<const S*>(src[j])[i];
-    if (mode == 2) {
-      dst[i] = tree_fold<Tr, OP>(e, ns);
-    } else {
-      S acc = e[0];
-#pragma unroll
-      for (int j = 1; j < GLOO_HIP_MAX_SRCS; j++)
-        if (j < ns) acc = mode == 1 ? apply<Tr, OP>(e[j], acc) : apply<Tr, OP>(acc, e[j]);
-      dst[i] = acc;
-    }
-  }
+  // the head [0, head) and the ragged tail [head + nv * kV, n), one loop
+  const uint64_t tail0 = head + nv * kV, edge = head + (n - tail0);
+  for (uint64_t k = t; k < edge; k += kInterpBlock) one(k < head ? k : tail0 + (k - head));
 }
 
 template <class Tr, int OP>
@@ -721,6 +789,19 @@ int launch_vec(void* c, const void* a, const void* b, size_t n, size_t head, hip
   return check_launch("reduce_vec_kernel");
 }
 
+template <class Tr, int OP, int UNROLL, int BLOCK, int LAUX, int SAUX>
+int launch_vec_pipe(void* c, const void* a, const void* b, size_t n, size_t head, size_t maxGrid, hipStream_t s) {
+  using S = typename Tr::Storage;
+  constexpr int kV = 16 / sizeof(S);
+  const size_t nvec = (n - head) / kV;
+  size_t grid = ceil_div(nvec, (size_t)BLOCK * UNROLL);
+  if (grid > maxGrid) grid = maxGrid;
+  if (grid == 0) grid = 1;
+  reduce_vec_pipe_kernel<Tr, OP, UNROLL, BLOCK, LAUX, SAUX><<<dim3((unsigned)grid), dim3(BLOCK), 0, s>>>(
+      static_cast<S*>(c), static_cast<const S*>(a), static_cast<const S*>(b), n, head);
+  return check_launch("reduce_vec_pipe_kernel");
+}
+
 template <class Tr, int OP>
 int launch3(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
   using S = typename Tr::Storage;
@@ -740,6 +821,12 @@ int launch3(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
       case 3: return launch_vec<Tr, OP, 1, 512, kAuxNT, kAuxNT>(c, a, b, n, head, s);
       case 4: return launch_vec<Tr, OP, 2, 512, kAuxNT, 0>(c, a, b, n, head, s);
       case 5: return launch_vec<Tr, OP, 2, 1024, kAuxNT, kAuxNT>(c, a, b, n, head, s);
+      case 9: return launch_vec_pipe<Tr, OP, 2, 512, kAuxNT, kAuxNT>(c, a, b, n, head, 256, s);
+      case 10: return launch_vec_pipe<Tr, OP, 2, 512, kAuxNT, kAuxNT>(c, a, b, n, head, 512, s);
+      case 11: return launch_vec_pipe<Tr, OP, 2, 512, kAuxNT, kAuxNT>(c, a, b, n, head, 1024, s);
+      case 12: return launch_vec_pipe<Tr, OP, 2, 512, kAuxNT, kAuxNT>(c, a, b, n, head, 2048, s);
+      case 13: return launch_vec_pipe<Tr, OP, 1, 512, kAuxNT, kAuxNT>(c, a, b, n, head, 1024, s);
+      case 14: return launch_vec_pipe<Tr, OP, 2, 256, kAuxNT, kAuxNT>(c, a, b, n, head, 2048, s);
       default: break;
     }
   }

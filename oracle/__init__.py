@@ -82,6 +82,11 @@ def ref():
                                              ctypes.c_void_p, ctypes.c_void_p]
         L.ref_reduce_new.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
                                      ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.ref_allreduce_timed.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_double)]
+        L.ref_allreduce_samples.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                            ctypes.c_double, ctypes.POINTER(ctypes.c_double), ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_int)]
         L.ref_last_error.restype = ctypes.c_char_p
         _ref = L
     return _ref
@@ -94,6 +99,7 @@ def ref_baseline():
         L = ctypes.CDLL(os.path.join(HERE, "_ref", "libgloo_ref_baseline.so"))
         L.ref_base_sum_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_size_t, ctypes.c_int]
+        L.ref_base_sum2_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         _ref_base = L
     return _ref_base
 

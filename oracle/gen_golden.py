@@ -270,9 +270,87 @@ def gen_newstyle():
     print("newstyle_golden.npz:", len(out), "arrays")
 
 
+def gen_bw():
+    """bw_golden.json + bw_golden.npz: the reference's outputs in the
+    bandwidth regime of BASELINE configs 3-5 and at the reference's large-P
+    test grid (gloo/test/allreduce_test.cc:261-269,
+    gloo/test/reduce_scatter_test.cc:79-196).
+
+    The big cases keep only seed + per-rank SHA-256 digest + sampled values
+    (tests/bw_inputs.py draws the inputs identically on the GPU box); the
+    large-P cases are small and keep whole arrays."""
+    import json
+    import time
+    sys.path.insert(0, os.path.join(os.path.dirname(OUT)))
+    import bw_inputs as bw
+    seed = SEED + 3
+    big = [("ring_chunked", "sum", "f32", 8, 1 << 26),        # config 3: 256 MiB per rank
+           ("halving_doubling", "sum", "f32", 8, 1 << 22),    # config 4, 16 MiB per rank
+           ("halving_doubling", "sum", "f32", 8, 5000011),    # ragged: misaligned chunk offsets
+           ("ring_chunked", "max", "f32", 8, 10000019)]
+    big += [("reduce_scatter", op, dt, 8, 1 << 20) for dt in ("f16", "bf16")
+            for op in ("sum", "product", "max", "min")]          # config 5
+    big += [("reduce_scatter", "sum", "f32", 8, 1000003)]
+    cases = []
+    for i, (algo, op, dtype, P, n) in enumerate(big):
+        t0 = time.time()
+        cs = seed + i
+        x = np.stack([bw.make_input(dtype, op, n, cs, r) for r in range(P)])
+        key = f"{algo}/{op}/{dtype}/P{P}/n{n}"
+        if algo == "reduce_scatter":
+            recv = bw.even_recv(P, n)
+            y = ref_reduce_scatter(op, dtype, x, np.array(recv, np.int32))
+            outs = [y[r, :recv[r]] for r in range(P)]
+        else:
+            recv = None
+            y = ref_allreduce(algo, op, dtype, x[:, None, :])[:, 0]
+            outs = [y[r] for r in range(P)]
+            assert all((o.view(np.uint8) == outs[0].view(np.uint8)).all() for o in outs), key
+        samples = []
+        for r in range(P):
+            idx = bw.sample_index(len(outs[r]))
+            samples.append({"idx": idx.tolist(), "val": outs[r][idx].view(
+                np.uint32 if outs[r].dtype.itemsize == 4 else np.uint16).tolist()})
+        cases.append({"key": key, "algo": algo, "op": op, "dtype": dtype, "P": P, "n": n, "seed": cs,
+                      "recv": recv, "digests": [bw.digest(o) for o in outs], "samples": samples})
+        print(f"bw {key}: {time.time() - t0:.1f} s", flush=True)
+        del x, y, outs
+    with open(os.path.join(OUT, "bw_golden.json"), "w") as f:
+        json.dump({"generator": "oracle/gen_golden.py bw (reference: oracle/_ref/libgloo_ref.so)",
+                   "inputs": "tests/bw_inputs.py make_input(dtype, op, n, seed, rank)",
+                   "cases": cases}, f, indent=0)
+    # large P: the reference's own test grid beyond the mesh range (P > 8)
+    rng = np.random.default_rng(seed + 100)
+    out = {}
+    for P in (9, 13, 16, 24, 32):
+        for n in (1, 64, 1000):
+            x = sched_inputs("f32", "sum", (P, 1, n), rng)
+            y = ref_allreduce("halving_doubling", "sum", "f32", x)
+            assert all((y[r, 0].view(np.uint8) == y[0, 0].view(np.uint8)).all() for r in range(P))
+            key = f"halving_doubling/sum/f32/P{P}/k1/n{n}"
+            out[key + "/in"], out[key + "/out"] = x, y[0, 0].copy()
+    for P in (9, 13, 16, 24, 32):
+        for n in (100, 1000):
+            x = sched_inputs("f32", "sum", (P, n), rng)
+            recv = even_recv(P, n)
+            y = ref_reduce_scatter("sum", "f32", x, recv)
+            key = f"reduce_scatter/sum/f32/P{P}/n{n}"
+            out[key + "/in"], out[key + "/recv"] = x, recv
+            out[key + "/out"] = np.concatenate([y[r, :recv[r]] for r in range(P)])
+    x = sched_inputs("f16", "max", (16, 1000), rng)
+    recv = even_recv(16, 1000)
+    y = ref_reduce_scatter("max", "f16", x, recv)
+    out["reduce_scatter/max/f16/P16/n1000/in"], out["reduce_scatter/max/f16/P16/n1000/recv"] = x, recv
+    out["reduce_scatter/max/f16/P16/n1000/out"] = np.concatenate([y[r, :recv[r]] for r in range(16)])
+    np.savez_compressed(os.path.join(OUT, "bw_golden.npz"), **out)
+    print("bw_golden.json:", len(cases), "cases; bw_golden.npz:", len(out), "arrays")
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["math", "sched", "newstyle"]
+    if "bw" in which:
+        gen_bw()
     if "math" in which:
         gen_math()
     if "sched" in which:

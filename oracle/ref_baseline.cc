@@ -10,11 +10,12 @@
 
 #include "gloo/math.h"
 
-extern "C" {
+namespace {
 
-void ref_base_sum_f32(float* c, const float* a, const float* b, size_t n, int nthreads) {
+template <typename F>
+void split(size_t n, int nthreads, F&& fn) {
   if (nthreads <= 1) {
-    gloo::sum<float>(c, a, b, n);
+    fn(0, n);
     return;
   }
   std::vector<std::thread> ts;
@@ -23,9 +24,26 @@ void ref_base_sum_f32(float* c, const float* a, const float* b, size_t n, int nt
     const size_t lo = per * t;
     if (lo >= n) break;
     const size_t len = (lo + per > n) ? n - lo : per;
-    ts.emplace_back([=] { gloo::sum<float>(c + lo, a + lo, b + lo, len); });
+    ts.emplace_back([=] { fn(lo, len); });
   }
   for (auto& t : ts) t.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+// The 3-operand form gloo::sum<T>(void* c, const void* a, const void* b,
+// size_t n) (gloo/math.h:15-23); c may alias a.
+void ref_base_sum_f32(float* c, const float* a, const float* b, size_t n, int nthreads) {
+  split(n, nthreads, [=](size_t lo, size_t len) { gloo::sum<float>(c + lo, a + lo, b + lo, len); });
+}
+
+// The in-place 2-operand form gloo::sum<T>(T* a, const T* b, size_t n)
+// (gloo/math.h:25-28), the pointer ReductionFunction<T>::sum holds
+// (gloo/algorithm.h:84-86).
+void ref_base_sum2_f32(float* a, const float* b, size_t n, int nthreads) {
+  split(n, nthreads, [=](size_t lo, size_t len) { gloo::sum<float>(a + lo, b + lo, len); });
 }
 
 }  // extern "C"

@@ -19,6 +19,7 @@
 // bf16 uses c10::BFloat16 from the installed PyTorch headers, the type the
 // reference's CUDA bf16 instantiations name (gloo/cuda.cu:394-401).
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -351,6 +352,62 @@ int ref_allreduce_timed(int algo, int P, size_t n, int iters, double* sec) {
   double m = 0;
   for (double v : per) m = v > m ? v : m;
   *sec = m;
+  return rc;
+}
+
+// BASELINE config 1 with the reference benchmark's methodology
+// (gloo/benchmark/runner.cc:311-363): `warmup` untimed-for-the-result runs,
+// an iteration count from the warmup median so one batch lasts about
+// `min_seconds`, batches grown x2 until a batch's per-rank time exceeds
+// `min_seconds` (rank 0 decides, every rank follows), and every iteration of
+// every rank of the last batch kept as a latency sample (seconds).  At most
+// `max_samples` are written; *count receives how many.
+int ref_allreduce_samples(int algo, int P, size_t n, int warmup, double min_seconds, double* samples,
+                          int max_samples, int* count) {
+  std::vector<float> data((size_t)P * n, 1.0f);
+  const auto* fn = gloo::ReductionFunction<float>::sum;
+  Barrier bar(P);
+  std::atomic<long> iterations{0};
+  std::atomic<int> done{0};
+  std::vector<std::vector<double>> per(P);
+  int rc = spawn(P, [&](std::shared_ptr<gloo::Context> ctx) {
+    const int r = ctx->rank;
+    std::vector<float*> ptrs{data.data() + (size_t)r * n};
+    std::unique_ptr<gloo::Algorithm> a;
+    if (algo == ALGO_RING_CHUNKED) a.reset(new gloo::AllreduceRingChunked<float>(ctx, ptrs, (int)n, fn));
+    else a.reset(new gloo::AllreduceHalvingDoubling<float>(ctx, ptrs, (int)n, fn));
+    auto timeOne = [&] {
+      const auto t0 = std::chrono::steady_clock::now();
+      a->run();
+      return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    };
+    std::vector<double> w;
+    for (int i = 0; i < std::max(1, warmup); i++) w.push_back(timeOne());
+    std::sort(w.begin(), w.end());
+    if (r == 0) iterations = std::max(1L, (long)(min_seconds / std::max(1e-9, w[w.size() / 2])));
+    bar.wait();
+    for (;;) {
+      const long it = iterations.load();
+      std::vector<double> s;
+      for (long i = 0; i < it; i++) s.push_back(timeOne());
+      double total = 0;
+      for (double v : s) total += v;
+      per[r] = std::move(s);
+      if (r == 0) {
+        const bool enough = total > min_seconds || it >= 1000000;
+        done = enough ? 1 : 0;
+        if (!enough) iterations = std::max(it + 1, (long)(it * 2));
+      }
+      bar.wait();
+      if (done.load()) break;
+      bar.wait();  // nobody re-reads `done` before rank 0 rewrites it
+    }
+  });
+  int k = 0;
+  for (auto& s : per)
+    for (double v : s)
+      if (k < max_samples) samples[k++] = v;
+  *count = k;
   return rc;
 }
 

@@ -20,14 +20,16 @@ FOOT = 1 << 30
 
 VARIANTS = {0: "default: unroll2 block512 nt-load nt-store", 1: "unroll2 block256", 2: "unroll4 block256",
             3: "unroll1 block512", 4: "unroll2 block512 nt-load plain-store", 5: "unroll2 block1024",
-            6: "unroll1 block1024", 7: "unroll2 block512 store nt|sc1", 8: "unroll3 block512"}
+            6: "unroll1 block1024", 7: "unroll2 block512 store nt|sc1", 8: "unroll3 block512",
+            9: "pipelined persistent grid<=256", 10: "pipelined grid<=512", 11: "pipelined grid<=1024",
+            12: "pipelined grid<=2048", 13: "pipelined unroll1 grid<=1024", 14: "pipelined block256 grid<=2048"}
 
 
 def main():
     sizes = [64, 256, 1024, 4096, 16384, 65536, 262144]
     variants = [0]
     if "--variants" in sys.argv:  # the ring-chunk regime per kernel variant
-        sizes, variants = [4096, 16384], list(VARIANTS)
+        sizes, variants = [4096, 16384, 65536], [0, 9, 10, 11, 12, 13, 14]
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream().cuda_stream
     pool_a = torch.empty(FOOT // 4, device=dev).uniform_(-1, 1)
