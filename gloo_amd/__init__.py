@@ -48,7 +48,7 @@ OP_NAMES = {"sum": ReductionType.SUM, "product": ReductionType.PRODUCT,
 
 EXPORTED = ("gloo_hip_reduce", "gloo_hip_reduce3", "gloo_hip_reduce_multi",
             "gloo_hip_dtype_size", "gloo_hip_last_error", "gloo_hip_version",
-            "gloo_hip_set_variant", "gloo_hip_plan")
+            "gloo_hip_set_variant", "gloo_hip_plan", "gloo_hip_reduce_staged")
 
 
 class GlooHipError(RuntimeError):
@@ -76,6 +76,7 @@ def _load():
     L.gloo_hip_last_error.restype = ctypes.c_char_p
     L.gloo_hip_version.restype = ctypes.c_char_p
     L.gloo_hip_set_variant.argtypes = [ctypes.c_int]
+    L.gloo_hip_reduce_staged.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, vp, vp, sz, vp]
     return L
 
 
@@ -119,6 +120,13 @@ def reduce_multi_ptr(op, dtype, dst, srcs, n, stream=0):
     arr = (ctypes.c_void_p * len(srcs))(*srcs)
     _check(lib.gloo_hip_reduce_multi(_as_op(op), _as_dtype(dtype), dst, arr, len(srcs), n,
                                      stream or None))
+
+
+def reduce_staged(op, dtype, host_dst, host_src, n, dev_dst, dev_src, piece_elems=0, stream=0):
+    """Host-staged chunk reduction (gloo_hip_reduce_staged): host_dst op=
+    host_src through device scratch, copies and kernel pipelined in pieces."""
+    _check(lib.gloo_hip_reduce_staged(_as_op(op), _as_dtype(dtype), host_dst, host_src, n, dev_dst, dev_src,
+                                      piece_elems, stream or None))
 
 
 def set_variant(v):
@@ -219,7 +227,7 @@ def _bind_collectives(L):
 
 
 _bind_collectives(lib)
-EXPORTED = EXPORTED + ("gloo_hip_context_create", "gloo_hip_context_destroy",
+EXPORTED = EXPORTED + ("gloo_hip_context_create", "gloo_hip_context_create_ex", "gloo_hip_context_destroy",
                        "gloo_hip_algorithm_create", "gloo_hip_algorithm_run",
                        "gloo_hip_algorithm_destroy", "gloo_hip_algorithm_wait_seconds",
                        "gloo_hip_algorithm_set_profiling", "gloo_hip_algorithm_stats",

@@ -27,7 +27,7 @@ int guarded(F&& f) {
     f();
     return GLOO_HIP_OK;
   } catch (const gloo_amd::IoException& e) {
-    return gloo_amd::setError(-5, std::string("IoException: ") + e.what());
+    return gloo_amd::setError(GLOO_HIP_EIO, std::string("IoException: ") + e.what());
   } catch (const std::exception& e) {
     return gloo_amd::setError(GLOO_HIP_EINVAL_ARG, e.what());
   } catch (...) {
@@ -74,6 +74,18 @@ int gloo_hip_context_create(int rank, int size, const char* store_url, int devic
     c->ctx = std::make_shared<gloo_amd::Context>(
         rank, size, std::chrono::milliseconds(timeout_ms > 0 ? timeout_ms : 30000));
     c->ctx->connect(gloo_amd::openStore(store_url), device);
+    *out = c.release();
+  });
+}
+
+int gloo_hip_context_create_ex(int rank, int size, int device, int timeout_ms, gloo_hip_allgather_fn allgather,
+                               void* user, gloo_hip_context_t* out) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(out && allgather, "null argument");
+    auto c = std::make_unique<gloo_hip_context>();
+    c->ctx = std::make_shared<gloo_amd::Context>(
+        rank, size, std::chrono::milliseconds(timeout_ms > 0 ? timeout_ms : 30000));
+    c->ctx->connect(std::make_shared<gloo_amd::CallbackStore>(allgather, user), device);
     *out = c.release();
   });
 }
@@ -156,7 +168,10 @@ double gloo_hip_algorithm_wait_seconds(gloo_hip_algorithm_t a) { return a ? a->e
 int gloo_hip_algorithm_set_profiling(gloo_hip_algorithm_t a, int on) {
   return guarded([&] {
     GLOO_AMD_ENFORCE(a, "null algorithm");
-    a->exec->setProfiling(on != 0);
+    // 1: HIP events around every chunk reduction (eager runs);
+    // 2: device stamps inside the kernels (graph replay kept)
+    a->exec->setProfiling(on == 1);
+    a->exec->setStamping(on == 2);
   });
 }
 

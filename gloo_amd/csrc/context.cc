@@ -58,10 +58,11 @@ void Context::connect(std::shared_ptr<Store> store, int device) {
     h->slots = GLOO_HIP_NUM_SLOTS;
     std::atomic_thread_fence(std::memory_order_release);
     h->magic = kMagic;
-    store_->set("gloo_amd/shm", bytes(shmName_));
-  } else {
-    auto v = store_->get("gloo_amd/shm", timeout_);
-    shmName_.assign(v.begin(), v.end());
+  }
+  // rank 0 publishes the control block's name
+  const auto names = allgather("shm", rank == 0 ? bytes(shmName_) : std::vector<char>{});
+  if (rank != 0) {
+    shmName_.assign(names[0].begin(), names[0].end());
     int fd = ::shm_open(shmName_.c_str(), O_RDWR, 0600);
     GLOO_AMD_ENFORCE(fd >= 0, "shm_open failed for ", shmName_);
     shm_ = ::mmap(nullptr, shmBytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
@@ -106,11 +107,11 @@ uint32_t* Context::errorWordDevicePtr(int r) {
   return reinterpret_cast<uint32_t*>(static_cast<char*>(shmDev_) + off);
 }
 
-void Context::barrier(const std::string& tag) {
+void Context::barrier(const std::string& tag) { (void)allgather("barrier/" + tag, {}); }
+
+std::vector<std::vector<char>> Context::allgather(const std::string& tag, const std::vector<char>& mine) {
   const uint64_t gen = barrierGen_++;
-  const std::string prefix = strcat_("gloo_amd/barrier/", tag, "/", gen, "/");
-  store_->set(prefix + std::to_string(rank), {'1'});
-  for (int r = 0; r < size; r++) store_->get(prefix + std::to_string(r), timeout_);
+  return store_->allgather(strcat_("gloo_amd/ag/", gen, "/", tag), rank, size, mine, timeout_);
 }
 
 }  // namespace gloo_amd

@@ -511,16 +511,17 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     if (s.kind == GLOO_HIP_STEP_SEND) sendPeers.insert(s.peer);
     if (s.kind == GLOO_HIP_STEP_DECL_RECV) recvPeers.insert(s.peer);
   }
+  std::vector<std::vector<char>> where;
   {
     int32_t hello[2] = {ctx_->pid(), ctx_->device()};
     std::vector<char> blob(sizeof(hello));
     std::memcpy(blob.data(), hello, sizeof(hello));
-    ctx_->store().set(strcat_("gloo_amd/inst", inst_, "/where/", me), blob);
+    where = ctx_->allgather(strcat_("inst", inst_, "/where"), blob);
   }
   peers_.resize(P);
   bool sharesDeviceInProcess = false, crossDeviceSender = false;
   for (int peer : planPeers) {
-    auto v = ctx_->store().get(strcat_("gloo_amd/inst", inst_, "/where/", peer), ctx_->timeout());
+    const std::vector<char>& v = where.at(peer);
     GLOO_AMD_ENFORCE(v.size() == 2 * sizeof(int32_t), "bad record from rank ", peer);
     int32_t w[2];
     std::memcpy(w, v.data(), sizeof(w));
@@ -624,7 +625,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   }
   std::vector<char> blob(sizeof(rec));
   std::memcpy(blob.data(), &rec, sizeof(rec));
-  ctx_->store().set(strcat_("gloo_amd/inst", inst_, "/arena/", me), blob);
+  const std::vector<std::vector<char>> arenas = ctx_->allgather(strcat_("inst", inst_, "/arena"), blob);
 
   // Every plan peer's record: its mailbox (a channel uses mailboxes when
   // both ends signal from the device and have one — both ends decide alike),
@@ -633,7 +634,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   peerMailbox_.assign(P, nullptr);
   peerMailboxIpc_.assign(P, false);
   for (int peer : planPeers) {
-    auto v = ctx_->store().get(strcat_("gloo_amd/inst", inst_, "/arena/", peer), ctx_->timeout());
+    const std::vector<char>& v = arenas.at(peer);
     GLOO_AMD_ENFORCE(v.size() == sizeof(ArenaRecord), "bad arena record from rank ", peer);
     ArenaRecord pr;
     std::memcpy(&pr, v.data(), sizeof(pr));
@@ -686,7 +687,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   int32_t agreed = proposal;
   for (int r = 0; r < P && agreed > 1; r++) {
     if (r == me) continue;
-    auto v = ctx_->store().get(strcat_("gloo_amd/inst", inst_, "/arena/", r), ctx_->timeout());
+    const std::vector<char>& v = arenas.at(r);
     GLOO_AMD_ENFORCE(v.size() == sizeof(ArenaRecord), "bad arena record from rank ", r);
     ArenaRecord pr;
     std::memcpy(&pr, v.data(), sizeof(pr));
@@ -761,6 +762,7 @@ PlanExecutor::~PlanExecutor() {
     if (epoch_) GLOO_AMD_HIP_RELEASE(hipFree(epoch_));
     if (interpSteps_) GLOO_AMD_HIP_RELEASE(hipFree(interpSteps_));
     if (ticket_) GLOO_AMD_HIP_RELEASE(hipFree(ticket_));
+    if (stamps_) GLOO_AMD_HIP_RELEASE(hipFree(stamps_));
     for (char* p : outStage_)
       if (p) GLOO_AMD_HIP_RELEASE(hipFree(p));
     for (char* p : inStage_)
@@ -835,6 +837,43 @@ Seq PlanExecutor::seqOf(size_t i, uint64_t r, bool graph) const {
   return graph ? Seq{q.base, q.perRun} : Seq{q.base + r * q.perRun, 0};
 }
 
+void PlanExecutor::setStamping(bool on) {
+  if (on == stamping_) return;
+  dropGraph();  // the captured work differs with stamps
+  stableRuns_ = 0;
+  stamping_ = on;
+  if (on && !stamps_) {
+    // one slot per REDUCE / FOLD step, in step order, with its algorithmic
+    // bytes: 2 reads + 1 write, or k source reads + 1 write
+    stampBytes_.clear();
+    stampSlotOf_.clear();
+    size_t srcs = 0;
+    for (size_t i = 0; i < plan_.steps.size(); i++) {
+      const Step& s = plan_.steps[i];
+      if (s.kind == GLOO_HIP_STEP_FOLD_SRC) srcs++;
+      if (s.kind != GLOO_HIP_STEP_REDUCE && s.kind != GLOO_HIP_STEP_FOLD) continue;
+      stampSlotOf_[i] = (int)stampBytes_.size();
+      stampBytes_.push_back((s.kind == GLOO_HIP_STEP_REDUCE ? 3.0 : srcs + 1.0) * s.length * es_);
+      if (s.kind == GLOO_HIP_STEP_FOLD) srcs = 0;
+    }
+    stampSlots_ = (int)stampBytes_.size();
+    GLOO_AMD_HIP_ALLOC(hipMalloc(&stamps_, std::max<size_t>(16, 2 * sizeof(uint64_t) * stampSlots_)));
+  }
+}
+
+void PlanExecutor::readStamps() {
+  std::vector<uint64_t> h(2 * (size_t)stampSlots_);
+  if (h.empty()) return;
+  GLOO_AMD_HIP_CHECK(hipMemcpy(h.data(), stamps_, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  for (int i = 0; i < stampSlots_; i++) {
+    const uint64_t b = h[2 * i], e = h[2 * i + 1];
+    if (e == 0 || e < b) continue;  // not launched this run (a fused or empty step)
+    reduceSeconds_ += (e - b) * 1e-8;  // 100 MHz
+    reduceBytes_ += stampBytes_[i];
+    reduceCount_++;
+  }
+}
+
 void PlanExecutor::run() {
   GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
   const int me = ctx_->rank;
@@ -850,7 +889,7 @@ void PlanExecutor::run() {
   const uint64_t r = runs_ + 1;
   // sliced plans must run sliced on every rank (their flags are per slice);
   // profiling then reports no reduce events
-  const bool interp = deviceSignal_ && interpMode_ && (!profiling_ || slices_ > 1);
+  const bool interp = deviceSignal_ && interpMode_ && (!(profiling_ || stamping_) || slices_ > 1);
   if (interp && interpDirty_) buildInterp();
   const bool graphable = deviceSignal_ && graphMode_ && !profiling_;
   if (interp && interpCount_ > 0) {
@@ -873,7 +912,7 @@ void PlanExecutor::run() {
   }
   runs_ = r;
   stableRuns_++;
-  if (ownStream_ || profiling_) {
+  if (ownStream_ || profiling_ || stamping_) {
     const auto t0 = std::chrono::steady_clock::now();
     GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
     if (deviceSignal_) waitSeconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -881,6 +920,7 @@ void PlanExecutor::run() {
       throw IoException(strcat_("Timed out on rank ", me, " waiting for a peer (device-side wait, ",
                                 ctx_->timeout().count(), " ms)"));
   }
+  if (stamping_ && !(interp && interpCount_ > 0)) readStamps();
   for (size_t i = 0; profiling_ && i + 1 < evUsed_; i += 2) {
     float ms = 0;
     GLOO_AMD_HIP_CHECK(hipEventElapsedTime(&ms, events_[i], events_[i + 1]));
@@ -1102,6 +1142,14 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
   };
   auto isWaitKind = [](int k) { return k == GLOO_HIP_STEP_WAIT_RECV || k == GLOO_HIP_STEP_WAIT_NOTIFY; };
   std::vector<const void*> foldSrcs;
+  if (stamping_) checkRc(launchStampInit(stamps_, stampSlots_, stream_), "stamp init");
+  // the stamp slot of the next REDUCE / FOLD launch (none when not stamping)
+  struct StampScope {
+    explicit StampScope(uint64_t* slot) : prev(setLaunchStamp(slot)) {}
+    ~StampScope() { setLaunchStamp(prev); }
+    uint64_t* prev;
+  };
+  auto slotOf = [&](size_t step) { return stamping_ ? stamps_ + 2 * (size_t)stampSlotOf_.at(step) : nullptr; };
   for (size_t i = 0; i < steps.size(); i++) {
     const Step& s = steps[i];
     // A run of consecutive SENDs (a mesh schedule's sends to every peer):
@@ -1272,8 +1320,9 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         }
         break;
       }
-      case GLOO_HIP_STEP_REDUCE:
+      case GLOO_HIP_STEP_REDUCE: {
         if (profiling_) GLOO_AMD_HIP_CHECK(hipEventRecord(event(), stream_));
+        StampScope stamp(slotOf(i));
         if (s.flags & GLOO_HIP_FROM_INPUTS) {  // out = in op inbox (gloo/reduce.cc:180-184)
           checkRc(gloo_hip_reduce3(op_, dtype_, userPtr(0) + s.dst_off * es_,
                                    static_cast<const char*>(inputs_.at(0)) + s.dst_off * es_,
@@ -1290,6 +1339,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
           reduceCount_++;
         }
         break;
+      }
       case GLOO_HIP_STEP_COPY: {
         char* dst = (s.flags & GLOO_HIP_DST_ARENA ? arena_ : userPtr(0)) + s.dst_off * es_;
         const char* src = (s.flags & GLOO_HIP_SRC_ARENA ? arena_ : userPtr(0)) + s.src_off * es_;
@@ -1349,9 +1399,12 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         GLOO_AMD_ENFORCE(!foldSrcs.empty() && foldSrcs.size() <= GLOO_HIP_MAX_SRCS, "bad fold");
         if (profiling_) GLOO_AMD_HIP_CHECK(hipEventRecord(event(), stream_));
         const int mode = s.flags & GLOO_HIP_FOLD_TREE ? 2 : s.flags & GLOO_HIP_FOLD_REVERSE ? 1 : 0;
-        checkRc(launchFold(op_, dtype_, userOrArena(s.flags & GLOO_HIP_DST_ARENA) + s.dst_off * es_,
-                           foldSrcs.data(), (int)foldSrcs.size(), s.length, mode, stream_),
-                "fold");
+        {
+          StampScope stamp(slotOf(i));
+          checkRc(launchFold(op_, dtype_, userOrArena(s.flags & GLOO_HIP_DST_ARENA) + s.dst_off * es_,
+                             foldSrcs.data(), (int)foldSrcs.size(), s.length, mode, stream_),
+                  "fold");
+        }
         if (profiling_) {
           GLOO_AMD_HIP_CHECK(hipEventRecord(event(), stream_));
           reduceBytes_ += (foldSrcs.size() + 1.0) * s.length * es_;

@@ -230,6 +230,34 @@ __device__ __forceinline__ void edges(typename Tr::Storage* c,
   if (j < n) c[j] = apply<Tr, OP>(a[j], b[j]);
 }
 
+// Device-side kernel timing (the executor's stamp mode, executor.h): every
+// workgroup folds its start time into stamp[0] (min) and, once all its waves'
+// stores have completed, its end time into stamp[1] (max), on the 100 MHz
+// constant clock.  stamp == nullptr (every other launch): two uniform
+// branches, nothing else.  Unlike host events, stamps survive hipGraph
+// capture and replay and exclude the dispatch gap between launches.
+__device__ __forceinline__ void stamp_begin(uint64_t* stamp) {
+  if (stamp && threadIdx.x == 0)
+    __hip_atomic_fetch_min(stamp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stamp_end(uint64_t* stamp) {
+  if (!stamp) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_max(stamp + 1, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void stamp_init_kernel(uint64_t* stamps, int k) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < k) {
+    stamps[2 * i] = ~0ull;
+    stamps[2 * i + 1] = 0;
+  }
+}
+
+thread_local uint64_t* t_stamp = nullptr;  // stamp slot of the next reduce launch on this thread
+
 // Vector body.  `head` elements bring the destination c to a 16-B boundary;
 // a and b may sit at any element offset relative to it (Src).  One workgroup = one tile of BLOCK lanes x UNROLL
 // 16-B packets per operand; packet u of lane t sits at (t + u*BLOCK)*16 bytes
@@ -240,10 +268,11 @@ __device__ __forceinline__ void edges(typename Tr::Storage* c,
 template <class Tr, int OP, int UNROLL, int BLOCK, int LAUX, int SAUX>
 __global__ __launch_bounds__(BLOCK) void reduce_vec_kernel(
     typename Tr::Storage* c, const typename Tr::Storage* a,
-    const typename Tr::Storage* b, size_t n, size_t head) {
+    const typename Tr::Storage* b, size_t n, size_t head, uint64_t* stamp) {
   using S = typename Tr::Storage;
   constexpr int kV = 16 / sizeof(S);
   constexpr uint32_t kTileBytes = (uint32_t)BLOCK * UNROLL * 16;
+  stamp_begin(stamp);
   const size_t nvec = (n - head) / kV;
   if (blockIdx.x == 0) edges<Tr, OP>(c, a, b, head, head + nvec * kV, n);
 
@@ -264,6 +293,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_vec_kernel(
 #pragma unroll
   for (int u = 0; u < UNROLL; u++)
     bstore<SAUX>(rc, lane_off + u * BLOCK * 16, apply_packet<Tr, OP>(x[u], y[u]));
+  stamp_end(stamp);
 }
 
 // Software-pipelined persistent form (measurement variants 9-12): a grid of
@@ -344,10 +374,11 @@ __device__ __forceinline__ typename Tr::Storage tree_fold(typename Tr::Storage* 
 
 template <class Tr, int OP, int UNROLL, int BLOCK, int MODE>
 __global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
-    typename Tr::Storage* dst, SrcList srcs, int k, size_t n, size_t head) {
+    typename Tr::Storage* dst, SrcList srcs, int k, size_t n, size_t head, uint64_t* stamp) {
   using S = typename Tr::Storage;
   constexpr int kV = 16 / sizeof(S);
   constexpr uint32_t kTileBytes = (uint32_t)BLOCK * UNROLL * 16;
+  stamp_begin(stamp);
   const size_t nvec = (n - head) / kV;
   const size_t tail0 = head + nvec * kV;
   if (blockIdx.x == 0) {
@@ -420,6 +451,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
   const auto rd = make_rsrc(reinterpret_cast<const char*>(dst + head) + base, bytes);
 #pragma unroll
   for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rd, lane_off + u * BLOCK * 16, acc[u]);
+  stamp_end(stamp);
 }
 
 // ---------------------------------------------------------------------------
@@ -785,7 +817,7 @@ int launch_vec(void* c, const void* a, const void* b, size_t n, size_t head, hip
   size_t grid = ceil_div(nvec, (size_t)BLOCK * UNROLL);
   if (grid == 0) grid = 1;
   reduce_vec_kernel<Tr, OP, UNROLL, BLOCK, LAUX, SAUX><<<dim3((unsigned)grid), dim3(BLOCK), 0, s>>>(
-      static_cast<S*>(c), static_cast<const S*>(a), static_cast<const S*>(b), n, head);
+      static_cast<S*>(c), static_cast<const S*>(a), static_cast<const S*>(b), n, head, t_stamp);
   return check_launch("reduce_vec_kernel");
 }
 
@@ -854,7 +886,7 @@ int launch_multi(void* dst, const void* const* srcs, int k, size_t n, hipStream_
   size_t grid = ceil_div(nvec, (size_t)kVecBlock * kMultiUnroll);
   if (grid == 0) grid = 1;
   reduce_multi_vec_kernel<Tr, OP, kMultiUnroll, kVecBlock, MODE><<<dim3((unsigned)grid), dim3(kVecBlock), 0, s>>>(
-      static_cast<S*>(dst), list, k, n, head);
+      static_cast<S*>(dst), list, k, n, head, t_stamp);
   return check_launch("reduce_multi_vec_kernel");
 }
 
@@ -962,6 +994,18 @@ int launchFold(int op, int dtype, void* dst, const void* const* srcs, int k, siz
     case 2: return dispatch_multi<2>(op, dtype, dst, srcs, k, n, s);
     default: return set_error(GLOO_HIP_EINVAL_ARG, "unknown fold mode");
   }
+}
+
+uint64_t* setLaunchStamp(uint64_t* stamp) {
+  uint64_t* prev = t_stamp;
+  t_stamp = stamp;
+  return prev;
+}
+
+int launchStampInit(uint64_t* stamps, int k, hipStream_t s) {
+  if (k <= 0) return GLOO_HIP_OK;
+  stamp_init_kernel<<<(k + 255) / 256, 256, 0, s>>>(stamps, k);
+  return check_launch("stamp_init_kernel");
 }
 
 // Internal entry for the plan executor (see gloo_amd/signal.h).

@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <cstring>
 #include <fstream>
 #include <iterator>
 #include <thread>
@@ -62,6 +63,41 @@ std::vector<char> HashStore::get(const std::string& key, std::chrono::millisecon
   if (!cv_.wait_for(lk, timeout, [&] { return map_.count(key) > 0; }))
     throw IoException("HashStore: timed out waiting for key " + key);
   return map_[key];
+}
+
+std::vector<std::vector<char>> Store::allgather(const std::string& tag, int rank, int size,
+                                               const std::vector<char>& mine, std::chrono::milliseconds timeout) {
+  set(tag + "/" + std::to_string(rank), mine);
+  std::vector<std::vector<char>> all(size);
+  for (int r = 0; r < size; r++) all[r] = r == rank ? mine : get(tag + "/" + std::to_string(r), timeout);
+  return all;
+}
+
+void CallbackStore::set(const std::string&, const std::vector<char>&) {
+  throw EnforceNotMet("CallbackStore supports only collective all-gathers");
+}
+
+std::vector<char> CallbackStore::get(const std::string&, std::chrono::milliseconds) {
+  throw EnforceNotMet("CallbackStore supports only collective all-gathers");
+}
+
+std::vector<std::vector<char>> CallbackStore::allgather(const std::string& tag, int, int size,
+                                                       const std::vector<char>& mine, std::chrono::milliseconds) {
+  GLOO_AMD_ENFORCE(mine.size() + 4 <= kBlock, "bootstrap record of ", mine.size(), " bytes exceeds the block");
+  std::vector<char> in(kBlock, 0), out(kBlock * (size_t)size, 0);
+  const uint32_t len = (uint32_t)mine.size();
+  std::memcpy(in.data(), &len, 4);
+  if (len) std::memcpy(in.data() + 4, mine.data(), len);
+  if (fn_(user_, in.data(), out.data(), kBlock) != 0)
+    throw IoException("bootstrap all-gather failed (" + tag + ")");
+  std::vector<std::vector<char>> all(size);
+  for (int r = 0; r < size; r++) {
+    uint32_t l = 0;
+    std::memcpy(&l, out.data() + (size_t)r * kBlock, 4);
+    GLOO_AMD_ENFORCE(l + 4 <= kBlock, "bad bootstrap block from rank ", r);
+    all[r].assign(out.data() + (size_t)r * kBlock + 4, out.data() + (size_t)r * kBlock + 4 + l);
+  }
+  return all;
 }
 
 std::shared_ptr<Store> openStore(const std::string& url) {

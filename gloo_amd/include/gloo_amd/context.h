@@ -56,6 +56,9 @@ class Context : public std::enable_shared_from_this<Context> {
 
   // Store-based barrier among all ranks (setup / teardown only).
   void barrier(const std::string& tag);
+  // Collective exchange of one small blob per rank (setup / teardown only);
+  // every rank calls it in the same order.
+  std::vector<std::vector<char>> allgather(const std::string& tag, const std::vector<char>& mine);
 
  private:
   std::chrono::milliseconds timeout_;

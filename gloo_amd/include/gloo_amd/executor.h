@@ -111,6 +111,12 @@ class PlanExecutor {
   // When enabled, every REDUCE of run() is bracketed by HIP events; after the
   // run: summed kernel seconds and algorithmic bytes (3 * n * sizeof(T)).
   void setProfiling(bool on) { profiling_ = on; }
+  // Device stamps instead (reduce.hip stamp_begin / stamp_end): every REDUCE
+  // and FOLD kernel of a run records its first-workgroup start and
+  // last-workgroup end on the GPU's constant clock, which also works inside a
+  // replayed hipGraph (events around the steps would force eager runs).
+  // After each run the same accessors report the summed kernel durations.
+  void setStamping(bool on);
   double lastReduceSeconds() const { return reduceSeconds_; }
   double lastReduceBytes() const { return reduceBytes_; }
   size_t lastReduceCount() const { return reduceCount_; }
@@ -211,6 +217,12 @@ class PlanExecutor {
   std::vector<hipEvent_t> forkEvents_;
   double waitSeconds_ = 0;
   bool profiling_ = false;
+  bool stamping_ = false;
+  uint64_t* stamps_ = nullptr;    // 2 x stampSlots_ device words: (start min, end max) per reduce step
+  int stampSlots_ = 0;
+  std::vector<double> stampBytes_;  // algorithmic bytes per slot
+  std::map<size_t, int> stampSlotOf_;  // plan step -> slot
+  void readStamps();
   std::vector<hipEvent_t> events_;
   size_t evUsed_ = 0;
   double reduceSeconds_ = 0, reduceBytes_ = 0;

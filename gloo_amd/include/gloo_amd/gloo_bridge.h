@@ -1,0 +1,230 @@
+// gloo_bridge.h — the MI355X-native GPU algorithms behind Gloo's own
+// gloo::Context / gloo::Algorithm surface.  HEADER-ONLY and compiled on the
+// GLOO side: it includes the reference's headers and links against the
+// user's libgloo plus libgloo_amd.so, while libgloo_amd.so itself never
+// links (or includes) Gloo — everything below crosses the C-ABI of
+// include/gloo_amd.h.
+//
+//   gloo::CudaAllreduceRingChunked<T, W>     -> gloo::HipAllreduceRingChunked<T, W>
+//        (gloo/cuda_allreduce_ring_chunked.h:19-26)
+//   gloo::CudaAllreduceHalvingDoubling<T, W> -> gloo::HipAllreduceHalvingDoubling<T, W>
+//        (gloo/cuda_allreduce_halving_doubling.h:22-30)
+//   gloo::CudaAllreduceRing<T, W>            -> gloo::HipAllreduceRing<T, W>
+//        (gloo/cuda_allreduce_ring.h:20-24)
+//   gloo::CudaAllreduceLocal<T, W>           -> gloo::HipAllreduceLocal<T, W>
+//        (gloo/cuda_allreduce_local.h:19-23)
+//   gloo::ReduceScatterHalvingDoubling<T>    -> gloo::HipReduceScatterHalvingDoubling<T, W>
+//        (gloo/reduce_scatter.h:112-117; CPU-only in the reference)
+//   gloo::CudaHostWorkspace / CudaDeviceWorkspace -> gloo::HipHostWorkspace / HipDeviceWorkspace
+//        (gloo/cuda_workspace.h:20-31)
+//
+// Every class derives from gloo::Algorithm (gloo/algorithm.h:20-38) and is
+// constructed from the program's existing std::shared_ptr<gloo::Context>,
+// device pointers, `int count` and (optionally) one hipStream_t per pointer,
+// exactly like the CUDA classes.  There is no second rendezvous: the
+// library's own context (inbox arenas, IPC handles, signal mailboxes) is
+// bootstrapped by gloo_hip_context_create_ex with gloo::allgather over the
+// gloo::Context's pairs (gloo/allgather.h) as its only exchange.  Like the
+// reference's algorithms, construction and destruction are collective:
+// every rank constructs (and destroys) its algorithms in the same order.
+//
+// Errors follow the reference: a peer that does not answer within the
+// context timeout raises gloo::IoException (gloo/common/error.h:42-48),
+// anything else gloo::EnforceNotMet (gloo/common/logging.h:32-59).
+//
+// Stream semantics (docs/cuda.md:6-13 of the reference): without streams,
+// run() returns with the outputs complete; with streams, the work is ordered
+// on streams[0] and the caller synchronises.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <chrono>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "gloo/algorithm.h"
+#include "gloo/allgather.h"
+#include "gloo/common/error.h"
+#include "gloo/common/logging.h"
+#include "gloo/context.h"
+#include "gloo/types.h"
+#include "gloo_amd.h"
+
+namespace gloo {
+
+// Where the inboxes (the transport's receive buffers) live.
+template <typename T>
+struct HipDeviceWorkspace {
+  static constexpr int kind = GLOO_HIP_WORKSPACE_DEVICE;
+};
+template <typename T>
+struct HipHostWorkspace {
+  static constexpr int kind = GLOO_HIP_WORKSPACE_HOST;
+};
+
+namespace hip_bridge {
+
+template <typename T>
+struct DType;
+template <> struct DType<int8_t> { static constexpr int value = GLOO_HIP_I8; };
+template <> struct DType<uint8_t> { static constexpr int value = GLOO_HIP_U8; };
+template <> struct DType<int32_t> { static constexpr int value = GLOO_HIP_I32; };
+template <> struct DType<uint32_t> { static constexpr int value = GLOO_HIP_U32; };
+template <> struct DType<int64_t> { static constexpr int value = GLOO_HIP_I64; };
+template <> struct DType<uint64_t> { static constexpr int value = GLOO_HIP_U64; };
+template <> struct DType<float16> { static constexpr int value = GLOO_HIP_F16; };
+template <> struct DType<float> { static constexpr int value = GLOO_HIP_F32; };
+template <> struct DType<double> { static constexpr int value = GLOO_HIP_F64; };
+
+// gloo::ReductionType (gloo/algorithm.h:49-57) -> gloo_hip_op_t (same values).
+inline int opOf(ReductionType t) {
+  GLOO_ENFORCE(t == SUM || t == PRODUCT || t == MAX || t == MIN,
+               "the device path runs the built-in reduction types; CUSTOM needs a device function");
+  return static_cast<int>(t);
+}
+
+inline void check(int rc, const char* what) {
+  if (rc == GLOO_HIP_OK) return;
+  const std::string msg = std::string(what) + ": " + gloo_hip_last_error();
+  if (rc == GLOO_HIP_EIO) throw ::gloo::IoException(msg);  // timed out waiting for a peer
+  GLOO_ENFORCE(false, msg);
+}
+
+inline int deviceOf(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) == hipSuccess && attr.device >= 0) return attr.device;
+  (void)hipGetLastError();
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return d;
+}
+
+// The library context of one algorithm, bootstrapped over the gloo::Context:
+// its only exchange is gloo::allgather of fixed records on a tag of its own
+// (Slot::build(kAllgatherSlotPrefix, tag) — no context slot is consumed).
+class BootstrapContext {
+ public:
+  static constexpr uint32_t kTag = 0x6e617664;  // distinct from a user's default tag 0
+
+  BootstrapContext(const std::shared_ptr<Context>& context, int device) : context_(context) {
+    check(gloo_hip_context_create_ex(context->rank, context->size, device,
+                                     (int)context->getTimeout().count(), &BootstrapContext::allgather, this,
+                                     &handle_),
+          "gloo_hip_context_create_ex");
+  }
+  ~BootstrapContext() {
+    if (handle_) (void)gloo_hip_context_destroy(handle_);
+  }
+  BootstrapContext(const BootstrapContext&) = delete;
+  BootstrapContext& operator=(const BootstrapContext&) = delete;
+  gloo_hip_context_t handle() const { return handle_; }
+
+ private:
+  static int allgather(void* user, const void* in, void* out, size_t block) {
+    auto* self = static_cast<BootstrapContext*>(user);
+    try {
+      AllgatherOptions opts(self->context_);
+      opts.setInput(const_cast<uint8_t*>(static_cast<const uint8_t*>(in)), block);
+      opts.setOutput(static_cast<uint8_t*>(out), block * (size_t)self->context_->size);
+      opts.setTag(kTag);
+      ::gloo::allgather(opts);
+      return 0;
+    } catch (const std::exception&) {
+      return 1;  // the library raises IoException for the failed exchange
+    }
+  }
+
+  std::shared_ptr<Context> context_;
+  gloo_hip_context_t handle_ = nullptr;
+};
+
+}  // namespace hip_bridge
+
+// One of the library's schedule executors as a gloo::Algorithm.
+template <typename T, int ALGO, typename W>
+class HipPlanAlgorithm : public Algorithm {
+ public:
+  HipPlanAlgorithm(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
+                   const std::vector<int>& recvElems, const std::vector<hipStream_t>& streams, ReductionType op)
+      : Algorithm(context) {
+    GLOO_ENFORCE(!ptrs.empty(), "need at least one pointer");
+    GLOO_ENFORCE(streams.empty() || streams.size() == ptrs.size(), "one stream per pointer, or none");
+    boot_.reset(new hip_bridge::BootstrapContext(context, hip_bridge::deviceOf(ptrs[0])));
+    std::vector<void*> p(ptrs.begin(), ptrs.end());
+    hip_bridge::check(
+        gloo_hip_algorithm_create_ws(boot_->handle(), ALGO, hip_bridge::opOf(op), hip_bridge::DType<T>::value,
+                                     p.data(), (int)p.size(), (size_t)(count > 0 ? count : 0),
+                                     recvElems.empty() ? nullptr : recvElems.data(),
+                                     streams.empty() ? nullptr : streams[0], W::kind, &algo_),
+        "gloo_hip_algorithm_create");
+  }
+
+  ~HipPlanAlgorithm() override {
+    if (algo_) (void)gloo_hip_algorithm_destroy(algo_);  // collective: a tear-down barrier
+  }
+
+  void run() override { hip_bridge::check(gloo_hip_algorithm_run(algo_), "run"); }
+
+ protected:
+  std::unique_ptr<hip_bridge::BootstrapContext> boot_;
+  gloo_hip_algorithm_t algo_ = nullptr;
+};
+
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipAllreduceRingChunked : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING_CHUNKED, W> {
+ public:
+  HipAllreduceRingChunked(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, const int count,
+                          const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
+                          const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING_CHUNKED, W>(context, ptrs, count, {}, streams, fn->type()) {}
+};
+
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipAllreduceHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING, W> {
+ public:
+  // pipelineBroadcastAndReduce (gloo/cuda_allreduce_halving_doubling.h:29)
+  // overlaps the reference's per-chunk local reduce / broadcast with the
+  // exchange; here a rank's pointers are folded in one fused pass before the
+  // exchange, so the flag changes no byte and is accepted for source
+  // compatibility.
+  HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, const int count,
+                              const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
+                              bool /*pipelineBroadcastAndReduce*/ = false,
+                              const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING, W>(context, ptrs, count, {}, streams, fn->type()) {}
+};
+
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipAllreduceRing : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING, W> {
+ public:
+  HipAllreduceRing(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, const int count,
+                   const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
+                   const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING, W>(context, ptrs, count, {}, streams, fn->type()) {}
+};
+
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipAllreduceLocal : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_LOCAL, W> {
+ public:
+  HipAllreduceLocal(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, const int count,
+                    const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
+                    const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_LOCAL, W>(context, ptrs, count, {}, streams, fn->type()) {}
+};
+
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipReduceScatterHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_REDUCE_SCATTER, W> {
+ public:
+  HipReduceScatterHalvingDoubling(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
+                                  const int count, const std::vector<int>& recvElems,
+                                  const ReductionFunction<T>* fn = ReductionFunction<T>::sum,
+                                  const std::vector<hipStream_t>& streams = std::vector<hipStream_t>())
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_REDUCE_SCATTER, W>(context, ptrs, count, recvElems, streams, fn->type()) {
+    GLOO_ENFORCE_EQ((int)recvElems.size(), context->size, "recvElems needs one entry per rank");
+  }
+};
+
+}  // namespace gloo

@@ -113,6 +113,14 @@ int launchPlanInterp(int op, int dtype, const InterpStep* steps, int nsteps, uin
 // Multi-source fold in one pass, k <= GLOO_HIP_MAX_SRCS.  mode 0: left fold
 // acc = acc op s_j; 1: reverse, acc = s_j op acc; 2: balanced pairwise tree
 // over the sources in order (k a power of two).  Returns a gloo_hip status.
+// Device-side timing of the reduce kernels (reduce_vec_kernel,
+// reduce_multi_vec_kernel): while a stamp slot is set on the calling thread,
+// each of those launches folds its first workgroup start into slot[0] (min)
+// and its last workgroup end into slot[1] (max), 100 MHz clock ticks.
+// Returns the previous slot.  launchStampInit sets k slots to (~0, 0).
+uint64_t* setLaunchStamp(uint64_t* slot);
+int launchStampInit(uint64_t* stamps, int k, hipStream_t stream);
+
 int launchFold(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n, int mode,
                hipStream_t stream);
 

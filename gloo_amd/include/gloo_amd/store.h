@@ -20,6 +20,32 @@ class Store {
   virtual void set(const std::string& key, const std::vector<char>& data) = 0;
   // Blocks until `key` exists (or throws IoException after `timeout`).
   virtual std::vector<char> get(const std::string& key, std::chrono::milliseconds timeout) = 0;
+  // Collective: each of the `size` ranks contributes `mine` under a `tag`
+  // unique to this call; returns every rank's blob in rank order.  Every
+  // exchange gloo_amd makes is one of these (context connect, an
+  // algorithm's arena records, barriers), so a store that can only all-gather
+  // (CallbackStore) is enough.  Default: set(tag/rank) + get of every rank.
+  virtual std::vector<std::vector<char>> allgather(const std::string& tag, int rank, int size,
+                                                   const std::vector<char>& mine, std::chrono::milliseconds timeout);
+};
+
+// The all-gather of an existing collective context supplied by the caller:
+// gloo_hip_context_create_ex, through which a Gloo program bootstraps over
+// its own gloo::Context (gloo_amd/include/gloo_amd/gloo_bridge.h).  Fixed
+// blocks of kBlock bytes per rank: a 4-byte length, then the blob.
+class CallbackStore : public Store {
+ public:
+  using Fn = int (*)(void* user, const void* in, void* out, size_t block);
+  static constexpr size_t kBlock = 1024;
+  CallbackStore(Fn fn, void* user) : fn_(fn), user_(user) {}
+  void set(const std::string& key, const std::vector<char>& data) override;
+  std::vector<char> get(const std::string& key, std::chrono::milliseconds timeout) override;
+  std::vector<std::vector<char>> allgather(const std::string& tag, int rank, int size, const std::vector<char>& mine,
+                                           std::chrono::milliseconds timeout) override;
+
+ private:
+  Fn fn_;
+  void* user_;
 };
 
 // Shared directory, one file per key (atomic rename), for ranks that are

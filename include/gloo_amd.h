@@ -76,6 +76,7 @@ typedef enum {
 #define GLOO_HIP_EINVAL_DTYPE (-2)
 #define GLOO_HIP_EINVAL_PTR (-3)
 #define GLOO_HIP_EINVAL_ARG (-4)
+#define GLOO_HIP_EIO (-5) /* a peer did not answer within the context timeout (gloo::IoException) */
 
 /* A hipStream_t passed as an opaque pointer (NULL = the default stream). */
 typedef void* gloo_hip_stream_t;
@@ -102,6 +103,19 @@ int gloo_hip_reduce3(int op, int dtype, void* c, const void* a, const void* b,
 int gloo_hip_reduce_multi(int op, int dtype, void* dst,
                           const void* const* srcs, int k, size_t n,
                           gloo_hip_stream_t stream);
+
+/* Host-staged chunk reduction: host_dst[i] = host_dst[i] (op) host_src[i]
+ * for a chunk that starts and ends in (pinned) host memory — a transport's
+ * receive buffer — computed by the HIP kernel through device scratch
+ * dev_dst / dev_src (n elements each, caller-owned).  The chunk moves in
+ * pieces of piece_elems (0 = n / 8): the host-to-device copies of piece k+1,
+ * the kernel of piece k and the device-to-host copy of piece k-1 run at
+ * once on separate streams (both PCIe directions busy).  Ordered after the
+ * work already on `stream`; the host result is complete once `stream` has
+ * drained.  The device side of the reference's CudaLocalHostReduce
+ * (gloo/cuda_collectives_host.h:22-136), with the reduction on the GPU. */
+int gloo_hip_reduce_staged(int op, int dtype, void* host_dst, const void* host_src, size_t n,
+                           void* dev_dst, void* dev_src, size_t piece_elems, gloo_hip_stream_t stream);
 
 /* Size in bytes of one element of `dtype`, or 0 when dtype is unknown. */
 size_t gloo_hip_dtype_size(int dtype);
@@ -258,6 +272,21 @@ int gloo_hip_context_create(int rank, int size, const char* store_url, int devic
                             int timeout_ms, gloo_hip_context_t* out);
 int gloo_hip_context_destroy(gloo_hip_context_t ctx);
 
+/* Bootstrap over an existing collective context instead of a store: the
+ * caller supplies an all-gather of fixed `block`-byte records (every rank
+ * passes `in`; `out` receives size * block bytes, rank r's record at
+ * r * block; return 0 on success).  Every exchange the library makes (the
+ * control block's name, each algorithm's inbox-arena / IPC records,
+ * set-up and tear-down barriers) is one such collective call, made in the
+ * same order on every rank from the calling thread.  This is how a Gloo
+ * program hands over its own gloo::Context (gloo/context.h:26-59): the
+ * header-only bridge gloo_amd/include/gloo_amd/gloo_bridge.h passes
+ * gloo::allgather over that context's pairs, so there is no second
+ * rendezvous. */
+typedef int (*gloo_hip_allgather_fn)(void* user, const void* in, void* out, size_t block);
+int gloo_hip_context_create_ex(int rank, int size, int device, int timeout_ms, gloo_hip_allgather_fn allgather,
+                               void* user, gloo_hip_context_t* out);
+
 int gloo_hip_algorithm_create(gloo_hip_context_t ctx, int algo, int op, int dtype,
                               void* const* ptrs, int nptrs, size_t count,
                               const int* recv_elems, gloo_hip_stream_t stream,
@@ -280,10 +309,14 @@ int gloo_hip_algorithm_run(gloo_hip_algorithm_t algo);
 int gloo_hip_algorithm_destroy(gloo_hip_algorithm_t algo);
 /* Host seconds the last run() spent blocked waiting for peers. */
 double gloo_hip_algorithm_wait_seconds(gloo_hip_algorithm_t algo);
-/* Measurement: bracket every chunk reduction of run() with HIP events.  After
- * a run: stats[0] = summed reduce-kernel seconds, stats[1] = algorithmic
- * bytes reduced (3 * n * sizeof(T) per chunk), stats[2] = chunks reduced,
- * stats[3] = host seconds blocked on peers. */
+/* Measurement.  on = 1: bracket every chunk reduction of run() with HIP
+ * events (runs are then enqueued eagerly); on = 2: device-side stamps inside
+ * the reduce kernels (each records its first-workgroup start and
+ * last-workgroup end on the GPU's 100 MHz clock), which keeps hipGraph
+ * replay; 0: off.  After a run: stats[0] = summed reduce-kernel seconds,
+ * stats[1] = algorithmic bytes reduced (3 * n * sizeof(T) per two-operand
+ * chunk, (k + 1) * n * sizeof(T) per k-source fold), stats[2] = chunk
+ * reductions, stats[3] = host seconds blocked on peers. */
 int gloo_hip_algorithm_set_profiling(gloo_hip_algorithm_t algo, int on);
 int gloo_hip_algorithm_stats(gloo_hip_algorithm_t algo, double* stats4);
 

@@ -1,0 +1,294 @@
+// bridge_test.cc — TEST PROGRAM (built by oracle/Makefile where the reference
+// sources exist; the binary travels to the GPU box, the reference does not).
+//
+// A Gloo program that uses the MI355X-native algorithms through Gloo's own
+// surface (gloo_amd/include/gloo_amd/gloo_bridge.h): ranks are threads with
+// a gloo::rendezvous::Context each, connected over the reference's TCP
+// transport (gloo/test/base_test.h:107-152); every rank hands its
+// std::shared_ptr<gloo::Context> to gloo::HipAllreduce*<T>, which derives from
+// gloo::Algorithm.  Mirrors gloo/test/cuda_allreduce_test.cc:60-349:
+// SinglePointer / MultiPointer / MultiPointerAsync (user streams) across
+// ring, ring-chunked, halving-doubling (+ pipelined), fp16, plus the
+// reduce-scatter, the host workspace and the IoException on a silent peer.
+// Expected values: the closed form of gloo/test/base_test.h:184-236.
+//
+// Usage: bridge_test [case-filter]   (prints one line per case, exit 0 = ok)
+#include <hip/hip_runtime_api.h>
+
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <stdexcept>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gloo/rendezvous/context.h"
+#include "gloo/rendezvous/hash_store.h"
+#include "gloo/transport/tcp/device.h"
+#include "gloo_amd/gloo_bridge.h"
+
+namespace {
+
+#define HIPOK(x)                                                                 \
+  do {                                                                           \
+    hipError_t e_ = (x);                                                         \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+class Barrier {
+ public:
+  explicit Barrier(int n) : n_(n) {}
+  void wait() {
+    std::unique_lock<std::mutex> lk(m_);
+    const int gen = gen_;
+    if (++count_ == n_) {
+      count_ = 0;
+      gen_++;
+      cv_.notify_all();
+    } else {
+      cv_.wait(lk, [&] { return gen != gen_; });
+    }
+  }
+
+ private:
+  std::mutex m_;
+  std::condition_variable cv_;
+  int n_, count_ = 0, gen_ = 0;
+};
+
+// P ranks as threads; each gets a connected gloo::Context (timeout `ms`).
+std::string spawn(int P, int ms, const std::function<void(std::shared_ptr<gloo::Context>)>& fn) {
+  auto store = std::make_shared<gloo::rendezvous::HashStore>();
+  Barrier barrier(P);
+  std::vector<std::thread> ts;
+  std::mutex em;
+  std::string err;
+  for (int rank = 0; rank < P; rank++) {
+    ts.emplace_back([&, rank] {
+      try {
+        HIPOK(hipSetDevice(0));
+        auto ctx = std::make_shared<gloo::rendezvous::Context>(rank, P);
+        ctx->setTimeout(std::chrono::milliseconds(ms));
+        if (P > 1) {
+          gloo::transport::tcp::attr attr("localhost");
+          auto dev = gloo::transport::tcp::CreateDevice(attr);
+          ctx->connectFullMesh(store, dev);
+        }
+        fn(ctx);
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> lk(em);
+        if (err.empty()) err = "rank " + std::to_string(rank) + ": " + e.what();
+      }
+      barrier.wait();
+    });
+  }
+  for (auto& t : ts) t.join();
+  return err;
+}
+
+template <typename T>
+T fromDouble(double v) { return T(v); }
+template <>
+gloo::float16 fromDouble<gloo::float16>(double v) { return gloo::cpu_float2half_rn((float)v); }
+template <typename T>
+double toDouble(T v) { return (double)v; }
+template <>
+double toDouble<gloo::float16>(gloo::float16 v) { return gloo::cpu_half2float(v); }
+
+using Make = std::function<std::unique_ptr<gloo::Algorithm>(std::shared_ptr<gloo::Context>&, std::vector<void*>&,
+                                                            int, std::vector<hipStream_t>&)>;
+
+// Fixture<T>::assignValues / checkAllreduceResult (gloo/test/base_test.h:184-236)
+// on k device buffers per rank; `async` passes one user stream per pointer
+// and synchronises them itself (MultiPointerAsync).
+template <typename T>
+std::string allreduceCase(int P, int k, int count, bool async, int runs, const Make& make) {
+  return spawn(P, 30000, [&](std::shared_ptr<gloo::Context> ctx) {
+    const size_t stride = (size_t)P * k;
+    std::vector<void*> ptrs(k);
+    std::vector<hipStream_t> streams;
+    std::vector<T> host((size_t)count);
+    for (int i = 0; i < k; i++) {
+      HIPOK(hipMalloc(&ptrs[i], std::max<size_t>(1, count * sizeof(T))));
+      const size_t val = (size_t)ctx->rank * k + i;
+      for (int j = 0; j < count; j++) host[j] = fromDouble<T>((double)(j * stride + val));
+      HIPOK(hipMemcpy(ptrs[i], host.data(), count * sizeof(T), hipMemcpyHostToDevice));
+      if (async) {
+        hipStream_t s;
+        HIPOK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        streams.push_back(s);
+      }
+    }
+    {
+      auto a = make(ctx, ptrs, count, streams);
+      for (int r = 0; r < runs; r++) {
+        if (r > 0)  // reset the inputs between runs
+          for (int i = 0; i < k; i++) {
+            const size_t val = (size_t)ctx->rank * k + i;
+            for (int j = 0; j < count; j++) host[j] = fromDouble<T>((double)(j * stride + val));
+            HIPOK(hipMemcpy(ptrs[i], host.data(), count * sizeof(T), hipMemcpyHostToDevice));
+          }
+        a->run();
+        for (auto s : streams) HIPOK(hipStreamSynchronize(s));
+        for (int i = 0; i < k; i++) {
+          HIPOK(hipMemcpy(host.data(), ptrs[i], count * sizeof(T), hipMemcpyDeviceToHost));
+          for (int j = 0; j < count; j++) {
+            const double want = (double)j * stride * stride + stride * (stride - 1) / 2.0;
+            if (toDouble<T>(fromDouble<T>(want)) != toDouble<T>(host[j]))
+              throw std::runtime_error("mismatch in ptr " + std::to_string(i) + " element " + std::to_string(j) +
+                                       " run " + std::to_string(r) + ": " + std::to_string(toDouble<T>(host[j])) +
+                                       " != " + std::to_string(want));
+          }
+        }
+      }
+    }
+    for (auto s : streams) HIPOK(hipStreamDestroy(s));
+    for (void* p : ptrs) HIPOK(hipFree(p));
+  });
+}
+
+template <typename T>
+Make ringChunked() {
+  return [](std::shared_ptr<gloo::Context>& c, std::vector<void*>& p, int n, std::vector<hipStream_t>& s) {
+    std::vector<T*> tp;
+    for (void* x : p) tp.push_back(static_cast<T*>(x));
+    return std::unique_ptr<gloo::Algorithm>(new gloo::HipAllreduceRingChunked<T>(c, tp, n, s));
+  };
+}
+template <typename T>
+Make ringChunkedHost() {
+  return [](std::shared_ptr<gloo::Context>& c, std::vector<void*>& p, int n, std::vector<hipStream_t>& s) {
+    std::vector<T*> tp;
+    for (void* x : p) tp.push_back(static_cast<T*>(x));
+    return std::unique_ptr<gloo::Algorithm>(new gloo::HipAllreduceRingChunked<T, gloo::HipHostWorkspace<T>>(c, tp, n, s));
+  };
+}
+template <typename T>
+Make ring() {
+  return [](std::shared_ptr<gloo::Context>& c, std::vector<void*>& p, int n, std::vector<hipStream_t>& s) {
+    std::vector<T*> tp;
+    for (void* x : p) tp.push_back(static_cast<T*>(x));
+    return std::unique_ptr<gloo::Algorithm>(new gloo::HipAllreduceRing<T>(c, tp, n, s));
+  };
+}
+template <typename T>
+Make halvingDoubling(bool pipelined) {
+  return [pipelined](std::shared_ptr<gloo::Context>& c, std::vector<void*>& p, int n, std::vector<hipStream_t>& s) {
+    std::vector<T*> tp;
+    for (void* x : p) tp.push_back(static_cast<T*>(x));
+    return std::unique_ptr<gloo::Algorithm>(new gloo::HipAllreduceHalvingDoubling<T>(c, tp, n, s, pipelined));
+  };
+}
+
+// ReduceScatterHalvingDoubling (gloo/test/reduce_scatter_test.cc:79-196):
+// rank r's block [off_r, off_r + recvElems[r]) lands at the start of its buffer.
+std::string reduceScatterCase(int P, int count) {
+  std::vector<int> recv;
+  for (int r = 0, rem = count, chunk = (count + P - 1) / P; r < P; r++) {
+    recv.push_back(std::min(chunk, rem));
+    rem = rem > chunk ? rem - chunk : 0;
+  }
+  return spawn(P, 30000, [&](std::shared_ptr<gloo::Context> ctx) {
+    std::vector<float> host(count);
+    for (int j = 0; j < count; j++) host[j] = (float)(j * P + ctx->rank);
+    float* d = nullptr;
+    HIPOK(hipMalloc(&d, count * sizeof(float)));
+    HIPOK(hipMemcpy(d, host.data(), count * sizeof(float), hipMemcpyHostToDevice));
+    {
+      gloo::HipReduceScatterHalvingDoubling<float> a(ctx, {d}, count, recv);
+      a.run();
+    }
+    HIPOK(hipMemcpy(host.data(), d, count * sizeof(float), hipMemcpyDeviceToHost));
+    int off = 0;
+    for (int r = 0; r < ctx->rank; r++) off += recv[r];
+    for (int j = 0; j < recv[ctx->rank]; j++) {
+      const double want = (double)(off + j) * P * P + P * (P - 1) / 2.0;
+      if (want != (double)host[j])
+        throw std::runtime_error("reduce-scatter mismatch at " + std::to_string(j));
+    }
+    HIPOK(hipFree(d));
+  });
+}
+
+// A peer that never runs: run() must raise gloo::IoException after the
+// context timeout (gloo/common/error.h:42-48), and tear-down still completes.
+std::string silentPeerCase() {
+  std::string seen;
+  std::mutex m;
+  std::string err = spawn(2, 2000, [&](std::shared_ptr<gloo::Context> ctx) {
+    float* d = nullptr;
+    HIPOK(hipMalloc(&d, 4096 * sizeof(float)));
+    {
+      gloo::HipAllreduceRingChunked<float> a(ctx, {d}, 4096);
+      if (ctx->rank == 0) {
+        try {
+          a.run();
+        } catch (const gloo::IoException& e) {
+          std::lock_guard<std::mutex> lk(m);
+          seen = e.what();
+        }
+      }
+    }
+    HIPOK(hipFree(d));
+  });
+  if (!err.empty()) return err;
+  return seen.empty() ? std::string("no IoException from a silent peer") : std::string();
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const std::string filter = argc > 1 ? argv[1] : "";
+  struct Case {
+    std::string name;
+    std::function<std::string()> fn;
+  };
+  std::vector<Case> cases;
+  for (int P : {1, 2, 3, 4, 5}) {
+    for (int n : {1, 1000, 100003}) {
+      cases.push_back({"ring_chunked/P" + std::to_string(P) + "/n" + std::to_string(n),
+                       [=] { return allreduceCase<float>(P, 1, n, false, 2, ringChunked<float>()); }});
+      cases.push_back({"halving_doubling/P" + std::to_string(P) + "/n" + std::to_string(n),
+                       [=] { return allreduceCase<float>(P, 1, n, false, 2, halvingDoubling<float>(false)); }});
+    }
+    cases.push_back({"ring/P" + std::to_string(P) + "/n1000",
+                     [=] { return allreduceCase<float>(P, 1, 1000, false, 1, ring<float>()); }});
+  }
+  cases.push_back({"halving_doubling_pipelined/P4/n4099",
+                   [] { return allreduceCase<float>(4, 1, 4099, false, 1, halvingDoubling<float>(true)); }});
+  cases.push_back({"multi_pointer/ring_chunked/P3/k2/n1000",
+                   [] { return allreduceCase<float>(3, 2, 1000, false, 1, ringChunked<float>()); }});
+  cases.push_back({"multi_pointer_async/ring_chunked/P2/k2/n10007",
+                   [] { return allreduceCase<float>(2, 2, 10007, true, 3, ringChunked<float>()); }});
+  cases.push_back({"multi_pointer_async/halving_doubling/P4/k2/n1000",
+                   [] { return allreduceCase<float>(4, 2, 1000, true, 2, halvingDoubling<float>(false)); }});
+  cases.push_back({"half/ring_chunked/P4/n128",  // cuda_allreduce_test.cc HalfPrecision shape
+                   [] { return allreduceCase<gloo::float16>(4, 1, 128, false, 1, ringChunked<gloo::float16>()); }});
+  cases.push_back({"half/halving_doubling/P4/n128",
+                   [] { return allreduceCase<gloo::float16>(4, 1, 128, false, 1, halvingDoubling<gloo::float16>(false)); }});
+  cases.push_back({"host_workspace/ring_chunked/P3/n10007",
+                   [] { return allreduceCase<float>(3, 1, 10007, false, 2, ringChunkedHost<float>()); }});
+  cases.push_back({"reduce_scatter/P4/n1000", [] { return reduceScatterCase(4, 1000); }});
+  cases.push_back({"reduce_scatter/P5/n10007", [] { return reduceScatterCase(5, 10007); }});
+  cases.push_back({"io_exception/silent_peer", [] { return silentPeerCase(); }});
+  int failed = 0, ran = 0;
+  for (auto& c : cases) {
+    if (!filter.empty() && c.name.find(filter) == std::string::npos) continue;
+    ran++;
+    std::string e;
+    try {
+      e = c.fn();
+    } catch (const std::exception& ex) {
+      e = ex.what();
+    }
+    std::printf("%s %s%s%s\n", e.empty() ? "ok  " : "FAIL", c.name.c_str(), e.empty() ? "" : ": ", e.c_str());
+    std::fflush(stdout);
+    failed += !e.empty();
+  }
+  std::printf("%d cases, %d failed\n", ran, failed);
+  return failed ? 1 : 0;
+}
