@@ -48,7 +48,8 @@ OP_NAMES = {"sum": ReductionType.SUM, "product": ReductionType.PRODUCT,
 
 EXPORTED = ("gloo_hip_reduce", "gloo_hip_reduce3", "gloo_hip_reduce_multi",
             "gloo_hip_dtype_size", "gloo_hip_last_error", "gloo_hip_version",
-            "gloo_hip_set_variant", "gloo_hip_plan", "gloo_hip_reduce_staged")
+            "gloo_hip_set_variant", "gloo_hip_plan", "gloo_hip_reduce_staged", "gloo_hip_register_op",
+            "gloo_hip_copy_kernel")
 
 
 class GlooHipError(RuntimeError):
@@ -77,6 +78,8 @@ def _load():
     L.gloo_hip_version.restype = ctypes.c_char_p
     L.gloo_hip_set_variant.argtypes = [ctypes.c_int]
     L.gloo_hip_reduce_staged.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, vp, vp, sz, vp]
+    L.gloo_hip_register_op.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int)]
+    L.gloo_hip_copy_kernel.argtypes = [vp, vp, sz, ctypes.c_uint, vp]
     return L
 
 
@@ -89,7 +92,7 @@ def _check(rc):
 
 
 def _as_op(op):
-    return int(OP_NAMES[op]) if isinstance(op, str) else int(op)
+    return int(OP_NAMES[op]) if isinstance(op, str) else int(op)  # ints: built-in or registered (>= 1000)
 
 
 def _as_dtype(dtype):
@@ -127,6 +130,21 @@ def reduce_staged(op, dtype, host_dst, host_src, n, dev_dst, dev_src, piece_elem
     host_src through device scratch, copies and kernel pipelined in pieces."""
     _check(lib.gloo_hip_reduce_staged(_as_op(op), _as_dtype(dtype), host_dst, host_src, n, dev_dst, dev_src,
                                       piece_elems, stream or None))
+
+
+def register_op(fn_ptr, user=None):
+    """gloo_hip_register_op: a caller-supplied device reduction (a C function
+    pointer, as int, of type gloo_hip_custom_fn) -> an op code >= 1000
+    (gloo::ReductionType::CUSTOM, gloo/algorithm.h:49-57) accepted by every
+    entry point that takes `op`."""
+    out = ctypes.c_int()
+    _check(lib.gloo_hip_register_op(ctypes.c_void_p(fn_ptr), user, ctypes.byref(out)))
+    return out.value
+
+
+def copy_kernel(dst, src, nbytes, blocks=0, stream=0):
+    """gloo_hip_copy_kernel: the SEND steps' kernel copy engine."""
+    _check(lib.gloo_hip_copy_kernel(dst, src, nbytes, blocks, stream or None))
 
 
 def set_variant(v):
@@ -224,6 +242,7 @@ def _bind_collectives(L):
     L.gloo_hip_algorithm_set_profiling.argtypes = [vp, ctypes.c_int]
     L.gloo_hip_algorithm_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
     L.gloo_hip_algorithm_mode.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    L.gloo_hip_context_mode.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
 
 
 _bind_collectives(lib)
@@ -231,9 +250,19 @@ EXPORTED = EXPORTED + ("gloo_hip_context_create", "gloo_hip_context_create_ex", 
                        "gloo_hip_algorithm_create", "gloo_hip_algorithm_run",
                        "gloo_hip_algorithm_destroy", "gloo_hip_algorithm_wait_seconds",
                        "gloo_hip_algorithm_set_profiling", "gloo_hip_algorithm_stats",
-                       "gloo_hip_algorithm_mode", "gloo_hip_algorithm_create_ws")
+                       "gloo_hip_algorithm_mode", "gloo_hip_algorithm_create_ws", "gloo_hip_context_mode")
 
 WORKSPACES = {"device": 0, "host": 1}
+
+
+def _mode_dict(out):
+    err = lib.gloo_hip_last_error()
+    err = err.decode() if isinstance(err, bytes) else (err or "")
+    return {"device_signal": bool(out[0]), "fine_arena": out[1] == 1,
+            "host_arena": out[1] == 2, "kernel_copy": bool(out[2]),
+            "graph": out[3] == 1, "interp": out[3] >= 2, "interp_slices": max(0, out[3] - 1),
+            "graph_error": err[len("graph capture abandoned: "):]
+            if err.startswith("graph capture abandoned: ") else ""}
 
 
 class Context:
@@ -247,6 +276,13 @@ class Context:
         _check(lib.gloo_hip_context_create(rank, size, store_url.encode(), device, timeout_ms,
                                            ctypes.byref(h)))
         self._h = h
+
+    def last_mode(self):
+        """How the latest function-style call (allreduce / reduce_to_root)
+        on this context ran (see Algorithm.mode)."""
+        out = (ctypes.c_int * 4)()
+        _check(lib.gloo_hip_context_mode(self._h, out))
+        return _mode_dict(out)
 
     def close(self):
         if self._h:
@@ -301,13 +337,7 @@ class Algorithm:
         'graph_error' says why capture was abandoned (empty if it was not)."""
         out = (ctypes.c_int * 4)()
         _check(lib.gloo_hip_algorithm_mode(self._h, out))
-        err = lib.gloo_hip_last_error()
-        err = err.decode() if isinstance(err, bytes) else (err or "")
-        return {"device_signal": bool(out[0]), "fine_arena": out[1] == 1,
-                "host_arena": out[1] == 2, "kernel_copy": bool(out[2]),
-                "graph": out[3] == 1, "interp": out[3] >= 2, "interp_slices": max(0, out[3] - 1),
-                "graph_error": err[len("graph capture abandoned: "):]
-                if err.startswith("graph capture abandoned: ") else ""}
+        return _mode_dict(out)
 
     def close(self):
         if self._h:

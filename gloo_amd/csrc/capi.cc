@@ -15,6 +15,7 @@ struct gloo_hip_context {
   // function-style allreduce: one executor per option set, least recently
   // used first (every rank makes the same calls, so hits and evictions agree)
   std::list<std::pair<std::string, std::unique_ptr<gloo_amd::PlanExecutor>>> cache;
+  gloo_amd::PlanExecutor* last = nullptr;  // the executor of the latest function-style call
 };
 struct gloo_hip_algorithm {
   std::unique_ptr<gloo_amd::PlanExecutor> exec;
@@ -41,8 +42,12 @@ int guarded(F&& f) {
 void runCached(gloo_hip_context_t ctx, int algo, int op, int dtype, const std::vector<void*>& ins,
                const std::vector<void*>& outs, size_t elements, size_t maxSeg, uint32_t tag,
                gloo_hip_stream_t stream, const std::vector<int>& extra) {
+  // The key holds what the schedule depends on, never a rank-local value
+  // such as the stream: ranks that pass different streams for the same call
+  // must still hit and evict alike (their construction and tear-down are
+  // collective).  The stream is rebound per call, like the buffers.
   std::string key = gloo_amd::strcat_(algo, "/", op, "/", dtype, "/", ins.size(), "/", outs.size(), "/", elements,
-                                      "/", maxSeg, "/", tag, "/", reinterpret_cast<uintptr_t>(stream));
+                                      "/", maxSeg, "/", tag);
   for (int v : extra) key += gloo_amd::strcat_("/", v);
   auto& cache = ctx->cache;
   auto it = cache.begin();
@@ -59,7 +64,9 @@ void runCached(gloo_hip_context_t ctx, int algo, int op, int dtype, const std::v
     cache.splice(cache.begin(), cache, it);
     it = cache.begin();
   }
+  it->second->setStream(static_cast<hipStream_t>(stream));
   it->second->setBuffers(ins, outs);
+  ctx->last = it->second.get();
   it->second->run();
 }
 }  // namespace
@@ -185,14 +192,28 @@ int gloo_hip_algorithm_stats(gloo_hip_algorithm_t a, double* stats) {
   });
 }
 
+namespace {
+void modeOf(const gloo_amd::PlanExecutor& e, int* mode) {
+  mode[0] = e.deviceSignalling() ? 1 : 0;
+  mode[1] = e.hostArena() ? 2 : e.fineGrainedArena() ? 1 : 0;
+  mode[2] = e.kernelCopy() ? 1 : 0;
+  mode[3] = e.graphed() ? 1 : e.interpreted() ? 1 + e.interpSlices() : 0;
+  gloo_amd::setError(0, e.graphError().empty() ? "" : "graph capture abandoned: " + e.graphError());
+}
+}  // namespace
+
 int gloo_hip_algorithm_mode(gloo_hip_algorithm_t a, int* mode) {
   return guarded([&] {
     GLOO_AMD_ENFORCE(a && mode, "null argument");
-    mode[0] = a->exec->deviceSignalling() ? 1 : 0;
-    mode[1] = a->exec->hostArena() ? 2 : a->exec->fineGrainedArena() ? 1 : 0;
-    mode[2] = a->exec->kernelCopy() ? 1 : 0;
-    mode[3] = a->exec->graphed() ? 1 : a->exec->interpreted() ? 1 + a->exec->interpSlices() : 0;
-    gloo_amd::setError(0, a->exec->graphError().empty() ? "" : "graph capture abandoned: " + a->exec->graphError());
+    modeOf(*a->exec, mode);
+  });
+}
+
+int gloo_hip_context_mode(gloo_hip_context_t ctx, int* mode) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(ctx && mode, "null argument");
+    GLOO_AMD_ENFORCE(ctx->last, "no function-style call on this context yet");
+    modeOf(*ctx->last, mode);
   });
 }
 

@@ -377,6 +377,23 @@ void PlanExecutor::setBuffers(const std::vector<void*>& inputs, const std::vecto
   classifyPointers();
 }
 
+void PlanExecutor::setStream(hipStream_t s) {
+  hipStream_t next = s;
+  if (!next) {
+    if (!ownedStream_) GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&ownedStream_, hipStreamNonBlocking));
+    next = ownedStream_;
+  }
+  if (next != stream_) {
+    // the new stream's work (which reuses the inboxes and this rank's
+    // buffers) starts after everything queued on the old one
+    if (!switchEvent_) GLOO_AMD_HIP_CHECK(hipEventCreateWithFlags(&switchEvent_, hipEventDisableTiming));
+    GLOO_AMD_HIP_CHECK(hipEventRecord(switchEvent_, stream_));
+    GLOO_AMD_HIP_CHECK(hipStreamWaitEvent(next, switchEvent_, 0));
+    stream_ = next;
+  }
+  ownStream_ = stream_ == ownedStream_;
+}
+
 void PlanExecutor::dropGraph() {
   if (!graphExec_) return;
   if (stream_) (void)hipStreamSynchronize(stream_);
@@ -387,6 +404,7 @@ void PlanExecutor::dropGraph() {
 void PlanExecutor::classifyPointers() {
   const char* forced = std::getenv("GLOO_AMD_FORCE_STAGING");  // tests: stage even same-device pointers
   const bool force = forced && forced[0] == '1';
+  anyRemote_ = false;  // recomputed for every buffer set (setBuffers)
   auto classify = [&](const std::vector<void*>& v, std::vector<bool>& remote, std::vector<char*>& stage,
                       size_t first) {
     remote.assign(v.size(), false);
@@ -423,7 +441,12 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       maxSegmentBytes_(maxSegmentBytes), recvElems_(recvElems) {
   es_ = gloo_hip_dtype_size(dtype_);
   GLOO_AMD_ENFORCE(es_ > 0, "unknown dtype ", dtype_);
-  GLOO_AMD_ENFORCE(op_ >= GLOO_HIP_SUM && op_ <= GLOO_HIP_MIN, "unknown op ", op_);
+  {
+    gloo_hip_custom_fn fn;
+    void* user;
+    custom_ = customOp(op_, &fn, &user);
+    GLOO_AMD_ENFORCE(custom_ || isBuiltinOp(op_), "unknown op ", op_);
+  }
   GLOO_AMD_ENFORCE(!ptrs_.empty(), "need at least one pointer");
   for (void* p : ptrs_) GLOO_AMD_ENFORCE(p != nullptr || count_ == 0, "null device pointer");
   const int me = ctx_->rank, P = ctx_->size;
@@ -436,7 +459,10 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   // GLOO_AMD_RING_MESH=0 only ring-chunked's.
   planAlgo_ = algo_;
   const char* m = std::getenv("GLOO_AMD_MESH");
-  const bool mesh = !(m && m[0] == '0') && P >= 2 && P <= GLOO_HIP_MAX_SRCS;
+  // a custom op is called as the reference calls its function: two operands
+  // at a time on the reference's own routes (the mesh plans fold with
+  // reverse / tree association)
+  const bool mesh = !(m && m[0] == '0') && P >= 2 && P <= GLOO_HIP_MAX_SRCS && !custom_;
   if (mesh && algo_ == GLOO_HIP_ALGO_RING_CHUNKED) {
     const char* rm = std::getenv("GLOO_AMD_RING_MESH");
     if (!(rm && rm[0] == '0')) planAlgo_ = GLOO_HIP_ALGO_RING_CHUNKED_MESH;
@@ -460,6 +486,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     stream_ = stream;
   } else {
     GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    ownedStream_ = stream_;
     ownStream_ = true;
   }
   // Baseline every channel before anyone can signal this instance (instance
@@ -574,7 +601,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     const char* im = std::getenv("GLOO_AMD_INTERP");
     const char* gm = std::getenv("GLOO_AMD_GRAPH");
     interpMode_ = deviceSignal_ && !(im && std::string(im) == "0") && !(gm && std::string(gm) == "1") &&
-                  interpBytes() > 0;
+                  interpBytes() > 0 && !custom_;
   }
   int32_t proposal = 0;
   if (interpMode_ && mailbox_ && !anyRemote_ && !hostArena_) {
@@ -719,7 +746,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     // one-workgroup launches (measured); "1" / "0" force it.
     const char* gm = std::getenv("GLOO_AMD_GRAPH");
     const std::string gmode = gm ? gm : "auto";
-    bool unfused = fuseBytes() == 0;
+    bool unfused = fuseBytes() == 0 || custom_;
     for (const Step& s : plan_.steps)
       if ((s.kind == GLOO_HIP_STEP_SEND || s.kind == GLOO_HIP_STEP_REDUCE || s.kind == GLOO_HIP_STEP_COPY ||
            s.kind == GLOO_HIP_STEP_LOCAL_REDUCE || s.kind == GLOO_HIP_STEP_LOCAL_BCAST ||
@@ -767,7 +794,11 @@ PlanExecutor::~PlanExecutor() {
       if (p) GLOO_AMD_HIP_RELEASE(hipFree(p));
     for (char* p : inStage_)
       if (p) GLOO_AMD_HIP_RELEASE(hipFree(p));
-    if (ownStream_ && stream_) (void)hipStreamDestroy(stream_);
+    if (ownedStream_) {
+      (void)hipStreamSynchronize(ownedStream_);
+      (void)hipStreamDestroy(ownedStream_);
+    }
+    if (switchEvent_) (void)hipEventDestroy(switchEvent_);
   } catch (...) {
     // teardown is best effort; never throw from a destructor
   }
@@ -894,9 +925,18 @@ void PlanExecutor::run() {
   const bool graphable = deviceSignal_ && graphMode_ && !profiling_;
   if (interp && interpCount_ > 0) {
     const uint64_t timeoutTicks = (uint64_t)ctx_->timeout().count() * 100000ull;  // 100 MHz realtime clock
+    const size_t bytes = count_ * es_;
+    // buffers on other GPUs of the process: the step list reads and writes
+    // their local copies (buildInterp)
+    for (size_t j = 0; anyRemote_ && j < inputs_.size(); j++)
+      if (inRemote_[j]) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(inStage_[j], inputs_[j], bytes, hipMemcpyDeviceToDevice, stream_));
+    for (size_t j = 1; anyRemote_ && j < ptrs_.size(); j++)
+      if (outRemote_[j]) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(outStage_[j], ptrs_[j], bytes, hipMemcpyDeviceToDevice, stream_));
     checkRc(launchPlanInterp(op_, dtype_, interpSteps_, interpCount_, r, timeoutTicks, ctx_->errorWordDevicePtr(me),
                              slices_, stream_),
             "plan interpreter");
+    for (size_t j = 1; anyRemote_ && j < ptrs_.size(); j++)
+      if (outRemote_[j]) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(ptrs_[j], outStage_[j], bytes, hipMemcpyDeviceToDevice, stream_));
   } else if (graphable && (graphExec_ || stableRuns_ >= 1)) {
     if (!graphExec_) tryCapture(r);  // sets the device epoch to r - 1
     if (graphExec_) {
@@ -962,17 +1002,22 @@ void PlanExecutor::tryCapture(uint64_t r) {
 void PlanExecutor::buildInterp() {
   interpDirty_ = false;
   interpCount_ = 0;
-  // a sliced plan has no other route: every rank's flags are per slice
-  GLOO_AMD_ENFORCE(slices_ == 1 || !anyRemote_,
-                   "buffers on another GPU of the process with a sliced interpreter plan");
-  if (anyRemote_) return;
+  // Buffers on another GPU of the process: the step list runs over their
+  // local staging copies (run() pulls them in before the launch and pushes
+  // the broadcast outputs back after it), so the launch touches local HBM
+  // only.  A sliced plan has no other route, its flags being per slice.
+  auto outPtr = [&](size_t j) -> char* {
+    return j < outRemote_.size() && outRemote_[j] ? outStage_[j] : static_cast<char*>(ptrs_[j]);
+  };
+  auto inPtr = [&](size_t j) -> const char* {
+    return j < inRemote_.size() && inRemote_[j] ? static_cast<const char*>(inStage_[j])
+                                                 : static_cast<const char*>(inputs_.at(j));
+  };
   // a sliced plan's message sizes were vetted when the ranks agreed on it
   const size_t limit = slices_ > 1 ? SIZE_MAX : interpBytes();
   auto userOrArena = [&](bool arena) { return arena ? arena_ : userPtr(0); };
   auto sendSrc = [&](const Step& t) -> const char* {
-    const char* base = t.flags & GLOO_HIP_SRC_ARENA ? arena_
-                       : t.flags & GLOO_HIP_FROM_INPUTS ? static_cast<const char*>(inputs_.at(0))
-                                                        : userPtr(0);
+    const char* base = t.flags & GLOO_HIP_SRC_ARENA ? arena_ : t.flags & GLOO_HIP_FROM_INPUTS ? inPtr(0) : userPtr(0);
     return base + t.src_off * es_;
   };
   std::vector<InterpStep> v;
@@ -1040,8 +1085,7 @@ void PlanExecutor::buildInterp() {
         withSeq(push(kInterpWait), i, waitFlag(s.peer, s.slot));
         break;
       case GLOO_HIP_STEP_REDUCE: {  // out = (in | out) op inbox
-        const char* a = (s.flags & GLOO_HIP_FROM_INPUTS ? static_cast<const char*>(inputs_.at(0))
-                                                         : static_cast<const char*>(userPtr(0))) +
+        const char* a = (s.flags & GLOO_HIP_FROM_INPUTS ? inPtr(0) : static_cast<const char*>(userPtr(0))) +
                         s.dst_off * es_;
         fold(userPtr(0) + s.dst_off * es_, {a, arena_ + s.src_off * es_}, s.length, 0);
         break;
@@ -1055,21 +1099,21 @@ void PlanExecutor::buildInterp() {
         // sliced: one piece per range the other steps use (userCuts)
         for (const auto& pc : pieces(s)) {
           const size_t off = pc.first * es_, len = pc.second;
-          const std::vector<void*>& from = s.flags & GLOO_HIP_FROM_INPUTS ? inputs_ : ptrs_;
+          const bool fromIn = s.flags & GLOO_HIP_FROM_INPUTS;
+          const size_t nfrom = fromIn ? inputs_.size() : ptrs_.size();
+          auto from = [&](size_t j) -> const char* { return (fromIn ? inPtr(j) : outPtr(j)) + off; };
           char* out0 = userPtr(0) + off;
-          if (from.size() == 1) {
-            if (!copy(out0, static_cast<const char*>(from[0]) + off, len)) return fail();
+          if (nfrom == 1) {
+            if (!copy(out0, from(0), len)) return fail();
             continue;
           }
           std::vector<const char*> srcs;
           size_t j = 0;
-          for (; j < from.size() && srcs.size() < GLOO_HIP_MAX_SRCS; j++)
-            srcs.push_back(static_cast<const char*>(from[j]) + off);
+          for (; j < nfrom && srcs.size() < GLOO_HIP_MAX_SRCS; j++) srcs.push_back(from(j));
           fold(out0, srcs, len, 0);
-          while (j < from.size()) {
+          while (j < nfrom) {
             srcs.assign(1, out0);
-            for (; j < from.size() && srcs.size() < GLOO_HIP_MAX_SRCS; j++)
-              srcs.push_back(static_cast<const char*>(from[j]) + off);
+            for (; j < nfrom && srcs.size() < GLOO_HIP_MAX_SRCS; j++) srcs.push_back(from(j));
             fold(out0, srcs, len, 0);
           }
         }
@@ -1077,7 +1121,7 @@ void PlanExecutor::buildInterp() {
       case GLOO_HIP_STEP_LOCAL_BCAST:
         for (const auto& pc : pieces(s))
           for (size_t j = 1; j < ptrs_.size(); j++)
-            if (!copy(userPtr(j) + pc.first * es_, userPtr(0) + pc.first * es_, pc.second)) return fail();
+            if (!copy(outPtr(j) + pc.first * es_, userPtr(0) + pc.first * es_, pc.second)) return fail();
         break;
       case GLOO_HIP_STEP_FOLD_SRC:
         foldSrcs.push_back(sendSrc(s));
@@ -1127,7 +1171,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
   // becomes ONE one-workgroup launch (launchFusedSmall): below a few KiB a
   // hop costs dispatches, not bytes.  Off while profiling reduce kernels.
   const size_t kFuseBytes = fuseBytes();
-  const bool fuse = deviceSignal_ && !profiling_ && kFuseBytes > 0;
+  const bool fuse = deviceSignal_ && !profiling_ && kFuseBytes > 0 && !custom_;
   auto userOrArena = [&](bool arena) { return arena ? arena_ : userPtr(0); };
   // a SEND's source: the arena, input 0 (gloo::reduce's first segments) or output 0
   auto sendSrc = [&](const Step& t) -> const char* {
@@ -1157,6 +1201,14 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
     if (s.kind == GLOO_HIP_STEP_SEND && i + 1 < steps.size() && steps[i + 1].kind == GLOO_HIP_STEP_SEND) {
       size_t j = i;
       while (j < steps.size() && steps[j].kind == GLOO_HIP_STEP_SEND) j++;
+      {
+        // one ticket counter and flag per (peer, slot): a batch sharing a
+        // channel would interleave tickets and publish out of order
+        std::set<std::pair<int, int>> chans;
+        for (size_t k = i; k < j; k++)
+          GLOO_AMD_ENFORCE(chans.insert({steps[k].peer, steps[k].slot}).second, "a SEND batch repeats channel (peer ",
+                           steps[k].peer, ", slot ", steps[k].slot, ")");
+      }
       if (deviceSignal_ && batchKernelCopy_) {
         for (size_t b = i; b < j; b += kMaxCopyEntries) {
           CopyDesc d[kMaxCopyEntries];

@@ -31,8 +31,10 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <mutex>
 #include <string>
 #include <type_traits>
+#include <vector>
 
 #include "gloo_amd.h"
 #include "gloo_amd/errors.h"
@@ -983,9 +985,64 @@ int launchCopySignal(void* dst, const void* src, size_t bytes, uint64_t* flag, S
   return launchCopySignalMulti(&d, 1, epoch, s);
 }
 
+struct CustomEntry {
+  gloo_hip_custom_fn fn;
+  void* user;
+};
+std::mutex& customMutex() {
+  static std::mutex m;
+  return m;
+}
+std::vector<CustomEntry>& customOps() {
+  static std::vector<CustomEntry> v;
+  return v;
+}
+
+bool isBuiltinOp(int op) { return op >= GLOO_HIP_SUM && op <= GLOO_HIP_MIN; }
+
+bool customOp(int op, gloo_hip_custom_fn* fn, void** user) {
+  if (op < GLOO_HIP_CUSTOM) return false;
+  std::lock_guard<std::mutex> lk(customMutex());
+  const size_t i = (size_t)(op - GLOO_HIP_CUSTOM);
+  if (i >= customOps().size()) return false;
+  *fn = customOps()[i].fn;
+  *user = customOps()[i].user;
+  return true;
+}
+
+// A k-source fold with a custom op: k - 1 calls of the 3-operand function,
+// left to right (the association of the reference's sequential calls).  The
+// destination may alias the first source only.
+int customFold(gloo_hip_custom_fn fn, void* user, int dtype, void* dst, const void* const* srcs, int k, size_t n,
+               int mode, hipStream_t s) {
+  if (mode != 0) return set_error(GLOO_HIP_EINVAL_ARG, "custom ops fold left to right only");
+  const size_t bytes = n * gloo_hip_dtype_size(dtype);
+  for (int j = 1; j < k; j++) {
+    const char* p = static_cast<const char*>(srcs[j]);
+    const char* d = static_cast<const char*>(dst);
+    if (d < p + bytes && p < d + bytes) return set_error(GLOO_HIP_EINVAL_ARG, "custom fold: dst overlaps a source");
+  }
+  if (k == 1) {
+    if (dst != srcs[0]) {
+      hipError_t e = hipMemcpyAsync(dst, srcs[0], bytes, hipMemcpyDeviceToDevice, s);
+      if (e != hipSuccess) return set_error((int)e, hipGetErrorString(e));
+    }
+    return GLOO_HIP_OK;
+  }
+  fn(user, dst, srcs[0], srcs[1], n, s);
+  for (int j = 2; j < k; j++) fn(user, dst, dst, srcs[j], n, s);
+  return check_launch("custom reduction");
+}
+
 int launchFold(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n, int mode,
                hipStream_t s) {
   if (k < 1 || k > GLOO_HIP_MAX_SRCS) return set_error(GLOO_HIP_EINVAL_ARG, "source count out of range");
+  gloo_hip_custom_fn cfn;
+  void* cuser;
+  if (customOp(op, &cfn, &cuser)) {
+    if (n == 0) return GLOO_HIP_OK;
+    return customFold(cfn, cuser, dtype, dst, srcs, k, n, mode, s);
+  }
   if (mode == 2 && (k & (k - 1))) return set_error(GLOO_HIP_EINVAL_ARG, "tree fold needs a power-of-two count");
   if (n == 0) return GLOO_HIP_OK;
   switch (mode) {
@@ -1061,13 +1118,36 @@ extern "C" {
 
 int gloo_hip_reduce3(int op, int dtype, void* c, const void* a, const void* b, size_t n,
                      gloo_hip_stream_t stream) {
+  gloo_hip_custom_fn cfn = nullptr;
+  void* cuser = nullptr;
+  const bool custom = customOp(op, &cfn, &cuser);
   if (n == 0) {
-    if (op < GLOO_HIP_SUM || op > GLOO_HIP_MIN) return set_error(GLOO_HIP_EINVAL_OP, "unknown reduction op");
+    if (!custom && (op < GLOO_HIP_SUM || op > GLOO_HIP_MIN)) return set_error(GLOO_HIP_EINVAL_OP, "unknown reduction op");
     if (dtype < 0 || dtype >= GLOO_HIP_NUM_DTYPES) return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
     return GLOO_HIP_OK;
   }
   if (!c || !a || !b) return set_error(GLOO_HIP_EINVAL_PTR, "null buffer pointer");
+  if (custom) {
+    if (dtype < 0 || dtype >= GLOO_HIP_NUM_DTYPES) return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
+    cfn(cuser, c, a, b, n, stream);
+    return check_launch("custom reduction");
+  }
   return dispatch3(op, dtype, c, a, b, n, static_cast<hipStream_t>(stream));
+}
+
+int gloo_hip_copy_kernel(void* dst, const void* src, size_t bytes, unsigned blocks, gloo_hip_stream_t stream) {
+  if (bytes == 0) return GLOO_HIP_OK;
+  if (!dst || !src) return set_error(GLOO_HIP_EINVAL_PTR, "null buffer pointer");
+  CopyDesc d{dst, src, bytes, nullptr, Seq{}, nullptr, copySignalGrid(bytes, blocks ? blocks : 1024u)};
+  return launchCopySignalMulti(&d, 1, nullptr, static_cast<hipStream_t>(stream));
+}
+
+int gloo_hip_register_op(gloo_hip_custom_fn fn, void* user, int* op_out) {
+  if (!fn || !op_out) return set_error(GLOO_HIP_EINVAL_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(customMutex());
+  customOps().push_back(CustomEntry{fn, user});
+  *op_out = GLOO_HIP_CUSTOM + (int)customOps().size() - 1;
+  return GLOO_HIP_OK;
 }
 
 int gloo_hip_reduce(int op, int dtype, void* dst, const void* src, size_t n,
@@ -1078,10 +1158,14 @@ int gloo_hip_reduce(int op, int dtype, void* dst, const void* src, size_t n,
 int gloo_hip_reduce_multi(int op, int dtype, void* dst, const void* const* srcs, int k,
                           size_t n, gloo_hip_stream_t stream) {
   if (k < 1 || k > GLOO_HIP_MAX_SRCS) return set_error(GLOO_HIP_EINVAL_ARG, "source count out of range");
-  if (op < GLOO_HIP_SUM || op > GLOO_HIP_MIN) return set_error(GLOO_HIP_EINVAL_OP, "unknown reduction op");
+  gloo_hip_custom_fn cfn = nullptr;
+  void* cuser = nullptr;
+  const bool custom = customOp(op, &cfn, &cuser);
+  if (!custom && (op < GLOO_HIP_SUM || op > GLOO_HIP_MIN)) return set_error(GLOO_HIP_EINVAL_OP, "unknown reduction op");
   if (dtype < 0 || dtype >= GLOO_HIP_NUM_DTYPES) return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
   if (n == 0) return GLOO_HIP_OK;
   if (!dst || !srcs) return set_error(GLOO_HIP_EINVAL_PTR, "null buffer pointer");
+  if (custom) return customFold(cfn, cuser, dtype, dst, srcs, k, n, 0, static_cast<hipStream_t>(stream));
   return dispatch_multi(op, dtype, dst, srcs, k, n, static_cast<hipStream_t>(stream));
 }
 

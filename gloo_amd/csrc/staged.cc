@@ -23,6 +23,7 @@
 #include "gloo_amd.h"
 #include "gloo_amd/common.h"
 #include "gloo_amd/errors.h"
+#include "gloo_amd/signal.h"
 
 namespace gloo_amd {
 namespace {
@@ -60,7 +61,9 @@ extern "C" int gloo_hip_reduce_staged(int op, int dtype, void* host_dst, const v
   try {
     const size_t es = gloo_hip_dtype_size(dtype);
     if (es == 0) return setError(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
-    if (op < GLOO_HIP_SUM || op > GLOO_HIP_MIN) return setError(GLOO_HIP_EINVAL_OP, "unknown reduction op");
+    gloo_hip_custom_fn cfn;
+    void* cuser;
+    if (!isBuiltinOp(op) && !customOp(op, &cfn, &cuser)) return setError(GLOO_HIP_EINVAL_OP, "unknown reduction op");
     if (n == 0) return GLOO_HIP_OK;
     if (!host_dst || !host_src || !dev_dst || !dev_src) return setError(GLOO_HIP_EINVAL_PTR, "null buffer pointer");
     int device = 0;

@@ -85,6 +85,10 @@ class PlanExecutor {
   // Function-style calls (gloo::allreduce(opts)) reuse one executor for a
   // given option set and rebind the buffers before each run.
   void setBuffers(const std::vector<void*>& inputs, const std::vector<void*>& outputs);
+  // ... and to the call's stream (nullptr: the executor's own stream, and
+  // run() returns with the outputs complete).  Work on the new stream is
+  // ordered after everything queued on the previous one.
+  void setStream(hipStream_t stream);
   ~PlanExecutor();
   PlanExecutor(const PlanExecutor&) = delete;
   PlanExecutor& operator=(const PlanExecutor&) = delete;
@@ -150,6 +154,7 @@ class PlanExecutor {
 
   std::shared_ptr<Context> ctx_;
   int algo_, op_, dtype_;
+  bool custom_ = false;  // op_ is a registered custom reduction (gloo_hip_register_op)
   int planAlgo_;  // the plan executed (RING_CHUNKED may run as RING_CHUNKED_MESH)
   size_t es_;
   std::vector<void*> ptrs_;     // outputs (the reference's ptrs_ / out)
@@ -173,7 +178,9 @@ class PlanExecutor {
   std::unique_ptr<HostShm> arenaShm_;
   std::vector<std::unique_ptr<HostShm>> peerShm_;
   hipStream_t stream_ = nullptr;
-  bool ownStream_ = false;
+  bool ownStream_ = false;            // stream_ is the executor's own: run() returns with outputs complete
+  hipStream_t ownedStream_ = nullptr;  // the executor's own stream, if created
+  hipEvent_t switchEvent_ = nullptr;
   std::vector<Peer> peers_;
   std::map<std::pair<int, int>, uint64_t> remoteRegion_;  // (peer, slot) -> elts into peer arena
   // Sequence numbers.  Channel (peer, slot) carries perRun messages per run;

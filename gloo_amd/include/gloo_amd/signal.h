@@ -23,6 +23,8 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include "gloo_amd.h"
+
 #include <cstdint>
 
 namespace gloo_amd {
@@ -120,6 +122,12 @@ int launchPlanInterp(int op, int dtype, const InterpStep* steps, int nsteps, uin
 // Returns the previous slot.  launchStampInit sets k slots to (~0, 0).
 uint64_t* setLaunchStamp(uint64_t* slot);
 int launchStampInit(uint64_t* stamps, int k, hipStream_t stream);
+
+// Registered custom reductions (gloo_hip_register_op): op codes
+// GLOO_HIP_CUSTOM + i.  customOp fills fn/user and returns true for a
+// registered code.
+bool isBuiltinOp(int op);
+bool customOp(int op, gloo_hip_custom_fn* fn, void** user);
 
 int launchFold(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n, int mode,
                hipStream_t stream);

@@ -117,6 +117,28 @@ int gloo_hip_reduce_multi(int op, int dtype, void* dst,
 int gloo_hip_reduce_staged(int op, int dtype, void* host_dst, const void* host_src, size_t n,
                            void* dev_dst, void* dev_src, size_t piece_elems, gloo_hip_stream_t stream);
 
+/* Custom reductions: gloo::ReductionType::CUSTOM (= 1000) with a user
+ * function (gloo/algorithm.h:49-95) and the new-style reduce `Func`
+ * (gloo/allreduce.h:36), on device memory.  The function enqueues
+ * c[i] = a[i] (op) b[i], i < n, on `stream` (c may alias a; it must not
+ * allocate, free or synchronise — it may be captured into a hipGraph).
+ * gloo_hip_register_op returns an op code >= GLOO_HIP_CUSTOM that every
+ * entry point taking an `op` accepts.  Algorithms with a custom op run the
+ * reference's own exchange routes (no mesh plans), call the function for
+ * every REDUCE and FOLD step (a k-source fold as k - 1 calls, left to
+ * right), and never use the fused or interpreted kernels. */
+#define GLOO_HIP_CUSTOM 1000
+typedef void (*gloo_hip_custom_fn)(void* user, void* c, const void* a, const void* b, size_t n,
+                                   gloo_hip_stream_t stream);
+int gloo_hip_register_op(gloo_hip_custom_fn fn, void* user, int* op_out);
+
+/* The kernel copy engine of a plan's SEND steps (copy_signal_kernel
+ * without a flag): dst[0, bytes) = src[0, bytes) in 16-byte packets at any
+ * relative misalignment, with `blocks` workgroups (0: one per 16 KiB tile,
+ * capped at 1024).  Exported for measurement tools (blit vs kernel copies;
+ * DESIGN.md §4) and callers that want a copy with no DMA-engine dependence. */
+int gloo_hip_copy_kernel(void* dst, const void* src, size_t bytes, unsigned blocks, gloo_hip_stream_t stream);
+
 /* Size in bytes of one element of `dtype`, or 0 when dtype is unknown. */
 size_t gloo_hip_dtype_size(int dtype);
 
@@ -328,6 +350,9 @@ int gloo_hip_algorithm_stats(gloo_hip_algorithm_t algo, double* stats4);
  * interpreter with k - 1 workgroups (> 1: sliced).  If graph capture was
  * abandoned, gloo_hip_last_error() says why. */
 int gloo_hip_algorithm_mode(gloo_hip_algorithm_t algo, int* mode4);
+/* The same for the schedule that ran the latest function-style call
+ * (gloo_hip_allreduce / gloo_hip_reduce_to_root) on `ctx`. */
+int gloo_hip_context_mode(gloo_hip_context_t ctx, int* mode4);
 
 /* ------------------------------------------------------------------------
  * New-style function API: gloo::allreduce(const AllreduceOptions&)

@@ -61,7 +61,7 @@ class Barrier {
 };
 
 // P ranks as threads; each gets a connected gloo::Context (timeout `ms`).
-std::string spawn(int P, int ms, const std::function<void(std::shared_ptr<gloo::Context>)>& fn) {
+std::string spawn(int P, int ms, const std::function<void(std::shared_ptr<gloo::Context>)>& fn, bool gpu = true) {
   auto store = std::make_shared<gloo::rendezvous::HashStore>();
   Barrier barrier(P);
   std::vector<std::thread> ts;
@@ -70,7 +70,7 @@ std::string spawn(int P, int ms, const std::function<void(std::shared_ptr<gloo::
   for (int rank = 0; rank < P; rank++) {
     ts.emplace_back([&, rank] {
       try {
-        HIPOK(hipSetDevice(0));
+        if (gpu) HIPOK(hipSetDevice(0));
         auto ctx = std::make_shared<gloo::rendezvous::Context>(rank, P);
         ctx->setTimeout(std::chrono::milliseconds(ms));
         if (P > 1) {
@@ -239,6 +239,14 @@ std::string silentPeerCase() {
   return seen.empty() ? std::string("no IoException from a silent peer") : std::string();
 }
 
+// CPU only (no HIP call): the library context bootstrapped over the
+// gloo::Context's all-gather, created and destroyed twice per rank.
+std::string bootstrapCase(int P) {
+  return spawn(P, 10000, [&](std::shared_ptr<gloo::Context> ctx) {
+    for (int i = 0; i < 2; i++) gloo::hip_bridge::BootstrapContext b(ctx, 0);
+  }, false);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -248,6 +256,8 @@ int main(int argc, char** argv) {
     std::function<std::string()> fn;
   };
   std::vector<Case> cases;
+  for (int P : {1, 2, 3, 5})
+    cases.push_back({"bootstrap_cpu/P" + std::to_string(P), [=] { return bootstrapCase(P); }});
   for (int P : {1, 2, 3, 4, 5}) {
     for (int n : {1, 1000, 100003}) {
       cases.push_back({"ring_chunked/P" + std::to_string(P) + "/n" + std::to_string(n),

@@ -103,13 +103,23 @@ def test_bridge_header_is_gloo_side_only():
     assert "_ZN4gloo" not in out  # no symbol of namespace gloo (the reference's)
 
 
+def test_bridge_bootstrap_cpu():
+    """The bridge's BootstrapContext (gloo::allgather over the reference's
+    own TCP pairs) creates and destroys the library context — no GPU call."""
+    if not os.path.exists(BRIDGE_TEST):
+        pytest.skip("oracle/_ref/bridge_test not built (needs /root/reference at build time)")
+    r = subprocess.run([BRIDGE_TEST, "bootstrap_cpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("ok   bootstrap_cpu") == 4, r.stdout
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
 def test_bridge_program_on_gpu():
     pytest.importorskip("torch")
     if not os.path.exists(BRIDGE_TEST):
         pytest.skip("oracle/_ref/bridge_test not built (needs /root/reference at build time)")
-    r = subprocess.run([BRIDGE_TEST], capture_output=True, text=True, timeout=540)
+    r = subprocess.run([BRIDGE_TEST, "/"], capture_output=True, text=True, timeout=540)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith(("ok", "FAIL"))]
     assert lines and all(l.startswith("ok") for l in lines), r.stdout

@@ -147,6 +147,7 @@ torch.cuda.set_device(dev)
 ctx = gloo_amd.Context(rank, size, store, device=dev, timeout_ms=60000)
 sets = [(torch.empty(n, device=dev), torch.empty(n, device=dev)) for _ in range(2)]
 res = []
+modes = []
 for it, s in enumerate([0, 0, 0, 1, 1, 0]):
     inp, outp = sets[s]
     inp.fill_((rank + 1) * (it + 1))
@@ -159,8 +160,10 @@ for it, s in enumerate([0, 0, 0, 1, 1, 0]):
         gloo_amd.reduce_to_root(ctx, outp.data_ptr(), n, "f32", it % size, "sum", input=inp.data_ptr(),
                                 max_segment_bytes=256 << 10)
     res.append(outp.cpu().numpy())
+    modes.append(ctx.last_mode()["interp_slices"])
 ctx.close()
 np.save(out, np.array(res))
+np.save(out + ".slices.npy", np.array(modes))
 '''
 
 
@@ -197,6 +200,12 @@ def test_processes(torch, kind, P, env):
                                    os.path.join(d, f"o{r}.npy")], env=e) for r in range(P)]
         assert [p.wait(timeout=300) for p in procs] == [0] * P
         ys = [np.load(os.path.join(d, f"o{r}.npy")) for r in range(P)]
+        slices = [np.load(os.path.join(d, f"o{r}.npy.slices.npy")) for r in range(P)]
+    if env.get("GLOO_AMD_TEST_N") == "8000000":
+        # the step list would overflow the device list: slicing refused
+        assert all((s == 0).all() for s in slices), slices
+    elif "GLOO_AMD_INTERP_SLICE_BYTES" in env:
+        assert all((s > 1).all() for s in slices), slices
     for it in range(ys[0].shape[0]):
         want = (it + 1) * P * (P + 1) / 2
         if kind in ("bcube", "ring"):

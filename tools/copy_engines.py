@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Copy engines of a SEND step on one MI355X:
+the blit engine (hipMemcpyAsync, what GLOO_AMD_COPY=memcpy uses) against the
+kernel copy engine (copy_signal_kernel via gloo_hip_copy_kernel) at 4, 16 and
+64 MiB, with the workgroup counts the executor uses (64 per peer) and more.
+Same-GPU (HBM -> HBM) copies only: that is all one GPU can show; run under
+`rocprofv3 --kernel-trace --stats` for the kernel's own durations.  Buffers
+rotate over a 1 GiB footprint (> 256 MiB Infinity Cache).  One JSON line per
+measurement; achieved GB/s counts read + write bytes (2 x size)."""
+import ctypes
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import gloo_amd as hip  # noqa: E402
+
+FOOT = 1 << 30
+
+
+HIPRT = ctypes.CDLL("libamdhip64.so")
+HIPRT.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+
+
+def blit(d, x, nbytes, stream):
+    rc = HIPRT.hipMemcpyAsync(d, x, nbytes, 3, stream)  # hipMemcpyDeviceToDevice
+    assert rc == 0, rc
+
+
+def main():
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream()
+    src = torch.empty(FOOT // 4, device=dev).uniform_(-1, 1)
+    dst = torch.empty(FOOT // 4, device=dev)
+    for mib in (4, 16, 64):
+        nbytes = mib << 20
+        slots = FOOT // nbytes
+        k = max(40, 2560 // mib)
+        engines = [("memcpy", None)] + [("kernel", b) for b in (64, 256, 1024)]
+        for name, blocks in engines:
+            def once(i):
+                d = dst.data_ptr() + (i % slots) * nbytes
+                x = src.data_ptr() + ((i + 1) % slots) * nbytes
+                if name == "memcpy":
+                    blit(d, x, nbytes, s.cuda_stream)
+                else:
+                    hip.copy_kernel(d, x, nbytes, blocks, s.cuda_stream)
+            for i in range(10):
+                once(i)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for i in range(k):
+                once(i)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / k
+            print(json.dumps({"mib": mib, "engine": name, "blocks": blocks, "launches": k,
+                              "us_per_copy": round(us, 2), "GBs_rw": round(2 * nbytes / us / 1e3, 1)}), flush=True)
+    # the multi-destination form a mesh SEND batch issues: 7 peers' pieces of
+    # one 256 MiB buffer (config 3's mesh route at P = 8: 32 MiB per peer)
+    piece = 32 << 20
+    for name in ("kernel7", "memcpy7"):
+        def batch():
+            for j in range(7):
+                d, x = dst.data_ptr() + j * piece, src.data_ptr() + j * piece
+                if name == "memcpy7":
+                    blit(d, x, piece, s.cuda_stream)
+                else:
+                    hip.copy_kernel(d, x, piece, 64, s.cuda_stream)
+        batch()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            batch()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / 10
+        print(json.dumps({"mib": 7 * 32, "engine": name, "us_per_batch": round(us, 2),
+                          "GBs_rw": round(2 * 7 * piece / us / 1e3, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
