@@ -107,6 +107,19 @@ uint32_t* Context::errorWordDevicePtr(int r) {
   return reinterpret_cast<uint32_t*>(static_cast<char*>(shmDev_) + off);
 }
 
+uint64_t Context::acquireInstance() {
+  const uint64_t inst = nextInstance();
+  std::lock_guard<std::mutex> lk(liveMutex_);
+  GLOO_AMD_ENFORCE(live_.insert(inst % kMaxLiveInstances).second, "more than ", kMaxLiveInstances,
+                   " live algorithm instances on one context");
+  return inst;
+}
+
+void Context::releaseInstance(uint64_t inst) {
+  std::lock_guard<std::mutex> lk(liveMutex_);
+  live_.erase(inst % kMaxLiveInstances);
+}
+
 void Context::barrier(const std::string& tag) { (void)allgather("barrier/" + tag, {}); }
 
 std::vector<std::vector<char>> Context::allgather(const std::string& tag, const std::vector<char>& mine) {

@@ -278,15 +278,6 @@ int maxSlices() {
   return v;
 }
 
-std::set<std::pair<const Context*, uint64_t>>& liveInstances() {
-  static std::set<std::pair<const Context*, uint64_t>> s;
-  return s;
-}
-std::mutex& liveMutex() {
-  static std::mutex m;
-  return m;
-}
-
 }  // namespace
 
 // A pinned host-memory segment every rank of the node can map (HOST workspace).
@@ -474,13 +465,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
                   recvElems_);
   GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
   classifyPointers();
-  inst_ = ctx_->nextInstance();
-  {
-    std::lock_guard<std::mutex> lk(liveMutex());
-    auto key = std::make_pair((const Context*)ctx_.get(), inst_ % Context::kMaxLiveInstances);
-    GLOO_AMD_ENFORCE(liveInstances().insert(key).second, "more than ", Context::kMaxLiveInstances,
-                     " live algorithm instances on one context");
-  }
+  inst_ = ctx_->acquireInstance();
   GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
   if (stream) {
     stream_ = stream;
@@ -802,8 +787,7 @@ PlanExecutor::~PlanExecutor() {
   } catch (...) {
     // teardown is best effort; never throw from a destructor
   }
-  std::lock_guard<std::mutex> lk(liveMutex());
-  liveInstances().erase(std::make_pair((const Context*)ctx_.get(), inst_ % Context::kMaxLiveInstances));
+  ctx_->releaseInstance(inst_);
 }
 
 void PlanExecutor::waitCounter(std::atomic<uint64_t>& c, uint64_t target, int peer, int slot) {

@@ -15,6 +15,8 @@
 #include <chrono>
 #include <cstdint>
 #include <memory>
+#include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -44,6 +46,12 @@ class Context : public std::enable_shared_from_this<Context> {
   // the same on every rank (the role of gloo::Context::nextSlot).
   uint64_t nextInstance() { return nextInstance_++; }
   static constexpr uint64_t kMaxLiveInstances = 64;
+  // nextInstance() for a user of the control block's counters (an
+  // algorithm's executor, a transport device), registered live until
+  // releaseInstance: counters are recycled modulo kMaxLiveInstances, so at
+  // most that many may be live at once.
+  uint64_t acquireInstance();
+  void releaseInstance(uint64_t inst);
 
   // Counter for messages src -> dst on `slot` of instance `inst`.
   std::atomic<uint64_t>& counter(uint64_t inst, int src, int dst, int slot);
@@ -66,6 +74,8 @@ class Context : public std::enable_shared_from_this<Context> {
   int device_ = -1;
   int pid_;
   uint64_t nextInstance_ = 0;
+  std::mutex liveMutex_;
+  std::set<uint64_t> live_;
   std::string shmName_;
   void* shm_ = nullptr;
   void* shmDev_ = nullptr;
