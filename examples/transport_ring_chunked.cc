@@ -40,6 +40,15 @@ using gloo_amd::transport::Device;
     if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
+static bool g_trace = std::getenv("TRANSPORT_TRACE") != nullptr;
+
+template <typename T>
+float firstValue(const T* p) {
+  T v;
+  if (hipMemcpy(&v, p, sizeof(T), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return (float)v;
+}
+
 template <typename T>
 class RingChunked {
  public:
@@ -91,6 +100,10 @@ class RingChunked {
         length = 0;
       }
       recvDataBuf_[chunkOffset & 1]->waitRecv();
+      if (g_trace)
+        std::fprintf(stderr, "r%d pass1 round %d chunk %d off %zu len %zu inbox %g mine %g\n", rank_, round,
+                     (int)chunkOffset, offset, length, length ? firstValue(inbox_[chunkOffset & 1]) : 0.f,
+                     length ? firstValue(&ptrs_[0][offset]) : 0.f);
       if (length > 0) reduce(&ptrs_[0][offset], inbox_[chunkOffset & 1], length);
       sendNotificationBuf_->send();
       recvNotificationBuf_->waitRecv();
@@ -106,6 +119,9 @@ class RingChunked {
         length = 0;
       }
       recvDataBuf_[chunkOffset & 1]->waitRecv();
+      if (g_trace)
+        std::fprintf(stderr, "r%d pass2 round %d chunk %d off %zu len %zu inbox %g\n", rank_, round, (int)chunkOffset,
+                     offset, length, length ? firstValue(inbox_[chunkOffset & 1]) : 0.f);
       if (length > 0)
         CHECK(hipMemcpy(&ptrs_[0][offset], inbox_[chunkOffset & 1], length * sizeof(T), hipMemcpyDeviceToDevice));
       if (round < (chunks_ - 4)) {
@@ -136,6 +152,9 @@ class RingChunked {
       offset = 0;
       length = 1;  // gloo/allreduce_ring_chunked.h:224-231
     }
+    if (g_trace)
+      std::fprintf(stderr, "r%d send chunk %d buf %d off %zu len %zu value %g\n", rank_, chunkOffset, chunkOffset & 1,
+                   offset, length, firstValue(&ptrs_[0][offset]));
     sendDataBuf_[chunkOffset & 0x1]->send(offset * sizeof(T), length * sizeof(T));
   }
 

@@ -717,6 +717,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     const char* cp = std::getenv("GLOO_AMD_COPY");
     const std::string cmode = cp ? cp : "auto";
     kernelCopy_ = cmode == "kernel";
+    autoCopy_ = cmode == "auto";
     batchKernelCopy_ = cmode != "memcpy";
     // Workgroups per copy (executor.h): a few dozen saturate an xGMI link.
     // GLOO_AMD_COPY_BLOCKS overrides both the remote and the same-GPU size.
@@ -1122,6 +1123,10 @@ void PlanExecutor::buildInterp() {
     if (v.size() > (size_t)kInterpMaxSteps) return fail();
   }
   if (v.empty()) return;
+  // the bound the ranks agreed on (slicedInterpSteps) must cover what was
+  // emitted; an under-count would have let an unrunnable plan be proposed
+  GLOO_AMD_ENFORCE(slices_ == 1 || v.size() <= slicedInterpSteps(plan_, (int)inputs_.size(), (int)ptrs_.size()),
+                   "sliced step list of ", v.size(), " entries exceeds its proposed bound");
   // an earlier launch may still read the list
   GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
   GLOO_AMD_HIP_CHECK(hipMemcpy(interpSteps_, v.data(), v.size() * sizeof(InterpStep), hipMemcpyHostToDevice));
@@ -1334,8 +1339,15 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
       case GLOO_HIP_STEP_SEND: {
         char* dst = peers_[s.peer].base + (remoteRegion_[{s.peer, s.slot}] + s.dst_off) * es_;
         const char* src = sendSrc(s);
-        if (kernelCopy_) {
-          const unsigned grid = copySignalGrid(s.length * es_, copyBlocksFor(s.peer));
+        // GLOO_AMD_COPY=auto: a lone SEND of >= 16 MiB to a rank on this
+        // same GPU goes to the copy kernel with 256 workgroups, which moves
+        // HBM -> HBM faster than the blit engine from 16 MiB up (one MI355X:
+        // 8.1 vs 9.7 us at 16 MiB, 22.0 vs 26.0 us at 64 MiB kernel time,
+        // profiles/round2/r2d_rocprof_copy_engines_segments.csv); below that,
+        // and over xGMI, hipMemcpyAsync + signal
+        const bool bigLocal = autoCopy_ && s.length * es_ >= (16u << 20) && peers_[s.peer].device == ctx_->device();
+        if (kernelCopy_ || bigLocal) {
+          const unsigned grid = copySignalGrid(s.length * es_, bigLocal ? 256u : copyBlocksFor(s.peer));
           checkRc(launchCopySignal(dst, src, s.length * es_, sigFlag(s.peer, s.slot),
                                    seqOf(i, r, graph), ticket_ + (size_t)s.peer * GLOO_HIP_NUM_SLOTS + s.slot, epoch,
                                    grid, stream_),

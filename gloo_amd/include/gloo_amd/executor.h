@@ -209,6 +209,7 @@ class PlanExecutor {
   std::vector<bool> peerMailboxIpc_;
   bool fineArena_ = false;     // inbox arena in fine-grained (cross-device coherent) memory
   bool kernelCopy_ = false;    // SEND = copy_signal_kernel instead of hipMemcpyAsync + signal
+  bool autoCopy_ = false;      // GLOO_AMD_COPY=auto: the engine picked per SEND by size and peer placement
   unsigned copyBlocks_ = 64;        // per copy to a peer on another GPU (xGMI)
   // per copy to a peer on this GPU: also 64 — ranks sharing a GPU run their
   // copies concurrently, and whole-chip copy grids convoy behind each other

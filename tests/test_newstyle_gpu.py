@@ -205,7 +205,11 @@ def test_processes(torch, kind, P, env):
         # the step list would overflow the device list: slicing refused
         assert all((s == 0).all() for s in slices), slices
     elif "GLOO_AMD_INTERP_SLICE_BYTES" in env:
-        assert all((s > 1).all() for s in slices), slices
+        # the interpreter runs (sliced where the plan allows: the 2 x 3 BCUBE
+        # mesh's pairwise folds through arena temporaries keep one workgroup)
+        assert all((s >= 1).all() for s in slices), slices
+        if kind != "bcube":
+            assert all((s > 1).all() for s in slices), slices
     for it in range(ys[0].shape[0]):
         want = (it + 1) * P * (P + 1) / 2
         if kind in ("bcube", "ring"):
