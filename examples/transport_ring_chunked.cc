@@ -85,7 +85,7 @@ class RingChunked {
     if (count_ == 0) return;
     for (size_t i = 1; i < ptrs_.size(); i++) reduce(ptrs_[0], ptrs_[i], count_);
     if (size_ == 1) {
-      for (size_t i = 1; i < ptrs_.size(); i++) CHECK(hipMemcpy(ptrs_[i], ptrs_[0], bytes_, hipMemcpyDeviceToDevice));
+      for (size_t i = 1; i < ptrs_.size(); i++) copy(ptrs_[i], ptrs_[0], bytes_);
       return;
     }
     copyChunkAtOffset(2 * rank_);
@@ -122,8 +122,7 @@ class RingChunked {
       if (g_trace)
         std::fprintf(stderr, "r%d pass2 round %d chunk %d off %zu len %zu inbox %g\n", rank_, round, (int)chunkOffset,
                      offset, length, length ? firstValue(inbox_[chunkOffset & 1]) : 0.f);
-      if (length > 0)
-        CHECK(hipMemcpy(&ptrs_[0][offset], inbox_[chunkOffset & 1], length * sizeof(T), hipMemcpyDeviceToDevice));
+      if (length > 0) copy(&ptrs_[0][offset], inbox_[chunkOffset & 1], length * sizeof(T));
       if (round < (chunks_ - 4)) {
         sendNotificationBuf_->send();
         recvNotificationBuf_->waitRecv();
@@ -133,7 +132,7 @@ class RingChunked {
     sendNotificationBuf_->send();
     recvNotificationBuf_->waitRecv();
     for (int i = 0; i < 2; i++) sendDataBuf_[i]->waitSend();
-    for (size_t i = 1; i < ptrs_.size(); i++) CHECK(hipMemcpy(ptrs_[i], ptrs_[0], bytes_, hipMemcpyDeviceToDevice));
+    for (size_t i = 1; i < ptrs_.size(); i++) copy(ptrs_[i], ptrs_[0], bytes_);
   }
 
  private:
@@ -141,6 +140,13 @@ class RingChunked {
   // gloo/cuda_allreduce_ring_chunked.cc:185-190
   void reduce(T* dst, const T* src, size_t n) {
     fn_->call(dst, src, n, stream_);
+    CHECK(hipStreamSynchronize(stream_));
+  }
+  // The reference's memcpy: a device copy that has COMPLETED on return.
+  // (hipMemcpy device-to-device may return before the copy ran, and a
+  // notification sent after it would let the peer overwrite the inbox first.)
+  void copy(void* dst, const void* src, size_t bytes) {
+    CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream_));
     CHECK(hipStreamSynchronize(stream_));
   }
   void copyChunkAtOffset(int chunkOffset) {
