@@ -181,10 +181,15 @@ int main(int argc, char** argv) {
   const int P = argc > 1 ? std::atoi(argv[1]) : 4;
   const int count = argc > 2 ? std::atoi(argv[2]) : 100003;
   const int runs = argc > 3 ? std::atoi(argv[3]) : 2;
-  const std::string url = "mem:transport_ring_chunked_" + std::to_string(::getpid());
+  // process mode: `transport_ring_chunked P count runs RANK STORE_DIR` runs
+  // one rank in this process (receive buffers shared through HIP IPC)
+  const int only = argc > 5 ? std::atoi(argv[4]) : -1;
+  const std::string url = only >= 0 ? std::string("file:") + argv[5]
+                                    : "mem:transport_ring_chunked_" + std::to_string(::getpid());
   std::vector<std::string> errors(P);
   std::vector<std::thread> ts;
   for (int rank = 0; rank < P; rank++) {
+    if (only >= 0 && rank != only) continue;
     ts.emplace_back([&, rank] {
       try {
         CHECK(hipSetDevice(0));

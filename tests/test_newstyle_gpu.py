@@ -6,6 +6,7 @@ Ranks as threads of one process (host-signalled, the pattern of
 gloo/test/base_test.h:107-152) and as processes (device-signalled, inboxes
 over HIP IPC, hipGraph replay of the cached schedule).
 """
+import json
 import os
 import subprocess
 import sys
@@ -217,3 +218,54 @@ def test_processes(torch, kind, P, env):
                 assert (ys[r][it] == want).all(), (r, it)
         else:
             assert (ys[it % P][it] == want).all(), it
+
+
+STAGING_WORKER = r'''
+import os, sys, json, numpy as np
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, size, store = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+torch.cuda.set_device(0)
+n = 50_000
+ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=60000)
+res = []
+for it, staged in enumerate([False, True, True, False]):
+    # a second output "on another GPU" (GLOO_AMD_FORCE_STAGING marks it so)
+    # from the second call on: the cached sliced schedule is rebound to it
+    if staged:
+        os.environ["GLOO_AMD_FORCE_STAGING"] = "1"
+    else:
+        os.environ.pop("GLOO_AMD_FORCE_STAGING", None)
+    outs = [torch.full((n,), float((rank + 1) * (j + 1) * (it + 1)), device="cuda:0") for j in range(2)]
+    torch.cuda.synchronize()
+    gloo_amd.allreduce(ctx, [o.data_ptr() for o in outs], n, "f32", "sum")
+    m = ctx.last_mode()
+    res.append({"vals": [float(o[0]) for o in outs] + [float(o[-1]) for o in outs],
+                "ok": all(bool((o == o[0]).all()) for o in outs), "slices": m["interp_slices"]})
+ctx.close()
+print("RESULT" + json.dumps(res), flush=True)
+'''
+
+
+def test_processes_sliced_rebind_to_staged_output(torch):
+    """ADVICE r1: a cached sliced schedule rebound to an output on another GPU
+    of the process used to throw on that rank only (its peers then waited
+    out the timeout).  Now the step list runs over a local staging copy of
+    that output and keeps the sliced form; a later local rebinding runs
+    without staging again."""
+    P = 2
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(STAGING_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT)
+        e.pop("GLOO_AMD_FORCE_STAGING", None)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s")], env=e,
+                                  stdout=subprocess.PIPE, text=True) for r in range(P)]
+        outs = [p.communicate(timeout=240)[0] for p in procs]
+        assert [p.returncode for p in procs] == [0] * P
+    for r in range(P):
+        res = json.loads(outs[r].split("RESULT", 1)[1])
+        for it, x in enumerate(res):
+            want = (it + 1) * 3 * P * (P + 1) / 2
+            assert x["ok"] and x["vals"] == [want] * 4, (r, it, x)
+            assert x["slices"] > 1, (r, it, x)

@@ -27,3 +27,18 @@ def test_transport_ring_chunked(P, count, runs):
     r = subprocess.run([EXE, str(P), str(count), str(runs)], capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("ok"), r.stdout
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("P,count", [(2, 100003), (4, 1 << 20)])
+def test_transport_ring_chunked_processes(tmp_path, P, count):
+    """The same with ranks as processes: receive buffers exported as HIP IPC
+    handles through a file store, arrivals through the node's control block."""
+    pytest.importorskip("torch")
+    if not os.path.exists(EXE):
+        pytest.skip("example not built")
+    procs = [subprocess.Popen([EXE, str(P), str(count), "2", str(r), str(tmp_path / "store")],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(P)]
+    outs = [p.communicate(timeout=280)[0] for p in procs]
+    assert [p.returncode for p in procs] == [0] * P, outs
+    assert all(o.startswith("ok") for o in outs), outs
