@@ -249,6 +249,7 @@ def host_staged(torch, hip, n, dev, iters=20):
     out = {}
     for name, fn in (("serial", serial), ("pipelined_4MiB", pipelined(1 << 20)),
                      ("pipelined_8MiB", pipelined(1 << 21)), ("pipelined_16MiB", pipelined(1 << 22)),
+                     ("pipelined_32MiB", pipelined(1 << 23)),
                      ("zero_copy_src", zc_src), ("zero_copy_both", zc_both)):
         dt = timed(fn)
         out[name] = {"gib_s_alg": round(3.0 * n * 4 / dt / GIB, 2), "ms_per_chunk": round(dt * 1e3, 3)}
@@ -670,18 +671,25 @@ def main():
     torch.cuda.synchronize(dev)
 
     # Timed region: barrier + sync on both sides, exactly K back-to-back
-    # launches bracketed by two HIP events on the launch stream.  The event
-    # average (region / K) is the kernel's launch-to-launch duration; it
-    # includes the ~1-2 us dispatch boundary that rocprofv3's per-kernel
-    # duration excludes (profiles/ keeps both for comparison).
+    # launches.  Kernel duration: two HIP events on the launch stream, the
+    # first recorded right AFTER launch 1 is enqueued and the second after
+    # launch K, so region / (K - 1) is the launch-to-launch duration of
+    # kernels 2..K running back to back.  (An event recorded before launch 1
+    # reaches the idle GPU first and would add launch 1's host submission
+    # latency, ~4 us, to the region: 0.2 us per step at K = 20.)  It still
+    # includes the dispatch boundary between launches that rocprofv3's
+    # per-kernel duration excludes (profiles/ keeps both for comparison).
     e_start = torch.cuda.Event(enable_timing=True)
     e_end = torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    skip = 1 if args.steps >= 2 else 0   # K = 1: the whole single launch
+    for i in range(skip):
+        step(i)
     e_start.record(stream)
-    for i in range(args.steps):
+    for i in range(skip, args.steps):
         step(i)
     e_end.record(stream)
     torch.cuda.synchronize(dev)
@@ -689,7 +697,7 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     region_ms = e_start.elapsed_time(e_end)
-    kern_ms = region_ms / args.steps
+    kern_ms = region_ms / (args.steps - skip)
 
     t_local = torch.tensor([wall], dtype=torch.float64)
     k_all = torch.tensor([kern_ms], dtype=torch.float64)
@@ -732,7 +740,8 @@ def main():
                          "algorithmic_bytes_per_launch": int(alg_bytes),
                          "kernel_avg_us": round(kern_ms * 1e3, 3),
                          "per_rank_kernel_avg_us": [round(x * 1e3, 3) for x in per_rank_kernel_ms],
-                         "event_region_ms": round(region_ms, 4)},
+                         "event_region_ms": round(region_ms, 4),
+                         "event_region_launches": args.steps - skip},
             "per_gpu_gib_s": round(value / world, 2),
             "kernel_gib_s": round(alg_bytes / (kern_ms / 1e3) / GIB, 2),
         }

@@ -70,7 +70,10 @@ extern "C" int gloo_hip_reduce_staged(int op, int dtype, void* host_dst, const v
     GLOO_AMD_HIP_CHECK(hipGetDevice(&device));
     StagingStreams& st = streamsFor(device);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const size_t piece = piece_elems ? piece_elems : std::max<size_t>(1, (n + 7) / 8);
+    // default: 16 MiB pieces (one MI355X: a 64 MiB fp32 chunk took 3.05 ms
+    // in 16 MiB pieces against 5.2-5.8 ms in 4-8 MiB ones and 3.64 ms
+    // unpipelined; profiles/round2/r2c_bench_n1.json host_staged)
+    const size_t piece = piece_elems ? piece_elems : std::max<size_t>(1, (size_t)(16u << 20) / es);
     char* hd = static_cast<char*>(host_dst);
     const char* hs = static_cast<const char*>(host_src);
     char* dd = static_cast<char*>(dev_dst);

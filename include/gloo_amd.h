@@ -108,7 +108,7 @@ int gloo_hip_reduce_multi(int op, int dtype, void* dst,
  * for a chunk that starts and ends in (pinned) host memory — a transport's
  * receive buffer — computed by the HIP kernel through device scratch
  * dev_dst / dev_src (n elements each, caller-owned).  The chunk moves in
- * pieces of piece_elems (0 = n / 8): the host-to-device copies of piece k+1,
+ * pieces of piece_elems (0 = 16 MiB): the host-to-device copies of piece k+1,
  * the kernel of piece k and the device-to-host copy of piece k-1 run at
  * once on separate streams (both PCIe directions busy).  Ordered after the
  * work already on `stream`; the host result is complete once `stream` has

@@ -782,3 +782,56 @@ def test_processes_host_workspace(torch, golden_sched, case, env):
                 assert same_bytes(ys[r][it], want), (r, it)
     for r in range(P):
         assert json.loads(outs[r].split("MODE", 1)[1])["host_arena"]
+
+
+STAMP_WORKER = r'''
+import os, sys, json
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, size, store = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+torch.cuda.set_device(0)
+n = 1 << 22
+buf = torch.ones(n, device="cuda:0")
+ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=60000)
+a = gloo_amd.Algorithm(ctx, "ring_chunked", "sum", "f32", [buf.data_ptr()], n)
+out = []
+for mode in (1, 2):
+    a.set_profiling(mode)
+    for it in range(4):
+        buf.fill_(1.0); torch.cuda.synchronize()
+        a.run()
+        st = a.stats()
+        out.append({"mode": mode, "it": it, "graph": a.mode()["graph"], "ok": bool((buf == size).all()), **st})
+a.close(); ctx.close()
+print("RESULT" + json.dumps(out), flush=True)
+'''
+
+
+def test_device_stamps_keep_graph_replay(torch):
+    """Reduce-kernel timing by device stamps (set_profiling(2)): the runs keep
+    their graph replay, report the same algorithmic bytes as the event mode
+    (the mesh fold: (P + 1) * n/P elements), and kernel seconds of the same
+    order as the events'."""
+    P = 2
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(STAMP_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s")], env=e,
+                                  stdout=subprocess.PIPE, text=True) for r in range(P)]
+        outs = [p.communicate(timeout=240)[0] for p in procs]
+        assert [p.returncode for p in procs] == [0] * P
+    n = 1 << 22
+    for o in outs:
+        res = json.loads(o.split("RESULT", 1)[1])
+        assert all(x["ok"] for x in res)
+        ev = [x for x in res if x["mode"] == 1]
+        st = [x for x in res if x["mode"] == 2]
+        assert not any(x["graph"] for x in ev)          # events force eager runs
+        assert st[-1]["graph"] and st[-2]["graph"]       # stamps are captured and replayed
+        for x in ev + st:
+            assert x["reduce_bytes"] == (P + 1) * 4 * (n // P), x
+            assert x["reductions"] == P - 1, x
+        ev_s = min(x["reduce_s"] for x in ev)
+        st_s = min(x["reduce_s"] for x in st)
+        assert 0 < st_s < 3 * ev_s and 0 < ev_s < 3 * st_s, (ev_s, st_s)
