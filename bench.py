@@ -42,6 +42,10 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--config3-variants", default="",
+                   help="N>1: comma list of config-3 variants after the default (diagnosis)")
+    p.add_argument("--config3-only", action="store_true",
+                   help="N>1: stop the xGMI section after config 3 (diagnosis)")
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--chunk-mib", type=int, default=64)
     p.add_argument("--pairs", type=int, default=6, help="rotated (dst, src) pairs")
@@ -365,6 +369,11 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
             a.run()
             got = buf[torch.from_numpy(sample).to(dev)].cpu().numpy()
             ok_first = bool((got.view(np.uint32) == want_sample.view(np.uint32)).all())
+            badmask = got.view(np.uint32) != want_sample.view(np.uint32)
+            bad_first = int(badmask.sum())
+            # first few mismatches: position, value, expected, this rank's input
+            bad_detail = [[int(sample[i]), float(got[i]), float(want_sample[i]), float(x_np[sample[i]])]
+                          for i in np.nonzero(badmask)[0][:3]]
             # timed: steady state (the plan replays as a hipGraph from run 3 on)
             times = []
             for _ in range(args.allreduce_iters):
@@ -404,7 +413,8 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
             a.close()
             ctx.close()
             return {"ms": [round(t * 1e3, 3) for t in times], "reduce_s": red_s, "reduce_b": red_b,
-                    "wait_ms_per_run": round(wait_s / 3 * 1e3, 3), "first_run_ok": ok_first, "digest": dig,
+                    "wait_ms_per_run": round(wait_s / 3 * 1e3, 3), "first_run_ok": ok_first,
+                    "first_run_bad_samples": bad_first, "first_run_bad_detail": bad_detail, "digest": dig,
                     "graph": graphed, "stamp_s": st_s, "stamp_b": st_b, "stamp_graph": all(st_graph)}
         try:
             res = with_env({"GLOO_AMD_COPY": engine, "GLOO_AMD_RING_MESH": mesh}, body)
@@ -431,6 +441,9 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                 "host_wait_ms_per_run_max_profiled": max(g["wait_ms_per_run"] for g in gathered),
                 "verified": bool(all(g["first_run_ok"] for g in gathered) and
                                  len({g["digest"] for g in gathered}) == 1),
+                "first_run_bad_samples_per_rank": [g["first_run_bad_samples"] for g in gathered],
+                "first_run_bad_detail_per_rank": [g["first_run_bad_detail"] for g in gathered],
+                "final_digests_equal": len({g["digest"] for g in gathered}) == 1,
                 "verify": "run 1 vs the reference ring fold at 4096 sampled positions on every rank, "
                           "bit-exact; after the last run every rank's 256 MiB digest equal"}
 
@@ -444,11 +457,20 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         return dict(partial)
     variants = {}
     partial["variants"] = variants
-    variants["ring_memcpy"] = ring_once("memcpy", mesh="0")
-    if not args.quick:
-        variants["mesh_memcpy_forked"] = ring_once("memcpy")
-        variants["ring_kernel"] = ring_once("kernel", mesh="0")
-        variants["mesh_host_workspace"] = ring_once("auto", "host")
+    # ring_kernel runs before ring_memcpy: a ring-route executor created
+    # right after one whose sends were hipMemcpyAsync copies into the peer's
+    # same-size inbox has been seen to import the previous inbox (DESIGN.md
+    # §4, "IPC imports"); the executor refuses such a mapping, and this order
+    # keeps every variant measured
+    specs = {"ring_kernel": ("kernel", "device", "0"), "ring_memcpy": ("memcpy", "device", "0"),
+             "mesh_memcpy_forked": ("memcpy", "device", "1"), "mesh_host_workspace": ("auto", "host", "1")}
+    chosen = (args.config3_variants.split(",") if args.config3_variants
+              else ["ring_memcpy"] if args.quick else list(specs))
+    for name in chosen:
+        engine, workspace, mesh = specs[name]
+        variants[name] = ring_once(engine, workspace, mesh)
+    if args.config3_only:
+        return dict(partial)
 
     short_sizes = (1 << 10, 64 << 10, 1 << 20, 64 << 20)
     full_sizes = tuple(1 << lg for lg in range(10, 31, 2))  # config 4: 1 KiB .. 1 GiB per rank

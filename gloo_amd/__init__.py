@@ -322,7 +322,11 @@ class Algorithm:
         return lib.gloo_hip_algorithm_wait_seconds(self._h)
 
     def set_profiling(self, on=True):
-        _check(lib.gloo_hip_algorithm_set_profiling(self._h, 1 if on else 0))
+        """0/False: off; 1/True: HIP events around every chunk reduction
+        (eager runs); 2: device stamps inside the reduce kernels (graph
+        replay kept)."""
+        mode = 2 if on == 2 and on is not True else 1 if on else 0
+        _check(lib.gloo_hip_algorithm_set_profiling(self._h, mode))
 
     def stats(self):
         """After run(): reduce-kernel seconds, algorithmic bytes reduced, chunk

@@ -8,11 +8,14 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <mutex>
 #include <cstring>
 #include <random>
 #include <set>
+#include <string>
 #include <thread>
 
 #include "gloo_amd.h"
@@ -36,7 +39,15 @@ struct ArenaRecord {
   uint64_t mailboxPtr;
   hipIpcMemHandle_t mailboxHandle;
   int32_t interpSlices;      // slices this rank could run its plan in (0: no sliced interpreter)
+  uint64_t nonce;            // written at the start of a DEVICE arena: the importer checks its mapping
 };
+
+// A value no earlier arena of this process or its peers is likely to hold.
+uint64_t arenaNonce() {
+  static std::atomic<uint64_t> k{0};
+  static const uint64_t seed = std::random_device{}() * 0x9e3779b97f4a7c15ull ^ ((uint64_t)::getpid() << 32);
+  return (seed + (++k) * 0xbf58476d1ce4e5b9ull) | 1;
+}
 
 bool mailboxesEnabled() {
   const char* e = std::getenv("GLOO_AMD_MAILBOX");
@@ -531,7 +542,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     where = ctx_->allgather(strcat_("inst", inst_, "/where"), blob);
   }
   peers_.resize(P);
-  bool sharesDeviceInProcess = false, crossDeviceSender = false;
+  bool sharesDeviceInProcess = false, crossSender = false;
   for (int peer : planPeers) {
     const std::vector<char>& v = where.at(peer);
     GLOO_AMD_ENFORCE(v.size() == 2 * sizeof(int32_t), "bad record from rank ", peer);
@@ -540,19 +551,25 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     peers_[peer].pid = w[0];
     peers_[peer].device = w[1];
     if (w[0] == ctx_->pid() && w[1] == ctx_->device()) sharesDeviceInProcess = true;
-    if (recvPeers.count(peer) && w[1] != ctx_->device()) crossDeviceSender = true;
+    if (recvPeers.count(peer) && (w[1] != ctx_->device() || w[0] != ctx_->pid())) crossSender = true;
   }
   const char* sig = std::getenv("GLOO_AMD_SIGNAL");
   const std::string sigMode = sig ? sig : "auto";
   deviceSignal_ = sigMode == "device" || (sigMode == "auto" && !sharesDeviceInProcess);
-  // A peer GPU writes this rank's inboxes over xGMI; keep them in
-  // fine-grained memory so no stale line of this GPU's L2 can be read.
+  // A peer GPU (over xGMI) or a peer PROCESS (through its own IPC mapping)
+  // writes this rank's inboxes: keep them in fine-grained memory, so no
+  // stale line of an L2 can be read on either side.  Measured with
+  // coarse-grained inboxes and two processes on one MI355X: after an
+  // executor of the same size had run, the importer read the previous
+  // contents through its mapping even after a device synchronise, and a
+  // ring route's messages were not seen by the receiver (bench.py
+  // config-3 variants back to back, tests/test_bench_gpu.py).
   const char* ar = std::getenv("GLOO_AMD_ARENA");
   const std::string arMode = ar ? ar : "auto";
   GLOO_AMD_ENFORCE(workspace == GLOO_HIP_WORKSPACE_DEVICE || workspace == GLOO_HIP_WORKSPACE_HOST,
                    "unknown workspace ", workspace);
   hostArena_ = workspace == GLOO_HIP_WORKSPACE_HOST || arMode == "host";
-  fineArena_ = !hostArena_ && (arMode == "fine" || (arMode == "auto" && crossDeviceSender));
+  fineArena_ = !hostArena_ && (arMode == "fine" || (arMode == "auto" && crossSender));
 
   // Phase 2: the inbox arena.
   const size_t arenaBytes = std::max<size_t>(256, plan_.arena * es_);
@@ -623,6 +640,13 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   rec.ptr = reinterpret_cast<uint64_t>(arena_);
   rec.bytes = arenaBytes;
   rec.deviceSignal = deviceSignal_ ? 1 : 0;
+  if (!hostArena_) {
+    // the first 8 bytes of the arena carry a nonce until the first message
+    // lands; a peer that maps the arena over IPC reads it back (below)
+    rec.nonce = arenaNonce();
+    GLOO_AMD_HIP_CHECK(hipMemcpyAsync(arena_, &rec.nonce, sizeof(rec.nonce), hipMemcpyHostToDevice, stream_));
+    GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
   if (mailbox_) {
     rec.hasMailbox = 1;
     rec.mailboxPtr = reinterpret_cast<uint64_t>(mailbox_);
@@ -680,9 +704,40 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       }
     } else {
       void* p = nullptr;
-      GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&p, pr.handle, hipIpcMemLazyEnablePeerAccess));
+      // The mapping must show the peer's CURRENT arena.  Measured on MI355X /
+      // ROCm 7 with two rank processes on one GPU (bench.py's config-3
+      // variants back to back, tests/test_bench_gpu.py): after a ring-route
+      // executor had written its peer's inbox with hipMemcpyAsync and was
+      // destroyed, an import of the peer's next inbox could show the
+      // previous inbox's final contents, so every message would have gone
+      // there while the signals still arrived.  The nonce the owner wrote
+      // at the arena's start tells; a stale import is closed and opened
+      // again, and a mapping that never shows the nonce is an error, never
+      // a silent misdelivery.
+      uint64_t seen = 0;
+      for (int attempt = 0;; attempt++) {
+        GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&p, pr.handle, hipIpcMemLazyEnablePeerAccess));
+        GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, p, sizeof(seen), hipMemcpyDeviceToHost, stream_));
+        GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+        if (seen == pr.nonce || attempt == 4) break;
+        GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(p));
+        GLOO_AMD_HIP_CHECK(hipDeviceSynchronize());
+        std::this_thread::sleep_for(std::chrono::milliseconds(2 << attempt));
+      }
       peers_[peer].base = static_cast<char*>(p);
       peers_[peer].ipc = true;
+      if (seen != pr.nonce) {
+        const unsigned char* hb = reinterpret_cast<const unsigned char*>(&pr.handle);
+        std::string hex;
+        char t[3];
+        for (size_t i = 0; i < sizeof(pr.handle); i++) {
+          std::snprintf(t, sizeof(t), "%02x", hb[i]);
+          hex += t;
+        }
+        GLOO_AMD_ENFORCE(false, "rank ", me, ": the IPC mapping of rank ", peer, "'s inbox arena (", (void*)pr.ptr,
+                         ", ", pr.bytes, " B, in pid ", pr.pid, ", mapped at ", p, ") does not show its contents: read ",
+                         seen, ", expected ", pr.nonce, "; handle ", hex);
+      }
     }
     const Plan theirs = planFor(planAlgo_, peer, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
     for (const Step& d : theirs.steps)
@@ -727,7 +782,10 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     }
     const size_t tickets = std::max<size_t>(256, (size_t)P * GLOO_HIP_NUM_SLOTS * sizeof(unsigned));
     GLOO_AMD_HIP_ALLOC(hipMalloc(&ticket_, tickets));
-    GLOO_AMD_HIP_CHECK(hipMemset(ticket_, 0, tickets));
+    // zeroed on the executor's stream and complete before any copy kernel
+    // (a plain hipMemset goes to the null stream, which a non-blocking
+    // stream does not wait for)
+    GLOO_AMD_HIP_CHECK(hipMemsetAsync(ticket_, 0, tickets, stream_));
     // Graph replay pays off once a plan has steps that are not fused
     // one-workgroup launches (measured); "1" / "0" force it.
     const char* gm = std::getenv("GLOO_AMD_GRAPH");
@@ -743,8 +801,9 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     if (interpMode_) GLOO_AMD_HIP_ALLOC(hipMalloc(&interpSteps_, kInterpMaxSteps * sizeof(InterpStep)));
     if (graphMode_) {
       GLOO_AMD_HIP_ALLOC(hipMalloc(&epoch_, sizeof(uint64_t)));
-      GLOO_AMD_HIP_CHECK(hipMemset(epoch_, 0, sizeof(uint64_t)));
+      GLOO_AMD_HIP_CHECK(hipMemsetAsync(epoch_, 0, sizeof(uint64_t), stream_));
     }
+    GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
   }
   ctx_->barrier(strcat_("inst", inst_, "/ready"));
   if (arenaShm_) arenaShm_->unlink();  // every peer has mapped it by now
@@ -753,6 +812,13 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
 PlanExecutor::~PlanExecutor() {
   try {
     if (stream_) (void)hipStreamSynchronize(stream_);
+    for (hipStream_t a : aux_) (void)hipStreamSynchronize(a);
+    // the captured graph holds copy nodes into the peers' mapped arenas: it
+    // goes before the mappings are closed, or a close leaves the import
+    // alive and a later import of an equal handle (the peer's next arena of
+    // the same size at the same address) was handed the old mapping
+    if (graphExec_) (void)hipGraphExecDestroy(graphExec_);
+    graphExec_ = nullptr;
     if (ctx_->size > 1) {
       for (auto& p : peers_)
         if (p.ipc && p.base) GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(p.base));
@@ -862,6 +928,7 @@ void PlanExecutor::setStamping(bool on) {
     // one slot per REDUCE / FOLD step, in step order, with its algorithmic
     // bytes: 2 reads + 1 write, or k source reads + 1 write
     stampBytes_.clear();
+    stampCount_.clear();
     stampSlotOf_.clear();
     size_t srcs = 0;
     for (size_t i = 0; i < plan_.steps.size(); i++) {
@@ -870,23 +937,24 @@ void PlanExecutor::setStamping(bool on) {
       if (s.kind != GLOO_HIP_STEP_REDUCE && s.kind != GLOO_HIP_STEP_FOLD) continue;
       stampSlotOf_[i] = (int)stampBytes_.size();
       stampBytes_.push_back((s.kind == GLOO_HIP_STEP_REDUCE ? 3.0 : srcs + 1.0) * s.length * es_);
+      stampCount_.push_back(s.kind == GLOO_HIP_STEP_REDUCE ? 1 : std::max<size_t>(srcs, 1) - 1);
       if (s.kind == GLOO_HIP_STEP_FOLD) srcs = 0;
     }
     stampSlots_ = (int)stampBytes_.size();
-    GLOO_AMD_HIP_ALLOC(hipMalloc(&stamps_, std::max<size_t>(16, 2 * sizeof(uint64_t) * stampSlots_)));
+    GLOO_AMD_HIP_ALLOC(hipMalloc(&stamps_, sizeof(uint64_t) * kStampSlotWords * std::max(1, stampSlots_)));
   }
 }
 
 void PlanExecutor::readStamps() {
-  std::vector<uint64_t> h(2 * (size_t)stampSlots_);
+  std::vector<uint64_t> h((size_t)kStampSlotWords * stampSlots_);
   if (h.empty()) return;
   GLOO_AMD_HIP_CHECK(hipMemcpy(h.data(), stamps_, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
   for (int i = 0; i < stampSlots_; i++) {
-    const uint64_t b = h[2 * i], e = h[2 * i + 1];
-    if (e == 0 || e < b) continue;  // not launched this run (a fused or empty step)
-    reduceSeconds_ += (e - b) * 1e-8;  // 100 MHz
+    uint64_t ticks = 0;
+    if (!stampSpan(&h[(size_t)kStampSlotWords * i], &ticks)) continue;  // not launched this run
+    reduceSeconds_ += ticks * 1e-8;  // 100 MHz
     reduceBytes_ += stampBytes_[i];
-    reduceCount_++;
+    reduceCount_ += stampCount_[i];
   }
 }
 
@@ -902,6 +970,7 @@ void PlanExecutor::run() {
   waitSeconds_ = 0;
   reduceSeconds_ = reduceBytes_ = 0;
   reduceCount_ = 0;
+  replayed_ = false;
   const uint64_t r = runs_ + 1;
   // sliced plans must run sliced on every rank (their flags are per slice);
   // profiling then reports no reduce events
@@ -929,6 +998,7 @@ void PlanExecutor::run() {
       if (epochRuns_ != r - 1) GLOO_AMD_HIP_CHECK(launchEpochSet(epoch_, r - 1, stream_));
       GLOO_AMD_HIP_CHECK(hipGraphLaunch(graphExec_, stream_));
       epochRuns_ = r;
+      replayed_ = true;
     } else {
       enqueue(r, false);
     }
@@ -1129,7 +1199,11 @@ void PlanExecutor::buildInterp() {
                    "sliced step list of ", v.size(), " entries exceeds its proposed bound");
   // an earlier launch may still read the list
   GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
-  GLOO_AMD_HIP_CHECK(hipMemcpy(interpSteps_, v.data(), v.size() * sizeof(InterpStep), hipMemcpyHostToDevice));
+  // on the stream the interpreter runs on (a null-stream copy is not ordered
+  // before it), complete before `v` goes away
+  GLOO_AMD_HIP_CHECK(
+      hipMemcpyAsync(interpSteps_, v.data(), v.size() * sizeof(InterpStep), hipMemcpyHostToDevice, stream_));
+  GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
   interpCount_ = (int)v.size();
 }
 
@@ -1182,7 +1256,9 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
     ~StampScope() { setLaunchStamp(prev); }
     uint64_t* prev;
   };
-  auto slotOf = [&](size_t step) { return stamping_ ? stamps_ + 2 * (size_t)stampSlotOf_.at(step) : nullptr; };
+  auto slotOf = [&](size_t step) {
+    return stamping_ ? stamps_ + (size_t)kStampSlotWords * stampSlotOf_.at(step) : nullptr;
+  };
   for (size_t i = 0; i < steps.size(); i++) {
     const Step& s = steps[i];
     // A run of consecutive SENDs (a mesh schedule's sends to every peer):

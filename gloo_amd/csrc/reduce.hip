@@ -232,30 +232,38 @@ __device__ __forceinline__ void edges(typename Tr::Storage* c,
   if (j < n) c[j] = apply<Tr, OP>(a[j], b[j]);
 }
 
-// Device-side kernel timing (the executor's stamp mode, executor.h): every
-// workgroup folds its start time into stamp[0] (min) and, once all its waves'
-// stores have completed, its end time into stamp[1] (max), on the 100 MHz
-// constant clock.  stamp == nullptr (every other launch): two uniform
-// branches, nothing else.  Unlike host events, stamps survive hipGraph
-// capture and replay and exclude the dispatch gap between launches.
+// Device-side kernel timing (the executor's stamp mode, executor.h).  A
+// stamp slot is kStampShards begin words and kStampShards end words, each on
+// its own 128-B line (signal.h).  Workgroups 0..kStampHead-1 fold their start
+// time into begin shard blockIdx % kStampShards (atomic min); the last
+// kStampTail workgroups of the grid, once all their waves' stores have
+// completed, fold their end time into an end shard (atomic max); the 100 MHz
+// constant clock.  Dispatch is in blockIdx order, so the first workgroup to
+// start is among the first kStampHead and the last to finish among the last
+// kStampTail.  Sharding matters: one device-scope atomic word retires about
+// 88 updates per microsecond, so one stamp per workgroup on a single word
+// stretched a 16,384-workgroup fold by ~100 us (profiles/round2/
+// r2k_stamp_check.jsonl).  stamp == nullptr (every other launch): one uniform
+// branch each.  Unlike host events, stamps survive hipGraph capture and
+// replay and exclude the dispatch gap between launches.
+constexpr unsigned kStampHead = 1024, kStampTail = 4096;
 __device__ __forceinline__ void stamp_begin(uint64_t* stamp) {
-  if (stamp && threadIdx.x == 0)
-    __hip_atomic_fetch_min(stamp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (stamp && threadIdx.x == 0 && blockIdx.x < kStampHead)
+    __hip_atomic_fetch_min(stamp + (blockIdx.x % kStampShards) * kStampLineWords, __builtin_amdgcn_s_memrealtime(),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void stamp_end(uint64_t* stamp) {
-  if (!stamp) return;
+  if (!stamp || blockIdx.x + kStampTail < gridDim.x) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0)
-    __hip_atomic_fetch_max(stamp + 1, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_max(stamp + (kStampShards + blockIdx.x % kStampShards) * kStampLineWords,
+                           __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void stamp_init_kernel(uint64_t* stamps, int k) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < k) {
-    stamps[2 * i] = ~0ull;
-    stamps[2 * i + 1] = 0;
-  }
+__global__ void stamp_init_kernel(uint64_t* stamps, size_t words) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < words) stamps[i] = (i % kStampSlotWords) < kStampShards * kStampLineWords ? ~0ull : 0ull;
 }
 
 thread_local uint64_t* t_stamp = nullptr;  // stamp slot of the next reduce launch on this thread
@@ -1061,7 +1069,8 @@ uint64_t* setLaunchStamp(uint64_t* stamp) {
 
 int launchStampInit(uint64_t* stamps, int k, hipStream_t s) {
   if (k <= 0) return GLOO_HIP_OK;
-  stamp_init_kernel<<<(k + 255) / 256, 256, 0, s>>>(stamps, k);
+  const size_t words = (size_t)k * kStampSlotWords;
+  stamp_init_kernel<<<(unsigned)((words + 255) / 256), 256, 0, s>>>(stamps, words);
   return check_launch("stamp_init_kernel");
 }
 

@@ -102,8 +102,9 @@ class PlanExecutor {
   bool fineGrainedArena() const { return fineArena_; }
   bool hostArena() const { return hostArena_; }
   bool kernelCopy() const { return kernelCopy_; }
-  // True once run() replays a captured hipGraph.
-  bool graphed() const { return graphExec_ != nullptr; }
+  // True when the last run() was a replay of the captured hipGraph (a run
+  // with profiling events on is enqueued eagerly even while a graph exists).
+  bool graphed() const { return replayed_; }
   // True once run() executes the plan as one interpreter launch.
   bool interpreted() const { return interpMode_ && interpCount_ > 0; }
   // Workgroups of that launch: > 1 when every rank runs the plan sliced.
@@ -194,6 +195,7 @@ class PlanExecutor {
   uint64_t runs_ = 0;          // runs enqueued so far
   uint64_t* epoch_ = nullptr;  // device: the run being executed (graph replay)
   hipGraphExec_t graphExec_ = nullptr;
+  bool replayed_ = false;      // the last run() launched graphExec_
   bool graphMode_ = false;
   uint64_t epochRuns_ = 0;     // the device epoch once the work queued so far has run
   uint64_t stableRuns_ = 0;    // runs since the buffers last changed
@@ -229,6 +231,7 @@ class PlanExecutor {
   uint64_t* stamps_ = nullptr;    // 2 x stampSlots_ device words: (start min, end max) per reduce step
   int stampSlots_ = 0;
   std::vector<double> stampBytes_;  // algorithmic bytes per slot
+  std::vector<size_t> stampCount_;  // chunk reductions per slot (a k-source fold counts k - 1, as with events)
   std::map<size_t, int> stampSlotOf_;  // plan step -> slot
   void readStamps();
   std::vector<hipEvent_t> events_;

@@ -21,6 +21,8 @@
 // null epoch pointer the value is `base` (host-computed).
 #pragma once
 
+#include <algorithm>
+
 #include <hip/hip_runtime_api.h>
 
 #include "gloo_amd.h"
@@ -117,9 +119,26 @@ int launchPlanInterp(int op, int dtype, const InterpStep* steps, int nsteps, uin
 // over the sources in order (k a power of two).  Returns a gloo_hip status.
 // Device-side timing of the reduce kernels (reduce_vec_kernel,
 // reduce_multi_vec_kernel): while a stamp slot is set on the calling thread,
-// each of those launches folds its first workgroup start into slot[0] (min)
-// and its last workgroup end into slot[1] (max), 100 MHz clock ticks.
-// Returns the previous slot.  launchStampInit sets k slots to (~0, 0).
+// each of those launches folds its first workgroup start into the slot's
+// begin shards (min) and its last workgroup end into its end shards (max),
+// 100 MHz clock ticks; the kernel's span is max(end shards) - min(begin
+// shards) (stampSpan).  A slot is kStampSlotWords words: kStampShards begin
+// words, then kStampShards end words, one per kStampLineWords-word (128-B)
+// line.  setLaunchStamp returns the previous slot; launchStampInit resets k
+// consecutive slots (begin ~0, end 0).
+constexpr int kStampShards = 64;
+constexpr int kStampLineWords = 16;
+constexpr int kStampSlotWords = 2 * kStampShards * kStampLineWords;
+inline bool stampSpan(const uint64_t* slot, uint64_t* ticks) {
+  uint64_t b = ~0ull, e = 0;
+  for (int i = 0; i < kStampShards; i++) {
+    b = std::min(b, slot[i * kStampLineWords]);
+    e = std::max(e, slot[(kStampShards + i) * kStampLineWords]);
+  }
+  if (e == 0 || e < b) return false;  // not launched (a fused or empty step)
+  *ticks = e - b;
+  return true;
+}
 uint64_t* setLaunchStamp(uint64_t* slot);
 int launchStampInit(uint64_t* stamps, int k, hipStream_t stream);
 

@@ -57,3 +57,20 @@ def test_op_and_dtype_codes_mirror_reference():
     assert [int(gloo_amd.ReductionType[x]) for x in ("SUM", "PRODUCT", "MAX", "MIN")] == [1, 2, 3, 4]
     for name, (code, _) in oracle.DTYPES.items():
         assert int(gloo_amd.DTYPE_NAMES[name]) == code
+
+
+def test_set_profiling_modes_reach_the_c_abi(monkeypatch):
+    """Algorithm.set_profiling passes 0 / 1 (events) / 2 (device stamps)
+    through unchanged; True stays the event mode."""
+    import gloo_amd
+    seen = []
+
+    def fake(h, mode):
+        seen.append(mode)
+        return 0
+    monkeypatch.setattr(gloo_amd.lib, "gloo_hip_algorithm_set_profiling", fake)
+    a = gloo_amd.Algorithm.__new__(gloo_amd.Algorithm)
+    a._h = None
+    for on in (True, False, 0, 1, 2):
+        a.set_profiling(on)
+    assert seen == [1, 0, 0, 1, 2]

@@ -116,8 +116,9 @@ CONFIG3 = "ring_chunked/sum/f32/P8/n67108864"
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("env", [{}, {"GLOO_AMD_RING_MESH": "0"}, {"GLOO_AMD_COPY": "memcpy"}],
-                         ids=["mesh", "ring_route", "mesh_memcpy"])
+@pytest.mark.parametrize("env", [{}, {"GLOO_AMD_RING_MESH": "0"}, {"GLOO_AMD_COPY": "memcpy"},
+                                 {"GLOO_AMD_RING_MESH": "0", "GLOO_AMD_COPY": "kernel"}],
+                         ids=["mesh", "ring_route", "mesh_memcpy", "ring_route_kernel_copy"])
 def test_config3_full_size(torch, env):
     """BASELINE config 3 at its configured size: 8 ranks x 256 MiB fp32,
     ring-chunked, every rank's buffer byte for byte the reference's output
@@ -178,3 +179,63 @@ def test_large_p_threads(torch, case):
         y = run_threads(torch, algo, op, dtype, x)
         for r in range(y.shape[0]):
             assert same_bytes(y[r, 0], want), r
+
+
+CLOSED_WORKER = r"""
+import json, os, sys
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, size, store, n, runs = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+dev = rank % torch.cuda.device_count()
+torch.cuda.set_device(dev)
+ctx = gloo_amd.Context(rank, size, store, device=dev, timeout_ms=120000)
+# element j of rank r: (j % 1024) * P + r, exact in fp32 for the sums here
+src = (torch.arange(n, device=f"cuda:{dev}", dtype=torch.int64) % 1024 * size + rank).float()
+want = (torch.arange(n, device=f"cuda:{dev}", dtype=torch.int64) % 1024 * size * size + size * (size - 1) // 2).float()
+buf = torch.empty_like(src)
+a = gloo_amd.Algorithm(ctx, "ring_chunked", "sum", "f32", [buf.data_ptr()], n)
+res = []
+# runs 0-2: eager, capture, replay; then the bench's profiled sequence:
+# HIP events (eager), device stamps (eager, capture, replays), off again
+prof = [0, 0, 0, 1, 1, 2, 2, 2, 2, 0, 0][:runs]
+for it in range(runs):
+    if it == 0 or prof[it] != prof[it - 1]:
+        a.set_profiling(prof[it])
+    buf.copy_(src)
+    torch.cuda.synchronize()
+    a.run()
+    torch.cuda.synchronize()
+    bad = (buf != want).nonzero().flatten()
+    res.append({"bad": int(bad.numel()), "first_bad": [int(i) for i in bad[:4].tolist()],
+                "got": [float(buf[i]) for i in bad[:4].tolist()], "mode": a.mode()})
+a.close(); ctx.close()
+print("RESULT" + json.dumps(res), flush=True)
+"""
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("P,n", [(2, 1 << 20), (2, 1 << 26), (4, 1 << 24), (3, 10000019)])
+@pytest.mark.parametrize("copy", ["kernel", "memcpy", "auto"])
+def test_ring_route_copy_engines_closed_form(torch, P, n, copy):
+    """The reference ring route (GLOO_AMD_RING_MESH=0) with each copy engine,
+    every element against the closed form of gloo/test/base_test.h:184-236,
+    in eleven runs: eager, capture, replay, then with HIP-event profiling,
+    with device stamps (eager, capture, replays) and with profiling off."""
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        with open(w, "w") as f:
+            f.write(CLOSED_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_RING_MESH="0", GLOO_AMD_COPY=copy)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), str(n), "11"],
+                                  env=e, stdout=subprocess.PIPE, text=True) for r in range(P)]
+        try:
+            outs = [p.communicate(timeout=300)[0] for p in procs]
+        finally:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        assert [p.returncode for p in procs] == [0] * P
+    res = [json.loads(o.split("RESULT", 1)[1]) for o in outs]
+    for r in range(P):
+        for it in range(11):
+            assert res[r][it]["bad"] == 0, (r, it, res[r][it])
