@@ -680,6 +680,12 @@ def main():
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pairs = [(torch.rand(n, device=dev, generator=g) * 2 - 1,
               torch.rand(n, device=dev, generator=g) * 2 - 1) for _ in range(args.pairs)]
+    # 1 % of the lanes hold +-0, denormals and +-inf
+    specials = torch.tensor([0.0, -0.0, 1e-40, -1e-40, float("inf"), float("-inf")], device=dev)
+    for d, s in pairs:
+        for t, off in ((d, 0), (s, 50)):
+            idx = torch.arange(off, n, 100, device=dev)
+            t[idx] = specials[torch.arange(idx.numel(), device=dev) % specials.numel()]
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
 
@@ -754,6 +760,7 @@ def main():
             "config": {"workload": WORKLOAD, "chunk_bytes": n * 4, "elements": n,
                        "op": "sum", "form": "in-place dst += src (ReductionFunction::call)",
                        "rotated_pairs": args.pairs, "footprint_mib": 2 * args.pairs * args.chunk_mib,
+                       "inputs": "U(-1,1), 1 % of lanes +-0 / denormal / +-inf",
                        "parallelism": f"{world} independent GPU(s), no data-path collective",
                        "kernel_variant": args.variant},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS,

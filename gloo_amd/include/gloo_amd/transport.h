@@ -24,6 +24,13 @@
 // as in Gloo (context->nextSlot()); per (direction, peer) at most
 // GLOO_HIP_NUM_SLOTS distinct slots modulo GLOO_HIP_NUM_SLOTS may be live.
 // The store must support set/get (file: or mem: contexts).
+//
+// Receive buffers are the caller's memory, so unlike the executor's inboxes
+// (executor.cc: a nonce at the arena's start, read back through every new
+// IPC mapping) their imports are not verified; on ROCm 7 an import has been
+// seen to show a previous allocation of the same size (DESIGN.md §4,
+// "IPC imports are verified").  Keep receive buffers alive for the life of
+// the pairs that use them, as Gloo's own transports require.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
