@@ -693,6 +693,15 @@ def main():
         d, s = pairs[i % len(pairs)]
         hip.reduce_ptr("sum", "f32", d.data_ptr(), s.data_ptr(), n, sh)
 
+    # The D2D copy ceiling reported beside the roofline is measured before
+    # the warmup (it also brings the GPU out of idle before the W warmup
+    # steps run), not after the timed region.
+    ceiling = None
+    if world == 1:
+        try:
+            ceiling = copy_ceiling(torch, dev)
+        except RuntimeError as e:  # pragma: no cover
+            ceiling = f"unavailable: {e}"
     progress(f"config 2: {args.warmup} warmup + {args.steps} timed steps")
     for i in range(args.warmup):
         step(i)
@@ -775,10 +784,7 @@ def main():
             "kernel_gib_s": round(alg_bytes / (kern_ms / 1e3) / GIB, 2),
         }
         if world == 1:
-            try:
-                out["hbm_copy_ceiling_gbs"] = copy_ceiling(torch, dev)
-            except RuntimeError as e:  # pragma: no cover
-                out["hbm_copy_ceiling_gbs"] = f"unavailable: {e}"
+            out["hbm_copy_ceiling_gbs"] = ceiling
             if not args.no_host_staged:
                 out["host_staged"] = host_staged(torch, hip, n, dev)
             if not args.no_cpu:
