@@ -251,6 +251,10 @@ EXPORTED = EXPORTED + ("gloo_hip_context_create", "gloo_hip_context_create_ex", 
                        "gloo_hip_algorithm_destroy", "gloo_hip_algorithm_wait_seconds",
                        "gloo_hip_algorithm_set_profiling", "gloo_hip_algorithm_stats",
                        "gloo_hip_algorithm_mode", "gloo_hip_algorithm_create_ws", "gloo_hip_context_mode")
+# the xGMI transport's bound buffers (gloo_amd/include/gloo_amd/gloo_transport.h)
+EXPORTED = EXPORTED + ("gloo_hip_context_create_kv", "gloo_hip_transport_create", "gloo_hip_transport_destroy",
+                       "gloo_hip_buffer_create", "gloo_hip_buffer_destroy", "gloo_hip_buffer_send",
+                       "gloo_hip_buffer_wait_recv", "gloo_hip_buffer_wait_send")
 
 WORKSPACES = {"device": 0, "host": 1}
 

@@ -9,6 +9,7 @@
 #include "gloo_amd/context.h"
 #include "gloo_amd/errors.h"
 #include "gloo_amd/executor.h"
+#include "gloo_amd/transport.h"
 
 struct gloo_hip_context {
   std::shared_ptr<gloo_amd::Context> ctx;
@@ -19,6 +20,12 @@ struct gloo_hip_context {
 };
 struct gloo_hip_algorithm {
   std::unique_ptr<gloo_amd::PlanExecutor> exec;
+};
+struct gloo_hip_transport {
+  std::unique_ptr<gloo_amd::transport::Device> dev;
+};
+struct gloo_hip_buffer {
+  std::unique_ptr<gloo_amd::transport::Buffer> buf;
 };
 
 namespace {
@@ -214,6 +221,67 @@ int gloo_hip_context_mode(gloo_hip_context_t ctx, int* mode) {
     GLOO_AMD_ENFORCE(ctx && mode, "null argument");
     GLOO_AMD_ENFORCE(ctx->last, "no function-style call on this context yet");
     modeOf(*ctx->last, mode);
+  });
+}
+
+int gloo_hip_context_create_kv(int rank, int size, int device, int timeout_ms, gloo_hip_kv_set_fn set,
+                               gloo_hip_kv_get_fn get, void* user, gloo_hip_context_t* out) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(out && set && get, "null argument");
+    auto c = std::make_unique<gloo_hip_context>();
+    c->ctx = std::make_shared<gloo_amd::Context>(
+        rank, size, std::chrono::milliseconds(timeout_ms > 0 ? timeout_ms : 30000));
+    c->ctx->connect(std::make_shared<gloo_amd::KvCallbackStore>(set, get, user), device);
+    *out = c.release();
+  });
+}
+
+int gloo_hip_transport_create(gloo_hip_context_t ctx, gloo_hip_stream_t stream, gloo_hip_transport_t* out) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(ctx && out, "null argument");
+    auto t = std::make_unique<gloo_hip_transport>();
+    t->dev = std::make_unique<gloo_amd::transport::Device>(ctx->ctx, static_cast<hipStream_t>(stream));
+    *out = t.release();
+  });
+}
+
+int gloo_hip_transport_destroy(gloo_hip_transport_t t) {
+  return guarded([&] { delete t; });
+}
+
+int gloo_hip_buffer_create(gloo_hip_transport_t t, int peer, int slot, void* ptr, size_t size, int is_send,
+                           gloo_hip_buffer_t* out) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(t && out, "null argument");
+    auto& pair = t->dev->getPair(peer);
+    auto b = std::make_unique<gloo_hip_buffer>();
+    b->buf = is_send ? pair.createSendBuffer(slot, ptr, size) : pair.createRecvBuffer(slot, ptr, size);
+    *out = b.release();
+  });
+}
+
+int gloo_hip_buffer_destroy(gloo_hip_buffer_t b) {
+  return guarded([&] { delete b; });
+}
+
+int gloo_hip_buffer_send(gloo_hip_buffer_t b, size_t offset, size_t length, size_t roffset) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(b, "null buffer");
+    b->buf->send(offset, length, roffset);
+  });
+}
+
+int gloo_hip_buffer_wait_recv(gloo_hip_buffer_t b) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(b, "null buffer");
+    b->buf->waitRecv();
+  });
+}
+
+int gloo_hip_buffer_wait_send(gloo_hip_buffer_t b) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(b, "null buffer");
+    b->buf->waitSend();
   });
 }
 

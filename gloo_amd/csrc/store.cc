@@ -100,6 +100,25 @@ std::vector<std::vector<char>> CallbackStore::allgather(const std::string& tag, 
   return all;
 }
 
+void KvCallbackStore::set(const std::string& key, const std::vector<char>& data) {
+  if (set_(user_, key.c_str(), data.data(), data.size()) != 0) throw IoException("store set failed: " + key);
+}
+
+std::vector<char> KvCallbackStore::get(const std::string& key, std::chrono::milliseconds timeout) {
+  std::vector<char> v(256);
+  for (int attempt = 0; attempt < 2; attempt++) {
+    size_t len = 0;
+    const int rc = get_(user_, key.c_str(), (int)timeout.count(), v.data(), v.size(), &len);
+    if (rc != 0) throw IoException(strcat_("store get of ", key, " failed or timed out after ", timeout.count(), " ms"));
+    if (len <= v.size()) {
+      v.resize(len);
+      return v;
+    }
+    v.resize(len);  // the value is longer than the buffer: fetch it again in full
+  }
+  throw EnforceNotMet("store value of " + key + " changed size between two gets");
+}
+
 std::shared_ptr<Store> openStore(const std::string& url) {
   static std::mutex m;
   static std::map<std::string, std::weak_ptr<Store>> named;

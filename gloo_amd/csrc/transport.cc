@@ -58,7 +58,7 @@ class SendBuffer : public Buffer {
     GLOO_AMD_ENFORCE(roffset + length <= peerSize_, "send of ", length, " bytes at ", roffset, " beyond rank ", peer_,
                      "'s ", peerSize_, "-byte receive buffer (slot ", slot_, ")");
     hipStream_t s = dev_->stream();
-    if (length) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(remote_ + roffset, ptr_ + offset, length, hipMemcpyDeviceToDevice, s));
+    if (length) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(remote_ + roffset, ptr_ + offset, length, hipMemcpyDefault, s));
     // stream-ordered: the arrival is published only once the bytes landed
     GLOO_AMD_HIP_CHECK(hipLaunchHostFunc(s, bump, &ctx.counter(dev_->instance(), ctx.rank, peer_, channel(slot_))));
     GLOO_AMD_HIP_CHECK(hipEventRecord(sent_, s));

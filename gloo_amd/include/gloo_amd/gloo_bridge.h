@@ -53,6 +53,7 @@
 #include "gloo/context.h"
 #include "gloo/types.h"
 #include "gloo_amd.h"
+#include "gloo_amd/gloo_transport.h"
 
 namespace gloo {
 
@@ -131,6 +132,11 @@ class BootstrapContext {
       return 0;
     }
     try {
+      // A gloo::Context on the xGMI transport (gloo_transport.h) has no
+      // unbound buffers for gloo::allgather: exchange through its store.
+      const int peer = self->context_->rank == 0 ? 1 : 0;
+      if (auto* hp = dynamic_cast<transport::hip::Pair*>(self->context_->getPair(peer).get()))
+        return hp->hipContext()->allgather(in, out, block);
       AllgatherOptions opts(self->context_);
       opts.setInput(const_cast<uint8_t*>(static_cast<const uint8_t*>(in)), block);
       opts.setOutput(static_cast<uint8_t*>(out), block * (size_t)self->context_->size);

@@ -48,6 +48,23 @@ class CallbackStore : public Store {
   void* user_;
 };
 
+// The key/value store of a caller (gloo gloo::IStore behind
+// gloo_hip_context_create_kv, gloo_amd/include/gloo_amd/gloo_transport.h):
+// set, and a get that waits for the key up to a timeout.
+class KvCallbackStore : public Store {
+ public:
+  using SetFn = int (*)(void* user, const char* key, const void* data, size_t len);
+  using GetFn = int (*)(void* user, const char* key, int timeout_ms, void* out, size_t cap, size_t* len);
+  KvCallbackStore(SetFn set, GetFn get, void* user) : set_(set), get_(get), user_(user) {}
+  void set(const std::string& key, const std::vector<char>& data) override;
+  std::vector<char> get(const std::string& key, std::chrono::milliseconds timeout) override;
+
+ private:
+  SetFn set_;
+  GetFn get_;
+  void* user_;
+};
+
 // Shared directory, one file per key (atomic rename), for ranks that are
 // separate processes on one node.
 class FileStore : public Store {

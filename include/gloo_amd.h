@@ -404,6 +404,53 @@ typedef struct {
 
 int gloo_hip_reduce_to_root(gloo_hip_context_t ctx, const gloo_hip_reduce_options_t* opts);
 
+/* ------------------------------------------------------------------------
+ * The xGMI transport: bound buffers of gloo::transport::Pair / Buffer
+ * (gloo/transport/pair.h:33-41, gloo/transport/buffer.h:26-34) over device
+ * memory.  gloo_amd/include/gloo_amd/gloo_transport.h wraps these into a
+ * gloo::transport::Device (gloo/transport/device.h:34-54) that
+ * gloo::rendezvous::Context::connectFullMesh accepts.
+ *
+ *   gloo_hip_context_create_kv  <- transport::Context::createAndConnectAllPairs
+ *       (gloo/transport/context.cc:26-89): the caller's key/value store
+ *       (gloo::IStore set / wait+get) carries the set-up records.  set: store
+ *       `len` bytes under `key`; get: wait up to timeout_ms for `key`, copy up
+ *       to `cap` bytes into `out` and its full length into *len (the library
+ *       calls again with a larger buffer when *len > cap).  Both return 0 on
+ *       success, nonzero on failure (a timeout: GLOO_HIP_EIO).  The store
+ *       must outlive the context: receive buffers publish records in it.
+ *   gloo_hip_transport_create   <- transport::Device::createContext: one per
+ *       context (collective, in the same order as algorithm creation); sends
+ *       are ordered on `stream` (NULL: a stream of its own).
+ *   gloo_hip_buffer_create      <- Pair::createSendBuffer (is_send = 1) /
+ *       createRecvBuffer (is_send = 0) for the pair to `peer`.  A receive
+ *       buffer is memory the peer writes into: device memory (HIP IPC across
+ *       processes, the pointer itself within one process) or, within one
+ *       process, host memory.  ptr == NULL / size 0: a notification buffer.
+ *   gloo_hip_buffer_send        <- Buffer::send(offset, length, roffset): a
+ *       copy into the peer's receive buffer (a direct xGMI copy between
+ *       GPUs), then, stream-ordered after the bytes landed, an arrival.
+ *   gloo_hip_buffer_wait_recv   <- Buffer::waitRecv: the next arrival, or
+ *       GLOO_HIP_EIO after the context timeout (gloo::IoException).
+ *   gloo_hip_buffer_wait_send   <- Buffer::waitSend: the last send's copy out
+ *       of this buffer has completed.
+ * ---------------------------------------------------------------------- */
+typedef int (*gloo_hip_kv_set_fn)(void* user, const char* key, const void* data, size_t len);
+typedef int (*gloo_hip_kv_get_fn)(void* user, const char* key, int timeout_ms, void* out, size_t cap, size_t* len);
+int gloo_hip_context_create_kv(int rank, int size, int device, int timeout_ms, gloo_hip_kv_set_fn set,
+                               gloo_hip_kv_get_fn get, void* user, gloo_hip_context_t* out);
+
+typedef struct gloo_hip_transport* gloo_hip_transport_t;
+typedef struct gloo_hip_buffer* gloo_hip_buffer_t;
+int gloo_hip_transport_create(gloo_hip_context_t ctx, gloo_hip_stream_t stream, gloo_hip_transport_t* out);
+int gloo_hip_transport_destroy(gloo_hip_transport_t t);
+int gloo_hip_buffer_create(gloo_hip_transport_t t, int peer, int slot, void* ptr, size_t size, int is_send,
+                           gloo_hip_buffer_t* out);
+int gloo_hip_buffer_destroy(gloo_hip_buffer_t b);
+int gloo_hip_buffer_send(gloo_hip_buffer_t b, size_t offset, size_t length, size_t roffset);
+int gloo_hip_buffer_wait_recv(gloo_hip_buffer_t b);
+int gloo_hip_buffer_wait_send(gloo_hip_buffer_t b);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif
