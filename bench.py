@@ -648,6 +648,40 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     return dict(partial)
 
 
+class HipEvent:
+    """A timing event of the HIP runtime torch has loaded (same soname),
+    created with hipEventDisableSystemFence (hip_runtime_api.h): recorded
+    between two kernels it stalls the stream ~1 us instead of the ~2.9 us of
+    a default event's system-scope release (profiles/round2/r2zv_*)."""
+    kDisableSystemFence = 0x20000000
+    _rt = None
+
+    def __init__(self, stream):
+        if HipEvent._rt is None:
+            HipEvent._rt = ctypes.CDLL("libamdhip64.so.7")
+        self.stream = ctypes.c_void_p(stream.cuda_stream)
+        self.h = ctypes.c_void_p()
+        rc = HipEvent._rt.hipEventCreateWithFlags(ctypes.byref(self.h), ctypes.c_uint(self.kDisableSystemFence))
+        if rc != 0:
+            raise RuntimeError(f"hipEventCreateWithFlags failed: {rc}")
+
+    def record(self):
+        rc = HipEvent._rt.hipEventRecord(self.h, self.stream)
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord failed: {rc}")
+
+    def elapsed_ms(self, other):
+        ms = ctypes.c_float()
+        rc = HipEvent._rt.hipEventElapsedTime(ctypes.byref(ms), self.h, other.h)
+        if rc != 0:
+            raise RuntimeError(f"hipEventElapsedTime failed: {rc}")
+        return ms.value
+
+    def __del__(self):
+        if HipEvent._rt is not None and self.h:
+            HipEvent._rt.hipEventDestroy(self.h)
+
+
 def arm_watchdog(seconds, on_fire):
     import threading
     t = threading.Timer(seconds, on_fire)
@@ -710,14 +744,16 @@ def main():
     # Timed region: barrier + sync on both sides, exactly K back-to-back
     # launches.  Kernel duration: two HIP events on the launch stream, the
     # first recorded right AFTER launch 1 is enqueued and the second after
-    # launch K, so region / (K - 1) is the launch-to-launch duration of
-    # kernels 2..K running back to back.  (An event recorded before launch 1
-    # reaches the idle GPU first and would add launch 1's host submission
-    # latency, ~4 us, to the region: 0.2 us per step at K = 20.)  It still
-    # includes the dispatch boundary between launches that rocprofv3's
-    # per-kernel duration excludes (profiles/ keeps both for comparison).
-    e_start = torch.cuda.Event(enable_timing=True)
-    e_end = torch.cuda.Event(enable_timing=True)
+    # launch K, so region / (K - 1) is the launch-to-launch time of kernels
+    # 2..K running back to back, dispatch boundaries included.  (An event
+    # recorded before launch 1 reaches the idle GPU first and would add launch
+    # 1's host submission latency.)  The events are created with
+    # hipEventDisableSystemFence: a default event between two kernels is a
+    # marker with a system-scope release that stalls the stream ~2.9 us; this
+    # one ~1.0 us (profiles/round2/r2zv_event_bubble.jsonl), so the region
+    # holds 1 us of marker instead of 3.
+    e_start = HipEvent(stream)
+    e_end = HipEvent(stream)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -725,15 +761,15 @@ def main():
     skip = 1 if args.steps >= 2 else 0   # K = 1: the whole single launch
     for i in range(skip):
         step(i)
-    e_start.record(stream)
+    e_start.record()
     for i in range(skip, args.steps):
         step(i)
-    e_end.record(stream)
+    e_end.record()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    region_ms = e_start.elapsed_time(e_end)
+    region_ms = e_start.elapsed_ms(e_end)
     kern_ms = region_ms / (args.steps - skip)
 
     t_local = torch.tensor([wall], dtype=torch.float64)
@@ -779,7 +815,9 @@ def main():
                          "kernel_avg_us": round(kern_ms * 1e3, 3),
                          "per_rank_kernel_avg_us": [round(x * 1e3, 3) for x in per_rank_kernel_ms],
                          "event_region_ms": round(region_ms, 4),
-                         "event_region_launches": args.steps - skip},
+                         "event_region_launches": args.steps - skip,
+                         "timing": ("HIP events (hipEventDisableSystemFence) after launch 1 and after launch K "
+                                    "on the launch stream, / (K - 1)")},
             "per_gpu_gib_s": round(value / world, 2),
             "kernel_gib_s": round(alg_bytes / (kern_ms / 1e3) / GIB, 2),
         }

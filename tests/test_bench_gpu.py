@@ -60,3 +60,4 @@ def test_stale_import_refused_never_misdelivered(gpu):
         if v.get("verified") is True:
             continue
         assert "does not show its contents" in v.get("error", ""), (name, v)
+
