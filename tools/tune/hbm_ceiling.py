@@ -1,0 +1,85 @@
+"""MEASUREMENT ONLY: the streaming ceiling of this chip for the config-2
+access mix, next to the product kernel, in one session.
+
+tools/tune/libceiling.so (hbm_ceiling.hip; build:
+  hipcc --offload-arch=gfx950 -O3 -fPIC -shared tools/tune/hbm_ceiling.hip -o tools/tune/libceiling.so)
+holds streaming kernels with reduce_vec_kernel's access shape and R read /
+W write streams of 64 MiB.  Six rotated buffer sets (1.1 GiB) keep every
+launch streaming from HBM.  Each pattern: 20 warm-up + 300 back-to-back
+launches between two events; bytes = (R + W) x 64 MiB per launch.  The
+product's in-place fp32 sum (gloo_hip_reduce) runs in the same loop.
+One JSON line per (rep, pattern).
+"""
+import ctypes
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import gloo_amd as hip
+
+    L = ctypes.CDLL(os.path.join(HERE, "libceiling.so"))
+    vp = ctypes.c_void_p
+    L.ceil_run.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_size_t, vp]
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+    nbytes = 64 << 20
+    n = nbytes // 4
+    sets = [tuple(torch.rand(n, device="cuda") for _ in range(3)) for _ in range(6)]
+    sink = torch.zeros(1024, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+
+    pats = []
+    for i in range(L.ceil_count()):
+        d = (ctypes.c_int * 4)()
+        L.ceil_desc(i, d)
+        r, w, u, b = list(d)
+        pats.append((f"R{r}W{w}_u{u}_b{b}", i, r + w, False))
+        if r == 2 and w == 1:
+            pats.append((f"R{r}W{w}_inplace_u{u}_b{b}", i, r + w, True))
+    pats.append(("product_reduce_inplace", -1, 3, True))
+
+    def launch(p, j):
+        name, i, streams, inplace = p
+        a, b, c = sets[j % 6]
+        if i < 0:
+            hip.reduce_ptr("sum", "f32", a.data_ptr(), b.data_ptr(), n, s)
+            return
+        rc = L.ceil_run(i, (a if inplace else c).data_ptr(), a.data_ptr(), b.data_ptr(), sink.data_ptr(), nbytes, s)
+        if rc:
+            raise RuntimeError(f"{name}: launch failed {rc}")
+
+    # correctness of the 3-operand and copy shapes
+    a, b, c = sets[0]
+    for p in pats:
+        name, i, streams, inplace = p
+        if i >= 0 and name.startswith(("R2W1_u", "R1W1")):
+            L.ceil_run(i, c.data_ptr(), a.data_ptr(), b.data_ptr(), sink.data_ptr(), nbytes, s)
+            torch.cuda.synchronize()
+            want = a + b if name.startswith("R2W1") else a
+            assert torch.equal(c, want), name
+
+    for rep in range(3):
+        for p in pats:
+            for j in range(20):
+                launch(p, j)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for j in range(steps):
+                launch(p, j)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / steps
+            tbs = p[2] * nbytes / us / 1e6
+            print(json.dumps({"rep": rep, "pattern": p[0], "streams": p[2], "us": round(us, 2),
+                              "TBs": round(tbs, 3), "frac_of_8TBs": round(tbs / 8.0, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
