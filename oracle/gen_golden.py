@@ -346,11 +346,58 @@ def gen_bw():
     print("bw_golden.json:", len(cases), "cases; bw_golden.npz:", len(out), "arrays")
 
 
+def gen_bw_extend():
+    """Append to bw_golden.json the largest BASELINE sizes:
+    config 5 at 16 Mi and 64 Mi elements per rank, config 4 at 256 MiB per
+    rank.  Existing cases are kept as they are; a key already present is
+    skipped, so the step is idempotent."""
+    import json
+    import time
+    sys.path.insert(0, os.path.join(os.path.dirname(OUT)))
+    import bw_inputs as bw
+    path = os.path.join(OUT, "bw_golden.json")
+    doc = json.load(open(path))
+    have = {c["key"] for c in doc["cases"]}
+    seed = SEED + 50
+    extra = [("reduce_scatter", "sum", "f16", 8, 1 << 24), ("reduce_scatter", "max", "bf16", 8, 1 << 24),
+             ("reduce_scatter", "product", "bf16", 8, 1 << 26), ("reduce_scatter", "sum", "f16", 8, 1 << 26),
+             ("halving_doubling", "sum", "f32", 8, 1 << 26)]
+    for i, (algo, op, dtype, P, n) in enumerate(extra):
+        key = f"{algo}/{op}/{dtype}/P{P}/n{n}"
+        if key in have:
+            continue
+        t0 = time.time()
+        cs = seed + i
+        x = np.stack([bw.make_input(dtype, op, n, cs, r) for r in range(P)])
+        if algo == "reduce_scatter":
+            recv = bw.even_recv(P, n)
+            y = ref_reduce_scatter(op, dtype, x, np.array(recv, np.int32))
+            outs = [y[r, :recv[r]] for r in range(P)]
+        else:
+            recv = None
+            y = ref_allreduce(algo, op, dtype, x[:, None, :])[:, 0]
+            outs = [y[r] for r in range(P)]
+            assert all((o.view(np.uint8) == outs[0].view(np.uint8)).all() for o in outs), key
+        samples = []
+        for r in range(P):
+            idx = bw.sample_index(len(outs[r]))
+            samples.append({"idx": idx.tolist(), "val": outs[r][idx].view(
+                np.uint32 if outs[r].dtype.itemsize == 4 else np.uint16).tolist()})
+        doc["cases"].append({"key": key, "algo": algo, "op": op, "dtype": dtype, "P": P, "n": n, "seed": cs,
+                             "recv": recv, "digests": [bw.digest(o) for o in outs], "samples": samples})
+        print(f"bw+ {key}: {time.time() - t0:.1f} s", flush=True)
+        del x, y, outs
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=0)
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["math", "sched", "newstyle"]
     if "bw" in which:
         gen_bw()
+    if "bw_extend" in which:
+        gen_bw_extend()
     if "math" in which:
         gen_math()
     if "sched" in which:

@@ -7,6 +7,8 @@ reference's own outputs at BASELINE sizes.
     5000011-element buffer (misaligned chunk offsets), both routes;
   * config 5: ReduceScatterHalvingDoubling fp16 / bf16 x sum / product /
     max / min at 1 Mi elements per rank, plus ragged fp32, both routes;
+  * configs 4 and 5 at their largest sizes: HD fp32 at 8 x 256 MiB, RS fp16 /
+    bf16 at 16 Mi and 64 Mi elements per rank;
   * the reference's large-P grid (gloo/test/allreduce_test.cc:261-269,
     gloo/test/reduce_scatter_test.cc:79-196): P = 9 ... 32 thread ranks on
     one GPU, whole arrays.
@@ -154,6 +156,22 @@ def test_reduce_scatter_bandwidth(torch, env):
     rank (+ ragged fp32); each rank's reduced block byte for byte."""
     res = run_processes(RS, 8, env)
     check(res, RS)
+
+
+# The largest BASELINE sizes (SURVEY 8(d)): config 5 at 16 Mi and 64 Mi
+# elements per rank, config 4 at 256 MiB per rank (gen_golden.py bw_extend).
+BIG = ["reduce_scatter/sum/f16/P8/n16777216", "reduce_scatter/max/bf16/P8/n16777216",
+       "reduce_scatter/product/bf16/P8/n67108864", "reduce_scatter/sum/f16/P8/n67108864",
+       "halving_doubling/sum/f32/P8/n67108864"]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("env", [{}, {"GLOO_AMD_MESH": "0"}], ids=["mesh", "reference_route"])
+def test_baseline_max_sizes(torch, env):
+    """Configs 4 and 5 at their largest BASELINE sizes, each rank's bytes the
+    reference's (eager run, then graph capture)."""
+    res = run_processes(BIG, 8, env, runs=2)
+    check(res, BIG, runs=2)
 
 
 def large_p_keys():
