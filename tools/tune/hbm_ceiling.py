@@ -27,10 +27,17 @@ def main():
     L = ctypes.CDLL(os.path.join(HERE, "libceiling.so"))
     vp = ctypes.c_void_p
     L.ceil_run.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_size_t, vp]
-    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 300
-    nbytes = 64 << 20
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--mib", type=int, default=64, help="MiB per stream per launch")
+    ap.add_argument("--only", default="", help="comma list of pattern prefixes")
+    args = ap.parse_args()
+    steps = args.steps
+    nbytes = args.mib << 20
     n = nbytes // 4
-    sets = [tuple(torch.rand(n, device="cuda") for _ in range(3)) for _ in range(6)]
+    nsets = max(6, -(-1152 // (3 * args.mib)))   # >= 1.1 GiB rotated, 4.5x the Infinity Cache
+    sets = [tuple(torch.rand(n, device="cuda") for _ in range(3)) for _ in range(nsets)]
     sink = torch.zeros(1024, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
 
@@ -43,10 +50,12 @@ def main():
         if r == 2 and w == 1:
             pats.append((f"R{r}W{w}_inplace_u{u}_b{b}", i, r + w, True))
     pats.append(("product_reduce_inplace", -1, 3, True))
+    if args.only:
+        pats = [p for p in pats if p[0].startswith(tuple(args.only.split(",")))]
 
     def launch(p, j):
         name, i, streams, inplace = p
-        a, b, c = sets[j % 6]
+        a, b, c = sets[j % nsets]
         if i < 0:
             hip.reduce_ptr("sum", "f32", a.data_ptr(), b.data_ptr(), n, s)
             return
@@ -77,7 +86,7 @@ def main():
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / steps
             tbs = p[2] * nbytes / us / 1e6
-            print(json.dumps({"rep": rep, "pattern": p[0], "streams": p[2], "us": round(us, 2),
+            print(json.dumps({"rep": rep, "mib": args.mib, "pattern": p[0], "streams": p[2], "us": round(us, 2),
                               "TBs": round(tbs, 3), "frac_of_8TBs": round(tbs / 8.0, 4)}), flush=True)
 
 
