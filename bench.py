@@ -677,9 +677,11 @@ class HipEvent:
             raise RuntimeError(f"hipEventElapsedTime failed: {rc}")
         return ms.value
 
-    def __del__(self):
-        if HipEvent._rt is not None and self.h:
+    def destroy(self):
+        """Explicitly, while the runtime is up (never from __del__ at exit)."""
+        if self.h:
             HipEvent._rt.hipEventDestroy(self.h)
+            self.h = ctypes.c_void_p()
 
 
 def arm_watchdog(seconds, on_fire):
@@ -771,6 +773,8 @@ def main():
     wall = time.perf_counter() - t0
     region_ms = e_start.elapsed_ms(e_end)
     kern_ms = region_ms / (args.steps - skip)
+    e_start.destroy()
+    e_end.destroy()
 
     t_local = torch.tensor([wall], dtype=torch.float64)
     k_all = torch.tensor([kern_ms], dtype=torch.float64)
