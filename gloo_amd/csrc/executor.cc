@@ -572,7 +572,14 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   fineArena_ = !hostArena_ && (arMode == "fine" || (arMode == "auto" && crossSender));
 
   // Phase 2: the inbox arena.
-  const size_t arenaBytes = std::max<size_t>(256, plan_.arena * es_);
+  // Whole 2 MiB granules: an importer's runtime may keep its record of an
+  // earlier arena that sat at the same address (ROCm 7, two rank processes
+  // on one MI355X: a 64 KiB arena imported as the 32 KiB one before it,
+  // after close and re-open; profiles/round2/r2zx_*, r2zz2_*).  With every
+  // arena a multiple of the granule, a reused address comes back at the
+  // same size class and the record spans the new arena.
+  constexpr size_t kArenaGranule = 2u << 20;
+  const size_t arenaBytes = (std::max<size_t>(256, plan_.arena * es_) + kArenaGranule - 1) / kArenaGranule * kArenaGranule;
   if (hostArena_) {
     arenaShm_ = HostShm::create(arenaBytes);
     arena_ = static_cast<char*>(arenaShm_->dev);
@@ -714,19 +721,35 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       // at the arena's start tells; a stale import is closed and opened
       // again, and a mapping that never shows the nonce is an error, never
       // a silent misdelivery.
+      // The runtime's record of the mapping must also span the whole arena:
+      // a mapping the runtime sizes as an earlier, smaller allocation at the
+      // same address lets the nonce through and then fails every copy past
+      // that size with "invalid argument" (seen in bench.py's 2-rank
+      // rehearsal, HD sweep, eager variants: profiles/round2/r2zx_*).
       uint64_t seen = 0;
+      size_t mapped = 0;
       for (int attempt = 0;; attempt++) {
         GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&p, pr.handle, hipIpcMemLazyEnablePeerAccess));
         GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, p, sizeof(seen), hipMemcpyDeviceToHost, stream_));
         GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
-        if (seen == pr.nonce || attempt == 4) break;
+        void* rb = nullptr;
+        size_t rs = 0;
+        if (hipMemGetAddressRange(&rb, &rs, p) == hipSuccess && rb) {
+          // bytes the runtime maps from p on (p may sit inside the range)
+          mapped = static_cast<char*>(rb) + rs > static_cast<char*>(p)
+                       ? (size_t)(static_cast<char*>(rb) + rs - static_cast<char*>(p)) : 0;
+        } else {
+          (void)hipGetLastError();
+          mapped = pr.bytes;  // the runtime cannot tell: rely on the nonce
+        }
+        if ((seen == pr.nonce && mapped >= pr.bytes) || attempt == 4) break;
         GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(p));
         GLOO_AMD_HIP_CHECK(hipDeviceSynchronize());
         std::this_thread::sleep_for(std::chrono::milliseconds(2 << attempt));
       }
       peers_[peer].base = static_cast<char*>(p);
       peers_[peer].ipc = true;
-      if (seen != pr.nonce) {
+      if (seen != pr.nonce || mapped < pr.bytes) {
         const unsigned char* hb = reinterpret_cast<const unsigned char*>(&pr.handle);
         std::string hex;
         char t[3];
@@ -736,7 +759,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
         }
         GLOO_AMD_ENFORCE(false, "rank ", me, ": the IPC mapping of rank ", peer, "'s inbox arena (", (void*)pr.ptr,
                          ", ", pr.bytes, " B, in pid ", pr.pid, ", mapped at ", p, ") does not show its contents: read ",
-                         seen, ", expected ", pr.nonce, "; handle ", hex);
+                         seen, ", expected ", pr.nonce, "; the runtime maps ", mapped, " B there; handle ", hex);
       }
     }
     const Plan theirs = planFor(planAlgo_, peer, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
