@@ -91,6 +91,18 @@ class SendBuffer : public Buffer {
       GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&base, r.handle, hipIpcMemLazyEnablePeerAccess));
       opened_ = base;
       remote_ = static_cast<char*>(base) + r.offset;
+      // the runtime's record of the mapping must reach the whole buffer (an
+      // import can come back at the size of an earlier allocation at the same
+      // address: executor.cc, DESIGN.md §4 "IPC imports must also be sized right")
+      void* rb = nullptr;
+      size_t rs = 0;
+      if (hipMemGetAddressRange(&rb, &rs, base) == hipSuccess && rb) {
+        GLOO_AMD_ENFORCE(static_cast<char*>(rb) + rs >= remote_ + r.size, "the IPC mapping of rank ", peer_,
+                         "'s receive buffer (slot ", slot_, ") reaches ", rs, " B from ", rb, ", short of its ",
+                         r.offset + r.size, " B");
+      } else {
+        (void)hipGetLastError();
+      }
     }
     resolved_ = true;
   }
