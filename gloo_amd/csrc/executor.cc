@@ -8,6 +8,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <deque>
+#include <exception>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -364,6 +366,38 @@ Plan planFor(int algo, int rank, int size, size_t count, int nin, int nout, size
   }
   return makePlan(algo, rank, size, count, nout, recvElems);
 }
+
+// Freed device inbox arenas wait here before hipFree, so the next arena of
+// this process does not come back at an address a peer process imported
+// moments ago.  On ROCm 7 / MI355X with rank processes on one GPU, an import
+// of an arena at such an address was handed the earlier arena's mapping
+// (contents, or the runtime's record of its size) even after the peer had
+// closed it ("IPC imports").  Bounded by count and bytes; the
+// oldest is freed first.
+class ArenaQuarantine {
+ public:
+  static ArenaQuarantine& get() {
+    static ArenaQuarantine* q = new ArenaQuarantine();  // never destroyed: process exit frees device memory
+    return *q;
+  }
+  void retire(void* p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(m_);
+    held_.push_back({p, bytes});
+    total_ += bytes;
+    while (!held_.empty() && (held_.size() > kMaxArenas || total_ > kMaxBytes)) {
+      GLOO_AMD_HIP_RELEASE(hipFree(held_.front().first));
+      total_ -= held_.front().second;
+      held_.pop_front();
+    }
+  }
+
+ private:
+  static constexpr size_t kMaxArenas = 8;
+  static constexpr size_t kMaxBytes = size_t(4) << 30;
+  std::mutex m_;
+  std::deque<std::pair<void*, size_t>> held_;
+  size_t total_ = 0;
+};
 }  // namespace
 
 void PlanExecutor::setBuffers(const std::vector<void*>& inputs, const std::vector<void*>& outputs) {
@@ -580,6 +614,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   // same size class and the record spans the new arena.
   constexpr size_t kArenaGranule = 2u << 20;
   const size_t arenaBytes = (std::max<size_t>(256, plan_.arena * es_) + kArenaGranule - 1) / kArenaGranule * kArenaGranule;
+  arenaBytes_ = arenaBytes;
   if (hostArena_) {
     arenaShm_ = HostShm::create(arenaBytes);
     arena_ = static_cast<char*>(arenaShm_->dev);
@@ -669,6 +704,14 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   std::vector<char> blob(sizeof(rec));
   std::memcpy(blob.data(), &rec, sizeof(rec));
   const std::vector<std::vector<char>> arenas = ctx_->allgather(strcat_("inst", inst_, "/arena"), blob);
+
+  // From here to "ready" a rank may fail on its own (a refused IPC mapping,
+  // an allocation): it still joins the ready exchange with its reason, so
+  // every rank of the collective construction fails together instead of
+  // its peers timing out at the barrier and the ranks falling out of step.
+  std::exception_ptr setupFailure;
+  std::string setupReason;
+  try {
 
   // Every plan peer's record: its mailbox (a channel uses mailboxes when
   // both ends signal from the device and have one — both ends decide alike),
@@ -828,7 +871,25 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     }
     GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
   }
-  ctx_->barrier(strcat_("inst", inst_, "/ready"));
+  } catch (const std::exception& e) {
+    setupFailure = std::current_exception();
+    setupReason = e.what();
+    if (setupReason.empty()) setupReason = "setup failed";
+    if (setupReason.size() > 900) setupReason.resize(900);  // one bootstrap record
+  }
+  const auto ready = ctx_->allgather(strcat_("inst", inst_, "/ready"),
+                                     std::vector<char>(setupReason.begin(), setupReason.end()));
+  bool anyFailed = false;
+  for (int r = 0; r < P; r++) anyFailed = anyFailed || !ready[r].empty();
+  if (anyFailed) {
+    // the destructor will not run: give the counter instance back (the
+    // arena and the imports stay, as a peer may still map them)
+    ctx_->releaseInstance(inst_);
+    if (setupFailure) std::rethrow_exception(setupFailure);
+    for (int r = 0; r < P; r++)
+      GLOO_AMD_ENFORCE(ready[r].empty(), "rank ", r, " could not set up its side of the collective: ",
+                       std::string(ready[r].begin(), ready[r].end()));
+  }
   if (arenaShm_) arenaShm_->unlink();  // every peer has mapped it by now
 }
 
@@ -853,7 +914,7 @@ PlanExecutor::~PlanExecutor() {
       if (arenaShm_) {
         arenaShm_.reset();
       } else if (arena_) {
-        GLOO_AMD_HIP_RELEASE(hipFree(arena_));
+        ArenaQuarantine::get().retire(arena_, arenaBytes_);
       }
       if (mailbox_) GLOO_AMD_HIP_RELEASE(hipFree(mailbox_));
     }

@@ -174,6 +174,7 @@ class PlanExecutor {
   Plan plan_;
   uint64_t inst_;
   char* arena_ = nullptr;       // device-visible address of this rank's inboxes
+  size_t arenaBytes_ = 0;       // its allocated size (whole 2 MiB granules)
   bool hostArena_ = false;      // inboxes in shared pinned host memory (HOST workspace)
   struct HostShm;
   std::unique_ptr<HostShm> arenaShm_;
