@@ -62,6 +62,8 @@ def parse():
                    help="N>1: skip the config-3 xGMI ring-chunked allreduce section")
     p.add_argument("--allreduce-mib", type=int, default=256, help="config 3: MiB per rank")
     p.add_argument("--allreduce-iters", type=int, default=5)
+    p.add_argument("--sweep-seconds", type=float, default=0.2,
+                   help="N>1 config-4 sweep: minimum seconds per timed batch (gloo/benchmark default 2 s)")
     p.add_argument("--quick", action="store_true",
                    help="N>1: config 3 + one variant, short HD sweep, RS at 16 Mi (rehearsals)")
     return p.parse_args()
@@ -472,6 +474,35 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     if args.config3_only:
         return dict(partial)
 
+    def runner_samples(run_once):
+        """gloo/benchmark/runner.cc:311-363: 5 warm-up runs; an iteration
+        count from the median warm-up time (the slowest rank's, so every rank
+        agrees), runs timed back to back, the count grown x2 until a batch
+        lasts args.sweep_seconds (the reference's default 2 s; less here so
+        the driver's run stays bounded) or reaches 10,000.  Returns this
+        rank's per-run seconds of the last batch."""
+        warm = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            run_once()
+            warm.append(time.perf_counter() - t0)
+        med = torch.tensor([sorted(warm)[2]], dtype=torch.float64)
+        dist.all_reduce(med, op=dist.ReduceOp.MAX)
+        iters_ = max(1, int(args.sweep_seconds / max(float(med[0]), 1e-9)))
+        while True:
+            iters_ = min(iters_, 10000)
+            dist.barrier()
+            ts = []
+            for _ in range(iters_):
+                t0 = time.perf_counter()
+                run_once()
+                ts.append(time.perf_counter() - t0)
+            tot = torch.tensor([sum(ts)], dtype=torch.float64)
+            dist.all_reduce(tot, op=dist.ReduceOp.MIN)
+            if float(tot[0]) >= args.sweep_seconds or iters_ >= 10000:
+                return ts
+            iters_ *= 2
+
     short_sizes = (1 << 10, 64 << 10, 1 << 20, 64 << 20)
     full_sizes = tuple(1 << lg for lg in range(10, 31, 2))  # config 4: 1 KiB .. 1 GiB per rank
     iters = 20
@@ -493,13 +524,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                     a2.run()
                     ok = bool((b2 == world * (world + 1) / 2).all())
                     b2.fill_(1.0)
-                    a2.run()
-                    ts = []
-                    for _ in range(iters):
-                        dist.barrier()
-                        t0 = time.perf_counter()
-                        a2.run()
-                        ts.append(time.perf_counter() - t0)
+                    ts = runner_samples(a2.run)
                     md = a2.mode()
                     a2.close()
                     ctx2.close()
@@ -515,13 +540,15 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                 summary.append({"bytes": nbytes,
                                 "error": next(h[i]["error"] for h in hd_all if "error" in h[i])})
                 continue
-            per = sorted(max(h[i]["us"][k] for h in hd_all) for k in range(iters))
-            summary.append({"bytes": nbytes, "us_p50": per[iters // 2], "us_max": per[-1],
+            k_all = min(len(h[i]["us"]) for h in hd_all)
+            per = sorted(max(h[i]["us"][k] for h in hd_all) for k in range(k_all))
+            p50, p99 = per[len(per) // 2], per[min(len(per) - 1, int(len(per) * 0.99))]
+            summary.append({"bytes": nbytes, "us_p50": p50, "us_p99": p99, "us_max": per[-1],
+                            "samples": len(per),
                             "verified": all(h[i]["ok"] for h in hd_all),
                             "launch": "interp" if all(h[i]["interp"] for h in hd_all)
                             else "graph" if all(h[i]["graph"] for h in hd_all) else "eager",
-                            "busbw_gib_s": round(2 * (world - 1) / world * nbytes / (per[iters // 2] / 1e6) / GIB,
-                                                 3)})
+                            "busbw_gib_s": round(2 * (world - 1) / world * nbytes / (p50 / 1e6) / GIB, 3)})
         return summary
 
     # mesh = the derived mesh plan (default); reference_route = the
