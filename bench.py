@@ -318,6 +318,14 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     dist.broadcast_object_list(obj, src=0)
     n = args.allreduce_mib * (1 << 20) // 4
 
+    stores = [0]
+
+    def store_url(name):
+        """A store directory of its own for every context: a repeated
+        variant must not read the keys an earlier context left behind."""
+        stores[0] += 1
+        return "file:%s/%s_%d" % (obj[0], name, stores[0])
+
     def gather(res):
         g = [None] * world
         dist.all_gather_object(g, res)
@@ -365,7 +373,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
             import hashlib
             buf = torch.from_numpy(x_np).to(dev)
             torch.cuda.synchronize(dev)
-            ctx = hip.Context(rank, world, "file:%s/ring_%s_%s_%s" % (obj[0], engine, workspace, mesh),
+            ctx = hip.Context(rank, world, store_url("ring_%s_%s_%s" % (engine, workspace, mesh)),
                               device=dev.index, timeout_ms=60000)
             a = hip.Algorithm(ctx, "ring_chunked", "sum", "f32", [buf.data_ptr()], n, workspace=workspace)
             a.run()
@@ -425,7 +433,8 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         gathered = gather(res)
         errs = [g["error"] for g in gathered if "error" in g]
         if errs:
-            return {"copy_engine": engine, "error": errs[0]}
+            return {"copy_engine": engine, "error": errs[0],
+                    "errors_per_rank": [g.get("error") for g in gathered]}
         ms = sorted(max(g["ms"][i] for g in gathered) for i in range(args.allreduce_iters))
         t = ms[len(ms) // 2] / 1e3
         per_gpu = [g["reduce_b"] / g["reduce_s"] / GIB for g in gathered if g["reduce_s"] > 0]
@@ -518,7 +527,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                     # every element (exact in fp32), whatever the fold order
                     b2 = torch.full((m,), float(rank + 1), device=dev)
                     torch.cuda.synchronize(dev)
-                    ctx2 = hip.Context(rank, world, "file:%s/hd_%s_%d" % (obj[0], label, nbytes),
+                    ctx2 = hip.Context(rank, world, store_url("hd_%s_%d" % (label, nbytes)),
                                        device=dev.index, timeout_ms=60000)
                     a2 = hip.Algorithm(ctx2, "halving_doubling", "sum", "f32", [b2.data_ptr()], m)
                     a2.run()
@@ -582,8 +591,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
             want = {"sum": sum(vals), "product": float(np.prod(vals)), "max": max(vals), "min": min(vals)}[op]
             b = torch.full((m,), vals[rank], dtype=torch.float16 if dtype == "f16" else torch.bfloat16, device=dev)
             torch.cuda.synchronize(dev)
-            c = hip.Context(rank, world, "file:%s/rs_%s_%s_%s_%d" % (obj[0], dtype, op, env.get("GLOO_AMD_MESH", "1"),
-                                                                     m), device=dev.index, timeout_ms=60000)
+            c = hip.Context(rank, world, store_url("rs_%s_%s_%s_%d" % (dtype, op, env.get("GLOO_AMD_MESH", "1"), m)), device=dev.index, timeout_ms=60000)
             a = hip.Algorithm(c, "reduce_scatter", op, dtype, [b.data_ptr()], m, recv_elems=recv)
             a.run()
             ok = bool((b[:recv[rank]].float() == want).all())
@@ -632,7 +640,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
             inp = torch.ones(m, device=dev)
             outp = torch.zeros(m, device=dev)
             torch.cuda.synchronize(dev)
-            c = hip.Context(rank, world, "file:%s/ns_%s_%d_%s" % (obj[0], kind, nbytes, bool(env)),
+            c = hip.Context(rank, world, store_url("ns_%s_%d_%s" % (kind, nbytes, bool(env))),
                             device=dev.index, timeout_ms=60000)
 
             def call():

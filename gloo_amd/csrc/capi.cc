@@ -63,7 +63,7 @@ void runCached(gloo_hip_context_t ctx, int algo, int op, int dtype, const std::v
   if (it == cache.end()) {
     constexpr size_t kMaxCached = 16;
     if (cache.size() == kMaxCached) cache.pop_back();
-    cache.emplace_front(key, std::make_unique<gloo_amd::PlanExecutor>(ctx->ctx, algo, op, dtype, outs, elements,
+    cache.emplace_front(key, gloo_amd::PlanExecutor::create(ctx->ctx, algo, op, dtype, outs, elements,
                                                                       extra, static_cast<hipStream_t>(stream), ins,
                                                                       maxSeg));
     it = cache.begin();
@@ -122,7 +122,7 @@ int gloo_hip_algorithm_create_ws(gloo_hip_context_t ctx, int algo, int op, int d
       re.assign(recv_elems, recv_elems + ctx->ctx->size);
     }
     auto a = std::make_unique<gloo_hip_algorithm>();
-    a->exec = std::make_unique<gloo_amd::PlanExecutor>(ctx->ctx, algo, op, dtype,
+    a->exec = gloo_amd::PlanExecutor::create(ctx->ctx, algo, op, dtype,
                                                        std::vector<void*>(ptrs, ptrs + nptrs), count, re,
                                                        static_cast<hipStream_t>(stream), std::vector<void*>{}, 0,
                                                        workspace);

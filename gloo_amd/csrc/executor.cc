@@ -367,6 +367,8 @@ Plan planFor(int algo, int rank, int size, size_t count, int nin, int nout, size
   return makePlan(algo, rank, size, count, nout, recvElems);
 }
 
+constexpr const char* kStaleImport = "does not show its contents";
+
 // Freed device inbox arenas wait here before hipFree, so the next arena of
 // this process does not come back at an address a peer process imported
 // moments ago.  On ROCm 7 / MI355X with rank processes on one GPU, an import
@@ -801,7 +803,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
           hex += t;
         }
         GLOO_AMD_ENFORCE(false, "rank ", me, ": the IPC mapping of rank ", peer, "'s inbox arena (", (void*)pr.ptr,
-                         ", ", pr.bytes, " B, in pid ", pr.pid, ", mapped at ", p, ") does not show its contents: read ",
+                         ", ", pr.bytes, " B, in pid ", pr.pid, ", mapped at ", p, ") ", kStaleImport, ": read ",
                          seen, ", expected ", pr.nonce, "; the runtime maps ", mapped, " B there; handle ", hex);
       }
     }
@@ -879,12 +881,23 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   }
   const auto ready = ctx_->allgather(strcat_("inst", inst_, "/ready"),
                                      std::vector<char>(setupReason.begin(), setupReason.end()));
-  bool anyFailed = false;
-  for (int r = 0; r < P; r++) anyFailed = anyFailed || !ready[r].empty();
+  bool anyFailed = false, allStale = true;
+  for (int r = 0; r < P; r++) {
+    if (ready[r].empty()) continue;
+    anyFailed = true;
+    allStale = allStale && std::string(ready[r].begin(), ready[r].end()).find(kStaleImport) != std::string::npos;
+  }
   if (anyFailed) {
     // the destructor will not run: give the counter instance back (the
     // arena and the imports stay, as a peer may still map them)
     ctx_->releaseInstance(inst_);
+    if (allStale) {
+      // every rank decides alike (the same ready records): a collective retry
+      // with new arenas can succeed (capi.cc makeExecutor)
+      for (int r = 0; r < P; r++)
+        if (!ready[r].empty())
+          throw StaleImport(strcat_("rank ", r, ": ", std::string(ready[r].begin(), ready[r].end())));
+    }
     if (setupFailure) std::rethrow_exception(setupFailure);
     for (int r = 0; r < P; r++)
       GLOO_AMD_ENFORCE(ready[r].empty(), "rank ", r, " could not set up its side of the collective: ",

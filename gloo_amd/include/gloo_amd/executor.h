@@ -65,6 +65,7 @@
 #include <utility>
 #include <vector>
 
+#include "gloo_amd/common.h"
 #include "gloo_amd/context.h"
 #include "gloo_amd/plan.h"
 #include "gloo_amd/signal.h"
@@ -90,6 +91,20 @@ class PlanExecutor {
   // ordered after everything queued on the previous one.
   void setStream(hipStream_t stream);
   ~PlanExecutor();
+
+  // Construct with up to `retries` collective retries after a StaleImport
+  // (common.h): every rank throws it together, so every rank retries
+  // together, and each attempt maps fresh arenas.
+  template <typename... Args>
+  static std::unique_ptr<PlanExecutor> create(Args&&... args) {
+    for (int attempt = 0;; attempt++) {
+      try {
+        return std::unique_ptr<PlanExecutor>(new PlanExecutor(args...));
+      } catch (const StaleImport&) {
+        if (attempt == 2) throw;
+      }
+    }
+  }
   PlanExecutor(const PlanExecutor&) = delete;
   PlanExecutor& operator=(const PlanExecutor&) = delete;
 

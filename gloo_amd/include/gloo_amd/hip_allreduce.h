@@ -120,7 +120,7 @@ class HipPlanAlgorithm : public Algorithm {
                    const HipReductionFunction<T>* fn)
       : Algorithm(context) {
     std::vector<void*> p(ptrs.begin(), ptrs.end());
-    exec_ = std::make_unique<PlanExecutor>(context, ALGO, fn->type(), DType<T>::value, p,
+    exec_ = PlanExecutor::create(context, ALGO, fn->type(), DType<T>::value, p,
                                            static_cast<size_t>(count), recvElems,
                                            streams.empty() ? nullptr : streams[0], std::vector<void*>{}, 0,
                                            W::kind);
