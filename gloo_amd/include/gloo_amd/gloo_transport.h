@@ -41,6 +41,9 @@
 //
 // All ranks of a context run on one node (the arrival counters live in a
 // node-local control block); each drives the HIP device given at CreateDevice.
+// As with Gloo's own transports, buffers must be destroyed before the
+// gloo::Context whose pairs created them, and a receive buffer must stay
+// allocated while its pair lives.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
