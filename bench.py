@@ -369,11 +369,13 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     def ring_once(engine, workspace="device", mesh="1"):
         progress(f"config 3: ring_chunked engine={engine} workspace={workspace} mesh={mesh}")
 
+        url = store_url("ring_%s_%s_%s" % (engine, workspace, mesh))  # taken first: every rank, same order
+
         def body():
             import hashlib
             buf = torch.from_numpy(x_np).to(dev)
             torch.cuda.synchronize(dev)
-            ctx = hip.Context(rank, world, store_url("ring_%s_%s_%s" % (engine, workspace, mesh)),
+            ctx = hip.Context(rank, world, url,
                               device=dev.index, timeout_ms=60000)
             a = hip.Algorithm(ctx, "ring_chunked", "sum", "f32", [buf.data_ptr()], n, workspace=workspace)
             a.run()
@@ -522,12 +524,13 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
             for nbytes in sizes:
                 progress(f"halving_doubling {label} {nbytes} B")
                 m = max(1, nbytes // 4)
+                url = store_url("hd_%s_%d" % (label, nbytes))
                 try:
                     # rank r contributes r + 1: run 1 must give P(P+1)/2 in
                     # every element (exact in fp32), whatever the fold order
                     b2 = torch.full((m,), float(rank + 1), device=dev)
                     torch.cuda.synchronize(dev)
-                    ctx2 = hip.Context(rank, world, store_url("hd_%s_%d" % (label, nbytes)),
+                    ctx2 = hip.Context(rank, world, url,
                                        device=dev.index, timeout_ms=60000)
                     a2 = hip.Algorithm(ctx2, "halving_doubling", "sum", "f32", [b2.data_ptr()], m)
                     a2.run()
@@ -582,6 +585,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     # elements per rank, recvElems = an even split.
     def rs_once(dtype, op, env, m=16 << 20):
         progress(f"reduce_scatter {dtype} {op} {env} {m}")
+        url = store_url("rs_%s_%s_%s_%d" % (dtype, op, env.get("GLOO_AMD_MESH", "1"), m))
 
         def body():
             recv = [m // world + (1 if r < m % world else 0) for r in range(world)]
@@ -591,7 +595,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
             want = {"sum": sum(vals), "product": float(np.prod(vals)), "max": max(vals), "min": min(vals)}[op]
             b = torch.full((m,), vals[rank], dtype=torch.float16 if dtype == "f16" else torch.bfloat16, device=dev)
             torch.cuda.synchronize(dev)
-            c = hip.Context(rank, world, store_url("rs_%s_%s_%s_%d" % (dtype, op, env.get("GLOO_AMD_MESH", "1"), m)), device=dev.index, timeout_ms=60000)
+            c = hip.Context(rank, world, url, device=dev.index, timeout_ms=60000)
             a = hip.Algorithm(c, "reduce_scatter", op, dtype, [b.data_ptr()], m, recv_elems=recv)
             a.run()
             ok = bool((b[:recv[rank]].float() == want).all())
@@ -634,13 +638,14 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     # derived mesh route (default) and the reference's exchange route.
     def newstyle(kind, nbytes, env=None):
         progress(f"new style {kind} {nbytes} B {env}")
+        url = store_url("ns_%s_%d_%s" % (kind, nbytes, bool(env)))
 
         def body():
             m = max(1, nbytes // 4)
             inp = torch.ones(m, device=dev)
             outp = torch.zeros(m, device=dev)
             torch.cuda.synchronize(dev)
-            c = hip.Context(rank, world, store_url("ns_%s_%d_%s" % (kind, nbytes, bool(env))),
+            c = hip.Context(rank, world, url,
                             device=dev.index, timeout_ms=60000)
 
             def call():
