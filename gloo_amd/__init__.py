@@ -235,6 +235,11 @@ def _bind_collectives(L):
     L.gloo_hip_algorithm_create_ws.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.POINTER(vp), ctypes.c_int, sz,
                                                ctypes.POINTER(ctypes.c_int), vp, ctypes.c_int, ctypes.POINTER(vp)]
+    L.gloo_hip_algorithm_create_streams.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.POINTER(vp), ctypes.c_int, sz,
+                                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp), ctypes.c_int,
+                                                    ctypes.c_int, ctypes.POINTER(vp)]
+    L.gloo_hip_algorithm_set_streams.argtypes = [vp, ctypes.POINTER(vp), ctypes.c_int]
     L.gloo_hip_algorithm_run.argtypes = [vp]
     L.gloo_hip_algorithm_destroy.argtypes = [vp]
     L.gloo_hip_algorithm_wait_seconds.argtypes = [vp]
@@ -250,7 +255,8 @@ EXPORTED = EXPORTED + ("gloo_hip_context_create", "gloo_hip_context_create_ex", 
                        "gloo_hip_algorithm_create", "gloo_hip_algorithm_run",
                        "gloo_hip_algorithm_destroy", "gloo_hip_algorithm_wait_seconds",
                        "gloo_hip_algorithm_set_profiling", "gloo_hip_algorithm_stats",
-                       "gloo_hip_algorithm_mode", "gloo_hip_algorithm_create_ws", "gloo_hip_context_mode")
+                       "gloo_hip_algorithm_mode", "gloo_hip_algorithm_create_ws", "gloo_hip_context_mode",
+                       "gloo_hip_algorithm_create_streams", "gloo_hip_algorithm_set_streams")
 # the xGMI transport's bound buffers (gloo_amd/include/gloo_amd/gloo_transport.h)
 EXPORTED = EXPORTED + ("gloo_hip_context_create_kv", "gloo_hip_transport_create", "gloo_hip_transport_destroy",
                        "gloo_hip_buffer_create", "gloo_hip_buffer_destroy", "gloo_hip_buffer_send",
@@ -306,7 +312,14 @@ class Algorithm:
     workspace: "device" (inboxes in HBM) or "host" (pinned host-memory
     inboxes, the CudaHostWorkspace placement; gloo/cuda_workspace.h:20-31)."""
 
-    def __init__(self, ctx, algo, op, dtype, ptrs, count, recv_elems=None, stream=0, workspace="device"):
+    def __init__(self, ctx, algo, op, dtype, ptrs, count, recv_elems=None, stream=0, workspace="device",
+                 streams=None):
+        """stream: one stream for the plan (0: the algorithm's own, run()
+        returns with outputs complete).  streams: one stream handle per
+        pointer instead (the reference's `streams` argument,
+        gloo/cuda_allreduce_ring_chunked.cc:55-67): run() orders pointer i
+        after the work queued on streams[i], and every streams[i] after the
+        collective."""
         self.ctx = ctx
         arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
         rp = None
@@ -315,9 +328,18 @@ class Algorithm:
         h = ctypes.c_void_p()
         a = ALGORITHMS[algo] if isinstance(algo, str) else int(algo)
         ws = WORKSPACES[workspace] if isinstance(workspace, str) else int(workspace)
-        _check(lib.gloo_hip_algorithm_create_ws(ctx._h, a, _as_op(op), _as_dtype(dtype), arr, len(ptrs),
-                                                int(count), rp, stream or None, ws, ctypes.byref(h)))
+        if streams is not None:
+            sarr = (ctypes.c_void_p * max(1, len(streams)))(*[int(x) for x in streams])
+            _check(lib.gloo_hip_algorithm_create_streams(ctx._h, a, _as_op(op), _as_dtype(dtype), arr, len(ptrs),
+                                                         int(count), rp, sarr, len(streams), ws, ctypes.byref(h)))
+        else:
+            _check(lib.gloo_hip_algorithm_create_ws(ctx._h, a, _as_op(op), _as_dtype(dtype), arr, len(ptrs),
+                                                    int(count), rp, stream or None, ws, ctypes.byref(h)))
         self._h = h
+
+    def set_streams(self, streams):
+        sarr = (ctypes.c_void_p * max(1, len(streams)))(*[int(x) for x in streams])
+        _check(lib.gloo_hip_algorithm_set_streams(self._h, sarr, len(streams)))
 
     def run(self):
         _check(lib.gloo_hip_algorithm_run(self._h))

@@ -130,6 +130,39 @@ int gloo_hip_algorithm_create_ws(gloo_hip_context_t ctx, int algo, int op, int d
   });
 }
 
+int gloo_hip_algorithm_create_streams(gloo_hip_context_t ctx, int algo, int op, int dtype, void* const* ptrs,
+                                      int nptrs, size_t count, const int* recv_elems,
+                                      const gloo_hip_stream_t* streams, int nstreams, int workspace,
+                                      gloo_hip_algorithm_t* out) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(ctx && out && ptrs && nptrs >= 1, "bad arguments");
+    // gloo/cuda_allreduce_ring_chunked.cc:55-58
+    GLOO_AMD_ENFORCE(nstreams == 0 || (streams && nstreams == nptrs), "streams: ", nstreams, ", pointers: ", nptrs,
+                     " (one stream per pointer, or none)");
+    std::vector<int> re;
+    if (algo == GLOO_HIP_ALGO_REDUCE_SCATTER) {
+      GLOO_AMD_ENFORCE(recv_elems, "reduce-scatter needs recv_elems");
+      re.assign(recv_elems, recv_elems + ctx->ctx->size);
+    }
+    std::vector<hipStream_t> ss;
+    for (int i = 0; i < nstreams; i++) ss.push_back(static_cast<hipStream_t>(streams[i]));
+    auto a = std::make_unique<gloo_hip_algorithm>();
+    a->exec = gloo_amd::PlanExecutor::create(ctx->ctx, algo, op, dtype, std::vector<void*>(ptrs, ptrs + nptrs), count,
+                                             re, ss.empty() ? nullptr : ss[0], std::vector<void*>{}, 0, workspace);
+    if (ss.size() > 1) a->exec->setStreams(ss);
+    *out = a.release();
+  });
+}
+
+int gloo_hip_algorithm_set_streams(gloo_hip_algorithm_t a, const gloo_hip_stream_t* streams, int nstreams) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(a && (nstreams == 0 || streams), "bad arguments");
+    std::vector<hipStream_t> ss;
+    for (int i = 0; i < nstreams; i++) ss.push_back(static_cast<hipStream_t>(streams[i]));
+    a->exec->setStreams(ss);
+  });
+}
+
 int gloo_hip_algorithm_create(gloo_hip_context_t ctx, int algo, int op, int dtype, void* const* ptrs, int nptrs,
                               size_t count, const int* recv_elems, gloo_hip_stream_t stream,
                               gloo_hip_algorithm_t* out) {

@@ -51,6 +51,67 @@ uint64_t arenaNonce() {
   return (seed + (++k) * 0xbf58476d1ce4e5b9ull) | 1;
 }
 
+// GLOO_AMD_IPC_DIAG=1: log every arena export / import / close to stderr and
+// probe a mapping that fails its check (diagnosis of stale IPC imports).
+bool ipcDiag() {
+  static const bool v = [] {
+    const char* e = std::getenv("GLOO_AMD_IPC_DIAG");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+std::string handleHex(const hipIpcMemHandle_t& h) {
+  const unsigned char* hb = reinterpret_cast<const unsigned char*>(&h);
+  std::string hex;
+  char t[3];
+  for (size_t i = 0; i < sizeof(h); i++) {
+    std::snprintf(t, sizeof(t), "%02x", hb[i]);
+    hex += t;
+  }
+  return hex;
+}
+
+struct DiagLog {
+  std::mutex m;
+  std::map<std::string, int> handles;  // handle bytes -> times opened
+  std::map<void*, int> mapped;         // importer address -> times handed out
+  std::map<void*, int> exported;       // own arena address -> times exported
+  static DiagLog& get() {
+    static DiagLog* d = new DiagLog();
+    return *d;
+  }
+};
+
+// The first word at p read through hipMemcpy (the runtime's record of the
+// pointer) and four ways by a kernel (the GPU's page tables), plus what the
+// runtime says about the pointer.
+std::string diagProbe(const void* p, hipStream_t s) {
+  uint64_t viaCopy = 0;
+  hipError_t e1 = hipMemcpy(&viaCopy, p, sizeof(viaCopy), hipMemcpyDeviceToHost);
+  uint64_t* out = nullptr;
+  uint64_t k[4] = {0, 0, 0, 0};
+  hipError_t e2 = hipHostMalloc(reinterpret_cast<void**>(&out), 4 * sizeof(uint64_t), hipHostMallocDefault);
+  if (e2 == hipSuccess) {
+    std::memset(out, 0, 4 * sizeof(uint64_t));
+    e2 = launchProbe(static_cast<const uint64_t*>(p), out, s);
+    if (e2 == hipSuccess) e2 = hipStreamSynchronize(s);
+    std::memcpy(k, out, sizeof(k));
+    (void)hipHostFree(out);
+  }
+  hipPointerAttribute_t a;
+  std::memset(&a, 0, sizeof(a));
+  hipError_t e3 = hipPointerGetAttributes(&a, p);
+  void* rb = nullptr;
+  size_t rs = 0;
+  hipError_t e4 = hipMemGetAddressRange(&rb, &rs, const_cast<void*>(p));
+  (void)hipGetLastError();
+  return strcat_("memcpy=", std::hex, viaCopy, " (rc ", std::dec, (int)e1, ") kernel plain/sys/nt/plain=", std::hex,
+                 k[0], "/", k[1], "/", k[2], "/", k[3], " (rc ", std::dec, (int)e2, ") attr(rc ", (int)e3,
+                 ") type=", (int)a.type, " dev=", a.device, " dptr=", a.devicePointer, " hptr=", a.hostPointer,
+                 " flags=", a.allocationFlags, " range(rc ", (int)e4, ")=", rb, "+", rs);
+}
+
 bool mailboxesEnabled() {
   const char* e = std::getenv("GLOO_AMD_MAILBOX");
   return !(e && e[0] == '0');
@@ -384,6 +445,14 @@ class ArenaQuarantine {
   }
   void retire(void* p, size_t bytes) {
     std::lock_guard<std::mutex> lk(m_);
+    static const bool off = [] {
+      const char* e = std::getenv("GLOO_AMD_QUARANTINE");
+      return e && e[0] == '0';
+    }();
+    if (off) {  // diagnosis: free at once
+      GLOO_AMD_HIP_RELEASE(hipFree(p));
+      return;
+    }
     held_.push_back({p, bytes});
     total_ += bytes;
     while (!held_.empty() && (held_.size() > kMaxArenas || total_ > kMaxBytes)) {
@@ -416,25 +485,45 @@ void PlanExecutor::setBuffers(const std::vector<void*>& inputs, const std::vecto
 }
 
 void PlanExecutor::setStream(hipStream_t s) {
-  hipStream_t next = s;
+  setStreams(s ? std::vector<hipStream_t>{s} : std::vector<hipStream_t>{});
+}
+
+void PlanExecutor::setStreams(const std::vector<hipStream_t>& streams) {
+  GLOO_AMD_ENFORCE(streams.size() <= 1 || streams.size() == ptrs_.size(), "one stream per pointer: ",
+                   ptrs_.size(), " pointers, ", streams.size(), " streams");
+  hipStream_t next = streams.empty() ? nullptr : streams[0];
+  for (hipStream_t t : streams) GLOO_AMD_ENFORCE(t != nullptr || streams.size() == 1, "null stream in the list");
   if (!next) {
     if (!ownedStream_) GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&ownedStream_, hipStreamNonBlocking));
     next = ownedStream_;
   }
   if (next != stream_) {
     // the new stream's work (which reuses the inboxes and this rank's
-    // buffers) starts after everything queued on the old one
-    if (!switchEvent_) GLOO_AMD_HIP_CHECK(hipEventCreateWithFlags(&switchEvent_, hipEventDisableTiming));
-    GLOO_AMD_HIP_CHECK(hipEventRecord(switchEvent_, stream_));
-    GLOO_AMD_HIP_CHECK(hipStreamWaitEvent(next, switchEvent_, 0));
+    // buffers) starts after everything queued before: a run on a caller's
+    // stream left doneEvent_ behind; a run on the own stream has completed
+    if (donePending_) GLOO_AMD_HIP_CHECK(hipStreamWaitEvent(next, doneEvent_, 0));
     stream_ = next;
   }
   ownStream_ = stream_ == ownedStream_;
+  sideStreams_.assign(streams.size() > 1 ? streams.begin() + 1 : streams.end(), streams.end());
+  while (sideEvents_.size() < sideStreams_.size()) {
+    hipEvent_t e;
+    GLOO_AMD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    sideEvents_.push_back(e);
+  }
+}
+
+void PlanExecutor::quiesce() {
+  if (ownedStream_) (void)hipStreamSynchronize(ownedStream_);
+  if (donePending_) {
+    (void)hipEventSynchronize(doneEvent_);
+    donePending_ = false;
+  }
 }
 
 void PlanExecutor::dropGraph() {
   if (!graphExec_) return;
-  if (stream_) (void)hipStreamSynchronize(stream_);
+  quiesce();
   (void)hipGraphExecDestroy(graphExec_);
   graphExec_ = nullptr;
 }
@@ -514,6 +603,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   classifyPointers();
   inst_ = ctx_->acquireInstance();
   GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
+  GLOO_AMD_HIP_CHECK(hipEventCreateWithFlags(&doneEvent_, hipEventDisableTiming));
   if (stream) {
     stream_ = stream;
   } else {
@@ -690,6 +780,17 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     rec.nonce = arenaNonce();
     GLOO_AMD_HIP_CHECK(hipMemcpyAsync(arena_, &rec.nonce, sizeof(rec.nonce), hipMemcpyHostToDevice, stream_));
     GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (ipcDiag()) {
+      int times;
+      {
+        DiagLog& d = DiagLog::get();
+        std::lock_guard<std::mutex> lk(d.m);
+        times = d.exported[arena_]++;
+      }
+      std::fprintf(stderr, "[ipc-diag %d r%d inst%llu] export arena %p %zu B fine=%d nonce %llx (exported here %d times before): %s\n",
+                   ctx_->pid(), me, (unsigned long long)inst_, (void*)arena_, arenaBytes, (int)fineArena_,
+                   (unsigned long long)rec.nonce, times, diagProbe(arena_, stream_).c_str());
+    }
   }
   if (mailbox_) {
     rec.hasMailbox = 1;
@@ -777,6 +878,22 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
         GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&p, pr.handle, hipIpcMemLazyEnablePeerAccess));
         GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, p, sizeof(seen), hipMemcpyDeviceToHost, stream_));
         GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+        if (ipcDiag()) {
+          const std::string hx = handleHex(pr.handle);
+          int hTimes, vTimes;
+          {
+            DiagLog& d = DiagLog::get();
+            std::lock_guard<std::mutex> lk(d.m);
+            hTimes = d.handles[hx]++;
+            vTimes = d.mapped[p]++;
+          }
+          std::fprintf(stderr, "[ipc-diag %d r%d inst%llu] import rank %d arena %p %llu B (pid %d) -> %p attempt %d: "
+                       "seen %llx want %llx (handle opened %d times before, address handed out %d times before)%s%s\n",
+                       ctx_->pid(), me, (unsigned long long)inst_, peer, (void*)pr.ptr, (unsigned long long)pr.bytes,
+                       pr.pid, p, attempt, (unsigned long long)seen, (unsigned long long)pr.nonce, hTimes, vTimes,
+                       seen == pr.nonce ? "" : " MISMATCH: ",
+                       seen == pr.nonce ? "" : diagProbe(p, stream_).c_str());
+        }
         void* rb = nullptr;
         size_t rs = 0;
         if (hipMemGetAddressRange(&rb, &rs, p) == hipSuccess && rb) {
@@ -888,9 +1005,11 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     allStale = allStale && std::string(ready[r].begin(), ready[r].end()).find(kStaleImport) != std::string::npos;
   }
   if (anyFailed) {
-    // the destructor will not run: give the counter instance back (the
-    // arena and the imports stay, as a peer may still map them)
-    ctx_->releaseInstance(inst_);
+    // the destructor will not run: release what this rank set up.  Every
+    // rank saw the same ready records and fails here together, so the
+    // tear-down barrier (no arena is freed while a peer maps it) is
+    // collective as in the destructor.
+    release();
     if (allStale) {
       // every rank decides alike (the same ready records): a collective retry
       // with new arenas can succeed (capi.cc makeExecutor)
@@ -906,9 +1025,11 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   if (arenaShm_) arenaShm_->unlink();  // every peer has mapped it by now
 }
 
-PlanExecutor::~PlanExecutor() {
+PlanExecutor::~PlanExecutor() { release(); }
+
+void PlanExecutor::release() {
   try {
-    if (stream_) (void)hipStreamSynchronize(stream_);
+    quiesce();
     for (hipStream_t a : aux_) (void)hipStreamSynchronize(a);
     // the captured graph holds copy nodes into the peers' mapped arenas: it
     // goes before the mappings are closed, or a close leaves the import
@@ -918,9 +1039,16 @@ PlanExecutor::~PlanExecutor() {
     graphExec_ = nullptr;
     if (ctx_->size > 1) {
       for (auto& p : peers_)
-        if (p.ipc && p.base) GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(p.base));
+        if (p.ipc && p.base) {
+          if (ipcDiag())
+            std::fprintf(stderr, "[ipc-diag %d r%d inst%llu] close %p\n", ctx_->pid(), ctx_->rank,
+                         (unsigned long long)inst_, (void*)p.base);
+          GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(p.base));
+        }
+      peers_.clear();
       for (size_t q = 0; q < peerMailbox_.size(); q++)
         if (peerMailboxIpc_[q] && peerMailbox_[q]) GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(peerMailbox_[q]));
+      peerMailbox_.clear();
       // nobody may free an arena a peer still maps
       ctx_->barrier(strcat_("inst", inst_, "/closed"));
       peerShm_.clear();
@@ -929,29 +1057,44 @@ PlanExecutor::~PlanExecutor() {
       } else if (arena_) {
         ArenaQuarantine::get().retire(arena_, arenaBytes_);
       }
+      arena_ = nullptr;
       if (mailbox_) GLOO_AMD_HIP_RELEASE(hipFree(mailbox_));
+      mailbox_ = nullptr;
     }
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+    events_.clear();
     for (hipEvent_t e : forkEvents_) (void)hipEventDestroy(e);
+    forkEvents_.clear();
     for (hipStream_t a : aux_) (void)hipStreamDestroy(a);
-    if (graphExec_) (void)hipGraphExecDestroy(graphExec_);
+    aux_.clear();
     if (epoch_) GLOO_AMD_HIP_RELEASE(hipFree(epoch_));
+    epoch_ = nullptr;
     if (interpSteps_) GLOO_AMD_HIP_RELEASE(hipFree(interpSteps_));
+    interpSteps_ = nullptr;
     if (ticket_) GLOO_AMD_HIP_RELEASE(hipFree(ticket_));
+    ticket_ = nullptr;
     if (stamps_) GLOO_AMD_HIP_RELEASE(hipFree(stamps_));
+    stamps_ = nullptr;
     for (char* p : outStage_)
       if (p) GLOO_AMD_HIP_RELEASE(hipFree(p));
+    outStage_.clear();
     for (char* p : inStage_)
       if (p) GLOO_AMD_HIP_RELEASE(hipFree(p));
+    inStage_.clear();
     if (ownedStream_) {
       (void)hipStreamSynchronize(ownedStream_);
       (void)hipStreamDestroy(ownedStream_);
     }
-    if (switchEvent_) (void)hipEventDestroy(switchEvent_);
+    ownedStream_ = nullptr;
+    for (hipEvent_t e : sideEvents_) (void)hipEventDestroy(e);
+    sideEvents_.clear();
+    if (doneEvent_) (void)hipEventDestroy(doneEvent_);
+    doneEvent_ = nullptr;
   } catch (...) {
     // teardown is best effort; never throw from a destructor
   }
-  ctx_->releaseInstance(inst_);
+  if (!released_) ctx_->releaseInstance(inst_);
+  released_ = true;
 }
 
 void PlanExecutor::waitCounter(std::atomic<uint64_t>& c, uint64_t target, int peer, int slot) {
@@ -1068,6 +1211,11 @@ void PlanExecutor::run() {
   reduceSeconds_ = reduceBytes_ = 0;
   reduceCount_ = 0;
   replayed_ = false;
+  // the caller's work on its other pointers' streams comes first
+  for (size_t i = 0; i < sideStreams_.size(); i++) {
+    GLOO_AMD_HIP_CHECK(hipEventRecord(sideEvents_[i], sideStreams_[i]));
+    GLOO_AMD_HIP_CHECK(hipStreamWaitEvent(stream_, sideEvents_[i], 0));
+  }
   const uint64_t r = runs_ + 1;
   // sliced plans must run sliced on every rank (their flags are per slice);
   // profiling then reports no reduce events
@@ -1104,6 +1252,13 @@ void PlanExecutor::run() {
   }
   runs_ = r;
   stableRuns_++;
+  if (!ownStream_) {
+    // every stream of the caller is ordered after the collective, and later
+    // host waits (teardown, a new stream) use this event, not the stream
+    GLOO_AMD_HIP_CHECK(hipEventRecord(doneEvent_, stream_));
+    donePending_ = true;
+    for (hipStream_t t : sideStreams_) GLOO_AMD_HIP_CHECK(hipStreamWaitEvent(t, doneEvent_, 0));
+  }
   if (ownStream_ || profiling_ || stamping_) {
     const auto t0 = std::chrono::steady_clock::now();
     GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));

@@ -1184,7 +1184,7 @@ size_t gloo_hip_dtype_size(int dtype) {
   return kSizes[dtype];
 }
 
-const char* gloo_hip_version(void) { return "0.1.0"; }
+
 
 int gloo_hip_set_variant(int variant) {
   const int prev = g_variant;

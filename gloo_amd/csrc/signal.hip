@@ -67,7 +67,24 @@ __global__ __launch_bounds__(64) void wait_multi_kernel(WaitList w, const uint64
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
+// Diagnosis of IPC mappings: the first word behind `p` read four ways.
+__global__ __launch_bounds__(64) void probe_kernel(const uint64_t* p, uint64_t* out) {
+  if (threadIdx.x == 0) {
+    out[0] = *reinterpret_cast<const volatile uint64_t*>(p);
+    out[1] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    out[2] = __builtin_nontemporal_load(p);
+    out[3] = *reinterpret_cast<const volatile uint64_t*>(p);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+}
+
 }  // namespace
+
+hipError_t launchProbe(const uint64_t* p, uint64_t* out, hipStream_t stream) {
+  probe_kernel<<<1, 64, 0, stream>>>(p, out);
+  return hipGetLastError();
+}
 
 hipError_t launchWaitMulti(const uint64_t* const* flags, const Seq* targets, int n, const uint64_t* epoch,
                            uint64_t timeoutTicks, uint32_t* err, hipStream_t stream) {

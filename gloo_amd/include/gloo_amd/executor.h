@@ -59,6 +59,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <cstdlib>
 #include <map>
 #include <string>
 #include <memory>
@@ -88,8 +89,18 @@ class PlanExecutor {
   void setBuffers(const std::vector<void*>& inputs, const std::vector<void*>& outputs);
   // ... and to the call's stream (nullptr: the executor's own stream, and
   // run() returns with the outputs complete).  Work on the new stream is
-  // ordered after everything queued on the previous one.
+  // ordered after everything this executor queued before.
   void setStream(hipStream_t stream);
+  // One stream per output pointer, the reference's `streams` argument
+  // (gloo/cuda_allreduce_ring_chunked.cc:55-67, GLOO_ENFORCE_EQ(streams.size(),
+  // ptrs.size())): run() orders its use of pointer i after the work already
+  // queued on streams[i] (docs/cuda.md:7-11) and, on return, every
+  // streams[i] is ordered after the collective, so the caller synchronises
+  // with any of them.  The plan itself runs on streams[0].  Empty: the
+  // executor's own stream, and run() returns with the outputs complete.
+  // The executor never holds a caller's stream past run(): later waits use
+  // an event it owns, so a caller may destroy its streams between calls.
+  void setStreams(const std::vector<hipStream_t>& streams);
   ~PlanExecutor();
 
   // Construct with up to `retries` collective retries after a StaleImport
@@ -97,11 +108,13 @@ class PlanExecutor {
   // together, and each attempt maps fresh arenas.
   template <typename... Args>
   static std::unique_ptr<PlanExecutor> create(Args&&... args) {
+    const char* e = std::getenv("GLOO_AMD_STALE_RETRIES");
+    const int retries = e ? std::atoi(e) : 2;
     for (int attempt = 0;; attempt++) {
       try {
         return std::unique_ptr<PlanExecutor>(new PlanExecutor(args...));
       } catch (const StaleImport&) {
-        if (attempt == 2) throw;
+        if (attempt >= retries) throw;
       }
     }
   }
@@ -197,7 +210,17 @@ class PlanExecutor {
   hipStream_t stream_ = nullptr;
   bool ownStream_ = false;            // stream_ is the executor's own: run() returns with outputs complete
   hipStream_t ownedStream_ = nullptr;  // the executor's own stream, if created
-  hipEvent_t switchEvent_ = nullptr;
+  std::vector<hipStream_t> sideStreams_;  // the caller's streams of pointers 1.. (setStreams)
+  std::vector<hipEvent_t> sideEvents_;
+  hipEvent_t doneEvent_ = nullptr;     // recorded on stream_ at the end of a run on a caller's stream
+  bool donePending_ = false;           // ... and not yet waited for on the host
+  // Host-wait for everything this executor has queued, without touching a
+  // caller's stream (it may be gone).
+  void quiesce();
+  // Tear-down (collective when P > 1): the destructor, and a construction
+  // that failed on any rank (every rank fails together at the ready point).
+  void release();
+  bool released_ = false;
   std::vector<Peer> peers_;
   std::map<std::pair<int, int>, uint64_t> remoteRegion_;  // (peer, slot) -> elts into peer arena
   // Sequence numbers.  Channel (peer, slot) carries perRun messages per run;

@@ -33,8 +33,16 @@
 // anything else gloo::EnforceNotMet (gloo/common/logging.h:32-59).
 //
 // Stream semantics (docs/cuda.md:6-13 of the reference): without streams,
-// run() returns with the outputs complete; with streams, the work is ordered
-// on streams[0] and the caller synchronises.
+// run() returns with the outputs complete; with one stream per pointer
+// (gloo/cuda_allreduce_ring_chunked.cc:55-67), run() orders its use of
+// ptrs[i] after the work already queued on streams[i], and every streams[i]
+// is ordered after the collective, so the caller synchronises with them.
+//
+// Element types: the reference's CUDA instantiations (gloo/cuda.cu:265-272),
+// plus c10::BFloat16 when built with GLOO_USE_TORCH_DTYPES (cuda.cu:394-401).
+// Reductions: the built-in ReductionType values run the library's kernels; a
+// CUSTOM reduction is a gloo::HipReductionFunction<T> carrying a device
+// function (the device half of CudaReductionFunction, gloo/cuda.h:286-358).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -54,6 +62,13 @@
 #include "gloo/types.h"
 #include "gloo_amd.h"
 #include "gloo_amd/gloo_transport.h"
+
+#if GLOO_USE_TORCH_DTYPES
+#include <c10/util/BFloat16.h>
+#endif
+
+#include <map>
+#include <mutex>
 
 namespace gloo {
 
@@ -80,12 +95,36 @@ template <> struct DType<uint64_t> { static constexpr int value = GLOO_HIP_U64; 
 template <> struct DType<float16> { static constexpr int value = GLOO_HIP_F16; };
 template <> struct DType<float> { static constexpr int value = GLOO_HIP_F32; };
 template <> struct DType<double> { static constexpr int value = GLOO_HIP_F64; };
+#if GLOO_USE_TORCH_DTYPES
+template <> struct DType<c10::BFloat16> { static constexpr int value = GLOO_HIP_BF16; };
+#endif
 
-// gloo::ReductionType (gloo/algorithm.h:49-57) -> gloo_hip_op_t (same values).
-inline int opOf(ReductionType t) {
-  GLOO_ENFORCE(t == SUM || t == PRODUCT || t == MAX || t == MIN,
-               "the device path runs the built-in reduction types; CUSTOM needs a device function");
-  return static_cast<int>(t);
+// CUSTOM reductions: ReductionFunction<T> has no virtual members, so a
+// HipReductionFunction<T> records its library op code here, keyed by its
+// address, for as long as it lives.
+struct CustomOps {
+  std::mutex m;
+  std::map<const void*, int> ops;
+  static CustomOps& get() {
+    static CustomOps* c = new CustomOps();
+    return *c;
+  }
+};
+
+// gloo::ReductionType (gloo/algorithm.h:49-57) -> gloo_hip_op_t (same values
+// for the built-ins; a registered code >= GLOO_HIP_CUSTOM for CUSTOM).
+template <typename T>
+inline int opOf(const ReductionFunction<T>* fn) {
+  GLOO_ENFORCE(fn != nullptr, "null reduction function");
+  const ReductionType t = fn->type();
+  if (t == SUM || t == PRODUCT || t == MAX || t == MIN) return static_cast<int>(t);
+  GLOO_ENFORCE(t == CUSTOM, "unknown reduction type ", static_cast<int>(t));
+  CustomOps& c = CustomOps::get();
+  std::lock_guard<std::mutex> lk(c.m);
+  auto it = c.ops.find(fn);
+  GLOO_ENFORCE(it != c.ops.end(),
+               "a CUSTOM reduction on device memory needs a device function: pass a gloo::HipReductionFunction<T>");
+  return it->second;
 }
 
 inline void check(int rc, const char* what) {
@@ -154,22 +193,73 @@ class BootstrapContext {
 
 }  // namespace hip_bridge
 
+// A CUSTOM reduction for the device path: the device half of
+// CudaReductionFunction<T> (gloo/cuda.h:286-358), whose device function
+// enqueues dst[i] = dst[i] op src[i] on a stream (cuda.h:288-290), with the
+// host function the reference's ReductionFunction<T> calls (algorithm.h:59-95;
+// optional: the device path never calls it).  The device function must not
+// allocate or synchronise, as the reference requires of its device
+// functions.  Pass it where a const ReductionFunction<T>* is taken; it must
+// outlive the algorithms built with it.
+template <typename T>
+class HipReductionFunction : public ReductionFunction<T> {
+ public:
+  using DeviceFunction = void(T* dst, const T* src, size_t n, hipStream_t stream);
+
+  explicit HipReductionFunction(DeviceFunction* dev, typename ReductionFunction<T>::Function* host = nullptr)
+      : ReductionFunction<T>(CUSTOM, host ? host : &HipReductionFunction::noHost), dev_(dev) {
+    GLOO_ENFORCE(dev != nullptr, "null device function");
+    hip_bridge::check(gloo_hip_register_op(&HipReductionFunction::trampoline, this, &op_), "gloo_hip_register_op");
+    auto& c = hip_bridge::CustomOps::get();
+    std::lock_guard<std::mutex> lk(c.m);
+    c.ops[this] = op_;
+  }
+  ~HipReductionFunction() {
+    auto& c = hip_bridge::CustomOps::get();
+    std::lock_guard<std::mutex> lk(c.m);
+    c.ops.erase(this);
+  }
+  HipReductionFunction(const HipReductionFunction&) = delete;
+  HipReductionFunction& operator=(const HipReductionFunction&) = delete;
+
+  int op() const { return op_; }
+  void callDevice(T* dst, const T* src, size_t n, hipStream_t stream) const { dev_(dst, src, n, stream); }
+
+ private:
+  // the library's custom op is three-operand (c = a op b, c may alias a)
+  static void trampoline(void* user, void* c, const void* a, const void* b, size_t n, gloo_hip_stream_t s) {
+    auto* self = static_cast<HipReductionFunction*>(user);
+    hipStream_t stream = static_cast<hipStream_t>(s);
+    if (c != a) (void)hipMemcpyAsync(c, a, n * sizeof(T), hipMemcpyDeviceToDevice, stream);
+    self->dev_(static_cast<T*>(c), static_cast<const T*>(b), n, stream);
+  }
+  static void noHost(T*, const T*, size_t) {
+    GLOO_ENFORCE(false, "this HipReductionFunction has no host function");
+  }
+  DeviceFunction* dev_;
+  int op_ = 0;
+};
+
 // One of the library's schedule executors as a gloo::Algorithm.
 template <typename T, int ALGO, typename W>
 class HipPlanAlgorithm : public Algorithm {
  public:
   HipPlanAlgorithm(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
-                   const std::vector<int>& recvElems, const std::vector<hipStream_t>& streams, ReductionType op)
+                   const std::vector<int>& recvElems, const std::vector<hipStream_t>& streams,
+                   const ReductionFunction<T>* fn)
       : Algorithm(context) {
     GLOO_ENFORCE(!ptrs.empty(), "need at least one pointer");
+    // gloo/cuda_allreduce_ring_chunked.cc:55-58
     GLOO_ENFORCE(streams.empty() || streams.size() == ptrs.size(), "one stream per pointer, or none");
+    const int op = hip_bridge::opOf(fn);
     boot_.reset(new hip_bridge::BootstrapContext(context, hip_bridge::deviceOf(ptrs[0])));
     std::vector<void*> p(ptrs.begin(), ptrs.end());
+    std::vector<gloo_hip_stream_t> s(streams.begin(), streams.end());
     hip_bridge::check(
-        gloo_hip_algorithm_create_ws(boot_->handle(), ALGO, hip_bridge::opOf(op), hip_bridge::DType<T>::value,
-                                     p.data(), (int)p.size(), (size_t)(count > 0 ? count : 0),
-                                     recvElems.empty() ? nullptr : recvElems.data(),
-                                     streams.empty() ? nullptr : streams[0], W::kind, &algo_),
+        gloo_hip_algorithm_create_streams(boot_->handle(), ALGO, op, hip_bridge::DType<T>::value, p.data(),
+                                          (int)p.size(), (size_t)(count > 0 ? count : 0),
+                                          recvElems.empty() ? nullptr : recvElems.data(),
+                                          s.empty() ? nullptr : s.data(), (int)s.size(), W::kind, &algo_),
         "gloo_hip_algorithm_create");
   }
 
@@ -190,7 +280,7 @@ class HipAllreduceRingChunked : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING_CH
   HipAllreduceRingChunked(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, const int count,
                           const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
                           const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
-      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING_CHUNKED, W>(context, ptrs, count, {}, streams, fn->type()) {}
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING_CHUNKED, W>(context, ptrs, count, {}, streams, fn) {}
 };
 
 template <typename T, typename W = HipDeviceWorkspace<T>>
@@ -205,7 +295,7 @@ class HipAllreduceHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_HAL
                               const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
                               bool /*pipelineBroadcastAndReduce*/ = false,
                               const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
-      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING, W>(context, ptrs, count, {}, streams, fn->type()) {}
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING, W>(context, ptrs, count, {}, streams, fn) {}
 };
 
 template <typename T, typename W = HipDeviceWorkspace<T>>
@@ -214,7 +304,7 @@ class HipAllreduceRing : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING, W> {
   HipAllreduceRing(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, const int count,
                    const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
                    const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
-      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING, W>(context, ptrs, count, {}, streams, fn->type()) {}
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING, W>(context, ptrs, count, {}, streams, fn) {}
 };
 
 template <typename T, typename W = HipDeviceWorkspace<T>>
@@ -223,7 +313,7 @@ class HipAllreduceLocal : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_LOCAL, W> {
   HipAllreduceLocal(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, const int count,
                     const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
                     const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
-      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_LOCAL, W>(context, ptrs, count, {}, streams, fn->type()) {}
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_LOCAL, W>(context, ptrs, count, {}, streams, fn) {}
 };
 
 template <typename T, typename W = HipDeviceWorkspace<T>>
@@ -233,7 +323,7 @@ class HipReduceScatterHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO
                                   const int count, const std::vector<int>& recvElems,
                                   const ReductionFunction<T>* fn = ReductionFunction<T>::sum,
                                   const std::vector<hipStream_t>& streams = std::vector<hipStream_t>())
-      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_REDUCE_SCATTER, W>(context, ptrs, count, recvElems, streams, fn->type()) {
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_REDUCE_SCATTER, W>(context, ptrs, count, recvElems, streams, fn) {
     GLOO_ENFORCE_EQ((int)recvElems.size(), context->size, "recvElems needs one entry per rank");
   }
 };

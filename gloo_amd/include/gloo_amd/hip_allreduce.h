@@ -119,11 +119,14 @@ class HipPlanAlgorithm : public Algorithm {
                    const std::vector<int>& recvElems, const std::vector<hipStream_t>& streams,
                    const HipReductionFunction<T>* fn)
       : Algorithm(context) {
+    // one stream per pointer, or none (gloo/cuda_allreduce_ring_chunked.cc:55-58)
+    GLOO_AMD_ENFORCE(streams.empty() || streams.size() == ptrs.size(), "one stream per pointer, or none");
     std::vector<void*> p(ptrs.begin(), ptrs.end());
     exec_ = PlanExecutor::create(context, ALGO, fn->type(), DType<T>::value, p,
                                            static_cast<size_t>(count), recvElems,
                                            streams.empty() ? nullptr : streams[0], std::vector<void*>{}, 0,
                                            W::kind);
+    if (streams.size() > 1) exec_->setStreams(streams);
   }
   void run() override { exec_->run(); }
 

@@ -41,6 +41,10 @@ hipError_t launchEpochSet(uint64_t* epoch, uint64_t value, hipStream_t stream); 
 hipError_t launchSignal(uint64_t* flag, Seq value, const uint64_t* epoch, hipStream_t stream);
 hipError_t launchWait(const uint64_t* flag, Seq target, const uint64_t* epoch, uint64_t timeoutTicks,
                       uint32_t* err, hipStream_t stream);
+// Diagnosis: out[0..3] = the word at p by a plain load, a system-scope
+// atomic load, a non-temporal load after a system-scope acquire, and a plain
+// load again (out: host-visible memory).
+hipError_t launchProbe(const uint64_t* p, uint64_t* out, hipStream_t stream);
 
 // One-workgroup fused step for small messages (reduce.hip): optionally wait
 // for `*waitFlag >= wait`, then dst[i] = dst[i] op src[i] (op 0: copy), then

@@ -327,6 +327,23 @@ int gloo_hip_algorithm_create_ws(gloo_hip_context_t ctx, int algo, int op, int d
                                  size_t count, const int* recv_elems, gloo_hip_stream_t stream, int workspace,
                                  gloo_hip_algorithm_t* out);
 
+/* gloo_hip_algorithm_create_ws with one stream per pointer, the reference's
+ * `const std::vector<cudaStream_t>& streams` (gloo/cuda_allreduce_ring_chunked.h:19-26,
+ * GLOO_ENFORCE_EQ(streams.size(), ptrs.size()) at .cc:55-58): nstreams is 0
+ * (run() returns with the outputs complete) or nptrs.  run() orders its use
+ * of ptrs[i] after the work already queued on streams[i], and on return
+ * every streams[i] is ordered after the collective (docs/cuda.md:7-11): the
+ * caller synchronises with any of them.  The library never uses a stream
+ * outside create/run, so a caller may destroy it between runs (each run()
+ * then needs the streams it was created with, or those of
+ * gloo_hip_algorithm_set_streams). */
+int gloo_hip_algorithm_create_streams(gloo_hip_context_t ctx, int algo, int op, int dtype, void* const* ptrs,
+                                      int nptrs, size_t count, const int* recv_elems,
+                                      const gloo_hip_stream_t* streams, int nstreams, int workspace,
+                                      gloo_hip_algorithm_t* out);
+/* Rebind the streams of later runs (same rule: 0 or nptrs of them). */
+int gloo_hip_algorithm_set_streams(gloo_hip_algorithm_t algo, const gloo_hip_stream_t* streams, int nstreams);
+
 int gloo_hip_algorithm_run(gloo_hip_algorithm_t algo);
 int gloo_hip_algorithm_destroy(gloo_hip_algorithm_t algo);
 /* Host seconds the last run() spent blocked waiting for peers. */

@@ -74,3 +74,21 @@ def test_set_profiling_modes_reach_the_c_abi(monkeypatch):
     for on in (True, False, 0, 1, 2):
         a.set_profiling(on)
     assert seen == [1, 0, 0, 1, 2]
+
+
+def test_library_built_from_this_tree():
+    """gloo_hip_version() carries a hash of the sources the library was built
+    from (gloo_amd/srchash.py); it must be this tree's, so no stale prebuilt
+    .so can stand in for the sources (smoke() checks the same on the GPU)."""
+    import gloo_amd
+    from gloo_amd import srchash
+    assert gloo_amd.version() == srchash.version_string()
+
+
+def test_source_hash_covers_every_library_source():
+    from gloo_amd import srchash
+    _, files = srchash.source_files()
+    src = os.path.join(ROOT, "gloo_amd", "csrc")
+    for f in os.listdir(src):
+        assert os.path.join("gloo_amd", "csrc", f) in files, f
+    assert os.path.join("include", "gloo_amd.h") in files

@@ -49,6 +49,35 @@ __global__ __launch_bounds__(B) void stream_k(float* c, const float* a, const fl
   }
 }
 
+// The same 2-read + 1-write mix with both reads by LDS-DMA (`buffer_load
+// ... lds`, 16 B per lane on gfx950, nt): each wave's packets land in LDS at
+// M0 + lane * 16, are read back with ds_read_b128 after vmcnt(0), added and
+// stored with raw nt buffer stores.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+template <int U, int B>
+__global__ __launch_bounds__(B) void stream_lds_k(float* c, const float* a, const float* b, uint32_t*) {
+  __shared__ u32x4 lds[2][U][B];
+  constexpr uint32_t kTile = (uint32_t)B * U * 16;
+  const size_t base = (size_t)blockIdx.x * kTile;
+  const auto ra = rsrc(reinterpret_cast<const char*>(a) + base, kTile);
+  const auto rb = rsrc(reinterpret_cast<const char*>(b) + base, kTile);
+  const auto rc = rsrc(reinterpret_cast<const char*>(c) + base, kTile);
+  const uint32_t lane = threadIdx.x * 16u;
+  const int w0 = (threadIdx.x / 64) * 64;
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)&lds[0][u][w0], 16, lane + u * B * 16, 0, 0, kNT);
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)&lds[1][u][w0], 16, lane + u * B * 16, 0, 0, kNT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const f32x4 s = __builtin_bit_cast(f32x4, lds[0][u][threadIdx.x]) + __builtin_bit_cast(f32x4, lds[1][u][threadIdx.x]);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, s), rc, lane + u * B * 16, 0, kNT);
+  }
+}
+
 struct P {
   int r, w, u, b;
   void (*launch)(float*, const float*, const float*, uint32_t*, size_t, hipStream_t);
@@ -58,9 +87,17 @@ struct P {
   {R, W, U, B, [](float* c, const float* a, const float* b, uint32_t* sink, size_t bytes, hipStream_t s) { \
      stream_k<R, W, U, B><<<(unsigned)(bytes / ((size_t)B * U * 16)), B, 0, s>>>(c, a, b, sink);           \
    }},
+#define XL(U, B)                                                                                        \
+  {2, 1 + 10 * U, U, B, [](float* c, const float* a, const float* b, uint32_t* sink, size_t bytes, hipStream_t s) { \
+     stream_lds_k<U, B><<<(unsigned)(bytes / ((size_t)B * U * 16)), B, 0, s>>>(c, a, b, sink);          \
+   }},
+// pattern 9 (R2W1 u2 b512) is the product kernel's shape: bench.py times it
+// beside the product in the same run; 10-12 read through LDS-DMA (w = 1 + 10 u)
 static const P kP[] = {X(1, 0, 2, 512) X(1, 0, 4, 512) X(0, 1, 2, 512) X(0, 1, 4, 512) X(1, 1, 2, 512)
-                           X(1, 1, 4, 512) X(2, 0, 2, 512) X(2, 0, 4, 512) X(2, 1, 2, 512) X(2, 1, 4, 256)};
+                           X(1, 1, 4, 512) X(2, 0, 2, 512) X(2, 0, 4, 512) X(2, 1, 2, 512) X(2, 1, 4, 256)
+                               XL(1, 512) XL(2, 512) XL(2, 256)};
 #undef X
+#undef XL
 
 extern "C" {
 int ceil_count() { return (int)(sizeof(kP) / sizeof(kP[0])); }
