@@ -280,20 +280,57 @@ def host_staged(torch, hip, n, dev, iters=20):
     return out
 
 
-def copy_ceiling(torch, dev, nbytes=1 << 30, iters=10):
-    """Device-to-device copy of 1 GiB (torch) as a measured HBM ceiling."""
-    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
-    b = torch.empty_like(a)
-    b.copy_(a)
+CEILING_LIB = os.path.join(ROOT, "tools", "tune", "libceiling.so")
+CEILING_PATTERN = 8  # hbm_ceiling.hip kP[8]: R2W1, unroll 2, 512 lanes (the product kernel's tile)
+
+
+def stream_ceiling(torch, dev, stream, pairs, n, steps):
+    """The chip's streaming rate for config 2's access mix, measured in the
+    same run as the product kernel: the stripped kernel of
+    tools/tune/hbm_ceiling.hip with reduce_vec_kernel's tile (raw nt buffer
+    loads / stores, 16 B per lane, 512 lanes x 2 packets per stream, one tile
+    per workgroup), two reads and one write IN PLACE (dst = dst + src over the
+    same rotated 64 MiB pairs), timed exactly as the headline kernel (K
+    back-to-back launches, fence-free events after launch 1 and launch K).
+    No edge handling, no misalignment support, no dtype/op dispatch: what is
+    left is the memory system's rate for 2R + 1W."""
+    import ctypes
+    if not os.path.exists(CEILING_LIB):
+        return {"error": f"{CEILING_LIB} missing (built by __graft_entry__.build())"}
+    L = ctypes.CDLL(CEILING_LIB)
+    vp = ctypes.c_void_p
+    L.ceil_run.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_size_t, vp]
+    d4 = (ctypes.c_int * 4)()
+    L.ceil_desc(CEILING_PATTERN, d4)
+    if list(d4) != [2, 1, 2, 512] or (n * 4) % (512 * 2 * 16):
+        return {"error": f"pattern {CEILING_PATTERN} is {list(d4)}; chunk not a whole number of tiles"}
+    sink = torch.zeros(1024, dtype=torch.int32, device=dev)
+    sh = stream.cuda_stream
+
+    def launch(i):
+        d, s = pairs[i % len(pairs)]
+        rc = L.ceil_run(CEILING_PATTERN, d.data_ptr(), d.data_ptr(), s.data_ptr(), sink.data_ptr(), n * 4, sh)
+        if rc:
+            raise RuntimeError(f"ceil_run: {rc}")
+
+    for i in range(3):
+        launch(i)
     torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0, e1 = HipEvent(stream), HipEvent(stream)
+    launch(0)
     e0.record()
-    for _ in range(iters):
-        b.copy_(a)
+    for i in range(1, steps):
+        launch(i)
     e1.record()
     torch.cuda.synchronize(dev)
-    t = e0.elapsed_time(e1) / 1e3 / iters
-    return round(2.0 * nbytes / t / 1e9, 1)
+    ms = e0.elapsed_ms(e1) / (steps - 1)
+    e0.destroy()
+    e1.destroy()
+    gbs = 3.0 * n * 4 / (ms / 1e3) / 1e9
+    return {"kernel": "tools/tune/hbm_ceiling.hip stream_k<R=2, W=1, U=2, B=512> in place (stripped 2R+1W, same "
+                      "tile, cache policy and rotation as the product kernel)",
+            "kernel_avg_us": round(ms * 1e3, 3), "achieved_gbs": round(gbs, 1),
+            "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4)}
 
 
 def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
@@ -470,18 +507,14 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         return dict(partial)
     variants = {}
     partial["variants"] = variants
-    # ring_kernel runs before ring_memcpy: a ring-route executor created
-    # right after one whose sends were hipMemcpyAsync copies into the peer's
-    # same-size inbox has been seen to import the previous inbox (DESIGN.md
-    # §4, "IPC imports"); the executor refuses such a mapping, and this order
-    # keeps every variant measured
-    specs = {"ring_kernel": ("kernel", "device", "0"), "ring_memcpy": ("memcpy", "device", "0"),
+    specs = {"ring_memcpy": ("memcpy", "device", "0"), "ring_kernel": ("kernel", "device", "0"),
              "mesh_memcpy_forked": ("memcpy", "device", "1"), "mesh_host_workspace": ("auto", "host", "1")}
     chosen = (args.config3_variants.split(",") if args.config3_variants
               else ["ring_memcpy"] if args.quick else list(specs))
-    for name in chosen:
+    for k, name in enumerate(chosen):
         engine, workspace, mesh = specs[name]
-        variants[name] = ring_once(engine, workspace, mesh)
+        variants[name if name not in variants else "%s#%d" % (name, k + 1)] = ring_once(engine, workspace, mesh)
+    partial["ipc_pool"] = hip.ipc_stats()
     if args.config3_only:
         return dict(partial)
 
@@ -769,15 +802,6 @@ def main():
         d, s = pairs[i % len(pairs)]
         hip.reduce_ptr("sum", "f32", d.data_ptr(), s.data_ptr(), n, sh)
 
-    # The D2D copy ceiling reported beside the roofline is measured before
-    # the warmup (it also brings the GPU out of idle before the W warmup
-    # steps run), not after the timed region.
-    ceiling = None
-    if world == 1:
-        try:
-            ceiling = copy_ceiling(torch, dev)
-        except RuntimeError as e:  # pragma: no cover
-            ceiling = f"unavailable: {e}"
     progress(f"config 2: {args.warmup} warmup + {args.steps} timed steps")
     for i in range(args.warmup):
         step(i)
@@ -827,6 +851,15 @@ def main():
         per_rank_kernel_ms = [kern_ms]
     tmax = float(t_local[0])
 
+    # the access mix's streaming ceiling, same run, same buffers, after the
+    # timed region (in the driver-run line)
+    ceiling = None
+    if world == 1 and args.steps >= 2:
+        try:
+            ceiling = stream_ceiling(torch, dev, stream, pairs, n, args.steps)
+        except (OSError, RuntimeError) as e:  # pragma: no cover
+            ceiling = {"error": repr(e)}
+
     alg_bytes = 3.0 * n * 4                       # 2 reads + 1 write per element
     value = world * args.steps * alg_bytes / tmax / GIB
     achieved_gbs = alg_bytes / (kern_ms / 1e3) / 1e9
@@ -866,7 +899,10 @@ def main():
             "kernel_gib_s": round(alg_bytes / (kern_ms / 1e3) / GIB, 2),
         }
         if world == 1:
-            out["hbm_copy_ceiling_gbs"] = ceiling
+            if ceiling and "achieved_gbs" in ceiling:
+                out["roofline"]["ceiling_gbs"] = ceiling["achieved_gbs"]
+                out["roofline"]["frac_of_ceiling"] = round(achieved_gbs / ceiling["achieved_gbs"], 4)
+            out["roofline"]["ceiling"] = ceiling
             if not args.no_host_staged:
                 out["host_staged"] = host_staged(torch, hip, n, dev)
             if not args.no_cpu:

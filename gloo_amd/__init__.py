@@ -240,6 +240,7 @@ def _bind_collectives(L):
                                                     ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp), ctypes.c_int,
                                                     ctypes.c_int, ctypes.POINTER(vp)]
     L.gloo_hip_algorithm_set_streams.argtypes = [vp, ctypes.POINTER(vp), ctypes.c_int]
+    L.gloo_hip_ipc_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     L.gloo_hip_algorithm_run.argtypes = [vp]
     L.gloo_hip_algorithm_destroy.argtypes = [vp]
     L.gloo_hip_algorithm_wait_seconds.argtypes = [vp]
@@ -256,13 +257,23 @@ EXPORTED = EXPORTED + ("gloo_hip_context_create", "gloo_hip_context_create_ex", 
                        "gloo_hip_algorithm_destroy", "gloo_hip_algorithm_wait_seconds",
                        "gloo_hip_algorithm_set_profiling", "gloo_hip_algorithm_stats",
                        "gloo_hip_algorithm_mode", "gloo_hip_algorithm_create_ws", "gloo_hip_context_mode",
-                       "gloo_hip_algorithm_create_streams", "gloo_hip_algorithm_set_streams")
+                       "gloo_hip_algorithm_create_streams", "gloo_hip_algorithm_set_streams", "gloo_hip_ipc_stats")
 # the xGMI transport's bound buffers (gloo_amd/include/gloo_amd/gloo_transport.h)
 EXPORTED = EXPORTED + ("gloo_hip_context_create_kv", "gloo_hip_transport_create", "gloo_hip_transport_destroy",
                        "gloo_hip_buffer_create", "gloo_hip_buffer_destroy", "gloo_hip_buffer_send",
                        "gloo_hip_buffer_wait_recv", "gloo_hip_buffer_wait_send")
 
 WORKSPACES = {"device": 0, "host": 1}
+
+
+def ipc_stats():
+    """This process's IPC slab pool (gloo_amd/include/gloo_amd/ipc.h): slabs
+    exported (never freed while the process lives) and their bytes, slabs free
+    for reuse, peer slabs mapped, hipIpcOpenMemHandle calls made."""
+    out = (ctypes.c_uint64 * 5)()
+    _check(lib.gloo_hip_ipc_stats(out))
+    return {"slabs": out[0], "slab_bytes": out[1], "free": out[2], "peer_slabs_mapped": out[3],
+            "ipc_opens": out[4]}
 
 
 def _mode_dict(out):

@@ -9,6 +9,7 @@
 #include "gloo_amd/context.h"
 #include "gloo_amd/errors.h"
 #include "gloo_amd/executor.h"
+#include "gloo_amd/ipc.h"
 #include "gloo_amd/transport.h"
 
 struct gloo_hip_context {
@@ -168,6 +169,18 @@ int gloo_hip_algorithm_create(gloo_hip_context_t ctx, int algo, int op, int dtyp
                               gloo_hip_algorithm_t* out) {
   return gloo_hip_algorithm_create_ws(ctx, algo, op, dtype, ptrs, nptrs, count, recv_elems, stream,
                                       GLOO_HIP_WORKSPACE_DEVICE, out);
+}
+
+int gloo_hip_ipc_stats(uint64_t* out) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(out, "null argument");
+    const gloo_amd::ipc::Stats st = gloo_amd::ipc::stats();
+    out[0] = st.slabs;
+    out[1] = st.slabBytes;
+    out[2] = st.free;
+    out[3] = st.imports;
+    out[4] = st.opens;
+  });
 }
 
 int gloo_hip_algorithm_run(gloo_hip_algorithm_t a) {

@@ -22,6 +22,7 @@
 
 #include "gloo_amd.h"
 #include "gloo_amd/common.h"
+#include "gloo_amd/ipc.h"
 #include "gloo_amd/signal.h"
 
 namespace gloo_amd {
@@ -42,6 +43,9 @@ struct ArenaRecord {
   hipIpcMemHandle_t mailboxHandle;
   int32_t interpSlices;      // slices this rank could run its plan in (0: no sliced interpreter)
   uint64_t nonce;            // written at the start of a DEVICE arena: the importer checks its mapping
+  uint64_t mailboxNonce;     // written behind the mailbox's counters: likewise
+  uint64_t incarnation;      // ipc::incarnation() of the exporting process
+  uint64_t mailboxBytes;
 };
 
 // A value no earlier arena of this process or its peers is likely to hold.
@@ -428,47 +432,8 @@ Plan planFor(int algo, int rank, int size, size_t count, int nin, int nout, size
   return makePlan(algo, rank, size, count, nout, recvElems);
 }
 
+// The text of a failed import check (tests and tools look for it).
 constexpr const char* kStaleImport = "does not show its contents";
-
-// Freed device inbox arenas wait here before hipFree, so the next arena of
-// this process does not come back at an address a peer process imported
-// moments ago.  On ROCm 7 / MI355X with rank processes on one GPU, an import
-// of an arena at such an address was handed the earlier arena's mapping
-// (contents, or the runtime's record of its size) even after the peer had
-// closed it ("IPC imports").  Bounded by count and bytes; the
-// oldest is freed first.
-class ArenaQuarantine {
- public:
-  static ArenaQuarantine& get() {
-    static ArenaQuarantine* q = new ArenaQuarantine();  // never destroyed: process exit frees device memory
-    return *q;
-  }
-  void retire(void* p, size_t bytes) {
-    std::lock_guard<std::mutex> lk(m_);
-    static const bool off = [] {
-      const char* e = std::getenv("GLOO_AMD_QUARANTINE");
-      return e && e[0] == '0';
-    }();
-    if (off) {  // diagnosis: free at once
-      GLOO_AMD_HIP_RELEASE(hipFree(p));
-      return;
-    }
-    held_.push_back({p, bytes});
-    total_ += bytes;
-    while (!held_.empty() && (held_.size() > kMaxArenas || total_ > kMaxBytes)) {
-      GLOO_AMD_HIP_RELEASE(hipFree(held_.front().first));
-      total_ -= held_.front().second;
-      held_.pop_front();
-    }
-  }
-
- private:
-  static constexpr size_t kMaxArenas = 8;
-  static constexpr size_t kMaxBytes = size_t(4) << 30;
-  std::mutex m_;
-  std::deque<std::pair<void*, size_t>> held_;
-  size_t total_ = 0;
-};
 }  // namespace
 
 void PlanExecutor::setBuffers(const std::vector<void*>& inputs, const std::vector<void*>& outputs) {
@@ -678,6 +643,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     peers_[peer].device = w[1];
     if (w[0] == ctx_->pid() && w[1] == ctx_->device()) sharesDeviceInProcess = true;
     if (recvPeers.count(peer) && (w[1] != ctx_->device() || w[0] != ctx_->pid())) crossSender = true;
+    if (w[0] != ctx_->pid()) crossProcess_ = true;
   }
   const char* sig = std::getenv("GLOO_AMD_SIGNAL");
   const std::string sigMode = sig ? sig : "auto";
@@ -697,19 +663,21 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   hostArena_ = workspace == GLOO_HIP_WORKSPACE_HOST || arMode == "host";
   fineArena_ = !hostArena_ && (arMode == "fine" || (arMode == "auto" && crossSender));
 
-  // Phase 2: the inbox arena.
-  // Whole 2 MiB granules: an importer's runtime may keep its record of an
-  // earlier arena that sat at the same address (ROCm 7, two rank processes
-  // on one MI355X: a 64 KiB arena imported as the 32 KiB one before it,
-  // after close and re-open; profiles/round2/r2zx_*, r2zz2_*).  With every
-  // arena a multiple of the granule, a reused address comes back at the
-  // same size class and the record spans the new arena.
+  // Phase 2: the inbox arena.  Whole 2 MiB granules.  When a peer in
+  // another process maps it, it is a slab of the process-wide IPC pool
+  // (ipc.h): exported once, never freed while the process lives, so an
+  // address a peer has imported always maps these pages (a freed and
+  // re-exported block of the same size at the same address was imported as
+  // the OLD block's pages: DESIGN.md §4, profiles/round3/r3b_*).
   constexpr size_t kArenaGranule = 2u << 20;
   const size_t arenaBytes = (std::max<size_t>(256, plan_.arena * es_) + kArenaGranule - 1) / kArenaGranule * kArenaGranule;
   arenaBytes_ = arenaBytes;
   if (hostArena_) {
     arenaShm_ = HostShm::create(arenaBytes);
     arena_ = static_cast<char*>(arenaShm_->dev);
+  } else if (crossProcess_) {
+    arenaSlab_ = ipc::acquire(ctx_->device(), arenaBytes, fineArena_);
+    arena_ = arenaSlab_->ptr;
   } else if (fineArena_) {
     GLOO_AMD_HIP_ALLOC(hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), arenaBytes,
                                              hipDeviceMallocFinegrained));
@@ -720,12 +688,25 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   // memory that the peers write over xGMI: one 64-bit counter per
   // (sender, slot).  Measured on MI355X: a cross-rank hop costs about 1 us
   // this way against about 2.4 us through the host control block
-  // (tools/pingpong.cc, profiles/round1/r1q_pingpong.jsonl).
+  // (tools/pingpong.cc, profiles/round1/r1q_pingpong.jsonl).  Shared with
+  // other processes, it is a pool slab too, and a nonce behind the counters
+  // lets every importer check its mapping.
+  size_t mbBytes = 0;
+  uint64_t mbNonce = 0;
   if (deviceSignal_ && mailboxesEnabled()) {
     // one word per (sender, slot, slice): slices of the sliced interpreter
-    const size_t mbBytes = ((size_t)P * GLOO_HIP_NUM_SLOTS * kMaxSlices * sizeof(uint64_t) + 4095) / 4096 * 4096;
-    GLOO_AMD_HIP_ALLOC(hipExtMallocWithFlags(reinterpret_cast<void**>(&mailbox_), mbBytes, hipDeviceMallocFinegrained));
+    mbBytes = ((size_t)P * GLOO_HIP_NUM_SLOTS * kMaxSlices * sizeof(uint64_t) + 4095) / 4096 * 4096;
+    if (crossProcess_) {
+      mailboxSlab_ = ipc::acquire(ctx_->device(), mbBytes + 4096, true);
+      mailbox_ = reinterpret_cast<uint64_t*>(mailboxSlab_->ptr);
+    } else {
+      GLOO_AMD_HIP_ALLOC(hipExtMallocWithFlags(reinterpret_cast<void**>(&mailbox_), mbBytes + 4096,
+                                               hipDeviceMallocFinegrained));
+    }
     GLOO_AMD_HIP_CHECK(hipMemsetAsync(mailbox_, 0, mbBytes, stream_));
+    mbNonce = arenaNonce();
+    GLOO_AMD_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<char*>(mailbox_) + mbBytes, &mbNonce, sizeof(mbNonce),
+                                      hipMemcpyHostToDevice, stream_));
     GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
   }
   // Interpreter (executor.h): the knobs every rank reads alike, and this
@@ -792,17 +773,20 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
                    (unsigned long long)rec.nonce, times, diagProbe(arena_, stream_).c_str());
     }
   }
+  rec.incarnation = ipc::incarnation();
   if (mailbox_) {
     rec.hasMailbox = 1;
     rec.mailboxPtr = reinterpret_cast<uint64_t>(mailbox_);
-    GLOO_AMD_HIP_ALLOC(hipIpcGetMemHandle(&rec.mailboxHandle, mailbox_));
+    rec.mailboxBytes = mbBytes;
+    rec.mailboxNonce = mbNonce;
+    if (mailboxSlab_) rec.mailboxHandle = mailboxSlab_->handle;
   }
   if (hostArena_) {
     rec.host = 1;
     GLOO_AMD_ENFORCE(arenaShm_->name.size() < sizeof(rec.shm), "shm name too long");
     std::memcpy(rec.shm, arenaShm_->name.c_str(), arenaShm_->name.size() + 1);
-  } else {
-    GLOO_AMD_HIP_ALLOC(hipIpcGetMemHandle(&rec.handle, arena_));
+  } else if (arenaSlab_) {
+    rec.handle = arenaSlab_->handle;  // exported once, when the pool allocated the slab
   }
   std::vector<char> blob(sizeof(rec));
   std::memcpy(blob.data(), &rec, sizeof(rec));
@@ -836,8 +820,14 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
           (void)hipGetLastError();
         }
       } else {
-        void* p = nullptr;
-        GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&p, pr.mailboxHandle, hipIpcMemLazyEnablePeerAccess));
+        void* p = ipc::import(pr.pid, pr.incarnation, pr.mailboxPtr, pr.mailboxBytes + 4096, pr.mailboxHandle);
+        uint64_t seen = 0;
+        GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, static_cast<char*>(p) + pr.mailboxBytes, sizeof(seen),
+                                          hipMemcpyDeviceToHost, stream_));
+        GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+        GLOO_AMD_ENFORCE(seen == pr.mailboxNonce, "rank ", me, ": the IPC mapping of rank ", peer, "'s mailbox (",
+                         (void*)pr.mailboxPtr, " in pid ", pr.pid, ", mapped at ", p, ") ", kStaleImport, ": read ",
+                         seen, ", expected ", pr.mailboxNonce);
         peerMailbox_[peer] = static_cast<uint64_t*>(p);
         peerMailboxIpc_[peer] = true;
       }
@@ -856,73 +846,35 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
         (void)hipGetLastError();
       }
     } else {
-      void* p = nullptr;
-      // The mapping must show the peer's CURRENT arena.  Measured on MI355X /
-      // ROCm 7 with two rank processes on one GPU (bench.py's config-3
-      // variants back to back, tests/test_bench_gpu.py): after a ring-route
-      // executor had written its peer's inbox with hipMemcpyAsync and was
-      // destroyed, an import of the peer's next inbox could show the
-      // previous inbox's final contents, so every message would have gone
-      // there while the signals still arrived.  The nonce the owner wrote
-      // at the arena's start tells; a stale import is closed and opened
-      // again, and a mapping that never shows the nonce is an error, never
-      // a silent misdelivery.
-      // The runtime's record of the mapping must also span the whole arena:
-      // a mapping the runtime sizes as an earlier, smaller allocation at the
-      // same address lets the nonce through and then fails every copy past
-      // that size with "invalid argument" (seen in bench.py's 2-rank
-      // rehearsal, HD sweep, eager variants: profiles/round2/r2zx_*).
+      // Another process's pool slab (ipc.h): mapped once, kept.  The mapping
+      // must show the nonce the owner just wrote at the slab's start, and
+      // the runtime's record of it must span the arena; anything else is a
+      // hard error, never a silent misdelivery.
+      void* p = ipc::import(pr.pid, pr.incarnation, pr.ptr, pr.bytes, pr.handle);
       uint64_t seen = 0;
-      size_t mapped = 0;
-      for (int attempt = 0;; attempt++) {
-        GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&p, pr.handle, hipIpcMemLazyEnablePeerAccess));
-        GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, p, sizeof(seen), hipMemcpyDeviceToHost, stream_));
-        GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
-        if (ipcDiag()) {
-          const std::string hx = handleHex(pr.handle);
-          int hTimes, vTimes;
-          {
-            DiagLog& d = DiagLog::get();
-            std::lock_guard<std::mutex> lk(d.m);
-            hTimes = d.handles[hx]++;
-            vTimes = d.mapped[p]++;
-          }
-          std::fprintf(stderr, "[ipc-diag %d r%d inst%llu] import rank %d arena %p %llu B (pid %d) -> %p attempt %d: "
-                       "seen %llx want %llx (handle opened %d times before, address handed out %d times before)%s%s\n",
-                       ctx_->pid(), me, (unsigned long long)inst_, peer, (void*)pr.ptr, (unsigned long long)pr.bytes,
-                       pr.pid, p, attempt, (unsigned long long)seen, (unsigned long long)pr.nonce, hTimes, vTimes,
-                       seen == pr.nonce ? "" : " MISMATCH: ",
-                       seen == pr.nonce ? "" : diagProbe(p, stream_).c_str());
-        }
+      GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, p, sizeof(seen), hipMemcpyDeviceToHost, stream_));
+      GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+      size_t mapped = pr.bytes;
+      {
         void* rb = nullptr;
         size_t rs = 0;
-        if (hipMemGetAddressRange(&rb, &rs, p) == hipSuccess && rb) {
-          // bytes the runtime maps from p on (p may sit inside the range)
+        if (hipMemGetAddressRange(&rb, &rs, p) == hipSuccess && rb)
           mapped = static_cast<char*>(rb) + rs > static_cast<char*>(p)
                        ? (size_t)(static_cast<char*>(rb) + rs - static_cast<char*>(p)) : 0;
-        } else {
-          (void)hipGetLastError();
-          mapped = pr.bytes;  // the runtime cannot tell: rely on the nonce
-        }
-        if ((seen == pr.nonce && mapped >= pr.bytes) || attempt == 4) break;
-        GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(p));
-        GLOO_AMD_HIP_CHECK(hipDeviceSynchronize());
-        std::this_thread::sleep_for(std::chrono::milliseconds(2 << attempt));
+        (void)hipGetLastError();
       }
+      if (ipcDiag())
+        std::fprintf(stderr, "[ipc-diag %d r%d inst%llu] import rank %d arena %p %llu B (pid %d) -> %p: seen %llx "
+                     "want %llx%s%s\n", ctx_->pid(), me, (unsigned long long)inst_, peer, (void*)pr.ptr,
+                     (unsigned long long)pr.bytes, pr.pid, p, (unsigned long long)seen,
+                     (unsigned long long)pr.nonce, seen == pr.nonce ? "" : " MISMATCH: ",
+                     seen == pr.nonce ? "" : diagProbe(p, stream_).c_str());
       peers_[peer].base = static_cast<char*>(p);
       peers_[peer].ipc = true;
-      if (seen != pr.nonce || mapped < pr.bytes) {
-        const unsigned char* hb = reinterpret_cast<const unsigned char*>(&pr.handle);
-        std::string hex;
-        char t[3];
-        for (size_t i = 0; i < sizeof(pr.handle); i++) {
-          std::snprintf(t, sizeof(t), "%02x", hb[i]);
-          hex += t;
-        }
-        GLOO_AMD_ENFORCE(false, "rank ", me, ": the IPC mapping of rank ", peer, "'s inbox arena (", (void*)pr.ptr,
-                         ", ", pr.bytes, " B, in pid ", pr.pid, ", mapped at ", p, ") ", kStaleImport, ": read ",
-                         seen, ", expected ", pr.nonce, "; the runtime maps ", mapped, " B there; handle ", hex);
-      }
+      GLOO_AMD_ENFORCE(seen == pr.nonce && mapped >= pr.bytes, "rank ", me, ": the IPC mapping of rank ", peer,
+                       "'s inbox arena (", (void*)pr.ptr, ", ", pr.bytes, " B, in pid ", pr.pid, ", mapped at ", p,
+                       ") ", kStaleImport, ": read ", seen, ", expected ", pr.nonce, "; the runtime maps ", mapped,
+                       " B there; handle ", handleHex(pr.handle));
     }
     const Plan theirs = planFor(planAlgo_, peer, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
     for (const Step& d : theirs.steps)
@@ -998,25 +950,14 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   }
   const auto ready = ctx_->allgather(strcat_("inst", inst_, "/ready"),
                                      std::vector<char>(setupReason.begin(), setupReason.end()));
-  bool anyFailed = false, allStale = true;
-  for (int r = 0; r < P; r++) {
-    if (ready[r].empty()) continue;
-    anyFailed = true;
-    allStale = allStale && std::string(ready[r].begin(), ready[r].end()).find(kStaleImport) != std::string::npos;
-  }
+  bool anyFailed = false;
+  for (int r = 0; r < P; r++) anyFailed = anyFailed || !ready[r].empty();
   if (anyFailed) {
     // the destructor will not run: release what this rank set up.  Every
     // rank saw the same ready records and fails here together, so the
-    // tear-down barrier (no arena is freed while a peer maps it) is
+    // tear-down barrier (no arena is reused while a peer writes it) is
     // collective as in the destructor.
     release();
-    if (allStale) {
-      // every rank decides alike (the same ready records): a collective retry
-      // with new arenas can succeed (capi.cc makeExecutor)
-      for (int r = 0; r < P; r++)
-        if (!ready[r].empty())
-          throw StaleImport(strcat_("rank ", r, ": ", std::string(ready[r].begin(), ready[r].end())));
-    }
     if (setupFailure) std::rethrow_exception(setupFailure);
     for (int r = 0; r < P; r++)
       GLOO_AMD_ENFORCE(ready[r].empty(), "rank ", r, " could not set up its side of the collective: ",
@@ -1038,27 +979,31 @@ void PlanExecutor::release() {
     if (graphExec_) (void)hipGraphExecDestroy(graphExec_);
     graphExec_ = nullptr;
     if (ctx_->size > 1) {
+      // IPC imports stay mapped (ipc.h: the process-wide import cache);
+      // nobody reuses or frees an arena a peer may still write
       for (auto& p : peers_)
-        if (p.ipc && p.base) {
-          if (ipcDiag())
-            std::fprintf(stderr, "[ipc-diag %d r%d inst%llu] close %p\n", ctx_->pid(), ctx_->rank,
-                         (unsigned long long)inst_, (void*)p.base);
-          GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(p.base));
-        }
-      peers_.clear();
+        if (p.ipc) ipc::unimport(p.base);
       for (size_t q = 0; q < peerMailbox_.size(); q++)
-        if (peerMailboxIpc_[q] && peerMailbox_[q]) GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(peerMailbox_[q]));
+        if (peerMailboxIpc_[q]) ipc::unimport(peerMailbox_[q]);
+      peers_.clear();
       peerMailbox_.clear();
-      // nobody may free an arena a peer still maps
       ctx_->barrier(strcat_("inst", inst_, "/closed"));
       peerShm_.clear();
       if (arenaShm_) {
         arenaShm_.reset();
+      } else if (arenaSlab_) {
+        ipc::release(arenaSlab_);  // back to the pool, never freed
       } else if (arena_) {
-        ArenaQuarantine::get().retire(arena_, arenaBytes_);
+        GLOO_AMD_HIP_RELEASE(hipFree(arena_));  // never exported
       }
+      arenaSlab_ = nullptr;
       arena_ = nullptr;
-      if (mailbox_) GLOO_AMD_HIP_RELEASE(hipFree(mailbox_));
+      if (mailboxSlab_) {
+        ipc::release(mailboxSlab_);
+      } else if (mailbox_) {
+        GLOO_AMD_HIP_RELEASE(hipFree(mailbox_));
+      }
+      mailboxSlab_ = nullptr;
       mailbox_ = nullptr;
     }
     for (hipEvent_t e : events_) (void)hipEventDestroy(e);

@@ -1,0 +1,163 @@
+// ipc.cc — see gloo_amd/ipc.h.
+#include "gloo_amd/ipc.h"
+
+#include <unistd.h>
+
+#include <cstdlib>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <tuple>
+#include <vector>
+
+#include "gloo_amd/common.h"
+
+namespace gloo_amd {
+namespace ipc {
+namespace {
+
+constexpr size_t kGranule = size_t(2) << 20;
+
+size_t sizeClass(size_t bytes) {
+  size_t c = kGranule;
+  while (c < bytes) c <<= 1;
+  return c;
+}
+
+struct Pool {
+  std::mutex m;
+  std::vector<std::unique_ptr<Slab>> slabs;  // every slab ever exported (never freed)
+  std::vector<Slab*> free;
+  struct Mapping {
+    uint64_t incarnation;
+    void* ptr;
+    size_t bytes;
+  };
+  std::map<std::pair<int, uint64_t>, Mapping> imports;  // (pid, exporter address)
+  size_t opens = 0;
+  static Pool& get() {
+    static Pool* p = new Pool();  // never destroyed: process exit releases device memory
+    return *p;
+  }
+};
+
+}  // namespace
+
+bool poolEnabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("GLOO_AMD_IPC_POOL");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+uint64_t incarnation() {
+  static const uint64_t v = [] {
+    std::random_device rd;
+    return ((uint64_t)rd() << 32 ^ rd()) ^ ((uint64_t)::getpid() << 17) ^ 0x9e3779b97f4a7c15ull;
+  }();
+  return v;
+}
+
+Slab* acquire(int device, size_t bytes, bool fine) {
+  const size_t want = sizeClass(bytes);
+  Pool& p = Pool::get();
+  std::lock_guard<std::mutex> lk(p.m);
+  for (size_t i = 0; poolEnabled() && i < p.free.size(); i++) {
+    Slab* s = p.free[i];
+    if (s->device == device && s->fine == fine && s->bytes == want) {
+      p.free.erase(p.free.begin() + (long)i);
+      return s;
+    }
+  }
+  auto s = std::make_unique<Slab>();
+  s->bytes = want;
+  s->device = device;
+  s->fine = fine;
+  int prev = -1;
+  GLOO_AMD_HIP_CHECK(hipGetDevice(&prev));
+  GLOO_AMD_HIP_CHECK(hipSetDevice(device));
+  void* ptr = nullptr;
+  if (fine) {
+    GLOO_AMD_HIP_ALLOC(hipExtMallocWithFlags(&ptr, want, hipDeviceMallocFinegrained));
+  } else {
+    GLOO_AMD_HIP_ALLOC(hipMalloc(&ptr, want));
+  }
+  s->ptr = static_cast<char*>(ptr);
+  const hipError_t e = hipIpcGetMemHandle(&s->handle, ptr);
+  if (e != hipSuccess) {
+    (void)hipFree(ptr);  // never exported: safe to free
+    (void)hipSetDevice(prev);
+    GLOO_AMD_HIP_ALLOC(e);
+  }
+  (void)hipSetDevice(prev);
+  p.slabs.push_back(std::move(s));
+  return p.slabs.back().get();
+}
+
+void release(Slab* s) {
+  if (!s) return;
+  Pool& p = Pool::get();
+  std::lock_guard<std::mutex> lk(p.m);
+  if (poolEnabled()) {
+    p.free.push_back(s);
+    return;
+  }
+  // diagnosis (GLOO_AMD_IPC_POOL=0): free at once, as before the pool
+  for (size_t i = 0; i < p.slabs.size(); i++)
+    if (p.slabs[i].get() == s) {
+      GLOO_AMD_HIP_RELEASE(hipFree(s->ptr));
+      p.slabs.erase(p.slabs.begin() + (long)i);
+      return;
+    }
+}
+
+void unimport(void* mapped) {
+  if (poolEnabled() || !mapped) return;  // mappings of pool slabs are kept
+  Pool& p = Pool::get();
+  std::lock_guard<std::mutex> lk(p.m);
+  for (auto it = p.imports.begin(); it != p.imports.end(); ++it)
+    if (it->second.ptr == mapped) {
+      GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(mapped));
+      p.imports.erase(it);
+      return;
+    }
+}
+
+void* import(int pid, uint64_t inc, uint64_t ptr, size_t bytes, const hipIpcMemHandle_t& handle) {
+  Pool& p = Pool::get();
+  std::lock_guard<std::mutex> lk(p.m);
+  const auto key = std::make_pair(pid, ptr);
+  auto it = p.imports.find(key);
+  if (it != p.imports.end()) {
+    if (it->second.incarnation == inc && poolEnabled()) {
+      GLOO_AMD_ENFORCE(it->second.bytes >= bytes, "slab of pid ", pid, " at ", (void*)ptr, " imported at ",
+                       it->second.bytes, " B, now published at ", bytes, " B");
+      return it->second.ptr;
+    }
+    // a new process reusing a dead one's pid: its mapping is of no use
+    GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(it->second.ptr));
+    p.imports.erase(it);
+  }
+  void* m = nullptr;
+  GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&m, handle, hipIpcMemLazyEnablePeerAccess));
+  p.opens++;
+  p.imports[key] = {inc, m, bytes};
+  return m;
+}
+
+Stats stats() {
+  Pool& p = Pool::get();
+  std::lock_guard<std::mutex> lk(p.m);
+  Stats s;
+  s.slabs = p.slabs.size();
+  for (const auto& x : p.slabs) s.slabBytes += x->bytes;
+  s.free = p.free.size();
+  s.imports = p.imports.size();
+  s.opens = p.opens;
+  return s;
+}
+
+}  // namespace ipc
+}  // namespace gloo_amd

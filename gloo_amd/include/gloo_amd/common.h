@@ -19,12 +19,6 @@ struct Exception : std::runtime_error {
 struct EnforceNotMet : Exception {
   explicit EnforceNotMet(const std::string& m) : Exception(m) {}
 };
-// Thrown on EVERY rank of a collective construction when each rank that
-// failed was refused an IPC mapping of a peer's inbox (executor.cc): a fresh
-// construction gets fresh arenas, so callers may retry it collectively.
-struct StaleImport : EnforceNotMet {
-  explicit StaleImport(const std::string& m) : EnforceNotMet(m) {}
-};
 // Transport failures and timeouts (gloo::IoException).
 struct IoException : Exception {
   explicit IoException(const std::string& m) : Exception(m) {}

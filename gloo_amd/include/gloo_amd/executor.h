@@ -68,6 +68,7 @@
 
 #include "gloo_amd/common.h"
 #include "gloo_amd/context.h"
+#include "gloo_amd/ipc.h"
 #include "gloo_amd/plan.h"
 #include "gloo_amd/signal.h"
 
@@ -103,20 +104,9 @@ class PlanExecutor {
   void setStreams(const std::vector<hipStream_t>& streams);
   ~PlanExecutor();
 
-  // Construct with up to `retries` collective retries after a StaleImport
-  // (common.h): every rank throws it together, so every rank retries
-  // together, and each attempt maps fresh arenas.
   template <typename... Args>
   static std::unique_ptr<PlanExecutor> create(Args&&... args) {
-    const char* e = std::getenv("GLOO_AMD_STALE_RETRIES");
-    const int retries = e ? std::atoi(e) : 2;
-    for (int attempt = 0;; attempt++) {
-      try {
-        return std::unique_ptr<PlanExecutor>(new PlanExecutor(args...));
-      } catch (const StaleImport&) {
-        if (attempt >= retries) throw;
-      }
-    }
+    return std::unique_ptr<PlanExecutor>(new PlanExecutor(std::forward<Args>(args)...));
   }
   PlanExecutor(const PlanExecutor&) = delete;
   PlanExecutor& operator=(const PlanExecutor&) = delete;
@@ -202,6 +192,9 @@ class PlanExecutor {
   Plan plan_;
   uint64_t inst_;
   char* arena_ = nullptr;       // device-visible address of this rank's inboxes
+  bool crossProcess_ = false;   // a plan peer lives in another process: arena and mailbox are IPC pool slabs
+  ipc::Slab* arenaSlab_ = nullptr;
+  ipc::Slab* mailboxSlab_ = nullptr;
   size_t arenaBytes_ = 0;       // its allocated size (whole 2 MiB granules)
   bool hostArena_ = false;      // inboxes in shared pinned host memory (HOST workspace)
   struct HostShm;

@@ -1,0 +1,72 @@
+// ipc.h — device memory shared between rank processes over HIP IPC.
+//
+// Why this exists ("IPC imports"): on ROCm 7 / MI355X an import
+// of a handle that is byte-identical to an earlier one — the exporter freed a
+// block and its next block of the same size came back at the same address,
+// and a HIP IPC handle encodes (address, pid, size) — was handed the EARLIER
+// import's mapping, i.e. the freed block's pages, after the importer had
+// closed it (profiles/round3/r3b_*: every read path through the mapping, the
+// runtime's copy and the GPU's own loads alike, showed the old contents).
+// Freeing and re-exporting a block is therefore never safe while any peer
+// process lives.  So:
+//
+//   Exporter side: every block that another process maps is a Slab from a
+//   process-wide pool.  A slab is allocated and exported ONCE and never freed
+//   while the process lives; an executor that no longer needs it returns it
+//   to the pool, and the next executor needing that size class on that device
+//   reuses it.  An address a peer has imported therefore always maps the
+//   same pages, and a byte-identical handle always means the same memory.
+//   Size classes are powers of two of 2 MiB granules, so the pool holds at
+//   most about twice the largest set of simultaneously live arenas.
+//
+//   Importer side: a mapping is opened once per (exporter pid, exporter
+//   incarnation, exporter address) and kept — never closed while the
+//   importer lives (the exporter never frees it, so it never goes stale).
+//   The incarnation (a random word per process) tells a new process that
+//   reuses a dead one's pid apart; its old mappings are closed first.
+//
+// Callers still verify each import (executor.cc writes a nonce at the slab's
+// start and every importer reads it back): a mismatch is a hard error.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace gloo_amd {
+namespace ipc {
+
+struct Slab {
+  char* ptr = nullptr;
+  size_t bytes = 0;  // the size class (>= what was asked for)
+  int device = -1;
+  bool fine = false;  // fine-grained (cross-device coherent) memory
+  hipIpcMemHandle_t handle;
+};
+
+// A random word fixed for the life of this process.
+uint64_t incarnation();
+
+// A slab of at least `bytes` on `device` (fine-grained or not), exported.
+Slab* acquire(int device, size_t bytes, bool fine);
+// Back to the pool (never hipFree'd).  The caller has made sure no peer
+// still writes into it (the executor's tear-down barrier).
+void release(Slab* s);
+
+// The mapping of a peer process's slab (opened once, kept).
+void* import(int pid, uint64_t incarnation, uint64_t ptr, size_t bytes, const hipIpcMemHandle_t& handle);
+// A no-op with the pool on.  GLOO_AMD_IPC_POOL=0 (diagnosis only) restores
+// the behaviour the pool replaced: release() frees the slab at once and
+// unimport() closes the mapping (tools/ipc_bisect.sh reproduces the stale
+// import with it).
+void unimport(void* mapped);
+bool poolEnabled();
+
+struct Stats {
+  size_t slabs = 0, slabBytes = 0, free = 0, imports = 0, opens = 0;
+};
+Stats stats();
+
+}  // namespace ipc
+}  // namespace gloo_amd

@@ -345,6 +345,13 @@ int gloo_hip_algorithm_create_streams(gloo_hip_context_t ctx, int algo, int op, 
 int gloo_hip_algorithm_set_streams(gloo_hip_algorithm_t algo, const gloo_hip_stream_t* streams, int nstreams);
 
 int gloo_hip_algorithm_run(gloo_hip_algorithm_t algo);
+
+/* This process's IPC slab pool (gloo_amd/include/gloo_amd/ipc.h; no
+ * reference counterpart, for tests and tools): out5[0] = slabs exported
+ * (never freed while the process lives), [1] = their bytes, [2] = slabs
+ * free for reuse, [3] = peer slabs mapped, [4] = hipIpcOpenMemHandle calls
+ * made (each peer slab is opened once and kept). */
+int gloo_hip_ipc_stats(uint64_t* out5);
 int gloo_hip_algorithm_destroy(gloo_hip_algorithm_t algo);
 /* Host seconds the last run() spent blocked waiting for peers. */
 double gloo_hip_algorithm_wait_seconds(gloo_hip_algorithm_t algo);

@@ -6,10 +6,10 @@ Two rank processes on one GPU (torch.distributed gloo for the barriers).
 Executor A (ring-chunked fp32 sum, --mib per rank, the ring route) is built
 with the env of --first, run --runs times (graph replay from run 3 unless
 GLOO_AMD_GRAPH=0), optionally with profiling, destroyed; executor B (the
-same size, kernel copies) is built next.  With GLOO_AMD_QUARANTINE=0 the
+same size, kernel copies) is built next.  With GLOO_AMD_IPC_POOL=0 the
 peer's arena of B comes back at A's address; B's construction reports
 whether its imports showed the peer's nonce (the executor's check), with no
-retry (GLOO_AMD_STALE_RETRIES=0).  One JSON line per rank.
+retry.  One JSON line per rank.
 
   python tools/ipc_bisect.py --first COPY=memcpy,GRAPH=1 --runs 3 --profile 0
 """

@@ -1,7 +1,7 @@
 #!/bin/bash
 # DIAGNOSIS ONLY: tools/ipc_bisect.py over a matrix of first-executor settings.
 set -o pipefail
-export GLOO_AMD_QUARANTINE=0 GLOO_AMD_STALE_RETRIES=0 GLOO_AMD_RING_MESH=0
+export GLOO_AMD_RING_MESH=0 GLOO_AMD_IPC_POOL=${POOL:-0}
 out=${OUT:-gpurun_out/ipc_bisect.jsonl}
 : > "$out"
 while read -r first runs prof; do
@@ -15,5 +15,6 @@ ${CASES:-COPY=memcpy 3 0
 COPY=memcpy,GRAPH=0 3 0
 COPY=memcpy 1 0
 COPY=kernel 3 0
-COPY=memcpy 3 1}
+COPY=memcpy 3 1
+COPY=memcpy 3 2}
 CASES

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Diagnosis of stale IPC imports: bench.py's config-3 variants
-# in the order that provoked them, no collective retry, every arena export /
+# in the order that provoked them, every arena export /
 # import / close logged with probes of a failing mapping.
 # usage (GPU box): bash tools/ipc_diag.sh TAG [REPEATS] [ORDER]
 set -o pipefail
@@ -9,7 +9,7 @@ reps=${2:-2}
 order=${3:-ring_memcpy,ring_kernel,mesh_memcpy_forked,ring_kernel}
 mkdir -p gpurun_out
 for i in $(seq 1 "$reps"); do
-  GLOO_AMD_STALE_RETRIES=${GLOO_AMD_STALE_RETRIES:-0} GLOO_AMD_IPC_DIAG=1 timeout -k 10 240 \
+  GLOO_AMD_IPC_DIAG=1 timeout -k 10 240 \
     python -u bench.py --gpus 2 --steps 5 --warmup 2 --config3-only --config3-variants "$order" \
     > gpurun_out/${tag}_$i.out 2> gpurun_out/${tag}_$i.err
   rc=$?

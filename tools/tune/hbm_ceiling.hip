@@ -91,7 +91,7 @@ struct P {
   {2, 1 + 10 * U, U, B, [](float* c, const float* a, const float* b, uint32_t* sink, size_t bytes, hipStream_t s) { \
      stream_lds_k<U, B><<<(unsigned)(bytes / ((size_t)B * U * 16)), B, 0, s>>>(c, a, b, sink);          \
    }},
-// pattern 9 (R2W1 u2 b512) is the product kernel's shape: bench.py times it
+// pattern 8 (R2W1 u2 b512) is the product kernel's shape: bench.py times it
 // beside the product in the same run; 10-12 read through LDS-DMA (w = 1 + 10 u)
 static const P kP[] = {X(1, 0, 2, 512) X(1, 0, 4, 512) X(0, 1, 2, 512) X(0, 1, 4, 512) X(1, 1, 2, 512)
                            X(1, 1, 4, 512) X(2, 0, 2, 512) X(2, 0, 4, 512) X(2, 1, 2, 512) X(2, 1, 4, 256)
