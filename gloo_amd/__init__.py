@@ -261,7 +261,11 @@ EXPORTED = EXPORTED + ("gloo_hip_context_create", "gloo_hip_context_create_ex", 
 # the xGMI transport's bound buffers (gloo_amd/include/gloo_amd/gloo_transport.h)
 EXPORTED = EXPORTED + ("gloo_hip_context_create_kv", "gloo_hip_transport_create", "gloo_hip_transport_destroy",
                        "gloo_hip_buffer_create", "gloo_hip_buffer_destroy", "gloo_hip_buffer_send",
-                       "gloo_hip_buffer_wait_recv", "gloo_hip_buffer_wait_send")
+                       "gloo_hip_buffer_wait_recv", "gloo_hip_buffer_wait_send",
+                       # unbound buffers (gloo/transport/unbound_buffer.h) on the same transport
+                       "gloo_hip_ubuf_create", "gloo_hip_ubuf_destroy", "gloo_hip_ubuf_send", "gloo_hip_ubuf_recv",
+                       "gloo_hip_ubuf_wait_recv", "gloo_hip_ubuf_wait_send", "gloo_hip_ubuf_abort_wait_recv",
+                       "gloo_hip_ubuf_abort_wait_send")
 
 WORKSPACES = {"device": 0, "host": 1}
 

@@ -1,4 +1,5 @@
 // capi.cc — C-ABI over Context / PlanExecutor; no exception crosses it.
+#include <chrono>
 #include <list>
 #include <memory>
 #include <string>
@@ -27,6 +28,9 @@ struct gloo_hip_transport {
 };
 struct gloo_hip_buffer {
   std::unique_ptr<gloo_amd::transport::Buffer> buf;
+};
+struct gloo_hip_ubuf {
+  std::unique_ptr<gloo_amd::transport::UnboundBuffer> buf;
 };
 
 namespace {
@@ -328,6 +332,69 @@ int gloo_hip_buffer_wait_send(gloo_hip_buffer_t b) {
   return guarded([&] {
     GLOO_AMD_ENFORCE(b, "null buffer");
     b->buf->waitSend();
+  });
+}
+
+int gloo_hip_ubuf_create(gloo_hip_transport_t t, void* ptr, size_t size, gloo_hip_ubuf_t* out) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(t && out && (ptr || size == 0), "bad arguments");
+    auto b = std::make_unique<gloo_hip_ubuf>();
+    b->buf = std::make_unique<gloo_amd::transport::UnboundBuffer>(t->dev.get(), ptr, size);
+    *out = b.release();
+  });
+}
+
+int gloo_hip_ubuf_destroy(gloo_hip_ubuf_t b) {
+  return guarded([&] { delete b; });
+}
+
+int gloo_hip_ubuf_send(gloo_hip_ubuf_t b, int dst, uint64_t slot, size_t offset, size_t nbytes) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(b, "null buffer");
+    b->buf->send(dst, slot, offset, nbytes);
+  });
+}
+
+int gloo_hip_ubuf_recv(gloo_hip_ubuf_t b, const int* srcs, int nsrcs, uint64_t slot, size_t offset, size_t nbytes) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(b && srcs && nsrcs > 0, "bad arguments");
+    b->buf->recv(std::vector<int>(srcs, srcs + nsrcs), slot, offset, nbytes);
+  });
+}
+
+namespace {
+int waitResult(int rc, bool done) { return rc == GLOO_HIP_OK && !done ? 1 : rc; }
+}  // namespace
+
+int gloo_hip_ubuf_wait_recv(gloo_hip_ubuf_t b, int* rank, int timeout_ms) {
+  bool done = false;
+  const int rc = guarded([&] {
+    GLOO_AMD_ENFORCE(b, "null buffer");
+    done = b->buf->waitRecv(rank, std::chrono::milliseconds(timeout_ms));
+  });
+  return waitResult(rc, done);
+}
+
+int gloo_hip_ubuf_wait_send(gloo_hip_ubuf_t b, int* rank, int timeout_ms) {
+  bool done = false;
+  const int rc = guarded([&] {
+    GLOO_AMD_ENFORCE(b, "null buffer");
+    done = b->buf->waitSend(rank, std::chrono::milliseconds(timeout_ms));
+  });
+  return waitResult(rc, done);
+}
+
+int gloo_hip_ubuf_abort_wait_recv(gloo_hip_ubuf_t b) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(b, "null buffer");
+    b->buf->abortWaitRecv();
+  });
+}
+
+int gloo_hip_ubuf_abort_wait_send(gloo_hip_ubuf_t b) {
+  return guarded([&] {
+    GLOO_AMD_ENFORCE(b, "null buffer");
+    b->buf->abortWaitSend();
   });
 }
 

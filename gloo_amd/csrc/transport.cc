@@ -1,11 +1,15 @@
 // transport.cc — see transport.h.
 #include "gloo_amd/transport.h"
 
+#include <fcntl.h>
 #include <sched.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <chrono>
 #include <cstring>
+#include <limits>
+#include <random>
 #include <string>
 #include <thread>
 
@@ -23,21 +27,72 @@ struct RecvRecord {
   uint64_t ptr;     // the buffer itself (same process)
   uint64_t size;    // bytes the peer may write
   uint64_t offset;  // from the start of its allocation (IPC maps whole allocations)
-  int32_t ipc;      // handle valid
+  int32_t ipc;      // handle valid (device memory)
+  int32_t host;     // host memory: written directly within one process, as payload words across processes
+  int32_t channel;  // this buffer's channel of the transport block
+  int32_t pad;
   hipIpcMemHandle_t handle;
 };
 
-std::string recordKey(uint64_t inst, int sender, int receiver, int slot) {
+// Channel::len of a message carried in the payload words.
+constexpr uint32_t kPayloadFlag = 0x80000000u;
+
+std::string recordKey(uint64_t inst, int sender, int receiver, uint64_t slot) {
   return strcat_("gloo_amd/xgmi/", inst, "/", sender, "->", receiver, "/", slot);
+}
+
+bool isDevice(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  std::memset(&a, 0, sizeof(a));
+  const bool dev = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeDevice;
+  (void)hipGetLastError();
+  return dev;
 }
 
 void bump(void* p) { static_cast<std::atomic<uint64_t>*>(p)->fetch_add(1, std::memory_order_acq_rel); }
 
-int channel(int slot) { return ((slot % GLOO_HIP_NUM_SLOTS) + GLOO_HIP_NUM_SLOTS) % GLOO_HIP_NUM_SLOTS; }
+// A message for a host receive buffer in another process: its bytes go into
+// the channel's payload words, then the arrival is published.
+struct PayloadSend {
+  Device::Channel* ch;
+  const char* src;  // read when the stream reaches this point
+  uint32_t off, len;
+};
+void payloadSend(void* p) {
+  auto* s = static_cast<PayloadSend*>(p);
+  if (s->len) std::memcpy(s->ch->payload, s->src, s->len);
+  s->ch->off = s->off;
+  s->ch->len = kPayloadFlag | s->len;
+  s->ch->count.fetch_add(1, std::memory_order_acq_rel);
+  delete s;
+}
+
+// Polls `done` with back-off until it holds, `abort` is set (returns false)
+// or the deadline passes (IoException with `what`).
+template <typename F>
+bool pollUntil(F done, const std::atomic<bool>* abort, std::chrono::milliseconds timeout, const std::string& what) {
+  const auto deadline = std::chrono::steady_clock::now() + timeout;
+  for (uint64_t i = 0;; i++) {
+    if (done()) return true;
+    if (abort && abort->load(std::memory_order_acquire)) return false;
+    if (i < 4096) {
+      __builtin_ia32_pause();
+    } else if (i < 8192) {
+      sched_yield();
+    } else {
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    if ((i & 255) == 255 && std::chrono::steady_clock::now() > deadline)
+      throw IoException(strcat_("Timed out ", what, " after ", timeout.count(), " ms"));
+  }
+}
+
+std::atomic<uint64_t> g_staged{0};
 
 class SendBuffer : public Buffer {
  public:
-  SendBuffer(Device* dev, int peer, int slot, void* ptr, size_t size)
+  SendBuffer(Device* dev, int peer, uint64_t slot, void* ptr, size_t size)
       : Buffer(slot, ptr, size), dev_(dev), peer_(peer) {
     dev_->claim(true, peer_, slot_);
     GLOO_AMD_HIP_CHECK(hipEventCreateWithFlags(&sent_, hipEventDisableTiming));
@@ -45,6 +100,7 @@ class SendBuffer : public Buffer {
   ~SendBuffer() override {
     (void)hipEventSynchronize(sent_);
     (void)hipEventDestroy(sent_);
+    if (staging_) (void)hipHostFree(staging_);
     if (opened_) GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(opened_));
     dev_->release(true, peer_, slot_);
   }
@@ -58,9 +114,23 @@ class SendBuffer : public Buffer {
     GLOO_AMD_ENFORCE(roffset + length <= peerSize_, "send of ", length, " bytes at ", roffset, " beyond rank ", peer_,
                      "'s ", peerSize_, "-byte receive buffer (slot ", slot_, ")");
     hipStream_t s = dev_->stream();
-    if (length) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(remote_ + roffset, ptr_ + offset, length, hipMemcpyDefault, s));
-    // stream-ordered: the arrival is published only once the bytes landed
-    GLOO_AMD_HIP_CHECK(hipLaunchHostFunc(s, bump, &ctx.counter(dev_->instance(), ctx.rank, peer_, channel(slot_))));
+    if (payload_) {
+      GLOO_AMD_ENFORCE(length <= kPayloadBytes, "rank ", peer_, "'s receive buffer (slot ", slot_,
+                       ") is host memory of another process: a message carries at most ", kPayloadBytes,
+                       " bytes there, not ", length);
+      const char* src = ptr_ + offset;
+      if (length && isDevice(ptr_)) {  // stage device bytes in pinned memory first, stream-ordered
+        if (!staging_) GLOO_AMD_HIP_ALLOC(hipHostMalloc(reinterpret_cast<void**>(&staging_), kPayloadBytes, 0));
+        GLOO_AMD_HIP_CHECK(hipMemcpyAsync(staging_, src, length, hipMemcpyDeviceToHost, s));
+        src = staging_;
+      }
+      GLOO_AMD_HIP_CHECK(hipLaunchHostFunc(
+          s, payloadSend, new PayloadSend{channel_, src, (uint32_t)roffset, (uint32_t)length}));
+    } else {
+      if (length) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(remote_ + roffset, ptr_ + offset, length, hipMemcpyDefault, s));
+      // stream-ordered: the arrival is published only once the bytes landed
+      GLOO_AMD_HIP_CHECK(hipLaunchHostFunc(s, bump, &channel_->count));
+    }
     GLOO_AMD_HIP_CHECK(hipEventRecord(sent_, s));
   }
   void waitRecv() override { throw EnforceNotMet("waitRecv on a send buffer"); }
@@ -76,24 +146,27 @@ class SendBuffer : public Buffer {
     RecvRecord r;
     std::memcpy(&r, v.data(), sizeof(r));
     peerSize_ = r.size;
+    channel_ = &dev_->channel(ctx.rank, peer_, r.channel);
     if (r.size == 0) {
       remote_ = nullptr;  // a notification buffer: arrivals only
     } else if (r.pid == ctx.pid()) {
       remote_ = reinterpret_cast<char*>(r.ptr);
-      if (r.device != ctx.device()) {
+      if (!r.host && r.device != ctx.device()) {
         hipError_t e = hipDeviceEnablePeerAccess(r.device, 0);
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
         (void)hipGetLastError();
       }
+    } else if (r.host) {
+      payload_ = true;  // host memory of another process: payload words
     } else {
       GLOO_AMD_ENFORCE(r.ipc, "rank ", peer_, "'s receive buffer is not IPC-exportable");
+      // The caller's memory cannot come from the IPC slab pool (ipc.h);
+      // this import is used by eager copies only, never captured into a
+      // graph, so closing it releases it (profiles/round3/r3g_ipc_bisect_*).
       void* base = nullptr;
       GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&base, r.handle, hipIpcMemLazyEnablePeerAccess));
       opened_ = base;
       remote_ = static_cast<char*>(base) + r.offset;
-      // the runtime's record of the mapping must reach the whole buffer (an
-      // import can come back at the size of an earlier allocation at the same
-      // address: executor.cc, DESIGN.md §4 "IPC imports must also be sized right")
       void* rb = nullptr;
       size_t rs = 0;
       if (hipMemGetAddressRange(&rb, &rs, base) == hipSuccess && rb) {
@@ -110,34 +183,44 @@ class SendBuffer : public Buffer {
   Device* dev_;
   int peer_;
   bool resolved_ = false;
+  bool payload_ = false;
   char* remote_ = nullptr;
   void* opened_ = nullptr;
+  char* staging_ = nullptr;
   size_t peerSize_ = 0;
+  Device::Channel* channel_ = nullptr;
   hipEvent_t sent_ = nullptr;
 };
 
 class RecvBuffer : public Buffer {
  public:
-  RecvBuffer(Device* dev, int peer, int slot, void* ptr, size_t size)
+  RecvBuffer(Device* dev, int peer, uint64_t slot, void* ptr, size_t size)
       : Buffer(slot, ptr, size), dev_(dev), peer_(peer) {
     Context& ctx = *dev_->context();
     dev_->claim(false, peer_, slot_);
+    idx_ = dev_->allocChannel(peer_);
+    channel_ = &dev_->channel(peer_, ctx.rank, idx_);
     // baseline before the record is published, i.e. before the peer's
     // first send can land (the sender resolves the record first)
-    baseline_ = ctx.counter(dev_->instance(), peer_, ctx.rank, channel(slot_)).load(std::memory_order_acquire);
+    baseline_ = channel_->count.load(std::memory_order_acquire);
     RecvRecord r;
     std::memset(&r, 0, sizeof(r));
     r.pid = ctx.pid();
     r.device = ctx.device();
     r.ptr = reinterpret_cast<uint64_t>(ptr_);
     r.size = ptr_ ? size_ : 0;
+    r.channel = idx_;
     if (ptr_ && size_) {
-      void* base = nullptr;
-      size_t allocSize = 0;
-      if (hipMemGetAddressRange(&base, &allocSize, ptr_) == hipSuccess && base &&
-          hipIpcGetMemHandle(&r.handle, base) == hipSuccess) {
-        r.ipc = 1;
-        r.offset = (uint64_t)(ptr_ - static_cast<char*>(base));
+      if (isDevice(ptr_)) {
+        void* base = nullptr;
+        size_t allocSize = 0;
+        if (hipMemGetAddressRange(&base, &allocSize, ptr_) == hipSuccess && base &&
+            hipIpcGetMemHandle(&r.handle, base) == hipSuccess) {
+          r.ipc = 1;
+          r.offset = (uint64_t)(ptr_ - static_cast<char*>(base));
+        }
+      } else {
+        r.host = 1;
       }
       (void)hipGetLastError();
     }
@@ -145,37 +228,37 @@ class RecvBuffer : public Buffer {
     std::memcpy(blob.data(), &r, sizeof(r));
     ctx.store().set(recordKey(dev_->instance(), peer_, ctx.rank, slot_), blob);
   }
-  ~RecvBuffer() override { dev_->release(false, peer_, slot_); }
+  ~RecvBuffer() override {
+    dev_->freeChannel(peer_, idx_);
+    dev_->release(false, peer_, slot_);
+  }
 
   void send(size_t, size_t, size_t) override { throw EnforceNotMet("send on a receive buffer"); }
   void waitSend() override {}
   void waitRecv() override {
     Context& ctx = *dev_->context();
-    auto& c = ctx.counter(dev_->instance(), peer_, ctx.rank, channel(slot_));
     const uint64_t target = baseline_ + ++received_;
-    auto met = [&] { return (int64_t)(c.load(std::memory_order_acquire) - target) >= 0; };
-    const auto deadline = std::chrono::steady_clock::now() + ctx.timeout();
-    for (uint64_t i = 0; !met(); i++) {
-      if (i < 4096) {
-        __builtin_ia32_pause();
-      } else if (i < 8192) {
-        sched_yield();
-      } else {
-        std::this_thread::sleep_for(std::chrono::microseconds(20));
-      }
-      if ((i & 255) == 255 && std::chrono::steady_clock::now() > deadline)
-        throw IoException(strcat_("Timed out waiting for rank ", peer_, " (slot ", slot_, ") on rank ", ctx.rank,
-                                  " after ", ctx.timeout().count(), " ms"));
+    pollUntil([&] { return (int64_t)(channel_->count.load(std::memory_order_acquire) - target) >= 0; }, nullptr,
+              ctx.timeout(), strcat_("waiting for rank ", peer_, " (slot ", slot_, ") on rank ", ctx.rank));
+    const uint32_t len = channel_->len;
+    if (len & kPayloadFlag) {  // carried in the payload words (host buffer, sender in another process)
+      const uint32_t n = len & ~kPayloadFlag;
+      GLOO_AMD_ENFORCE(channel_->off + n <= size_, "payload beyond the receive buffer");
+      if (n) std::memcpy(ptr_ + channel_->off, channel_->payload, n);
     }
   }
 
  private:
   Device* dev_;
   int peer_;
+  int idx_ = -1;
+  Device::Channel* channel_ = nullptr;
   uint64_t baseline_ = 0, received_ = 0;
 };
 
 }  // namespace
+
+// ---- Device ------------------------------------------------------------
 
 Device::Device(std::shared_ptr<Context> ctx, hipStream_t stream) : ctx_(std::move(ctx)) {
   GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
@@ -186,39 +269,263 @@ Device::Device(std::shared_ptr<Context> ctx, hipStream_t stream) : ctx_(std::mov
     GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     ownStream_ = true;
   }
+  const size_t P = (size_t)ctx_->size;
+  blockBytes_ = 4096 + P * P * kChannels * sizeof(Channel) + P * P * kAnnouncements * sizeof(Announcement) + P * 64;
+  blockBytes_ = (blockBytes_ + 4095) / 4096 * 4096;
+  std::string name;
+  if (ctx_->rank == 0) {
+    std::random_device rd;
+    name = strcat_("/gloo_amd_t_", ctx_->pid(), "_", rd(), rd());
+    const int fd = ::shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+    GLOO_AMD_ENFORCE(fd >= 0, "shm_open(create) failed for ", name);
+    const bool ok = ::ftruncate(fd, (off_t)blockBytes_) == 0;  // zero-filled
+    block_ = ok ? ::mmap(nullptr, blockBytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0) : MAP_FAILED;
+    ::close(fd);
+    GLOO_AMD_ENFORCE(block_ != MAP_FAILED, "transport block: ftruncate/mmap failed");
+  }
+  const auto names = ctx_->allgather(strcat_("tdev", inst_, "/block"),
+                                     ctx_->rank == 0 ? std::vector<char>(name.begin(), name.end())
+                                                     : std::vector<char>{});
+  if (ctx_->rank != 0) {
+    name.assign(names[0].begin(), names[0].end());
+    const int fd = ::shm_open(name.c_str(), O_RDWR, 0600);
+    GLOO_AMD_ENFORCE(fd >= 0, "shm_open failed for ", name);
+    block_ = ::mmap(nullptr, blockBytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    ::close(fd);
+    GLOO_AMD_ENFORCE(block_ != MAP_FAILED, "transport block: mmap failed");
+  }
+  ctx_->barrier(strcat_("tdev", inst_, "/mapped"));
+  if (ctx_->rank == 0) ::shm_unlink(name.c_str());  // every rank has it mapped now
+  channelUsed_.assign(P, std::vector<bool>(kChannels, false));
 }
 
 Device::~Device() {
   pairs_.clear();
   if (stream_) (void)hipStreamSynchronize(stream_);
   if (ownStream_) (void)hipStreamDestroy(stream_);
+  if (block_) {
+    // staged messages nobody took: their segments go with the transport
+    for (int dst = 0; dst < ctx_->size; dst++)
+      for (int i = 0; i < kAnnouncements; i++) {
+        Announcement& a = announcement(ctx_->rank, dst, i);
+        uint32_t ready = 2;
+        if (a.state.compare_exchange_strong(ready, 3) && a.name[0]) ::shm_unlink(a.name);
+      }
+    ::munmap(block_, blockBytes_);
+  }
   ctx_->releaseInstance(inst_);
 }
 
 Pair& Device::getPair(int peer) {
   GLOO_AMD_ENFORCE(peer >= 0 && peer < ctx_->size && peer != ctx_->rank, "no pair to rank ", peer);
+  std::lock_guard<std::mutex> lk(m_);
   auto& p = pairs_[peer];
   if (!p) p.reset(new Pair(this, peer));
   return *p;
 }
 
-void Device::claim(bool send, int peer, int slot) {
+void Device::claim(bool send, int peer, uint64_t slot) {
   std::lock_guard<std::mutex> lk(m_);
-  GLOO_AMD_ENFORCE(channels_.insert(std::make_tuple(send, peer, channel(slot))).second, "slot ", slot,
-                   " shares its channel with a live ", send ? "send" : "receive", " buffer to/from rank ", peer);
+  GLOO_AMD_ENFORCE(live_.insert(std::make_tuple(send, peer, slot)).second, "slot ", slot, " already has a live ",
+                   send ? "send" : "receive", " buffer to/from rank ", peer);
 }
 
-void Device::release(bool send, int peer, int slot) {
+void Device::release(bool send, int peer, uint64_t slot) {
   std::lock_guard<std::mutex> lk(m_);
-  channels_.erase(std::make_tuple(send, peer, channel(slot)));
+  live_.erase(std::make_tuple(send, peer, slot));
 }
 
-std::unique_ptr<Buffer> Pair::createSendBuffer(int slot, void* ptr, size_t size) {
+Device::Channel& Device::channel(int src, int dst, int idx) {
+  const size_t P = (size_t)ctx_->size;
+  GLOO_AMD_ENFORCE(idx >= 0 && idx < kChannels, "bad channel ", idx);
+  auto* base = reinterpret_cast<Channel*>(static_cast<char*>(block_) + 4096);
+  return base[((size_t)src * P + (size_t)dst) * kChannels + (size_t)idx];
+}
+
+Device::Announcement& Device::announcement(int src, int dst, int idx) {
+  const size_t P = (size_t)ctx_->size;
+  auto* base = reinterpret_cast<Announcement*>(static_cast<char*>(block_) + 4096 + P * P * kChannels * sizeof(Channel));
+  return base[((size_t)src * P + (size_t)dst) * kAnnouncements + (size_t)idx];
+}
+
+std::atomic<uint64_t>& Device::orderCounter(int dst) {
+  const size_t P = (size_t)ctx_->size;
+  char* p = static_cast<char*>(block_) + 4096 + P * P * kChannels * sizeof(Channel) +
+            P * P * kAnnouncements * sizeof(Announcement) + (size_t)dst * 64;
+  return *reinterpret_cast<std::atomic<uint64_t>*>(p);
+}
+
+int Device::allocChannel(int src) {
+  std::lock_guard<std::mutex> lk(m_);
+  auto& used = channelUsed_.at((size_t)src);
+  for (int i = 0; i < kChannels; i++)
+    if (!used[i]) {
+      used[i] = true;
+      return i;
+    }
+  GLOO_AMD_ENFORCE(false, "more than ", kChannels, " live receive buffers from rank ", src);
+  return -1;
+}
+
+void Device::freeChannel(int src, int idx) {
+  std::lock_guard<std::mutex> lk(m_);
+  if (idx >= 0) channelUsed_.at((size_t)src)[(size_t)idx] = false;
+}
+
+void Device::announce(int dst, uint64_t slot, const void* ptr, size_t n) {
+  GLOO_AMD_ENFORCE(dst >= 0 && dst < ctx_->size, "no rank ", dst);
+  char name[32] = {0};
+  if (n) {
+    std::snprintf(name, sizeof(name), "/gla_%d_%llu", ctx_->pid(), (unsigned long long)++g_staged);
+    const int fd = ::shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    GLOO_AMD_ENFORCE(fd >= 0, "shm_open(create) failed for ", name);
+    void* m = ::ftruncate(fd, (off_t)n) == 0 ? ::mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0)
+                                             : MAP_FAILED;
+    ::close(fd);
+    if (m == MAP_FAILED) {
+      ::shm_unlink(name);
+      GLOO_AMD_ENFORCE(false, "staging ", n, " bytes failed");
+    }
+    if (isDevice(ptr)) {
+      const hipError_t e = hipMemcpy(m, ptr, n, hipMemcpyDeviceToHost);
+      if (e != hipSuccess) {
+        ::munmap(m, n);
+        ::shm_unlink(name);
+        GLOO_AMD_HIP_CHECK(e);
+      }
+    } else {
+      std::memcpy(m, ptr, n);
+    }
+    ::munmap(m, n);
+  }
+  // a free entry of the (me -> dst) queue (the receiver frees them as it takes)
+  Announcement* a = nullptr;
+  pollUntil(
+      [&] {
+        for (int i = 0; i < kAnnouncements; i++) {
+          Announcement& x = announcement(ctx_->rank, dst, i);
+          uint32_t fr = 0;
+          if (x.state.load(std::memory_order_relaxed) == 0 && x.state.compare_exchange_strong(fr, 1)) {
+            a = &x;
+            return true;
+          }
+        }
+        return false;
+      },
+      nullptr, ctx_->timeout(), strcat_("waiting for rank ", dst, " to take ", kAnnouncements, " messages"));
+  a->slot = slot;
+  a->nbytes = n;
+  std::memcpy(a->name, name, sizeof(a->name));
+  a->order = orderCounter(dst).fetch_add(1, std::memory_order_acq_rel);
+  a->state.store(2, std::memory_order_release);
+}
+
+bool Device::take(const std::vector<int>& srcs, uint64_t slot, void* dst, size_t n, int* src) {
+  const int me = ctx_->rank;
+  for (;;) {
+    Announcement* best = nullptr;
+    int bestSrc = -1;
+    for (int s : srcs) {
+      GLOO_AMD_ENFORCE(s >= 0 && s < ctx_->size && s != me, "bad source rank ", s);
+      for (int i = 0; i < kAnnouncements; i++) {
+        Announcement& a = announcement(s, me, i);
+        if (a.state.load(std::memory_order_acquire) != 2 || a.slot != slot) continue;
+        if (!best || a.order < best->order) {
+          best = &a;
+          bestSrc = s;
+        }
+      }
+    }
+    if (!best) return false;
+    uint32_t ready = 2;
+    if (!best->state.compare_exchange_strong(ready, 3)) continue;  // another thread of this rank took it
+    const size_t nbytes = best->nbytes;
+    char name[32];
+    std::memcpy(name, best->name, sizeof(name));
+    if (nbytes != n) {
+      best->state.store(2, std::memory_order_release);  // leave it for a receive of the right size
+      GLOO_AMD_ENFORCE(false, "rank ", bestSrc, " sent ", nbytes, " bytes on slot ", slot, " to a ", n,
+                       "-byte receive");
+    }
+    if (nbytes) {
+      const int fd = ::shm_open(name, O_RDONLY, 0600);
+      GLOO_AMD_ENFORCE(fd >= 0, "shm_open failed for ", name);
+      void* m = ::mmap(nullptr, nbytes, PROT_READ, MAP_SHARED, fd, 0);
+      ::close(fd);
+      GLOO_AMD_ENFORCE(m != MAP_FAILED, "mmap of a staged message failed");
+      hipError_t e = hipSuccess;
+      if (isDevice(dst)) {
+        e = hipMemcpy(dst, m, nbytes, hipMemcpyHostToDevice);
+      } else {
+        std::memcpy(dst, m, nbytes);
+      }
+      ::munmap(m, nbytes);
+      ::shm_unlink(name);
+      GLOO_AMD_HIP_CHECK(e);
+    }
+    best->state.store(0, std::memory_order_release);
+    *src = bestSrc;
+    return true;
+  }
+}
+
+// ---- Pair / UnboundBuffer ----------------------------------------------
+
+std::unique_ptr<Buffer> Pair::createSendBuffer(uint64_t slot, void* ptr, size_t size) {
   return std::unique_ptr<Buffer>(new SendBuffer(dev_, peer_, slot, ptr, size));
 }
 
-std::unique_ptr<Buffer> Pair::createRecvBuffer(int slot, void* ptr, size_t size) {
+std::unique_ptr<Buffer> Pair::createRecvBuffer(uint64_t slot, void* ptr, size_t size) {
   return std::unique_ptr<Buffer>(new RecvBuffer(dev_, peer_, slot, ptr, size));
+}
+
+void UnboundBuffer::send(int dst, uint64_t slot, size_t offset, size_t nbytes) {
+  if (nbytes == std::numeric_limits<size_t>::max()) nbytes = offset <= size_ ? size_ - offset : 0;
+  GLOO_AMD_ENFORCE(offset + nbytes <= size_, "send of [", offset, ", +", nbytes, ") beyond a ", size_,
+                   "-byte buffer");
+  GLOO_AMD_ENFORCE(dst != dev_->context()->rank, "send to self");
+  dev_->announce(dst, slot, ptr_ + offset, nbytes);
+  sent_.push_back(dst);
+}
+
+void UnboundBuffer::recv(const std::vector<int>& srcs, uint64_t slot, size_t offset, size_t nbytes) {
+  if (nbytes == std::numeric_limits<size_t>::max()) nbytes = offset <= size_ ? size_ - offset : 0;
+  GLOO_AMD_ENFORCE(offset + nbytes <= size_, "recv of [", offset, ", +", nbytes, ") beyond a ", size_,
+                   "-byte buffer");
+  GLOO_AMD_ENFORCE(!srcs.empty(), "recv from no rank");
+  recvs_.push_back({srcs, slot, offset, nbytes});
+}
+
+bool UnboundBuffer::waitRecv(int* rank, std::chrono::milliseconds timeout) {
+  Context& ctx = *dev_->context();
+  GLOO_AMD_ENFORCE(!recvs_.empty(), "waitRecv without a pending recv");
+  if (timeout.count() < 0) timeout = ctx.timeout();
+  int src = -1;
+  const bool done = pollUntil(
+      [&] {
+        for (auto it = recvs_.begin(); it != recvs_.end(); ++it)
+          if (dev_->take(it->srcs, it->slot, ptr_ + it->offset, it->nbytes, &src)) {
+            recvs_.erase(it);
+            return true;
+          }
+        return false;
+      },
+      &abortRecv_, timeout, strcat_("waiting for a message on rank ", ctx.rank));
+  if (!done) {
+    abortRecv_ = false;
+    return false;
+  }
+  if (rank) *rank = src;
+  return true;
+}
+
+bool UnboundBuffer::waitSend(int* rank, std::chrono::milliseconds) {
+  // sends are eager: each completed when send() returned
+  if (abortSend_.exchange(false)) return false;
+  GLOO_AMD_ENFORCE(!sent_.empty(), "waitSend without a pending send");
+  if (rank) *rank = sent_.front();
+  sent_.pop_front();
+  return true;
 }
 
 }  // namespace transport

@@ -32,12 +32,17 @@
 // (gloo/cuda_allreduce_ring_chunked.cc:333-352) and relies on a transport
 // that writes into GPU memory (ibverbs GPUDirect in the reference).
 //
-// Not carried: unbound buffers (gloo/transport/unbound_buffer.h, the
-// two-sided send/recv of the new-style collectives, which the reference
-// reduces on the host from `new uint8_t[]` segments, gloo/allreduce.cc:221-223).
-// createUnboundBuffer and Pair::send/recv(UnboundBuffer*) throw
-// gloo::InvalidOperationException; the new-style collectives over device
-// memory are gloo_hip_allreduce / gloo_hip_reduce_to_root.
+// Unbound buffers (gloo/transport/unbound_buffer.h:32-121):
+//   Context::createUnboundBuffer(ptr, size), UnboundBuffer::send / recv
+//   (recv-from-any over a rank list too), waitSend / waitRecv(rank, timeout),
+//   abortWaitSend / abortWaitRecv, and Pair::send / recv(UnboundBuffer*):
+//   two-sided messages matched per (source, slot) in order, through the
+//   library's message queues (gloo_hip_ubuf_*: eager sends staged in node
+//   shared memory).  So the reference's own gloo::allreduce, gloo::allgather,
+//   gloo::reduce (gloo/allreduce.cc, allgather.cc, reduce.cc) run over this
+//   transport unchanged, on host buffers as in the reference (they reduce on
+//   the CPU with the options' reduce function).  The device-memory form of
+//   those collectives is gloo_collectives.h (gloo::hip::allreduce / reduce).
 //
 // All ranks of a context run on one node (the arrival counters live in a
 // node-local control block); each drives the HIP device given at CreateDevice.
@@ -127,6 +132,43 @@ class Buffer : public ::gloo::transport::Buffer {
   bool isSend_;
 };
 
+class UnboundBuffer : public ::gloo::transport::UnboundBuffer {
+ public:
+  UnboundBuffer(Context* ctx, void* ptr, size_t size);
+  ~UnboundBuffer() override { (void)gloo_hip_ubuf_destroy(h_); }
+
+  bool waitRecv(int* rank, std::chrono::milliseconds timeout) override {
+    return finish(gloo_hip_ubuf_wait_recv(h_, rank, (int)timeout.count()), "hip::UnboundBuffer::waitRecv");
+  }
+  bool waitSend(int* rank, std::chrono::milliseconds timeout) override {
+    return finish(gloo_hip_ubuf_wait_send(h_, rank, (int)timeout.count()), "hip::UnboundBuffer::waitSend");
+  }
+  void abortWaitRecv() override { detail::check(gloo_hip_ubuf_abort_wait_recv(h_), "abortWaitRecv"); }
+  void abortWaitSend() override { detail::check(gloo_hip_ubuf_abort_wait_send(h_), "abortWaitSend"); }
+
+  void send(int dstRank, uint64_t slot, size_t offset = 0, size_t nbytes = kUnspecifiedByteCount) override {
+    detail::check(gloo_hip_ubuf_send(h_, dstRank, slot, offset, nbytes), "hip::UnboundBuffer::send");
+  }
+  void recv(int srcRank, uint64_t slot, size_t offset = 0, size_t nbytes = kUnspecifiedByteCount) override {
+    detail::check(gloo_hip_ubuf_recv(h_, &srcRank, 1, slot, offset, nbytes), "hip::UnboundBuffer::recv");
+  }
+  void recv(std::vector<int> srcRanks, uint64_t slot, size_t offset = 0,
+            size_t nbytes = kUnspecifiedByteCount) override {
+    detail::check(gloo_hip_ubuf_recv(h_, srcRanks.data(), (int)srcRanks.size(), slot, offset, nbytes),
+                  "hip::UnboundBuffer::recv");
+  }
+
+ private:
+  // 0: done; 1: aborted (false); a timeout raises IoException as in the
+  // reference's transports
+  static bool finish(int rc, const char* what) {
+    if (rc == 1) return false;
+    detail::check(rc, what);
+    return true;
+  }
+  gloo_hip_ubuf_t h_ = nullptr;
+};
+
 class Pair : public ::gloo::transport::Pair {
  public:
   Pair(Context* ctx, int rank, int peer) : ctx_(ctx), address_(rank, peer), peer_(peer) { localRank_ = 0; }
@@ -150,11 +192,16 @@ class Pair : public ::gloo::transport::Pair {
   inline std::unique_ptr<::gloo::transport::Buffer> createSendBuffer(int slot, void* ptr, size_t size) override;
   inline std::unique_ptr<::gloo::transport::Buffer> createRecvBuffer(int slot, void* ptr, size_t size) override;
 
-  void send(::gloo::transport::UnboundBuffer*, uint64_t, size_t, size_t) override {
-    GLOO_THROW_INVALID_OPERATION_EXCEPTION("the hip transport carries bound buffers only");
+  // gloo/transport/pair.h:51-62: the buffer's send / recv with this pair's peer
+  void send(::gloo::transport::UnboundBuffer* buf, uint64_t slot, size_t offset, size_t nbytes) override {
+    auto* b = dynamic_cast<UnboundBuffer*>(buf);
+    GLOO_ENFORCE(b != nullptr, "not an unbound buffer of the hip transport");
+    b->send(peer_, slot, offset, nbytes);
   }
-  void recv(::gloo::transport::UnboundBuffer*, uint64_t, size_t, size_t) override {
-    GLOO_THROW_INVALID_OPERATION_EXCEPTION("the hip transport carries bound buffers only");
+  void recv(::gloo::transport::UnboundBuffer* buf, uint64_t slot, size_t offset, size_t nbytes) override {
+    auto* b = dynamic_cast<UnboundBuffer*>(buf);
+    GLOO_ENFORCE(b != nullptr, "not an unbound buffer of the hip transport");
+    b->recv(peer_, slot, offset, nbytes);
   }
 
  private:
@@ -203,8 +250,8 @@ class Context : public ::gloo::transport::Context {
     }
   }
 
-  std::unique_ptr<::gloo::transport::UnboundBuffer> createUnboundBuffer(void*, size_t) override {
-    GLOO_THROW_INVALID_OPERATION_EXCEPTION("the hip transport carries bound buffers only");
+  std::unique_ptr<::gloo::transport::UnboundBuffer> createUnboundBuffer(void* ptr, size_t size) override {
+    return std::unique_ptr<::gloo::transport::UnboundBuffer>(new UnboundBuffer(this, ptr, size));
   }
 
   gloo_hip_transport_t handle() const { return transport_; }
@@ -264,6 +311,12 @@ class Context : public ::gloo::transport::Context {
   gloo_hip_transport_t transport_ = nullptr;
   uint64_t allgatherSeq_ = 0;
 };
+
+inline UnboundBuffer::UnboundBuffer(Context* ctx, void* ptr, size_t size)
+    : ::gloo::transport::UnboundBuffer(ptr, size) {
+  GLOO_ENFORCE(ctx->handle() != nullptr, "transport not connected");
+  detail::check(gloo_hip_ubuf_create(ctx->handle(), ptr, size, &h_), "hip::Context::createUnboundBuffer");
+}
 
 inline std::unique_ptr<::gloo::transport::Buffer> Pair::createSendBuffer(int slot, void* ptr, size_t size) {
   gloo_hip_buffer_t h = nullptr;

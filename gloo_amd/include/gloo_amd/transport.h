@@ -1,45 +1,63 @@
 // transport.h — an xGMI transport with the shape of Gloo's
-// transport::Device / Pair / Buffer (gloo/transport/pair.h:21-81,
-// gloo/transport/buffer.h:16-41), so an algorithm written against those
-// interfaces moves device chunks GPU to GPU with no socket in between.
+// transport::Device / Pair / Buffer / UnboundBuffer (gloo/transport/pair.h:21-81,
+// gloo/transport/buffer.h:16-41, gloo/transport/unbound_buffer.h:32-121), so an
+// algorithm written against those interfaces moves device chunks GPU to GPU
+// with no socket in between.
 //
-//   Pair::createRecvBuffer(slot, ptr, size)   registers a DEVICE buffer the
-//        peer writes into: its allocation is exported (HIP IPC across
-//        processes, the raw pointer within one) through the context's store;
-//   Pair::createSendBuffer(slot, ptr, size)   a local device buffer; on its
-//        first send it resolves the peer's receive buffer of the same slot;
+// Bound buffers (the GPU algorithms' inboxes):
+//   Pair::createRecvBuffer(slot, ptr, size)   registers memory the peer writes
+//        into: DEVICE memory is exported (HIP IPC across processes, the raw
+//        pointer within one); HOST memory is written directly within one
+//        process, and across processes carried in the channel's payload
+//        words (at most kPayloadBytes: the reference's notification buffers,
+//        &dummy_ / sizeof(dummy_), gloo/cuda_allreduce_ring_chunked.cc:119-123);
+//   Pair::createSendBuffer(slot, ptr, size)   a local buffer; on its first send
+//        it resolves the peer's receive buffer of the same slot;
 //   Buffer::send(offset, length, roffset)     one-sided write: a device copy
 //        (over the direct xGMI link when the peer is another GPU) into the
-//        peer's buffer at roffset, then — stream-ordered, after the copy has
-//        landed — the arrival counter of (me -> peer, slot) is bumped in the
-//        node's control block (gloo_amd::Context);
+//        peer's buffer at roffset, then — stream-ordered, after the bytes
+//        landed — the channel's arrival counter is bumped;
 //   Buffer::waitRecv()                        blocks until the next message of
-//        this receive buffer has arrived (counter, bounded by the context
-//        timeout -> IoException, as gloo/transport/tcp/buffer.cc:67-73);
-//   Buffer::waitSend()                        blocks until the last send's
-//        copy out of this buffer has completed.
+//        this receive buffer has arrived (bounded by the context timeout ->
+//        IoException, as gloo/transport/tcp/buffer.cc:67-73);
+//   Buffer::waitSend()                        blocks until the last send's copy
+//        out of this buffer has completed.
+// Every receive buffer owns one channel (arrival counter + payload words) of
+// the transport block, allocated by the receiver per (sender, slot) and
+// published with its record, so any number of slots may be live — as many
+// as kChannels per (sender, receiver) at once — and Gloo's ever-increasing
+// context->nextSlot() values never collide.
 //
-// Chunks are written into the receiver's HBM and reduced there by the HIP
-// kernels; nothing is staged through host memory.  Slots are arbitrary ints
-// as in Gloo (context->nextSlot()); per (direction, peer) at most
-// GLOO_HIP_NUM_SLOTS distinct slots modulo GLOO_HIP_NUM_SLOTS may be live.
-// The store must support set/get (file: or mem: contexts).
+// Unbound buffers (the new-style collectives, gloo/allreduce.cc,
+// gloo/allgather.cc, gloo/reduce.cc): two-sided send / recv matched per
+// (source, slot) in order, recv-from-any over a set of source ranks (the
+// earliest announced message wins, as the reference's Tally keeps arrival
+// order, gloo/transport/context.h:107-125).  Sends are EAGER: the bytes are
+// staged in a shared-memory segment of their own (a device buffer through a
+// device-to-host copy) and announced in the (sender, receiver) queue of the
+// transport block; the send is complete at once (waitSend reports the
+// destination), and the receiver copies the bytes out in waitRecv.  So
+// neither side ever waits for the other to post first, and host buffers
+// work between processes.  This path moves bytes through host memory: it
+// serves the reference's host-memory algorithms (which reduce on the CPU
+// anyway), not the device hot path, which is the executor's (executor.h).
 //
-// Receive buffers are the caller's memory, so unlike the executor's inboxes
-// (executor.cc: a nonce at the arena's start, read back through every new
-// IPC mapping) their imports are not verified; on ROCm 7 an import has been
-// seen to show a previous allocation of the same size (DESIGN.md §4,
-// "IPC imports are verified").  Keep receive buffers alive for the life of
-// the pairs that use them, as Gloo's own transports require.
+// All ranks of a context run on one node; each drives the HIP device given
+// at construction.  The transport block is created by the transport's
+// collective construction (every rank, same order as its algorithms).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
+#include <chrono>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <set>
+#include <string>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -50,9 +68,13 @@ namespace transport {
 
 class Pair;
 
+constexpr int kChannels = 128;       // live receive buffers per (sender, receiver)
+constexpr int kAnnouncements = 128;  // unbound messages in flight per (sender, receiver)
+constexpr size_t kPayloadBytes = 48;
+
 // One per rank: the transport device over a connected gloo_amd::Context.
-// Construction reserves one of the context's counter instances; like
-// algorithm construction it is collective (every rank in the same order).
+// Construction is collective (every rank, in the same order as its
+// algorithms): it maps the transport block.
 class Device {
  public:
   explicit Device(std::shared_ptr<Context> ctx, hipStream_t stream = nullptr);
@@ -66,19 +88,50 @@ class Device {
   const std::shared_ptr<Context>& context() const { return ctx_; }
   uint64_t instance() const { return inst_; }
 
-  // (direction, peer, slot % kSlots) channels in use: a second live buffer
-  // on one channel would share its counter.
-  void claim(bool send, int peer, int slot);
-  void release(bool send, int peer, int slot);
+  // A (direction, peer, slot) may hold one live buffer at a time.
+  void claim(bool send, int peer, uint64_t slot);
+  void release(bool send, int peer, uint64_t slot);
+
+  struct Channel {
+    std::atomic<uint64_t> count;  // arrivals
+    uint32_t off, len;            // the last payload's place in the receive buffer
+    char payload[kPayloadBytes];
+  };
+  static_assert(sizeof(Channel) == 64, "one line per channel");
+  Channel& channel(int src, int dst, int idx);
+  int allocChannel(int src);  // receiver side: a free channel of (src -> me)
+  void freeChannel(int src, int idx);
+
+  // Unbound messages (transport.cc).
+  struct Announcement {
+    std::atomic<uint32_t> state;  // 0 free, 1 being written, 2 ready, 3 being taken
+    uint32_t pad;
+    uint64_t slot, nbytes, order;
+    char name[32];                // the staging segment ("" for 0 bytes)
+  };
+  static_assert(sizeof(Announcement) == 64, "one line per announcement");
+  // Eager send of [ptr, ptr + n) (host or device memory) to `dst` on `slot`.
+  void announce(int dst, uint64_t slot, const void* ptr, size_t n);
+  // Takes the earliest announced message on `slot` from any of `srcs` and
+  // copies it to `dst` (n bytes, which must be the message's size).
+  // Returns false if none has been announced yet.
+  bool take(const std::vector<int>& srcs, uint64_t slot, void* dst, size_t n, int* src);
 
  private:
+  Announcement& announcement(int src, int dst, int idx);
+  std::atomic<uint64_t>& orderCounter(int dst);
+
   std::shared_ptr<Context> ctx_;
   uint64_t inst_;
   hipStream_t stream_ = nullptr;
   bool ownStream_ = false;
   std::map<int, std::unique_ptr<Pair>> pairs_;
   std::mutex m_;
-  std::set<std::tuple<bool, int, int>> channels_;
+  std::set<std::tuple<bool, int, uint64_t>> live_;
+  std::vector<std::vector<bool>> channelUsed_;  // [src][idx], this rank as receiver
+  void* block_ = nullptr;
+  size_t blockBytes_ = 0;
+  uint64_t staged_ = 0;  // staging segments created so far (names)
 };
 
 class Buffer {
@@ -89,12 +142,12 @@ class Buffer {
   void send() { send(0, size_); }
   virtual void waitRecv() = 0;
   virtual void waitSend() = 0;
-  int slot() const { return slot_; }
+  uint64_t slot() const { return slot_; }
   size_t size() const { return size_; }
 
  protected:
-  Buffer(int slot, void* ptr, size_t size) : slot_(slot), ptr_(static_cast<char*>(ptr)), size_(size) {}
-  int slot_;
+  Buffer(uint64_t slot, void* ptr, size_t size) : slot_(slot), ptr_(static_cast<char*>(ptr)), size_(size) {}
+  uint64_t slot_;
   char* ptr_;
   size_t size_;
 };
@@ -102,13 +155,41 @@ class Buffer {
 class Pair {
  public:
   Pair(Device* dev, int peer) : dev_(dev), peer_(peer) {}
-  std::unique_ptr<Buffer> createSendBuffer(int slot, void* ptr, size_t size);
-  std::unique_ptr<Buffer> createRecvBuffer(int slot, void* ptr, size_t size);
+  std::unique_ptr<Buffer> createSendBuffer(uint64_t slot, void* ptr, size_t size);
+  std::unique_ptr<Buffer> createRecvBuffer(uint64_t slot, void* ptr, size_t size);
   int peer() const { return peer_; }
 
  private:
   Device* dev_;
   int peer_;
+};
+
+// gloo::transport::UnboundBuffer (gloo/transport/unbound_buffer.h:32-121) over
+// the Device's message queues.  One thread uses a buffer at a time.
+class UnboundBuffer {
+ public:
+  UnboundBuffer(Device* dev, void* ptr, size_t size) : dev_(dev), ptr_(static_cast<char*>(ptr)), size_(size) {}
+  void send(int dst, uint64_t slot, size_t offset, size_t nbytes);
+  void recv(const std::vector<int>& srcs, uint64_t slot, size_t offset, size_t nbytes);
+  // true: completed (*rank = the peer); false: aborted.  timeout < 0: the
+  // context's.  Throws IoException on timeout.
+  bool waitRecv(int* rank, std::chrono::milliseconds timeout);
+  bool waitSend(int* rank, std::chrono::milliseconds timeout);
+  void abortWaitRecv() { abortRecv_ = true; }
+  void abortWaitSend() { abortSend_ = true; }
+
+ private:
+  struct PendingRecv {
+    std::vector<int> srcs;
+    uint64_t slot;
+    size_t offset, nbytes;
+  };
+  Device* dev_;
+  char* ptr_;
+  size_t size_;
+  std::deque<PendingRecv> recvs_;
+  std::deque<int> sent_;  // destinations of completed sends not yet waited for
+  std::atomic<bool> abortRecv_{false}, abortSend_{false};
 };
 
 }  // namespace transport

@@ -449,8 +449,11 @@ int gloo_hip_reduce_to_root(gloo_hip_context_t ctx, const gloo_hip_reduce_option
  *   gloo_hip_buffer_create      <- Pair::createSendBuffer (is_send = 1) /
  *       createRecvBuffer (is_send = 0) for the pair to `peer`.  A receive
  *       buffer is memory the peer writes into: device memory (HIP IPC across
- *       processes, the pointer itself within one process) or, within one
- *       process, host memory.  ptr == NULL / size 0: a notification buffer.
+ *       processes, the pointer itself within one process) or host memory
+ *       (written directly within one process; across processes carried in
+ *       the channel's 48 payload bytes, the reference's notification
+ *       buffers).  ptr == NULL / size 0: a notification buffer.  Any number
+ *       of distinct slots may be live (up to 128 receive buffers per peer).
  *   gloo_hip_buffer_send        <- Buffer::send(offset, length, roffset): a
  *       copy into the peer's receive buffer (a direct xGMI copy between
  *       GPUs), then, stream-ordered after the bytes landed, an arrival.
@@ -474,6 +477,25 @@ int gloo_hip_buffer_destroy(gloo_hip_buffer_t b);
 int gloo_hip_buffer_send(gloo_hip_buffer_t b, size_t offset, size_t length, size_t roffset);
 int gloo_hip_buffer_wait_recv(gloo_hip_buffer_t b);
 int gloo_hip_buffer_wait_send(gloo_hip_buffer_t b);
+
+/* Unbound buffers (gloo/transport/unbound_buffer.h:32-121) on the same
+ * transport: two-sided send / recv matched per (source, slot) in order,
+ * recv-from-any over `srcs`.  Sends are eager (the bytes are staged in node
+ * shared memory at once, so waitSend never blocks); the receiver copies them
+ * out in wait_recv.  Host or device memory.  nbytes = SIZE_MAX: the rest of
+ * the buffer from offset.
+ *   gloo_hip_ubuf_wait_recv / wait_send: 0 = done (*rank = the peer),
+ *   1 = aborted (abort_wait_*), GLOO_HIP_EIO = timed out (timeout_ms < 0:
+ *   the context's timeout). */
+typedef struct gloo_hip_ubuf* gloo_hip_ubuf_t;
+int gloo_hip_ubuf_create(gloo_hip_transport_t t, void* ptr, size_t size, gloo_hip_ubuf_t* out);
+int gloo_hip_ubuf_destroy(gloo_hip_ubuf_t b);
+int gloo_hip_ubuf_send(gloo_hip_ubuf_t b, int dst, uint64_t slot, size_t offset, size_t nbytes);
+int gloo_hip_ubuf_recv(gloo_hip_ubuf_t b, const int* srcs, int nsrcs, uint64_t slot, size_t offset, size_t nbytes);
+int gloo_hip_ubuf_wait_recv(gloo_hip_ubuf_t b, int* rank, int timeout_ms);
+int gloo_hip_ubuf_wait_send(gloo_hip_ubuf_t b, int* rank, int timeout_ms);
+int gloo_hip_ubuf_abort_wait_recv(gloo_hip_ubuf_t b);
+int gloo_hip_ubuf_abort_wait_send(gloo_hip_ubuf_t b);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -22,7 +22,16 @@
 //                         (gloo/rendezvous/context.cc:37-162) bootstrapping a
 //                         TCP context over this transport's bound buffers;
 //   io_exception          a receive that never arrives raises gloo::IoException;
-//   unbound_refused       createUnboundBuffer raises InvalidOperationException.
+//   many_live             four DeviceRingChunked instances live at once on one
+//                         context (12 slots per pair) run interleaved;
+//   ref_allreduce_*, ref_allgather, ref_reduce
+//                         the reference's own gloo::allreduce (RING, BCUBE),
+//                         gloo::allgather and gloo::reduce, unmodified, on host
+//                         buffers over this transport's unbound buffers;
+//   unbound_*             recv-from-any, abort, device buffers, ordering.
+// DeviceRingChunked's notification buffers are the reference's own host
+// words (&dummy_, sizeof(dummy_), gloo/cuda_allreduce_ring_chunked.cc:119-123),
+// also with ranks as processes (their bytes travel in the channel's payload).
 // Expected values: the closed form of gloo/test/base_test.h:184-236.
 //
 // Usage: transport_test [case-filter]             ranks as threads (exit 0 = ok)
@@ -42,8 +51,12 @@
 #include <thread>
 #include <vector>
 
+#include "gloo/allgather.h"
+#include "gloo/allreduce.h"
 #include "gloo/allreduce_halving_doubling.h"
 #include "gloo/allreduce_ring_chunked.h"
+#include "gloo/math.h"
+#include "gloo/reduce.h"
 #include "gloo/rendezvous/context.h"
 #include "gloo/rendezvous/file_store.h"
 #include "gloo/rendezvous/hash_store.h"
@@ -139,9 +152,10 @@ class DeviceRingChunked : public gloo::Algorithm {
       sendDataBuf_[i] = rightPair->createSendBuffer(slot, ptr_, bytes_);
       recvDataBuf_[i] = leftPair->createRecvBuffer(slot, inbox_[i], chunkSize_ * sizeof(T));
     }
+    // host words, as the reference does (gloo/cuda_allreduce_ring_chunked.cc:119-123)
     auto notificationSlot = context_->nextSlot();
-    sendNotificationBuf_ = leftPair->createSendBuffer(notificationSlot, nullptr, 0);
-    recvNotificationBuf_ = rightPair->createRecvBuffer(notificationSlot, nullptr, 0);
+    sendNotificationBuf_ = leftPair->createSendBuffer(notificationSlot, &dummy_, sizeof(dummy_));
+    recvNotificationBuf_ = rightPair->createRecvBuffer(notificationSlot, &dummy_, sizeof(dummy_));
   }
   ~DeviceRingChunked() override {
     sendDataBuf_[0].reset();
@@ -225,6 +239,7 @@ class DeviceRingChunked : public gloo::Algorithm {
   int chunks_ = 0;
   size_t chunkSize_ = 0;
   T* inbox_[2] = {nullptr, nullptr};
+  int dummy_ = 0;
   hipStream_t stream_ = nullptr;
   std::unique_ptr<gloo::transport::Buffer> sendDataBuf_[2], recvDataBuf_[2], sendNotificationBuf_,
       recvNotificationBuf_;
@@ -348,18 +363,173 @@ std::string ioExceptionCase() {
   return seen.empty() ? std::string("no IoException") : std::string();
 }
 
-std::string unboundRefusedCase() {
-  bool refused = false;
-  std::string err = spawn(2, 10000, [&](std::shared_ptr<gloo::Context> ctx) {
-    char x[8];
-    try {
-      (void)ctx->createUnboundBuffer(x, sizeof(x));
-    } catch (const gloo::InvalidOperationException&) {
-      if (ctx->rank == 0) refused = true;
+// Four DeviceRingChunked instances live on one context (3 slots each per
+// pair, 12 in all), run interleaved: every slot needs its own channel.
+std::string manyLiveCase(int P, int count) {
+  return spawn(P, 30000, [&](std::shared_ptr<gloo::Context> ctx) {
+    constexpr int kLive = 4;
+    std::vector<float*> d(kLive, nullptr);
+    std::vector<std::unique_ptr<gloo::Algorithm>> algos;
+    for (int k = 0; k < kLive; k++) {
+      HIPOK(hipMalloc(&d[k], count * sizeof(float)));
+      algos.emplace_back(new DeviceRingChunked<float>(ctx, d[k], count));
+    }
+    std::vector<float> h(count);
+    for (int r = 0; r < 2; r++)
+      for (int k = 0; k < kLive; k++) {
+        fill(h, P, ctx->rank);
+        HIPOK(hipMemcpy(d[k], h.data(), count * sizeof(float), hipMemcpyHostToDevice));
+        algos[k]->run();
+        HIPOK(hipMemcpy(h.data(), d[k], count * sizeof(float), hipMemcpyDeviceToHost));
+        const std::string e = checkClosedForm(h, P, r);
+        if (!e.empty()) throw std::runtime_error("instance " + std::to_string(k) + ": " + e);
+      }
+    algos.clear();
+    for (float* p : d) HIPOK(hipFree(p));
+  });
+}
+
+using ReduceFn = void (*)(void*, const void*, const void*, size_t);
+
+// The reference's gloo::allreduce(opts) (RING / BCUBE), unmodified, on host
+// buffers over this transport's unbound buffers: two inputs per rank,
+// segments of 4 KiB so the ring has many.
+std::string refAllreduceCase(int P, int count, bool bcube) {
+  return spawn(P, 30000, [&](std::shared_ptr<gloo::Context> ctx) {
+    std::vector<float> a(count), b(count), out(count);
+    for (int r = 0; r < 2; r++) {
+      for (int j = 0; j < count; j++) {
+        a[j] = (float)((j % 4096) * P + ctx->rank);
+        b[j] = (float)(j % 7);
+      }
+      gloo::AllreduceOptions opts(ctx);
+      opts.setAlgorithm(bcube ? gloo::AllreduceOptions::Algorithm::BCUBE : gloo::AllreduceOptions::Algorithm::RING);
+      opts.setInputs(std::vector<float*>{a.data(), b.data()}, count);
+      opts.setOutput(out.data(), count);
+      opts.setReduceFunction(static_cast<ReduceFn>(&gloo::sum<float>));
+      opts.setMaxSegmentSize(4096);
+      opts.setTag(r);
+      gloo::allreduce(opts);
+      for (int j = 0; j < count; j++) {
+        const double want = (double)(j % 4096) * P * P + P * (P - 1) / 2.0 + (double)P * (j % 7);
+        if ((double)out[j] != want)
+          throw std::runtime_error("element " + std::to_string(j) + ": " + std::to_string(out[j]) + " != " +
+                                   std::to_string(want));
+      }
     }
   });
-  if (!err.empty()) return err;
-  return refused ? std::string() : std::string("createUnboundBuffer did not raise InvalidOperationException");
+}
+
+// gloo::allgather (gloo/allgather.cc), unmodified, over this transport.
+std::string refAllgatherCase(int P, int count) {
+  return spawn(P, 30000, [&](std::shared_ptr<gloo::Context> ctx) {
+    std::vector<int64_t> in(count), out((size_t)count * P);
+    for (int j = 0; j < count; j++) in[j] = (int64_t)ctx->rank * 1000003 + j;
+    gloo::AllgatherOptions opts(ctx);
+    opts.setInput(in.data(), count);
+    opts.setOutput(out.data(), (size_t)count * P);
+    gloo::allgather(opts);
+    for (int r = 0; r < P; r++)
+      for (int j = 0; j < count; j++)
+        if (out[(size_t)r * count + j] != (int64_t)r * 1000003 + j)
+          throw std::runtime_error("allgather mismatch at rank block " + std::to_string(r));
+  });
+}
+
+// gloo::reduce (gloo/reduce.cc), unmodified, over this transport.
+std::string refReduceCase(int P, int count, int root) {
+  return spawn(P, 30000, [&](std::shared_ptr<gloo::Context> ctx) {
+    std::vector<double> in(count), out(count);
+    for (int j = 0; j < count; j++) in[j] = (double)(j * P + ctx->rank);
+    gloo::ReduceOptions opts(ctx);
+    opts.setInput(in.data(), count);
+    opts.setOutput(out.data(), count);
+    opts.setRoot(root);
+    opts.setReduceFunction(static_cast<ReduceFn>(&gloo::sum<double>));
+    opts.setMaxSegmentSize(1024);
+    gloo::reduce(opts);
+    if (ctx->rank == root)
+      for (int j = 0; j < count; j++)
+        if (out[j] != (double)j * P * P + P * (P - 1) / 2.0)
+          throw std::runtime_error("reduce mismatch at " + std::to_string(j));
+  });
+}
+
+// Recv-from-any: rank 0 takes one message from each of ranks 1..P-1 on one
+// slot, in whatever order they arrive, and learns who sent which.
+std::string unboundRecvFromAnyCase(int P) {
+  return spawn(P, 30000, [&](std::shared_ptr<gloo::Context> ctx) {
+    const uint64_t slot = gloo::Slot::build(3, 0);
+    if (ctx->rank == 0) {
+      std::vector<int> got((size_t)P, -1);
+      std::vector<int> srcs;
+      for (int r = 1; r < P; r++) srcs.push_back(r);
+      for (int k = 1; k < P; k++) {
+        int v = -1, src = -1;
+        auto buf = ctx->createUnboundBuffer(&v, sizeof(v));
+        buf->recv(srcs, slot);
+        if (!buf->waitRecv(&src)) throw std::runtime_error("recv aborted");
+        if (src < 1 || src >= P || got[src] != -1 || v != 100 + src) throw std::runtime_error("bad message");
+        got[src] = v;
+      }
+    } else {
+      int v = 100 + ctx->rank;
+      auto buf = ctx->createUnboundBuffer(&v, sizeof(v));
+      buf->send(0, slot);
+      int dst = -1;
+      if (!buf->waitSend(&dst) || dst != 0) throw std::runtime_error("send not completed");
+    }
+  });
+}
+
+// Ordering per (source, slot), 0-byte messages, and device buffers.
+std::string unboundOrderDeviceCase() {
+  return spawn(2, 30000, [&](std::shared_ptr<gloo::Context> ctx) {
+    const uint64_t slot = gloo::Slot::build(4, 1);
+    constexpr int kMsgs = 200;  // more than the queue holds: the sender waits for the receiver
+    float* d = nullptr;
+    HIPOK(hipMalloc(&d, 1024 * sizeof(float)));
+    auto buf = ctx->createUnboundBuffer(d, 1024 * sizeof(float));
+    std::vector<float> h(1024);
+    if (ctx->rank == 1) {
+      for (int m = 0; m < kMsgs; m++) {
+        for (int j = 0; j < 1024; j++) h[j] = (float)(m * 1024 + j);
+        HIPOK(hipMemcpy(d, h.data(), sizeof(float) * 1024, hipMemcpyHostToDevice));
+        buf->send(0, slot, 0, m % 5 == 4 ? 0 : 1024 * sizeof(float));
+        buf->waitSend();
+      }
+    } else {
+      for (int m = 0; m < kMsgs; m++) {
+        const size_t n = m % 5 == 4 ? 0 : 1024 * sizeof(float);
+        buf->recv(1, slot, 0, n);
+        int src = -1;
+        if (!buf->waitRecv(&src) || src != 1) throw std::runtime_error("recv failed");
+        if (!n) continue;
+        HIPOK(hipMemcpy(h.data(), d, sizeof(float) * 1024, hipMemcpyDeviceToHost));
+        for (int j = 0; j < 1024; j++)
+          if (h[j] != (float)(m * 1024 + j)) throw std::runtime_error("message " + std::to_string(m) + " out of order");
+      }
+    }
+    buf.reset();
+    HIPOK(hipFree(d));
+  });
+}
+
+// abortWaitRecv from another thread ends a wait that would never complete.
+std::string unboundAbortCase() {
+  return spawn(2, 30000, [&](std::shared_ptr<gloo::Context> ctx) {
+    if (ctx->rank != 0) return;
+    int v = 0;
+    auto buf = ctx->createUnboundBuffer(&v, sizeof(v));
+    buf->recv(1, gloo::Slot::build(5, 0));
+    std::thread t([&] {
+      std::this_thread::sleep_for(std::chrono::milliseconds(200));
+      buf->abortWaitRecv();
+    });
+    const bool done = buf->waitRecv();
+    t.join();
+    if (done) throw std::runtime_error("aborted wait reported completion");
+  });
 }
 
 int procMain(int rank, int P, const std::string& dir, int count) {
@@ -368,6 +538,21 @@ int procMain(int rank, int P, const std::string& dir, int count) {
     auto ctx = connectHip(rank, P, 60000, store);
     deviceRank(ctx, count, 2, deviceRingChunked());
     deviceRank(ctx, count, 1, bridgeRingChunked());
+    // the reference's own gloo::allreduce on host buffers between processes
+    // (unbound buffers staged in node shared memory)
+    {
+      std::vector<float> a(4099), out(4099);
+      for (int j = 0; j < 4099; j++) a[j] = (float)(j * P + rank);
+      gloo::AllreduceOptions opts(ctx);
+      opts.setInput(a.data(), a.size());
+      opts.setOutput(out.data(), out.size());
+      opts.setReduceFunction(static_cast<void (*)(void*, const void*, const void*, size_t)>(&gloo::sum<float>));
+      opts.setMaxSegmentSize(1024);
+      gloo::allreduce(opts);
+      for (int j = 0; j < 4099; j++)
+        if ((double)out[j] != (double)j * P * P + P * (P - 1) / 2.0)
+          throw std::runtime_error("gloo::allreduce over processes: element " + std::to_string(j));
+    }
     // every rank finishes with the pairs before any tears down
     std::vector<char> done{1};
     store->set("done/" + std::to_string(rank), done);
@@ -421,7 +606,19 @@ int main(int argc, char** argv) {
   }
   cases.push_back({"context_factory/P3", [] { return contextFactoryCase(3); }});
   cases.push_back({"io_exception/silent_peer", [] { return ioExceptionCase(); }});
-  cases.push_back({"unbound_refused", [] { return unboundRefusedCase(); }});
+  cases.push_back({"many_live/P2/n10007", [] { return manyLiveCase(2, 10007); }});
+  cases.push_back({"many_live/P3/n1000", [] { return manyLiveCase(3, 1000); }});
+  for (int P : {2, 3, 4, 5}) {
+    cases.push_back({"ref_allreduce_ring_host/P" + std::to_string(P) + "/n10007",
+                     [=] { return refAllreduceCase(P, 10007, false); }});
+    cases.push_back({"ref_allreduce_bcube_host/P" + std::to_string(P) + "/n10007",
+                     [=] { return refAllreduceCase(P, 10007, true); }});
+  }
+  cases.push_back({"ref_allgather_host/P4/n777", [] { return refAllgatherCase(4, 777); }});
+  cases.push_back({"ref_reduce_host/P5/n3001", [] { return refReduceCase(5, 3001, 3); }});
+  cases.push_back({"unbound_recv_from_any/P4", [] { return unboundRecvFromAnyCase(4); }});
+  cases.push_back({"unbound_order_device/P2", [] { return unboundOrderDeviceCase(); }});
+  cases.push_back({"unbound_abort/P2", [] { return unboundAbortCase(); }});
   int failed = 0, ran = 0;
   for (auto& c : cases) {
     if (!filter.empty() && c.name.find(filter) == std::string::npos) continue;

@@ -12,8 +12,13 @@ headers and objects: connectFullMesh over the hip device, a device
 ring-chunked allreduce on its bound buffers (threads, and processes sharing
 receive buffers over HIP IPC), gloo::HipAllreduce* on that context, the
 reference's own AllreduceRingChunked / AllreduceHalvingDoubling templates and
-rendezvous::ContextFactory over it, IoException and the refusal of unbound
-buffers.  Closed form of gloo/test/base_test.h:184-236.
+rendezvous::ContextFactory over it, IoException, four ring-chunked instances
+live at once (12 slots per pair), and the unbound buffers: the reference's own
+gloo::allreduce (RING, BCUBE), gloo::allgather and gloo::reduce on host
+buffers over this transport, recv-from-any, per-slot ordering with device
+buffers, abort.  Processes: the device ring-chunked with the reference's
+host-word notification buffers (&dummy_) and gloo::allreduce on host
+buffers between processes.  Closed form of gloo/test/base_test.h:184-236.
 """
 import ctypes
 import os
@@ -124,7 +129,11 @@ def test_transport_program_on_gpu():
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith(("ok", "FAIL"))]
     assert lines and all(l.startswith("ok") for l in lines), r.stdout
-    assert len(lines) >= 30
+    assert len(lines) >= 45
+    names = " ".join(lines)
+    for case in ("many_live/", "ref_allreduce_ring_host/", "ref_allreduce_bcube_host/", "ref_allgather_host/",
+                 "ref_reduce_host/", "unbound_recv_from_any/", "unbound_order_device/", "unbound_abort/"):
+        assert case in names, case
 
 
 @pytest.mark.gpu
