@@ -501,10 +501,23 @@ bool UnboundBuffer::waitRecv(int* rank, std::chrono::milliseconds timeout) {
   GLOO_AMD_ENFORCE(!recvs_.empty(), "waitRecv without a pending recv");
   if (timeout.count() < 0) timeout = ctx.timeout();
   int src = -1;
+  // Receives on one slot from overlapping sources complete in the order they
+  // were posted: a receive is tried only when no earlier pending receive
+  // could take the same message (else a message arriving between two tries
+  // would land in the later receive's place).
+  auto blocked = [&](std::deque<PendingRecv>::iterator it) {
+    for (auto e = recvs_.begin(); e != it; ++e) {
+      if (e->slot != it->slot) continue;
+      for (int a : e->srcs)
+        for (int b : it->srcs)
+          if (a == b) return true;
+    }
+    return false;
+  };
   const bool done = pollUntil(
       [&] {
         for (auto it = recvs_.begin(); it != recvs_.end(); ++it)
-          if (dev_->take(it->srcs, it->slot, ptr_ + it->offset, it->nbytes, &src)) {
+          if (!blocked(it) && dev_->take(it->srcs, it->slot, ptr_ + it->offset, it->nbytes, &src)) {
             recvs_.erase(it);
             return true;
           }

@@ -128,12 +128,19 @@ struct Contexts {
 
 inline gloo_hip_context_t contextFor(const std::shared_ptr<::gloo::Context>& c, const void* anyDevicePtr) {
   Contexts& cs = Contexts::get();
+  {
+    std::lock_guard<std::mutex> lk(cs.m);
+    auto it = cs.byContext.find(c.get());
+    if (it != cs.byContext.end()) return it->second.second->handle();
+  }
+  // The bootstrap is collective: never under the registry's lock, which the
+  // other ranks of this process (threads) need for their own contexts.
+  std::unique_ptr<::gloo::hip_bridge::BootstrapContext> boot(
+      new ::gloo::hip_bridge::BootstrapContext(c, ::gloo::hip_bridge::deviceOf(anyDevicePtr)));
   std::lock_guard<std::mutex> lk(cs.m);
   auto& e = cs.byContext[c.get()];
-  if (!e.second) {
-    e.first = c;
-    e.second.reset(new ::gloo::hip_bridge::BootstrapContext(c, ::gloo::hip_bridge::deviceOf(anyDevicePtr)));
-  }
+  e.first = c;
+  e.second = std::move(boot);
   return e.second->handle();
 }
 

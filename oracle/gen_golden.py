@@ -361,7 +361,9 @@ def gen_bw_extend():
     seed = SEED + 50
     extra = [("reduce_scatter", "sum", "f16", 8, 1 << 24), ("reduce_scatter", "max", "bf16", 8, 1 << 24),
              ("reduce_scatter", "product", "bf16", 8, 1 << 26), ("reduce_scatter", "sum", "f16", 8, 1 << 26),
-             ("halving_doubling", "sum", "f32", 8, 1 << 26)]
+             ("halving_doubling", "sum", "f32", 8, 1 << 26),
+             # the top of the config-4 sweep: 1 GiB per rank
+             ("halving_doubling", "sum", "f32", 8, 1 << 28)]
     for i, (algo, op, dtype, P, n) in enumerate(extra):
         key = f"{algo}/{op}/{dtype}/P{P}/n{n}"
         if key in have:

@@ -174,6 +174,19 @@ def test_baseline_max_sizes(torch, env):
     check(res, BIG, runs=2)
 
 
+# The top of the config-4 sweep (S = 1 GiB per rank): HD fp32
+# 8 x 1 GiB, every rank's bytes against the reference's digest
+# (gen_golden.py bw_extend), eager run then graph capture, both routes.
+TOP = ["halving_doubling/sum/f32/P8/n268435456"]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("env", [{}, {"GLOO_AMD_MESH": "0"}], ids=["mesh", "reference_route"])
+def test_config4_sweep_top(torch, env):
+    res = run_processes(TOP, 8, env, runs=2, timeout=540)
+    check(res, TOP, runs=2)
+
+
 def large_p_keys():
     z = np.load(os.path.join(ROOT, "tests", "golden", "bw_golden.npz"))
     return sorted({k.rsplit("/", 1)[0] for k in z.files})

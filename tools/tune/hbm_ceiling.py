@@ -1,8 +1,7 @@
 """MEASUREMENT ONLY: the streaming ceiling of this chip for the config-2
 access mix, next to the product kernel, in one session.
 
-tools/tune/libceiling.so (hbm_ceiling.hip; build:
-  hipcc --offload-arch=gfx950 -O3 -fPIC -shared tools/tune/hbm_ceiling.hip -o tools/tune/libceiling.so)
+tools/tune/libceiling.so (hbm_ceiling.hip; built by gloo_amd/Makefile)
 holds streaming kernels with reduce_vec_kernel's access shape and R read /
 W write streams of 64 MiB.  Six rotated buffer sets (1.1 GiB) keep every
 launch streaming from HBM.  Each pattern: 20 warm-up + 300 back-to-back
@@ -46,9 +45,12 @@ def main():
         d = (ctypes.c_int * 4)()
         L.ceil_desc(i, d)
         r, w, u, b = list(d)
-        pats.append((f"R{r}W{w}_u{u}_b{b}", i, r + w, False))
+        lds = w >= 10  # w = 1 + 10 u: the reads go through LDS-DMA (buffer_load ... lds)
+        tag = "R2W1_ldsdma" if lds else f"R{r}W{w}"
+        w = w % 10
+        pats.append((f"{tag}_u{u}_b{b}", i, r + w, False))
         if r == 2 and w == 1:
-            pats.append((f"R{r}W{w}_inplace_u{u}_b{b}", i, r + w, True))
+            pats.append((f"{tag}_inplace_u{u}_b{b}", i, r + w, True))
     pats.append(("product_reduce_inplace", -1, 3, True))
     if args.only:
         pats = [p for p in pats if p[0].startswith(tuple(args.only.split(",")))]
@@ -67,7 +69,7 @@ def main():
     a, b, c = sets[0]
     for p in pats:
         name, i, streams, inplace = p
-        if i >= 0 and name.startswith(("R2W1_u", "R1W1")):
+        if i >= 0 and name.startswith(("R2W1_u", "R1W1", "R2W1_ldsdma_u")):
             L.ceil_run(i, c.data_ptr(), a.data_ptr(), b.data_ptr(), sink.data_ptr(), nbytes, s)
             torch.cuda.synchronize()
             want = a + b if name.startswith("R2W1") else a
