@@ -481,8 +481,10 @@ std::unique_ptr<Buffer> Pair::createRecvBuffer(uint64_t slot, void* ptr, size_t 
 
 void UnboundBuffer::send(int dst, uint64_t slot, size_t offset, size_t nbytes) {
   if (nbytes == std::numeric_limits<size_t>::max()) nbytes = offset <= size_ ? size_ - offset : 0;
-  GLOO_AMD_ENFORCE(offset + nbytes <= size_, "send of [", offset, ", +", nbytes, ") beyond a ", size_,
-                   "-byte buffer");
+  // an empty message may name any offset (BCUBE sends empty chunks past the
+  // end of short buffers, gloo/allreduce.cc:466-503)
+  GLOO_AMD_ENFORCE(nbytes == 0 || offset + nbytes <= size_, "send of [", offset, ", +", nbytes, ") beyond a ",
+                   size_, "-byte buffer");
   GLOO_AMD_ENFORCE(dst != dev_->context()->rank, "send to self");
   dev_->announce(dst, slot, ptr_ + offset, nbytes);
   sent_.push_back(dst);
@@ -490,8 +492,8 @@ void UnboundBuffer::send(int dst, uint64_t slot, size_t offset, size_t nbytes) {
 
 void UnboundBuffer::recv(const std::vector<int>& srcs, uint64_t slot, size_t offset, size_t nbytes) {
   if (nbytes == std::numeric_limits<size_t>::max()) nbytes = offset <= size_ ? size_ - offset : 0;
-  GLOO_AMD_ENFORCE(offset + nbytes <= size_, "recv of [", offset, ", +", nbytes, ") beyond a ", size_,
-                   "-byte buffer");
+  GLOO_AMD_ENFORCE(nbytes == 0 || offset + nbytes <= size_, "recv of [", offset, ", +", nbytes, ") beyond a ",
+                   size_, "-byte buffer");
   GLOO_AMD_ENFORCE(!srcs.empty(), "recv from no rank");
   recvs_.push_back({srcs, slot, offset, nbytes});
 }

@@ -363,7 +363,10 @@ def gen_bw_extend():
              ("reduce_scatter", "product", "bf16", 8, 1 << 26), ("reduce_scatter", "sum", "f16", 8, 1 << 26),
              ("halving_doubling", "sum", "f32", 8, 1 << 26),
              # the top of the config-4 sweep: 1 GiB per rank
-             ("halving_doubling", "sum", "f32", 8, 1 << 28)]
+             ("halving_doubling", "sum", "f32", 8, 1 << 28),
+             # the same per-rank size at 4 ranks: 4 rank processes fit one GPU's queues, so the
+             # one-GPU tests run the mesh route at 1 GiB per rank too
+             ("halving_doubling", "sum", "f32", 4, 1 << 28)]
     for i, (algo, op, dtype, P, n) in enumerate(extra):
         key = f"{algo}/{op}/{dtype}/P{P}/n{n}"
         if key in have:
