@@ -65,6 +65,20 @@ bool ipcDiag() {
   return v;
 }
 
+// GLOO_AMD_TRACE=1: construction phases to stderr (diagnosis of hangs).
+bool traceOn() {
+  static const bool v = [] {
+    const char* e = std::getenv("GLOO_AMD_TRACE");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+#define GLOO_AMD_TRACE_PHASE(...)                                                                       \
+  do {                                                                                                  \
+    if (traceOn()) std::fprintf(stderr, "[trace r%d inst%llu] %s\n", ctx_->rank, (unsigned long long)inst_, \
+                                strcat_(__VA_ARGS__).c_str());                                          \
+  } while (0)
+
 std::string handleHex(const hipIpcMemHandle_t& h) {
   const unsigned char* hb = reinterpret_cast<const unsigned char*>(&h);
   std::string hex;
@@ -434,6 +448,8 @@ Plan planFor(int algo, int rank, int size, size_t count, int nin, int nout, size
 
 // The text of a failed import check (tests and tools look for it).
 constexpr const char* kStaleImport = "does not show its contents";
+// Largest inbox arena shared between processes (see the constructor).
+constexpr size_t kMaxIpcArena = (size_t(2) << 30) - (size_t(2) << 20);
 }  // namespace
 
 void PlanExecutor::setBuffers(const std::vector<void*>& inputs, const std::vector<void*>& outputs) {
@@ -632,6 +648,33 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     std::memcpy(blob.data(), hello, sizeof(hello));
     where = ctx_->allgather(strcat_("inst", inst_, "/where"), blob);
   }
+  GLOO_AMD_TRACE_PHASE("where exchanged");
+  // Inbox arenas other processes map must stay below 2 GiB: importing a
+  // block of 2 GiB or more hangs in hipIpcOpenMemHandle on ROCm 7 / MI355X
+  // (profiles/round3/r3t_*, r3u_*; 1.5 GiB imports work).  Every rank
+  // decides from the same data (all ranks' plans, all ranks' pids), so all
+  // refuse together rather than some waiting at the next exchange.
+  {
+    bool anyCross = false;
+    for (int r = 0; r < P; r++) {
+      int32_t w[2];
+      GLOO_AMD_ENFORCE(where.at(r).size() == sizeof(w), "bad record from rank ", r);
+      std::memcpy(w, where[r].data(), sizeof(w));
+      if (w[0] != ctx_->pid()) anyCross = true;
+    }
+    const char* hm = std::getenv("GLOO_AMD_ARENA");
+    const bool host = workspace == GLOO_HIP_WORKSPACE_HOST || (hm && std::string(hm) == "host");
+    if (anyCross && !host) {
+      size_t maxArena = 0;
+      for (int r = 0; r < P; r++)
+        maxArena = std::max(maxArena, (size_t)planFor(planAlgo_, r, P, count_, (int)inputs_.size(),
+                                                      (int)ptrs_.size(), es_, maxSegmentBytes_, recvElems_).arena * es_);
+      GLOO_AMD_ENFORCE(maxArena < kMaxIpcArena, "an inbox arena of ", maxArena, " B (", count_, " elements of ", es_,
+                       " B) would be shared between processes; HIP IPC imports of 2 GiB and more hang on this "
+                       "platform: split the call into pieces of at most ", kMaxIpcArena / 2 / es_,
+                       " elements, or run the ranks as threads of one process");
+    }
+  }
   peers_.resize(P);
   bool sharesDeviceInProcess = false, crossSender = false;
   for (int peer : planPeers) {
@@ -676,8 +719,10 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     arenaShm_ = HostShm::create(arenaBytes);
     arena_ = static_cast<char*>(arenaShm_->dev);
   } else if (crossProcess_) {
+    GLOO_AMD_TRACE_PHASE("acquiring a slab of ", arenaBytes, " B fine=", fineArena_);
     arenaSlab_ = ipc::acquire(ctx_->device(), arenaBytes, fineArena_);
     arena_ = arenaSlab_->ptr;
+    GLOO_AMD_TRACE_PHASE("slab ", (void*)arena_, " of ", arenaSlab_->bytes, " B");
   } else if (fineArena_) {
     GLOO_AMD_HIP_ALLOC(hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), arenaBytes,
                                              hipDeviceMallocFinegrained));
@@ -790,7 +835,9 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   }
   std::vector<char> blob(sizeof(rec));
   std::memcpy(blob.data(), &rec, sizeof(rec));
+  GLOO_AMD_TRACE_PHASE("exchanging arena records");
   const std::vector<std::vector<char>> arenas = ctx_->allgather(strcat_("inst", inst_, "/arena"), blob);
+  GLOO_AMD_TRACE_PHASE("arena records exchanged");
 
   // From here to "ready" a rank may fail on its own (a refused IPC mapping,
   // an allocation): it still joins the ready exchange with its reason, so
@@ -850,7 +897,9 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       // must show the nonce the owner just wrote at the slab's start, and
       // the runtime's record of it must span the arena; anything else is a
       // hard error, never a silent misdelivery.
+      GLOO_AMD_TRACE_PHASE("importing rank ", peer, "'s arena ", (void*)pr.ptr, " (", pr.bytes, " B)");
       void* p = ipc::import(pr.pid, pr.incarnation, pr.ptr, pr.bytes, pr.handle);
+      GLOO_AMD_TRACE_PHASE("imported at ", p);
       uint64_t seen = 0;
       GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, p, sizeof(seen), hipMemcpyDeviceToHost, stream_));
       GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -948,6 +997,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     if (setupReason.empty()) setupReason = "setup failed";
     if (setupReason.size() > 900) setupReason.resize(900);  // one bootstrap record
   }
+  GLOO_AMD_TRACE_PHASE("ready: '", setupReason, "'");
   const auto ready = ctx_->allgather(strcat_("inst", inst_, "/ready"),
                                      std::vector<char>(setupReason.begin(), setupReason.end()));
   bool anyFailed = false;

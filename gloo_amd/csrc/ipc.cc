@@ -20,6 +20,16 @@ namespace {
 constexpr size_t kGranule = size_t(2) << 20;
 
 size_t sizeClass(size_t bytes) {
+  static const bool exact = [] {
+    const char* e = std::getenv("GLOO_AMD_IPC_EXACT");
+    return e && e[0] == '1';
+  }();
+  if (exact) return (bytes + kGranule - 1) / kGranule * kGranule;
+  // powers of two up to 1 GiB, then multiples of 256 MiB: a 1.5 GiB arena
+  // stays below 2^31 bytes (importing blocks of 2 GiB and more concurrently
+  // hangs: executor.cc)
+  constexpr size_t kBig = size_t(1) << 30, kStep = size_t(256) << 20;
+  if (bytes > kBig) return (bytes + kStep - 1) / kStep * kStep;
   size_t c = kGranule;
   while (c < bytes) c <<= 1;
   return c;

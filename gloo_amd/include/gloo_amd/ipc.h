@@ -16,8 +16,11 @@
 //   to the pool, and the next executor needing that size class on that device
 //   reuses it.  An address a peer has imported therefore always maps the
 //   same pages, and a byte-identical handle always means the same memory.
-//   Size classes are powers of two of 2 MiB granules, so the pool holds at
-//   most about twice the largest set of simultaneously live arenas.
+//   Size classes are powers of two of 2 MiB granules up to 1 GiB, then
+//   multiples of 256 MiB (a 1.5 GiB arena must not become a 2 GiB slab:
+//   importing blocks of 2 GiB or more hangs on this platform, so the
+//   executor refuses arenas that large between processes), so the pool holds
+//   at most about twice the largest set of simultaneously live arenas.
 //
 //   Importer side: a mapping is opened once per (exporter pid, exporter
 //   incarnation, exporter address) and kept — never closed while the

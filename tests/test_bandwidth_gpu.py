@@ -184,19 +184,53 @@ def test_baseline_max_sizes(torch, env):
 
 # The top of the config-4 sweep (S = 1 GiB per rank): HD fp32
 # at 1 GiB per rank, every rank's bytes against the reference's digest
-# (gen_golden.py bw_extend), eager run then graph capture.  8 ranks on the
-# reference route; the mesh route at 4 ranks: 8 rank processes oversubscribe
-# one GPU's hardware queues (4 each) and the mesh's concurrent 128 MiB copies
-# then stall behind time-sliced spinning waits for minutes
-# (profiles/round3/r3n_config4_8ranks_one_gpu.log); with one rank per GPU, as
-# on the driver's node, there is no such sharing.
+# (gen_golden.py bw_extend), eager run then graph capture, at 8 ranks (the
+# BASELINE config) and 4, on both routes.  The mesh route's inbox arena is
+# 1.75 GiB at P = 8 (14 x 128 MiB) and 1.5 GiB at P = 4; before the IPC
+# pool's size classes stopped at 256 MiB steps above 1 GiB, both were
+# rounded to 2 GiB slabs, whose import hangs (profiles/round3/r3s_*, r3t_*).
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("P,env", [(8, {"GLOO_AMD_MESH": "0"}), (4, {}), (4, {"GLOO_AMD_MESH": "0"})],
-                         ids=["P8_reference_route", "P4_mesh", "P4_reference_route"])
+@pytest.mark.parametrize("P,env", [(8, {}), (8, {"GLOO_AMD_MESH": "0"}), (4, {}), (4, {"GLOO_AMD_MESH": "0"})],
+                         ids=["P8_mesh", "P8_reference_route", "P4_mesh", "P4_reference_route"])
 def test_config4_sweep_top(torch, P, env):
     top = [f"halving_doubling/sum/f32/P{P}/n268435456"]
     res = run_processes(top, P, env, runs=2, timeout=540)
     check(res, top, runs=2)
+
+
+REFUSE_WORKER = r"""
+import os, sys
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, size, store = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+torch.cuda.set_device(0)
+ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=60000)
+n = 1 << 29   # 2 GiB of fp32 per rank: the mesh arena of P = 2 is 2 GiB
+buf = torch.zeros(n, device="cuda:0")
+try:
+    gloo_amd.Algorithm(ctx, "halving_doubling", "sum", "f32", [buf.data_ptr()], n)
+    print("RESULT accepted", flush=True)
+except gloo_amd.GlooHipError as e:
+    print("RESULT refused " + str(e), flush=True)
+ctx.close()
+"""
+
+
+@pytest.mark.timeout(200)
+def test_ipc_arena_of_2gib_refused_on_every_rank(torch):
+    """An inbox arena of 2 GiB or more shared between processes is refused by
+    every rank at once (importing one hangs in hipIpcOpenMemHandle), with the
+    way out in the message; nobody hangs."""
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(REFUSE_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT)
+        procs = [subprocess.Popen([sys.executable, w, str(r), "2", "file:" + os.path.join(d, "s")], env=e,
+                                  stdout=subprocess.PIPE, text=True) for r in range(2)]
+        outs = [p.communicate(timeout=180)[0] for p in procs]
+    for o in outs:
+        line = o.split("RESULT", 1)[1]
+        assert line.startswith(" refused") and "split the call" in line, o[-2000:]
 
 
 def large_p_keys():
