@@ -46,6 +46,8 @@ struct ArenaRecord {
   uint64_t mailboxNonce;     // written behind the mailbox's counters: likewise
   uint64_t incarnation;      // ipc::incarnation() of the exporting process
   uint64_t mailboxBytes;
+  uint64_t slabBytes;        // size class of the arena's pool slab (ipc.h): what an import maps
+  uint64_t mailboxSlabBytes; // likewise for the mailbox's slab
 };
 
 // A value no earlier arena of this process or its peers is likely to hold.
@@ -819,12 +821,16 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     }
   }
   rec.incarnation = ipc::incarnation();
+  if (arenaSlab_) rec.slabBytes = arenaSlab_->bytes;
   if (mailbox_) {
     rec.hasMailbox = 1;
     rec.mailboxPtr = reinterpret_cast<uint64_t>(mailbox_);
     rec.mailboxBytes = mbBytes;
     rec.mailboxNonce = mbNonce;
-    if (mailboxSlab_) rec.mailboxHandle = mailboxSlab_->handle;
+    if (mailboxSlab_) {
+      rec.mailboxHandle = mailboxSlab_->handle;
+      rec.mailboxSlabBytes = mailboxSlab_->bytes;
+    }
   }
   if (hostArena_) {
     rec.host = 1;
@@ -867,7 +873,8 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
           (void)hipGetLastError();
         }
       } else {
-        void* p = ipc::import(pr.pid, pr.incarnation, pr.mailboxPtr, pr.mailboxBytes + 4096, pr.mailboxHandle);
+        void* p = ipc::import(pr.pid, pr.incarnation, pr.mailboxPtr,
+                              std::max<uint64_t>(pr.mailboxBytes + 4096, pr.mailboxSlabBytes), pr.mailboxHandle);
         uint64_t seen = 0;
         GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, static_cast<char*>(p) + pr.mailboxBytes, sizeof(seen),
                                           hipMemcpyDeviceToHost, stream_));
@@ -898,7 +905,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       // the runtime's record of it must span the arena; anything else is a
       // hard error, never a silent misdelivery.
       GLOO_AMD_TRACE_PHASE("importing rank ", peer, "'s arena ", (void*)pr.ptr, " (", pr.bytes, " B)");
-      void* p = ipc::import(pr.pid, pr.incarnation, pr.ptr, pr.bytes, pr.handle);
+      void* p = ipc::import(pr.pid, pr.incarnation, pr.ptr, std::max<uint64_t>(pr.bytes, pr.slabBytes), pr.handle);
       GLOO_AMD_TRACE_PHASE("imported at ", p);
       uint64_t seen = 0;
       GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, p, sizeof(seen), hipMemcpyDeviceToHost, stream_));

@@ -3,6 +3,7 @@
 
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <map>
 #include <memory>
@@ -51,6 +52,18 @@ struct Pool {
     return *p;
   }
 };
+
+// Bytes the runtime maps from `m` to the end of its allocation (the
+// exporter's whole slab), or 0 when it keeps no record.
+size_t mappedSpan(void* m) {
+  void* rb = nullptr;
+  size_t rs = 0;
+  size_t span = 0;
+  if (hipMemGetAddressRange(&rb, &rs, m) == hipSuccess && rb && static_cast<char*>(rb) + rs > static_cast<char*>(m))
+    span = (size_t)(static_cast<char*>(rb) + rs - static_cast<char*>(m));
+  (void)hipGetLastError();
+  return span;
+}
 
 }  // namespace
 
@@ -142,6 +155,7 @@ void* import(int pid, uint64_t inc, uint64_t ptr, size_t bytes, const hipIpcMemH
   auto it = p.imports.find(key);
   if (it != p.imports.end()) {
     if (it->second.incarnation == inc && poolEnabled()) {
+      if (it->second.bytes < bytes) it->second.bytes = std::max(it->second.bytes, mappedSpan(it->second.ptr));
       GLOO_AMD_ENFORCE(it->second.bytes >= bytes, "slab of pid ", pid, " at ", (void*)ptr, " imported at ",
                        it->second.bytes, " B, now published at ", bytes, " B");
       return it->second.ptr;
@@ -153,7 +167,10 @@ void* import(int pid, uint64_t inc, uint64_t ptr, size_t bytes, const hipIpcMemH
   void* m = nullptr;
   GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&m, handle, hipIpcMemLazyEnablePeerAccess));
   p.opens++;
-  p.imports[key] = {inc, m, bytes};
+  // The mapping spans the exporter's whole slab (its size class), not just
+  // the bytes this first importer asked for: a later use of the same slab
+  // (a mailbox slab reused as an arena) may publish more of it.
+  p.imports[key] = {inc, m, std::max(bytes, mappedSpan(m))};
   return m;
 }
 
