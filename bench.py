@@ -914,12 +914,6 @@ def main():
         # the section marked as timed out, and the process exits.
         partial = {}
 
-        def fire():
-            if rank == 0:
-                out["xgmi_allreduce"] = dict(partial, error="watchdog: section exceeded 300 s")
-                print(json.dumps(out), flush=True)
-            os._exit(0)
-
         def efficiency(xr):
             """each GPU's reduce-kernel GiB/s while the config-3
             exchange runs (device stamps, graph replay) over the same GPU's

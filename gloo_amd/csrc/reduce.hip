@@ -544,11 +544,20 @@ int launch_fused(int op, void* dst, const void* src, size_t n, const uint64_t* w
 // has ONE lane poll relaxed, then ONE system-scope acquire, then a barrier
 // before any lane reads the inbox.
 // ---------------------------------------------------------------------------
-constexpr int kInterpBlock = 512;
+#ifndef GLOO_AMD_INTERP_BLOCK
+#define GLOO_AMD_INTERP_BLOCK 512
+#endif
+#ifndef GLOO_AMD_INTERP_COPY_UNROLL
+#define GLOO_AMD_INTERP_COPY_UNROLL 4
+#endif
+#ifndef GLOO_AMD_INTERP_FOLD_UNROLL
+#define GLOO_AMD_INTERP_FOLD_UNROLL 2
+#endif
+constexpr int kInterpBlock = GLOO_AMD_INTERP_BLOCK;
 // Packets per lane in flight per pass: a pass costs ONE memory latency (all
 // of its loads issue before the first use), so a 32 KiB copy is one pass.
-constexpr int kInterpCopyUnroll = 4;
-constexpr int kInterpFoldUnroll = 2;
+constexpr int kInterpCopyUnroll = GLOO_AMD_INTERP_COPY_UNROLL;
+constexpr int kInterpFoldUnroll = GLOO_AMD_INTERP_FOLD_UNROLL;
 
 // Bytes [0, n) of src to dst.  The destination is brought to a 16-byte
 // boundary element-wise (head); the body then moves in 16-byte packets
