@@ -198,6 +198,20 @@ size_t sliceBytes() {
   return v;
 }
 
+// Most bytes of the largest message per slice: above maxSlices() slices of
+// sliceBytes() the slices grow up to this, so plans with messages up to
+// maxSlices() x this run sliced (2 MiB with the defaults).  Measured, HD
+// fp32 4 MiB per rank, 2 rank processes on one MI355X: 32 x 64 KiB slices
+// 32.8 us against graph replay 40.9 us; at 8 MiB messages 128 x 64 KiB
+// slices lose to graph replay (profiles/round3/r3y_latency_*).
+size_t sliceCapBytes() {
+  static const size_t v = [] {
+    const char* e = std::getenv("GLOO_AMD_INTERP_SLICE_MAX_BYTES");
+    return e ? std::max<size_t>(sliceBytes(), std::strtoull(e, nullptr, 10)) : 2 * sliceBytes();
+  }();
+  return v;
+}
+
 // A range of one of a rank's buffers, symbolically: output j = j, input j =
 // kIn + j, the inbox arena = kArena.
 struct Access {
@@ -772,9 +786,8 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     size_t maxMsg = 0;
     for (const Step& s : plan_.steps) maxMsg = std::max(maxMsg, (size_t)s.length * es_);
     const size_t want = std::min<size_t>(maxSlices(), std::max<size_t>(1, (maxMsg + sliceBytes() - 1) / sliceBytes()));
-    // above maxSlices() slices of sliceBytes() graph replay is as fast
-    // (measured: 2 MiB messages, 32 slices 41.5 us vs graph 39.5 us)
-    if (maxMsg <= (size_t)maxSlices() * sliceBytes()) {
+    // above maxSlices() slices of sliceCapBytes() graph replay is as fast
+    if (maxMsg <= (size_t)maxSlices() * sliceCapBytes()) {
       std::map<std::pair<int, int>, size_t> decl;  // (sender, slot) -> arena offset
       for (const Step& d : plan_.steps)
         if (d.kind == GLOO_HIP_STEP_DECL_RECV) decl[{d.peer, d.slot}] = d.dst_off;

@@ -548,14 +548,17 @@ int launch_fused(int op, void* dst, const void* src, size_t n, const uint64_t* w
 #define GLOO_AMD_INTERP_BLOCK 512
 #endif
 #ifndef GLOO_AMD_INTERP_COPY_UNROLL
-#define GLOO_AMD_INTERP_COPY_UNROLL 4
+#define GLOO_AMD_INTERP_COPY_UNROLL 8
 #endif
 #ifndef GLOO_AMD_INTERP_FOLD_UNROLL
-#define GLOO_AMD_INTERP_FOLD_UNROLL 2
+#define GLOO_AMD_INTERP_FOLD_UNROLL 4
 #endif
 constexpr int kInterpBlock = GLOO_AMD_INTERP_BLOCK;
 // Packets per lane in flight per pass: a pass costs ONE memory latency (all
-// of its loads issue before the first use), so a 32 KiB copy is one pass.
+// of its loads issue before the first use), so a 64 KiB copy is one pass and
+// a fold moves 32 KiB per source per pass (210-223 VGPRs, no spills: still
+// one 512-lane workgroup per CU, as with 4 / 2 packets; 4 MiB HD per rank
+// 32.8 us against 34.2 us, profiles/round3/r3y_latency_interp_variants.jsonl).
 constexpr int kInterpCopyUnroll = GLOO_AMD_INTERP_COPY_UNROLL;
 constexpr int kInterpFoldUnroll = GLOO_AMD_INTERP_FOLD_UNROLL;
 

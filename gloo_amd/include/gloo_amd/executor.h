@@ -51,10 +51,11 @@
 // process, the steps are resolved once into a device-resident InterpStep
 // list (signal.h) and every run() is ONE one-workgroup launch walking it —
 // a small allreduce costs its cross-rank hops, not a kernel boundary each.
-// Larger plans (messages up to kMaxSlices x GLOO_AMD_INTERP_SLICE_BYTES) run
-// SLICED when every rank's plan allows it: one workgroup per
-// GLOO_AMD_INTERP_SLICE_BYTES of the largest message, each running the whole
-// plan on its slice of every step with its own flag words (signal.h).
+// Larger plans (messages up to GLOO_AMD_INTERP_MAX_SLICES (32) x
+// GLOO_AMD_INTERP_SLICE_MAX_BYTES (64 KiB)) run SLICED when every rank's plan
+// allows it: one workgroup per GLOO_AMD_INTERP_SLICE_BYTES (32 KiB) of the
+// largest message, at most 32, each running the whole plan on its slice of
+// every step with its own flag words (signal.h).
 #pragma once
 
 #include <hip/hip_runtime_api.h>

@@ -131,7 +131,6 @@ class Device {
   std::vector<std::vector<bool>> channelUsed_;  // [src][idx], this rank as receiver
   void* block_ = nullptr;
   size_t blockBytes_ = 0;
-  uint64_t staged_ = 0;  // staging segments created so far (names)
 };
 
 class Buffer {

@@ -603,9 +603,10 @@ def test_processes_interp(torch, golden_sched, case, env, interp):
 
 def _expected_slices(case, env):
     """The slice count the executor must agree on (executor.cc): per rank
-    ceil(largest message / GLOO_AMD_INTERP_SLICE_BYTES) if that is at most
-    32 and its plan is sliceable (plan_sim.sliceable, the rule restated), the
-    minimum over ranks, 1 if that is not above 1."""
+    min(32, ceil(largest message / GLOO_AMD_INTERP_SLICE_BYTES)) if the
+    largest message is at most 32 x GLOO_AMD_INTERP_SLICE_MAX_BYTES (default
+    twice the slice bytes) and its plan is sliceable (plan_sim.sliceable, the
+    rule restated), the minimum over ranks, 1 if that is not above 1."""
     from plan_sim import get_plan, sliceable
     algo, P = case.split("/")[0], int(case.split("/")[3][1:])
     n = int(case.split("/")[-1][1:])
@@ -622,11 +623,12 @@ def _expected_slices(case, env):
     if algo == "reduce_scatter":
         recv = np.array([n // P + (1 if r < n % P else 0) for r in range(P)], np.int32)
     sb = int(env.get("GLOO_AMD_INTERP_SLICE_BYTES", 32768))
+    cap = max(sb, int(env.get("GLOO_AMD_INTERP_SLICE_MAX_BYTES", 2 * sb)))
     props = []
     for r in range(P):
         steps, _ = get_plan(route, r, P, n, 1, recv, elem_size=es)
         biggest = max(s.length for s in steps) * es
-        ok = biggest <= 32 * sb and sliceable(route, P, n, r, recv=recv, elem_size=es)
+        ok = biggest <= 32 * cap and sliceable(route, P, n, r, recv=recv, elem_size=es)
         props.append(min(32, max(1, -(-biggest // sb))) if ok else 0)
     g = min(props)
     return g if g > 1 else 1
