@@ -78,6 +78,38 @@ __global__ __launch_bounds__(B) void stream_lds_k(float* c, const float* a, cons
   }
 }
 
+// 2-read + 1-write with explicit cache policies for the loads (LP) and the
+// store (SP), and optionally the two read streams interleaved packet by packet
+// (IL): round-3 variants of the config-2 mix (policy bits on gfx950: sc0 = 1,
+// nt = 2, sc1 = 16).
+template <int U, int B, int LP, int SP, int IL>
+__global__ __launch_bounds__(B) void stream_pol_k(float* c, const float* a, const float* b, uint32_t*) {
+  constexpr uint32_t kTile = (uint32_t)B * U * 16;
+  const size_t base = (size_t)blockIdx.x * kTile;
+  const auto ra = rsrc(reinterpret_cast<const char*>(a) + base, kTile);
+  const auto rb = rsrc(reinterpret_cast<const char*>(b) + base, kTile);
+  const auto rc = rsrc(reinterpret_cast<const char*>(c) + base, kTile);
+  const uint32_t lane = threadIdx.x * 16u;
+  u32x4 x[U], y[U];
+  if (IL) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      x[u] = __builtin_amdgcn_raw_buffer_load_b128(ra, lane + u * B * 16, 0, LP);
+      y[u] = __builtin_amdgcn_raw_buffer_load_b128(rb, lane + u * B * 16, 0, LP);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) x[u] = __builtin_amdgcn_raw_buffer_load_b128(ra, lane + u * B * 16, 0, LP);
+#pragma unroll
+    for (int u = 0; u < U; u++) y[u] = __builtin_amdgcn_raw_buffer_load_b128(rb, lane + u * B * 16, 0, LP);
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const f32x4 s = __builtin_bit_cast(f32x4, x[u]) + __builtin_bit_cast(f32x4, y[u]);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, s), rc, lane + u * B * 16, 0, SP);
+  }
+}
+
 struct P {
   int r, w, u, b;
   void (*launch)(float*, const float*, const float*, uint32_t*, size_t, hipStream_t);
@@ -91,13 +123,24 @@ struct P {
   {2, 1 + 10 * U, U, B, [](float* c, const float* a, const float* b, uint32_t* sink, size_t bytes, hipStream_t s) { \
      stream_lds_k<U, B><<<(unsigned)(bytes / ((size_t)B * U * 16)), B, 0, s>>>(c, a, b, sink);          \
    }},
+#define XP(U, B, LP, SP, IL)                                                                            \
+  {2, 1 + 100 * (1 + LP + 32 * SP + 1024 * IL), U, B,                                                   \
+   [](float* c, const float* a, const float* b, uint32_t* sink, size_t bytes, hipStream_t s) {          \
+     stream_pol_k<U, B, LP, SP, IL><<<(unsigned)(bytes / ((size_t)B * U * 16)), B, 0, s>>>(c, a, b, sink); \
+   }},
 // pattern 8 (R2W1 u2 b512) is the product kernel's shape: bench.py times it
 // beside the product in the same run; 10-12 read through LDS-DMA (w = 1 + 10 u)
 static const P kP[] = {X(1, 0, 2, 512) X(1, 0, 4, 512) X(0, 1, 2, 512) X(0, 1, 4, 512) X(1, 1, 2, 512)
                            X(1, 1, 4, 512) X(2, 0, 2, 512) X(2, 0, 4, 512) X(2, 1, 2, 512) X(2, 1, 4, 256)
-                               XL(1, 512) XL(2, 512) XL(2, 256)};
+                               XL(1, 512) XL(2, 512) XL(2, 256)
+                                   // 13..: cache policies, interleaved reads, wider tiles (w = 1 + 100 * code)
+                                   XP(2, 512, 2, 2, 1) XP(2, 512, 2, 18, 0) XP(2, 512, 2, 19, 0)
+                                       XP(2, 512, 2, 0, 0) XP(2, 512, 0, 2, 0) XP(2, 512, 3, 2, 0)
+                                           XP(2, 512, 18, 2, 0) XP(2, 1024, 2, 2, 0) XP(1, 1024, 2, 2, 0)
+                                               XP(4, 256, 2, 2, 1) XP(1, 512, 2, 2, 0)};
 #undef X
 #undef XL
+#undef XP
 
 extern "C" {
 int ceil_count() { return (int)(sizeof(kP) / sizeof(kP[0])); }

@@ -23,15 +23,16 @@ def main():
     import torch
     import gloo_amd as hip
 
-    L = ctypes.CDLL(os.path.join(HERE, "libceiling.so"))
-    vp = ctypes.c_void_p
-    L.ceil_run.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_size_t, vp]
     import argparse
     ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", default="libceiling.so", help="libceiling_pre.so: kernel arguments preloaded in SGPRs")
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--mib", type=int, default=64, help="MiB per stream per launch")
     ap.add_argument("--only", default="", help="comma list of pattern prefixes")
     args = ap.parse_args()
+    L = ctypes.CDLL(os.path.join(HERE, args.lib))
+    vp = ctypes.c_void_p
+    L.ceil_run.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_size_t, vp]
     steps = args.steps
     nbytes = args.mib << 20
     n = nbytes // 4
@@ -45,9 +46,15 @@ def main():
         d = (ctypes.c_int * 4)()
         L.ceil_desc(i, d)
         r, w, u, b = list(d)
-        lds = w >= 10  # w = 1 + 10 u: the reads go through LDS-DMA (buffer_load ... lds)
-        tag = "R2W1_ldsdma" if lds else f"R{r}W{w}"
-        w = w % 10
+        if w >= 100:  # w = 1 + 100 * (1 + LP + 32 SP + 1024 IL): stream_pol_k
+            code = w // 100 - 1
+            lp, sp, il = code % 32, (code // 32) % 32, code // 1024
+            tag = f"R2W1_pol_lp{lp}_sp{sp}{'_il' if il else ''}"
+            w = 1
+        else:
+            lds = w >= 10  # w = 1 + 10 u: the reads go through LDS-DMA (buffer_load ... lds)
+            tag = "R2W1_ldsdma" if lds else f"R{r}W{w}"
+            w = w % 10
         pats.append((f"{tag}_u{u}_b{b}", i, r + w, False))
         if r == 2 and w == 1:
             pats.append((f"{tag}_inplace_u{u}_b{b}", i, r + w, True))
@@ -69,7 +76,7 @@ def main():
     a, b, c = sets[0]
     for p in pats:
         name, i, streams, inplace = p
-        if i >= 0 and name.startswith(("R2W1_u", "R1W1", "R2W1_ldsdma_u")):
+        if i >= 0 and name.startswith(("R2W1_u", "R1W1", "R2W1_ldsdma_u", "R2W1_pol")):
             L.ceil_run(i, c.data_ptr(), a.data_ptr(), b.data_ptr(), sink.data_ptr(), nbytes, s)
             torch.cuda.synchronize()
             want = a + b if name.startswith("R2W1") else a
@@ -88,7 +95,7 @@ def main():
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / steps
             tbs = p[2] * nbytes / us / 1e6
-            print(json.dumps({"rep": rep, "mib": args.mib, "pattern": p[0], "streams": p[2], "us": round(us, 2),
+            print(json.dumps({"rep": rep, "lib": args.lib, "mib": args.mib, "pattern": p[0], "streams": p[2], "us": round(us, 2),
                               "TBs": round(tbs, 3), "frac_of_8TBs": round(tbs / 8.0, 4)}), flush=True)
 
 
