@@ -284,7 +284,8 @@ def _mode_dict(out):
     err = lib.gloo_hip_last_error()
     err = err.decode() if isinstance(err, bytes) else (err or "")
     return {"device_signal": bool(out[0]), "fine_arena": out[1] == 1,
-            "host_arena": out[1] == 2, "kernel_copy": bool(out[2]),
+            "host_arena": out[1] == 2, "kernel_copy": bool(out[2] & 1),
+            "fold_send": bool(out[2] & 2),
             "graph": out[3] == 1, "interp": out[3] >= 2, "interp_slices": max(0, out[3] - 1),
             "graph_error": err[len("graph capture abandoned: "):]
             if err.startswith("graph capture abandoned: ") else ""}

@@ -980,6 +980,9 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     kernelCopy_ = cmode == "kernel";
     autoCopy_ = cmode == "auto";
     batchKernelCopy_ = cmode != "memcpy";
+    // Fold + forward (enqueue, FOLD): "0" keeps the fold and its SENDs apart.
+    const char* fs = std::getenv("GLOO_AMD_FOLD_SEND");
+    foldSend_ = !(fs && std::string(fs) == "0");
     // Workgroups per copy (executor.h): a few dozen saturate an xGMI link.
     // GLOO_AMD_COPY_BLOCKS overrides both the remote and the same-GPU size.
     if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS")) {
@@ -1790,6 +1793,37 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         GLOO_AMD_ENFORCE(!foldSrcs.empty() && foldSrcs.size() <= GLOO_HIP_MAX_SRCS, "bad fold");
         if (profiling_) GLOO_AMD_HIP_CHECK(hipEventRecord(event(), stream_));
         const int mode = s.flags & GLOO_HIP_FOLD_TREE ? 2 : s.flags & GLOO_HIP_FOLD_REVERSE ? 1 : 0;
+        // Fold + forward: the SENDs right after a fold that ship its result
+        // unchanged (a mesh owner's return of its finished range) ride in the
+        // fold's own pass, and its last workgroup signals them.  Device
+        // signalling only; off while the reduce kernels are being timed, so
+        // events and stamps keep measuring a pure fold.
+        if (foldSend_ && deviceSignal_ && !custom_ && !profiling_ && !stamping_ && s.length > 0 &&
+            !(s.flags & GLOO_HIP_DST_ARENA)) {
+          char* fdst = userPtr(0) + s.dst_off * es_;
+          FwdDesc fwd[kMaxCopyEntries];
+          int nf = 0;
+          size_t j = i + 1;
+          for (; j < steps.size() && nf < kMaxCopyEntries; j++) {
+            const Step& t = steps[j];
+            if (t.kind != GLOO_HIP_STEP_SEND || (t.flags & (GLOO_HIP_SRC_ARENA | GLOO_HIP_FROM_INPUTS)) ||
+                t.src_off != s.dst_off || t.length != s.length)
+              break;
+            fwd[nf++] = FwdDesc{sendDst(t), sigFlag(t.peer, t.slot), seqOf(j, r, graph)};
+          }
+          // every SEND of the run must be taken, or the rest would still
+          // re-read the result; a partial run stays unfused
+          if (nf > 0 && (j == steps.size() || steps[j].kind != GLOO_HIP_STEP_SEND)) {
+            const Step& t0 = steps[i + 1];
+            checkRc(launchFoldSend(op_, dtype_, fdst, foldSrcs.data(), (int)foldSrcs.size(), s.length, mode, fwd,
+                                   nf, ticket_ + (size_t)t0.peer * GLOO_HIP_NUM_SLOTS + t0.slot, epoch, stream_),
+                    "fold+forward");
+            foldSendUsed_ = true;
+            foldSrcs.clear();
+            i = j - 1;
+            break;
+          }
+        }
         {
           StampScope stamp(slotOf(i));
           checkRc(launchFold(op_, dtype_, userOrArena(s.flags & GLOO_HIP_DST_ARENA) + s.dst_off * es_,

@@ -31,6 +31,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -190,6 +191,7 @@ __device__ __forceinline__ u32x4 apply_packet<TrU8, GLOO_HIP_SUM>(u32x4 a, u32x4
 // are discarded) without per-lane branches.
 constexpr int kRsrcFlags = 0x00020000;  // gfx950 raw-buffer word 3
 constexpr int kAuxNT = 2;               // cache policy `nt`: streamed once
+constexpr int kAuxWT = 1 | 2 | 16;      // `sc0 nt sc1`: streamed once, written through (not held in L2)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, kRsrcFlags);
@@ -214,8 +216,8 @@ __device__ __forceinline__ Src src_of(const void* body) {
   return Src{reinterpret_cast<const char*>(p & ~uintptr_t(15)), (uint32_t)(p & 15)};
 }
 template <int AUX>
-__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, AUX);
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v, uint32_t soff = 0) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, soff, AUX);
 }
 
 // Element-wise head / tail: elements [0, head) and [tail0, n) of the chunk,
@@ -275,7 +277,12 @@ thread_local uint64_t* t_stamp = nullptr;  // stamp slot of the next reduce laun
 // of the tile are issued before the first use.  Measured on MI355X (profiles/
 // round1): `nt` on both loads and stores, UNROLL 2, BLOCK 512, one tile per
 // workgroup is the fastest of 126 variants for the 64 MiB fp32 chunk.
-template <class Tr, int OP, int UNROLL, int BLOCK, int LAUX, int SAUX>
+//
+// IL: the two operands' loads are issued interleaved, packet by packet (a0 b0
+// a1 b1) rather than stream by stream (a0 a1 b0 b1).  Round 3, in the
+// stripped harness (tools/tune/hbm_ceiling.hip, profiles/round3/r3ab_*):
+// 0.800-0.802 against 0.796-0.800 of 8 TB/s for the in-place 2R + 1W mix.
+template <class Tr, int OP, int UNROLL, int BLOCK, int LAUX, int SAUX, int IL = 1>
 __global__ __launch_bounds__(BLOCK) void reduce_vec_kernel(
     typename Tr::Storage* c, const typename Tr::Storage* a,
     const typename Tr::Storage* b, size_t n, size_t head, uint64_t* stamp) {
@@ -296,10 +303,18 @@ __global__ __launch_bounds__(BLOCK) void reduce_vec_kernel(
   const auto rc = make_rsrc(reinterpret_cast<const char*>(c + head) + base, bytes);
   const uint32_t lane_off = threadIdx.x * 16u;
   u32x4 x[UNROLL], y[UNROLL];
+  if constexpr (IL) {
 #pragma unroll
-  for (int u = 0; u < UNROLL; u++) x[u] = bload<LAUX>(ra, lane_off + u * BLOCK * 16, sa.mis);
+    for (int u = 0; u < UNROLL; u++) {
+      x[u] = bload<LAUX>(ra, lane_off + u * BLOCK * 16, sa.mis);
+      y[u] = bload<LAUX>(rb, lane_off + u * BLOCK * 16, sb.mis);
+    }
+  } else {
 #pragma unroll
-  for (int u = 0; u < UNROLL; u++) y[u] = bload<LAUX>(rb, lane_off + u * BLOCK * 16, sb.mis);
+    for (int u = 0; u < UNROLL; u++) x[u] = bload<LAUX>(ra, lane_off + u * BLOCK * 16, sa.mis);
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) y[u] = bload<LAUX>(rb, lane_off + u * BLOCK * 16, sb.mis);
+  }
 #pragma unroll
   for (int u = 0; u < UNROLL; u++)
     bstore<SAUX>(rc, lane_off + u * BLOCK * 16, apply_packet<Tr, OP>(x[u], y[u]));
@@ -761,6 +776,7 @@ struct CopyList {
   uint64_t* flag[kMaxCopies];
   Seq seq[kMaxCopies];
   unsigned* ticket[kMaxCopies];
+  int lean;  // completion protocol (fwdLean): write-through stores, one release by the ticket holder
 };
 
 __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(CopyList L, const uint64_t* epoch) {
@@ -790,20 +806,32 @@ __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(CopyList L, con
     u32x4 v[kCopyUnroll];
 #pragma unroll
     for (int u = 0; u < kCopyUnroll; u++) v[u] = bload<kAuxNT>(rs, lane_off + u * kCopyBlock * 16, ss.mis);
+    if (L.lean && L.flag[j]) {
 #pragma unroll
-    for (int u = 0; u < kCopyUnroll; u++) bstore<kAuxNT>(rd, lane_off + u * kCopyBlock * 16, v[u]);
+      for (int u = 0; u < kCopyUnroll; u++) bstore<kAuxWT>(rd, lane_off + u * kCopyBlock * 16, v[u]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < kCopyUnroll; u++) bstore<kAuxNT>(rd, lane_off + u * kCopyBlock * 16, v[u]);
+    }
   }
   if (!L.flag[j]) return;  // a plain (local) copy: nobody to tell
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!L.lean) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     const uint64_t ep = epoch ? *epoch : 0;
-    const unsigned t = __hip_atomic_fetch_add(L.ticket[j], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned t = L.lean ? __hip_atomic_fetch_add(L.ticket[j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : __hip_atomic_fetch_add(L.ticket[j], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
     if (t == nb - 1) {
       // last workgroup of this entry: reset the counter for the next launch
       // (launches on one channel's counter are stream-ordered), publish
+      if (L.lean) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       __hip_atomic_store(L.ticket[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       __hip_atomic_store(L.flag[j], L.seq[j].base + ep * L.seq[j].perRun, __ATOMIC_RELEASE,
@@ -816,6 +844,20 @@ __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(CopyList L, con
 // Host-side dispatch.
 // ---------------------------------------------------------------------------
 int g_variant = 0;  // fp32 SUM kernel variant (measurement knob)
+
+// Completion protocol of the kernels that signal a peer after a multi-
+// workgroup write (copy_signal_kernel, fold_send_kernel), GLOO_AMD_FWD_RELEASE:
+// "last" (the default) = the signalled bytes are stored write-through
+// (sc0 nt sc1), each workgroup drains and takes a relaxed ticket, and only the
+// ticket holder releases at system scope (one L2 write-back per launch);
+// "each" = every workgroup releases at system scope before its ticket.
+int fwdLean() {
+  static const int v = [] {
+    const char* e = std::getenv("GLOO_AMD_FWD_RELEASE");
+    return e && std::string(e) == "each" ? 0 : 1;
+  }();
+  return v;
+}
 
 int set_error(int code, const char* what) { return setError(code, what); }
 
@@ -831,14 +873,190 @@ constexpr int kMultiUnroll = 2;
 
 inline size_t ceil_div(size_t a, size_t b) { return (a + b - 1) / b; }
 
-template <class Tr, int OP, int UNROLL, int BLOCK, int LAUX, int SAUX>
+// ---------------------------------------------------------------------------
+// Fold + forward (signal.h launchFoldSend): a FOLD whose finished range the
+// plan then SENDs unchanged to up to kMaxCopyEntries peers (a mesh owner
+// returning its range to every rank).  Each result tile is stored to dst AND
+// to every forward destination in the same pass — the result is never read
+// back, and the fold, the copies and their signal kernels become one launch.
+// Completion as copy_signal_kernel: every wave drains, one lane releases at
+// system scope and takes a ticket; the workgroup holding the launch's last
+// ticket resets the counter and publishes every forward's flag.  The mode is
+// a uniform runtime argument (0 left, 1 reverse, 2 tree), as in
+// reduce_multi_vec_kernel, whose element order this repeats exactly.
+// ---------------------------------------------------------------------------
+struct FwdList {
+  int n;
+  char* dst[kMaxCopyEntries];       // any element-aligned address
+  uint64_t* flag[kMaxCopyEntries];  // nullptr: no arrival flag for this entry
+  Seq seq[kMaxCopyEntries];
+  unsigned* ticket;                 // zero between launches; nullptr: no signals
+  int lean;                         // completion protocol (launchFoldSend)
+};
+
+template <class Tr, int OP>
+__global__ __launch_bounds__(kVecBlock) void fold_send_kernel(typename Tr::Storage* dst, SrcList srcs, int k,
+                                                              int mode, size_t n, size_t head, FwdList F,
+                                                              const uint64_t* epoch, uint64_t* stamp) {
+  using S = typename Tr::Storage;
+  constexpr int kV = 16 / sizeof(S);
+  constexpr int UNROLL = kMultiUnroll, BLOCK = kVecBlock;
+  constexpr uint32_t kTileBytes = (uint32_t)BLOCK * UNROLL * 16;
+  stamp_begin(stamp);
+  const size_t nvec = (n - head) / kV;
+  const size_t tail0 = head + nvec * kV;
+  if (blockIdx.x == 0) {
+    const size_t t = threadIdx.x;
+    for (int pass = 0; pass < 2; pass++) {
+      const size_t i = pass == 0 ? t : tail0 + t;
+      if ((pass == 0 && t < head) || (pass == 1 && i < n)) {
+        S acc;
+        if (mode == 2) {
+          S v[GLOO_HIP_MAX_SRCS];
+#pragma unroll
+          for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
+            if (j < k) v[j] = static_cast<const S*>(srcs.p[j])[i];
+          acc = tree_fold<Tr, OP>(v, k);
+        } else {
+          acc = static_cast<const S*>(srcs.p[0])[i];
+          for (int j = 1; j < k; j++) {
+            const S v = static_cast<const S*>(srcs.p[j])[i];
+            acc = mode == 1 ? apply<Tr, OP>(v, acc) : apply<Tr, OP>(acc, v);
+          }
+        }
+        dst[i] = acc;
+        for (int r = 0; r < F.n; r++) reinterpret_cast<S*>(F.dst[r])[i] = acc;
+      }
+    }
+  }
+  const size_t body = nvec * 16;
+  const size_t base = (size_t)blockIdx.x * kTileBytes;
+  if (base < body) {
+    const uint32_t bytes = (uint32_t)((body - base) < kTileBytes ? (body - base) : kTileBytes);
+    const uint32_t lane_off = threadIdx.x * 16u;
+    u32x4 acc[UNROLL];
+    if (mode == 2) {
+      u32x4 v[GLOO_HIP_MAX_SRCS][UNROLL];
+#pragma unroll
+      for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
+        if (j < k) {
+          const Src sj = src_of(static_cast<const S*>(srcs.p[j]) + head);
+          const auto rj = make_rsrc(sj.base + base, bytes + sj.mis);
+#pragma unroll
+          for (int u = 0; u < UNROLL; u++) v[j][u] = bload<kAuxNT>(rj, lane_off + u * BLOCK * 16, sj.mis);
+        }
+#pragma unroll
+      for (int w = GLOO_HIP_MAX_SRCS; w > 1; w >>= 1)
+        if (w <= k) {
+#pragma unroll
+          for (int j = 0; j < w / 2; j++)
+#pragma unroll
+            for (int u = 0; u < UNROLL; u++) v[j][u] = apply_packet<Tr, OP>(v[2 * j][u], v[2 * j + 1][u]);
+        }
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) acc[u] = v[0][u];
+    } else {
+      {
+        const Src s0 = src_of(static_cast<const S*>(srcs.p[0]) + head);
+        const auto r0 = make_rsrc(s0.base + base, bytes + s0.mis);
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++) acc[u] = bload<kAuxNT>(r0, lane_off + u * BLOCK * 16, s0.mis);
+      }
+      for (int j = 1; j < k; j++) {
+        const Src sj = src_of(static_cast<const S*>(srcs.p[j]) + head);
+        const auto rj = make_rsrc(sj.base + base, bytes + sj.mis);
+        u32x4 r[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++) r[u] = bload<kAuxNT>(rj, lane_off + u * BLOCK * 16, sj.mis);
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++)
+          acc[u] = mode == 1 ? apply_packet<Tr, OP>(r[u], acc[u]) : apply_packet<Tr, OP>(acc[u], r[u]);
+      }
+    }
+    const auto rd = make_rsrc(reinterpret_cast<const char*>(dst + head) + base, bytes);
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rd, lane_off + u * BLOCK * 16, acc[u]);
+    for (int r = 0; r < F.n; r++) {
+      // a forward destination may sit at another residue mod 16 B than dst
+      // (ragged inbox regions): its misalignment rides in soffset, as a
+      // relatively misaligned source's does
+      const Src fr = src_of(F.dst[r] + head * sizeof(S));
+      const auto rf = make_rsrc(fr.base + base, bytes + fr.mis);
+      if (F.lean) {
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++) bstore<kAuxWT>(rf, lane_off + u * BLOCK * 16, acc[u], fr.mis);
+      } else {
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rf, lane_off + u * BLOCK * 16, acc[u], fr.mis);
+      }
+    }
+  }
+  stamp_end(stamp);
+  if (!F.ticket) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // lean: the forwarded bytes were stored write-through (sc0 sc1) and this
+    // workgroup's waves have all seen them acknowledged, so only the ticket
+    // holder releases (one L2 write-back per launch instead of one per
+    // workgroup); otherwise every workgroup releases before its ticket
+    if (!F.lean) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const uint64_t ep = epoch ? *epoch : 0;
+    const unsigned t = F.lean ? __hip_atomic_fetch_add(F.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : __hip_atomic_fetch_add(F.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == gridDim.x - 1) {
+      if (F.lean) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __hip_atomic_store(F.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      for (int r = 0; r < F.n; r++)
+        if (F.flag[r])
+          __hip_atomic_store(F.flag[r], F.seq[r].base + ep * F.seq[r].perRun, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+template <class Tr, int OP>
+int launch_fold_send(void* dst, const SrcList& list, int k, int mode, size_t n, const FwdList& F,
+                     const uint64_t* epoch, hipStream_t s) {
+  using S = typename Tr::Storage;
+  size_t head = ((16 - ((uintptr_t)dst & 15)) & 15) / sizeof(S);
+  if (head > n) head = n;
+  constexpr int kV = 16 / sizeof(S);
+  const size_t nvec = (n - head) / kV;
+  size_t grid = ceil_div(nvec, (size_t)kVecBlock * kMultiUnroll);
+  if (grid == 0) grid = 1;
+  fold_send_kernel<Tr, OP><<<dim3((unsigned)grid), dim3(kVecBlock), 0, s>>>(static_cast<S*>(dst), list, k, mode, n,
+                                                                          head, F, epoch, t_stamp);
+  return check_launch("fold_send_kernel");
+}
+
+template <class Tr>
+int by_op_fold_send(int op, void* dst, const SrcList& list, int k, int mode, size_t n, const FwdList& F,
+                    const uint64_t* epoch, hipStream_t s) {
+  switch (op) {
+    case GLOO_HIP_SUM: return launch_fold_send<Tr, GLOO_HIP_SUM>(dst, list, k, mode, n, F, epoch, s);
+    case GLOO_HIP_PRODUCT: return launch_fold_send<Tr, GLOO_HIP_PRODUCT>(dst, list, k, mode, n, F, epoch, s);
+    case GLOO_HIP_MAX: return launch_fold_send<Tr, GLOO_HIP_MAX>(dst, list, k, mode, n, F, epoch, s);
+    case GLOO_HIP_MIN: return launch_fold_send<Tr, GLOO_HIP_MIN>(dst, list, k, mode, n, F, epoch, s);
+    default: return set_error(GLOO_HIP_EINVAL_OP, "fold+forward needs a built-in op");
+  }
+}
+
+template <class Tr, int OP, int UNROLL, int BLOCK, int LAUX, int SAUX, int IL = 1>
 int launch_vec(void* c, const void* a, const void* b, size_t n, size_t head, hipStream_t s) {
   using S = typename Tr::Storage;
   constexpr int kV = 16 / sizeof(S);
   const size_t nvec = (n - head) / kV;
   size_t grid = ceil_div(nvec, (size_t)BLOCK * UNROLL);
   if (grid == 0) grid = 1;
-  reduce_vec_kernel<Tr, OP, UNROLL, BLOCK, LAUX, SAUX><<<dim3((unsigned)grid), dim3(BLOCK), 0, s>>>(
+  reduce_vec_kernel<Tr, OP, UNROLL, BLOCK, LAUX, SAUX, IL><<<dim3((unsigned)grid), dim3(BLOCK), 0, s>>>(
       static_cast<S*>(c), static_cast<const S*>(a), static_cast<const S*>(b), n, head, t_stamp);
   return check_launch("reduce_vec_kernel");
 }
@@ -881,6 +1099,7 @@ int launch3(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
       case 12: return launch_vec_pipe<Tr, OP, 2, 512, kAuxNT, kAuxNT>(c, a, b, n, head, 2048, s);
       case 13: return launch_vec_pipe<Tr, OP, 1, 512, kAuxNT, kAuxNT>(c, a, b, n, head, 1024, s);
       case 14: return launch_vec_pipe<Tr, OP, 2, 256, kAuxNT, kAuxNT>(c, a, b, n, head, 2048, s);
+      case 15: return launch_vec<Tr, OP, 2, 512, kAuxNT, kAuxNT, 0>(c, a, b, n, head, s);  // rounds 1-2 load order
       default: break;
     }
   }
@@ -995,6 +1214,7 @@ int launchCopySignalMulti(const CopyDesc* d, int n, const uint64_t* epoch, hipSt
     L.ticket[j] = d[j].ticket;
   }
   L.first[n] = total;
+  L.lean = fwdLean();
   copy_signal_kernel<<<total, kCopyBlock, 0, s>>>(L, epoch);
   return check_launch("copy_signal_kernel");
 }
@@ -1070,6 +1290,49 @@ int launchFold(int op, int dtype, void* dst, const void* const* srcs, int k, siz
     case 1: return dispatch_multi<1>(op, dtype, dst, srcs, k, n, s);
     case 2: return dispatch_multi<2>(op, dtype, dst, srcs, k, n, s);
     default: return set_error(GLOO_HIP_EINVAL_ARG, "unknown fold mode");
+  }
+}
+
+int launchFoldSend(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n, int mode,
+                   const FwdDesc* fwd, int nf, unsigned* ticket, const uint64_t* epoch, hipStream_t s) {
+  if (k < 1 || k > GLOO_HIP_MAX_SRCS) return set_error(GLOO_HIP_EINVAL_ARG, "source count out of range");
+  if (nf < 1 || nf > kMaxCopyEntries) return set_error(GLOO_HIP_EINVAL_ARG, "forward count out of range");
+  if (mode < 0 || mode > 2 || (mode == 2 && (k & (k - 1))))
+    return set_error(GLOO_HIP_EINVAL_ARG, "bad fold mode for fold+forward");
+  const size_t es = gloo_hip_dtype_size(dtype);
+  if (es == 0) return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
+  if (!dst || (uintptr_t)dst % es) return set_error(GLOO_HIP_EINVAL_PTR, "dst not aligned to the element size");
+  SrcList list;
+  memset(&list, 0, sizeof(list));
+  for (int j = 0; j < k; j++) {
+    if (!srcs[j] || (uintptr_t)srcs[j] % es) return set_error(GLOO_HIP_EINVAL_PTR, "bad source pointer");
+    list.p[j] = srcs[j];
+  }
+  FwdList F;
+  memset(&F, 0, sizeof(F));
+  F.n = nf;
+  F.ticket = ticket;
+  F.lean = fwdLean();
+  for (int r = 0; r < nf; r++) {
+    if (!fwd[r].dst || (uintptr_t)fwd[r].dst % es)
+      return set_error(GLOO_HIP_EINVAL_PTR, "forward destination not aligned to the element size");
+    if (fwd[r].flag && !ticket) return set_error(GLOO_HIP_EINVAL_ARG, "forward flag without a ticket counter");
+    F.dst[r] = static_cast<char*>(fwd[r].dst);
+    F.flag[r] = fwd[r].flag;
+    F.seq[r] = fwd[r].seq;
+  }
+  switch (dtype) {
+    case GLOO_HIP_I8: return by_op_fold_send<TrI8>(op, dst, list, k, mode, n, F, epoch, s);
+    case GLOO_HIP_U8: return by_op_fold_send<TrU8>(op, dst, list, k, mode, n, F, epoch, s);
+    case GLOO_HIP_I32: return by_op_fold_send<TrI32>(op, dst, list, k, mode, n, F, epoch, s);
+    case GLOO_HIP_U32: return by_op_fold_send<TrU32>(op, dst, list, k, mode, n, F, epoch, s);
+    case GLOO_HIP_I64: return by_op_fold_send<TrI64>(op, dst, list, k, mode, n, F, epoch, s);
+    case GLOO_HIP_U64: return by_op_fold_send<TrU64>(op, dst, list, k, mode, n, F, epoch, s);
+    case GLOO_HIP_F16: return by_op_fold_send<TrF16>(op, dst, list, k, mode, n, F, epoch, s);
+    case GLOO_HIP_BF16: return by_op_fold_send<TrBF16>(op, dst, list, k, mode, n, F, epoch, s);
+    case GLOO_HIP_F32: return by_op_fold_send<TrF32>(op, dst, list, k, mode, n, F, epoch, s);
+    case GLOO_HIP_F64: return by_op_fold_send<TrF64>(op, dst, list, k, mode, n, F, epoch, s);
+    default: return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
   }
 }
 

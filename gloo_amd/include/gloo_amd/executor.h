@@ -121,6 +121,7 @@ class PlanExecutor {
   bool fineGrainedArena() const { return fineArena_; }
   bool hostArena() const { return hostArena_; }
   bool kernelCopy() const { return kernelCopy_; }
+  bool foldSendUsed() const { return foldSendUsed_; }
   // True when the last run() was a replay of the captured hipGraph (a run
   // with profiling events on is enqueued eagerly even while a graph exists).
   bool graphed() const { return replayed_; }
@@ -255,6 +256,8 @@ class PlanExecutor {
     return peers_[peer].device == ctx_->device() ? copyBlocksLocal_ : copyBlocks_;
   }
   bool batchKernelCopy_ = true;  // a batch of SENDs = one multi-destination copy kernel
+  bool foldSend_ = true;         // a FOLD's result SENDs ride in the fold's pass (launchFoldSend)
+  bool foldSendUsed_ = false;    // ... and some enqueue did so
   unsigned* ticket_ = nullptr;   // copy_signal_kernel tickets, one counter per (peer, slot)
   std::vector<hipStream_t> aux_;        // forked SEND batches (memcpy engine)
   std::vector<hipEvent_t> forkEvents_;

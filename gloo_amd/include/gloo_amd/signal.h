@@ -155,4 +155,17 @@ bool customOp(int op, gloo_hip_custom_fn* fn, void** user);
 int launchFold(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n, int mode,
                hipStream_t stream);
 
+// Fold + forward (reduce.hip fold_send_kernel): the fold above, with each
+// result tile also stored to every fwd[r].dst (peers' inboxes; any
+// element-aligned address) in the same pass; the workgroup taking the launch's
+// last ticket publishes every non-null fwd[r].flag = seq (epoch-scaled, as
+// launchCopySignal).  Built-in ops only.  Returns a gloo_hip status.
+struct FwdDesc {
+  void* dst;
+  uint64_t* flag;
+  Seq seq;
+};
+int launchFoldSend(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n, int mode,
+                   const FwdDesc* fwd, int nf, unsigned* ticket, const uint64_t* epoch, hipStream_t stream);
+
 }  // namespace gloo_amd

@@ -551,6 +551,55 @@ def test_processes_graph_replay(torch, golden_sched, case, env, graph):
         assert modes[-1]["graph_error"] == "", modes[-1]
 
 
+@pytest.mark.parametrize("case,env,fused", [
+    ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, True),      # tree fold, 7 forwards
+    ("halving_doubling/sum/f32/P2/k1/n1000", {"GLOO_AMD_GRAPH": "1"}, True),
+    ("halving_doubling/min/f32/P5/k1/n1000", {"GLOO_AMD_GRAPH": "1"}, True),       # pairwise temporaries
+    ("halving_doubling/sum/f64/P7/k1/n3001", {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_FUSE_BYTES": "0"}, True),
+    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, True),          # reverse fold
+    ("ring_chunked/product/f32/P3/k1/n777", {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_FUSE_BYTES": "0"}, True),
+    ("ring_chunked/max/f32/P5/k1/n999", {"GLOO_AMD_GRAPH": "1"}, True),           # ragged: misaligned forwards
+    ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_FWD_RELEASE": "each"}, True),
+    ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_FOLD_SEND": "0"}, False),
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_MESH": "0"}, False),  # no FOLD
+])
+def test_processes_fold_send(torch, golden_sched, case, env, fused):
+    """Fold + forward: a mesh owner's fold stores its finished range into
+    every peer's inbox in the same pass and signals them from its last
+    workgroup (executor.cc enqueue, reduce.hip fold_send_kernel).  Five runs
+    (eager, or enqueued / captured / replayed) must each equal the reference's
+    output byte for byte; `fused` says whether the mode query must report the
+    fused launch (None: not asserted)."""
+    algo = case.split("/")[0]
+    P = int(case.split("/")[3][1:])
+    runs = 5
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(GRAPH_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_INTERP="0", **env)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), case,
+                                   os.path.join(d, f"o{r}"), str(runs)], env=e, stdout=subprocess.PIPE, text=True)
+                 for r in range(P)]
+        outs = [p.communicate(timeout=300)[0] for p in procs]
+        assert [p.returncode for p in procs] == [0] * P
+        ys = [[np.load(os.path.join(d, f"o{r}.{it}.npy")) for it in range(runs)] for r in range(P)]
+    want = golden_sched[case + "/out"]
+    for it in range(runs):
+        for r in range(P):
+            assert same_bytes(ys[r][it], want), (r, it)
+    last = []
+    for r in range(P):
+        modes = json.loads(outs[r].split("MODES", 1)[1])
+        assert not any(m["interp"] for m in modes), modes
+        if env.get("GLOO_AMD_GRAPH") == "1":
+            assert modes[-1]["graph"], modes[-1]
+        last.append(modes[-1]["fold_send"])
+    # ranks that own no range of their own (the binary blocks' extra ranks of
+    # non-power-of-two HD, empty ring chunks) have no fold to fuse
+    if fused is not None:
+        assert any(last) == fused, last
+
+
 @pytest.mark.parametrize("case,env,interp", [
     ("halving_doubling/sum/f32/P5/k1/n10007", {}, True),
     ("halving_doubling/sum/f32/P8/k1/n1000", {}, True),             # tree fold

@@ -59,6 +59,8 @@ def main():
         if r == 2 and w == 1:
             pats.append((f"{tag}_inplace_u{u}_b{b}", i, r + w, True))
     pats.append(("product_reduce_inplace", -1, 3, True))
+    # the product kernel with the round-1/2 load order (gloo_hip_set_variant 15)
+    pats.append(("product_reduce_inplace_v15", -16, 3, True))
     if args.only:
         pats = [p for p in pats if p[0].startswith(tuple(args.only.split(",")))]
 
@@ -66,7 +68,9 @@ def main():
         name, i, streams, inplace = p
         a, b, c = sets[j % nsets]
         if i < 0:
+            hip.set_variant(-i - 1)
             hip.reduce_ptr("sum", "f32", a.data_ptr(), b.data_ptr(), n, s)
+            hip.set_variant(0)
             return
         rc = L.ceil_run(i, (a if inplace else c).data_ptr(), a.data_ptr(), b.data_ptr(), sink.data_ptr(), nbytes, s)
         if rc:
