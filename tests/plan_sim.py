@@ -187,7 +187,30 @@ def sliceable(algo, P, n, rank, k=1, nin=0, recv=None, elem_size=4, max_seg=0):
     return True
 
 
-def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, runs=1, slices=1):
+def reduce_forward_order(steps):
+    """The executor's reduce + forward rewrite (executor.cc enqueue): a window
+    REDUCE(range R) NOTIFY WAIT_NOTIFY SEND(R, unchanged) runs as
+    WAIT_NOTIFY, then ONE launch that reduces R and stores the result into
+    the peer's inbox as it goes (here: REDUCE then SEND), then NOTIFY.
+    Returns (new step list, number of windows rewritten)."""
+    out, i, hits = [], 0, 0
+    while i < len(steps):
+        s = steps[i]
+        if (s.kind == KIND["REDUCE"] and not s.flags & FROM_INPUTS and s.length > 0 and i + 3 < len(steps)
+                and steps[i + 1].kind == KIND["NOTIFY"] and steps[i + 2].kind == KIND["WAIT_NOTIFY"]
+                and steps[i + 3].kind == KIND["SEND"] and not steps[i + 3].flags & (SRC_ARENA | FROM_INPUTS)
+                and steps[i + 3].src_off == s.dst_off and steps[i + 3].length == s.length):
+            out += [steps[i + 2], s, steps[i + 3], steps[i + 1]]
+            hits += 1
+            i += 4
+            continue
+        out.append(s)
+        i += 1
+    return out, hits
+
+
+def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, runs=1, slices=1,
+             reduce_forward=False):
     """inputs: [P][k][n] array of the dtype's storage type (the outputs'
     initial contents); ins: optional [P][kin][n] separate inputs (new-style
     allreduce).  runs > 1 executes the plan back to back that many times
@@ -195,11 +218,14 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
     runs, as repeated Algorithm::run() calls do.  slices > 1 executes it as
     the sliced interpreter does: every (rank, slice) is its own process
     applying each step to its slice only, with its own channel counters,
-    interleaved at random with all the others.  Returns the outputs."""
+    interleaved at random with all the others.  reduce_forward: every plan
+    rewritten by reduce_forward_order first.  Returns the outputs."""
     P, k, n = inputs.shape
     nin = 0 if ins is None else ins.shape[1]
     es = inputs.dtype.itemsize
     plans = [get_plan(algo, r, P, n, k, recv, nin=nin, elem_size=es, max_seg=max_seg) for r in range(P)]
+    if reduce_forward:
+        plans = [(reduce_forward_order(steps)[0], a) for steps, a in plans]
     # previous-run credits: per channel, how many per run
     lag_per_run = {}
     for r, (steps, _) in enumerate(plans):
