@@ -193,6 +193,24 @@ constexpr int kRsrcFlags = 0x00020000;  // gfx950 raw-buffer word 3
 constexpr int kAuxNT = 2;               // cache policy `nt`: streamed once
 constexpr int kAuxWT = 1 | 2 | 16;      // `sc0 nt sc1`: streamed once, written through (not held in L2)
 
+// Completion protocol of the kernels that signal a peer after writing into
+// its inbox (copy_signal_kernel, fold_send_kernel, the interpreter), GLOO_AMD_FWD_RELEASE:
+// "last" (the default) = the signalled bytes are stored write-through
+// (sc0 nt sc1) and every wave waits for them (vmcnt 0) before its workgroup
+// takes a relaxed ticket; no L2 write-back is needed except by a workgroup
+// that also made plain stores (the edge elements), and the ticket holder
+// publishes the flag with a relaxed store.  The interpreter's sends work the
+// same way, and its credits (NOTIFY) publish no data, so neither releases.
+// "each" = every workgroup releases at system scope before its ticket or
+// flag (rounds 1-2).
+int fwdLean() {
+  static const int v = [] {
+    const char* e = std::getenv("GLOO_AMD_FWD_RELEASE");
+    return e && std::string(e) == "each" ? 0 : 1;
+  }();
+  return v;
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, kRsrcFlags);
 }
@@ -397,43 +415,32 @@ __device__ __forceinline__ typename Tr::Storage tree_fold(typename Tr::Storage* 
   return v[0];
 }
 
-template <class Tr, int OP, int UNROLL, int BLOCK, int MODE>
-__global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
-    typename Tr::Storage* dst, SrcList srcs, int k, size_t n, size_t head, uint64_t* stamp) {
+// One element of a k-source fold (block 0's head / tail), in MODE's order.
+template <class Tr, int OP, int MODE>
+__device__ __forceinline__ typename Tr::Storage fold_elem(const SrcList& srcs, int k, size_t i) {
   using S = typename Tr::Storage;
-  constexpr int kV = 16 / sizeof(S);
-  constexpr uint32_t kTileBytes = (uint32_t)BLOCK * UNROLL * 16;
-  stamp_begin(stamp);
-  const size_t nvec = (n - head) / kV;
-  const size_t tail0 = head + nvec * kV;
-  if (blockIdx.x == 0) {
-    const size_t t = threadIdx.x;
-    for (int pass = 0; pass < 2; pass++) {
-      const size_t i = pass == 0 ? t : tail0 + t;
-      if ((pass == 0 && t < head) || (pass == 1 && i < n)) {
-        if (MODE == 2) {
-          S v[GLOO_HIP_MAX_SRCS];
+  if (MODE == 2) {
+    S v[GLOO_HIP_MAX_SRCS];
 #pragma unroll
-          for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
-            if (j < k) v[j] = static_cast<const S*>(srcs.p[j])[i];
-          dst[i] = tree_fold<Tr, OP>(v, k);
-        } else {
-          S acc = static_cast<const S*>(srcs.p[0])[i];
-          for (int j = 1; j < k; j++) {
-            const S v = static_cast<const S*>(srcs.p[j])[i];
-            acc = MODE == 1 ? apply<Tr, OP>(v, acc) : apply<Tr, OP>(acc, v);
-          }
-          dst[i] = acc;
-        }
-      }
-    }
+    for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
+      if (j < k) v[j] = static_cast<const S*>(srcs.p[j])[i];
+    return tree_fold<Tr, OP>(v, k);
   }
-  const size_t body = nvec * 16;
-  const size_t base = (size_t)blockIdx.x * kTileBytes;
-  if (base >= body) return;
-  const uint32_t bytes = (uint32_t)((body - base) < kTileBytes ? (body - base) : kTileBytes);
+  S acc = static_cast<const S*>(srcs.p[0])[i];
+  for (int j = 1; j < k; j++) {
+    const S v = static_cast<const S*>(srcs.p[j])[i];
+    acc = MODE == 1 ? apply<Tr, OP>(v, acc) : apply<Tr, OP>(acc, v);
+  }
+  return acc;
+}
+
+// One vector tile of a k-source fold: `bytes` (<= BLOCK * UNROLL * 16) of
+// the body starting `base` bytes past element `head`, into acc.
+template <class Tr, int OP, int UNROLL, int BLOCK, int MODE>
+__device__ __forceinline__ void fold_tile(const SrcList& srcs, int k, size_t head, size_t base, uint32_t bytes,
+                                          u32x4 (&acc)[UNROLL]) {
+  using S = typename Tr::Storage;
   const uint32_t lane_off = threadIdx.x * 16u;
-  u32x4 acc[UNROLL];
   if (MODE == 2) {
     // all sources resident, then the tree level by level (k <= 8, uniform)
     u32x4 v[GLOO_HIP_MAX_SRCS][UNROLL];
@@ -473,6 +480,31 @@ __global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
         acc[u] = MODE == 1 ? apply_packet<Tr, OP>(r[u], acc[u]) : apply_packet<Tr, OP>(acc[u], r[u]);
     }
   }
+}
+
+template <class Tr, int OP, int UNROLL, int BLOCK, int MODE>
+__global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
+    typename Tr::Storage* dst, SrcList srcs, int k, size_t n, size_t head, uint64_t* stamp) {
+  using S = typename Tr::Storage;
+  constexpr int kV = 16 / sizeof(S);
+  constexpr uint32_t kTileBytes = (uint32_t)BLOCK * UNROLL * 16;
+  stamp_begin(stamp);
+  const size_t nvec = (n - head) / kV;
+  const size_t tail0 = head + nvec * kV;
+  if (blockIdx.x == 0) {
+    const size_t t = threadIdx.x;
+    for (int pass = 0; pass < 2; pass++) {
+      const size_t i = pass == 0 ? t : tail0 + t;
+      if ((pass == 0 && t < head) || (pass == 1 && i < n)) dst[i] = fold_elem<Tr, OP, MODE>(srcs, k, i);
+    }
+  }
+  const size_t body = nvec * 16;
+  const size_t base = (size_t)blockIdx.x * kTileBytes;
+  if (base >= body) return;
+  const uint32_t bytes = (uint32_t)((body - base) < kTileBytes ? (body - base) : kTileBytes);
+  const uint32_t lane_off = threadIdx.x * 16u;
+  u32x4 acc[UNROLL];
+  fold_tile<Tr, OP, UNROLL, BLOCK, MODE>(srcs, k, head, base, bytes, acc);
   const auto rd = make_rsrc(reinterpret_cast<const char*>(dst + head) + base, bytes);
 #pragma unroll
   for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rd, lane_off + u * BLOCK * 16, acc[u]);
@@ -526,9 +558,11 @@ __global__ __launch_bounds__(kFusedBlock) void fused_small_kernel(
     __syncthreads();
     if (threadIdx.x == 0) {
       const uint64_t sigValue = epoch ? sig.base + *epoch * sig.perRun : sig.base;
+      // one release, then a relaxed flag store: a release store would write
+      // the L2 back a second time (MI355X_MICROARCH.md: fence, wait, relaxed flag)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(sigFlag, sigValue, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(sigFlag, sigValue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -584,11 +618,22 @@ constexpr int kInterpFoldUnroll = GLOO_AMD_INTERP_FOLD_UNROLL;
 // the ragged tail goes byte-wise.  Per pass the descriptors are rebuilt at
 // the pass base, so 32-bit lane offsets suffice, and the range check drops
 // the packets past the body.
+// A byte stored write-through (`sc0 nt sc1`), for the edges of a WT copy.
+__device__ __forceinline__ void wt_byte(char* p, char v) {
+  __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, make_rsrc(p, 1), 0, 0, kAuxWT);
+}
+
+// WT: every byte of dst is stored write-through (an interpreter SEND under
+// the once-per-launch protocol, fwdLean: its flag then needs no release).
+template <bool WT = false>
 __device__ __forceinline__ void interp_copy(char* dst, const char* src, uint64_t n) {
   const uint64_t t = threadIdx.x;
   uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
   if (head > n) head = n;
-  if (t < head) dst[t] = src[t];
+  if (t < head) {
+    if (WT) wt_byte(dst + t, src[t]);
+    else dst[t] = src[t];
+  }
   const uint64_t body = (n - head) / 16 * 16;
   char* d = dst + head;
   const Src ss = src_of(src + head);
@@ -602,9 +647,12 @@ __device__ __forceinline__ void interp_copy(char* dst, const char* src, uint64_t
 #pragma unroll
     for (int u = 0; u < kInterpCopyUnroll; u++) v[u] = bload<0>(rs, lane_off + u * kInterpBlock * 16, ss.mis);
 #pragma unroll
-    for (int u = 0; u < kInterpCopyUnroll; u++) bstore<0>(rd, lane_off + u * kInterpBlock * 16, v[u]);
+    for (int u = 0; u < kInterpCopyUnroll; u++) bstore<WT ? kAuxWT : 0>(rd, lane_off + u * kInterpBlock * 16, v[u]);
   }
-  for (uint64_t i = head + body + t; i < n; i += kInterpBlock) dst[i] = src[i];
+  for (uint64_t i = head + body + t; i < n; i += kInterpBlock) {
+    if (WT) wt_byte(dst + i, src[i]);
+    else dst[i] = src[i];
+  }
 }
 
 // dst[i] = fold over the step's sources (mode as launchFold) for n elements:
@@ -686,7 +734,7 @@ __device__ __forceinline__ void interp_fold(const InterpStep& st, uint64_t lo, u
 
 template <class Tr, int OP>
 __global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpStep* steps, int nsteps, uint64_t run,
-                                                                   uint64_t timeoutTicks, uint32_t* err) {
+                                                                   uint64_t timeoutTicks, uint32_t* err, int lean) {
   using S = typename Tr::Storage;
   constexpr uint64_t kV = 16 / sizeof(S);
   __shared__ int ok;
@@ -721,17 +769,25 @@ __global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpS
     const uint64_t q = ((n + G - 1) / G + kV - 1) / kV * kV;
     const uint64_t lo = g * q < n ? g * q : n;
     const uint64_t hi = lo + q < n ? lo + q : n;
-    if (kind == kInterpCopy || kind == kInterpSend) {
+    if (kind == kInterpSend && lean) {
+      interp_copy<true>(st.dst + lo * sizeof(S), st.src[0] + lo * sizeof(S), (hi - lo) * sizeof(S));
+    } else if (kind == kInterpCopy || kind == kInterpSend) {
       interp_copy(st.dst + lo * sizeof(S), st.src[0] + lo * sizeof(S), (hi - lo) * sizeof(S));
     } else if (kind == kInterpFold) {
       interp_fold<Tr, OP>(st, lo, hi);
     }
-    // every wave's writes of this step are performed before the barrier
+    // every wave's reads and writes of this step are performed before the barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if ((kind == kInterpSend || kind == kInterpSignal) && threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      __hip_atomic_store(st.flag + g, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      // lean (fwdLean): a SEND's bytes went out write-through and a SIGNAL is
+      // a credit that publishes no data (its reads are complete), so neither
+      // needs the L2 write-back of a release
+      if (!lean) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __hip_atomic_store(st.flag + g, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -739,11 +795,12 @@ __global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpS
 template <class Tr>
 int launch_interp(int op, const InterpStep* steps, int nsteps, uint64_t run, uint64_t tt, uint32_t* err,
                   int G, hipStream_t s) {
+  const int lean = fwdLean();
   switch (op) {
-    case GLOO_HIP_SUM: plan_interp_kernel<Tr, GLOO_HIP_SUM><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
-    case GLOO_HIP_PRODUCT: plan_interp_kernel<Tr, GLOO_HIP_PRODUCT><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
-    case GLOO_HIP_MAX: plan_interp_kernel<Tr, GLOO_HIP_MAX><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
-    case GLOO_HIP_MIN: plan_interp_kernel<Tr, GLOO_HIP_MIN><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err); break;
+    case GLOO_HIP_SUM: plan_interp_kernel<Tr, GLOO_HIP_SUM><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean); break;
+    case GLOO_HIP_PRODUCT: plan_interp_kernel<Tr, GLOO_HIP_PRODUCT><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean); break;
+    case GLOO_HIP_MAX: plan_interp_kernel<Tr, GLOO_HIP_MAX><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean); break;
+    case GLOO_HIP_MIN: plan_interp_kernel<Tr, GLOO_HIP_MIN><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean); break;
     default: return GLOO_HIP_EINVAL_OP;
   }
   return GLOO_HIP_OK;
@@ -818,7 +875,10 @@ __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(CopyList L, con
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (!L.lean) {
+    // lean: the body went out write-through and every wave has waited for
+    // it; only the entry's block 0, whose head / tail bytes are plain
+    // stores, releases before its ticket
+    if (!L.lean || (lb == 0 && (head || tail0 < bytes))) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -828,14 +888,14 @@ __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(CopyList L, con
     if (t == nb - 1) {
       // last workgroup of this entry: reset the counter for the next launch
       // (launches on one channel's counter are stream-ordered), publish
-      if (L.lean) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
       __hip_atomic_store(L.ticket[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      __hip_atomic_store(L.flag[j], L.seq[j].base + ep * L.seq[j].perRun, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint64_t v = L.seq[j].base + ep * L.seq[j].perRun;
+      if (L.lean) {
+        __hip_atomic_store(L.flag[j], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        __hip_atomic_store(L.flag[j], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
   }
 }
@@ -845,19 +905,7 @@ __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(CopyList L, con
 // ---------------------------------------------------------------------------
 int g_variant = 0;  // fp32 SUM kernel variant (measurement knob)
 
-// Completion protocol of the kernels that signal a peer after a multi-
-// workgroup write (copy_signal_kernel, fold_send_kernel), GLOO_AMD_FWD_RELEASE:
-// "last" (the default) = the signalled bytes are stored write-through
-// (sc0 nt sc1), each workgroup drains and takes a relaxed ticket, and only the
-// ticket holder releases at system scope (one L2 write-back per launch);
-// "each" = every workgroup releases at system scope before its ticket.
-int fwdLean() {
-  static const int v = [] {
-    const char* e = std::getenv("GLOO_AMD_FWD_RELEASE");
-    return e && std::string(e) == "each" ? 0 : 1;
-  }();
-  return v;
-}
+
 
 int set_error(int code, const char* what) { return setError(code, what); }
 
@@ -882,8 +930,8 @@ inline size_t ceil_div(size_t a, size_t b) { return (a + b - 1) / b; }
 // Completion as copy_signal_kernel: every wave drains, one lane releases at
 // system scope and takes a ticket; the workgroup holding the launch's last
 // ticket resets the counter and publishes every forward's flag.  The mode is
-// a uniform runtime argument (0 left, 1 reverse, 2 tree), as in
-// reduce_multi_vec_kernel, whose element order this repeats exactly.
+// a uniform runtime argument (0 left, 1 reverse, 2 tree) selecting the same
+// fold_elem / fold_tile as reduce_multi_vec_kernel, so the bits are the same.
 // ---------------------------------------------------------------------------
 struct FwdList {
   int n;
@@ -910,20 +958,9 @@ __global__ __launch_bounds__(kVecBlock) void fold_send_kernel(typename Tr::Stora
     for (int pass = 0; pass < 2; pass++) {
       const size_t i = pass == 0 ? t : tail0 + t;
       if ((pass == 0 && t < head) || (pass == 1 && i < n)) {
-        S acc;
-        if (mode == 2) {
-          S v[GLOO_HIP_MAX_SRCS];
-#pragma unroll
-          for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
-            if (j < k) v[j] = static_cast<const S*>(srcs.p[j])[i];
-          acc = tree_fold<Tr, OP>(v, k);
-        } else {
-          acc = static_cast<const S*>(srcs.p[0])[i];
-          for (int j = 1; j < k; j++) {
-            const S v = static_cast<const S*>(srcs.p[j])[i];
-            acc = mode == 1 ? apply<Tr, OP>(v, acc) : apply<Tr, OP>(acc, v);
-          }
-        }
+        const S acc = mode == 2   ? fold_elem<Tr, OP, 2>(srcs, k, i)
+                      : mode == 1 ? fold_elem<Tr, OP, 1>(srcs, k, i)
+                                  : fold_elem<Tr, OP, 0>(srcs, k, i);
         dst[i] = acc;
         for (int r = 0; r < F.n; r++) reinterpret_cast<S*>(F.dst[r])[i] = acc;
       }
@@ -935,44 +972,9 @@ __global__ __launch_bounds__(kVecBlock) void fold_send_kernel(typename Tr::Stora
     const uint32_t bytes = (uint32_t)((body - base) < kTileBytes ? (body - base) : kTileBytes);
     const uint32_t lane_off = threadIdx.x * 16u;
     u32x4 acc[UNROLL];
-    if (mode == 2) {
-      u32x4 v[GLOO_HIP_MAX_SRCS][UNROLL];
-#pragma unroll
-      for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
-        if (j < k) {
-          const Src sj = src_of(static_cast<const S*>(srcs.p[j]) + head);
-          const auto rj = make_rsrc(sj.base + base, bytes + sj.mis);
-#pragma unroll
-          for (int u = 0; u < UNROLL; u++) v[j][u] = bload<kAuxNT>(rj, lane_off + u * BLOCK * 16, sj.mis);
-        }
-#pragma unroll
-      for (int w = GLOO_HIP_MAX_SRCS; w > 1; w >>= 1)
-        if (w <= k) {
-#pragma unroll
-          for (int j = 0; j < w / 2; j++)
-#pragma unroll
-            for (int u = 0; u < UNROLL; u++) v[j][u] = apply_packet<Tr, OP>(v[2 * j][u], v[2 * j + 1][u]);
-        }
-#pragma unroll
-      for (int u = 0; u < UNROLL; u++) acc[u] = v[0][u];
-    } else {
-      {
-        const Src s0 = src_of(static_cast<const S*>(srcs.p[0]) + head);
-        const auto r0 = make_rsrc(s0.base + base, bytes + s0.mis);
-#pragma unroll
-        for (int u = 0; u < UNROLL; u++) acc[u] = bload<kAuxNT>(r0, lane_off + u * BLOCK * 16, s0.mis);
-      }
-      for (int j = 1; j < k; j++) {
-        const Src sj = src_of(static_cast<const S*>(srcs.p[j]) + head);
-        const auto rj = make_rsrc(sj.base + base, bytes + sj.mis);
-        u32x4 r[UNROLL];
-#pragma unroll
-        for (int u = 0; u < UNROLL; u++) r[u] = bload<kAuxNT>(rj, lane_off + u * BLOCK * 16, sj.mis);
-#pragma unroll
-        for (int u = 0; u < UNROLL; u++)
-          acc[u] = mode == 1 ? apply_packet<Tr, OP>(r[u], acc[u]) : apply_packet<Tr, OP>(acc[u], r[u]);
-      }
-    }
+    if (mode == 2) fold_tile<Tr, OP, UNROLL, BLOCK, 2>(srcs, k, head, base, bytes, acc);
+    else if (mode == 1) fold_tile<Tr, OP, UNROLL, BLOCK, 1>(srcs, k, head, base, bytes, acc);
+    else fold_tile<Tr, OP, UNROLL, BLOCK, 0>(srcs, k, head, base, bytes, acc);
     const auto rd = make_rsrc(reinterpret_cast<const char*>(dst + head) + base, bytes);
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rd, lane_off + u * BLOCK * 16, acc[u]);
@@ -997,10 +999,11 @@ __global__ __launch_bounds__(kVecBlock) void fold_send_kernel(typename Tr::Stora
   __syncthreads();
   if (threadIdx.x == 0) {
     // lean: the forwarded bytes were stored write-through (sc0 sc1) and this
-    // workgroup's waves have all seen them acknowledged, so only the ticket
-    // holder releases (one L2 write-back per launch instead of one per
-    // workgroup); otherwise every workgroup releases before its ticket
-    if (!F.lean) {
+    // workgroup's waves have all seen them acknowledged, so no workgroup
+    // writes its L2 back except block 0 for its plain edge stores, and the
+    // ticket holder publishes with a relaxed store; otherwise every
+    // workgroup releases before its ticket
+    if (!F.lean || (blockIdx.x == 0 && (head || tail0 < n))) {  // block 0's edge elements are plain stores
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1008,16 +1011,16 @@ __global__ __launch_bounds__(kVecBlock) void fold_send_kernel(typename Tr::Stora
     const unsigned t = F.lean ? __hip_atomic_fetch_add(F.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                               : __hip_atomic_fetch_add(F.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
     if (t == gridDim.x - 1) {
-      if (F.lean) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
       __hip_atomic_store(F.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      if (!F.lean) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       for (int r = 0; r < F.n; r++)
-        if (F.flag[r])
-          __hip_atomic_store(F.flag[r], F.seq[r].base + ep * F.seq[r].perRun, __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
+        if (F.flag[r]) {
+          const uint64_t v = F.seq[r].base + ep * F.seq[r].perRun;
+          if (F.lean)
+            __hip_atomic_store(F.flag[r], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          else
+            __hip_atomic_store(F.flag[r], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
   }
 }

@@ -21,8 +21,11 @@ __global__ __launch_bounds__(64) void signal_kernel(uint64_t* flag, uint64_t bas
     // the reduction that consumed an inbox) is performed at system scope
     // before the flag can be observed
     const uint64_t v = seqValue(base, perRun, epoch);
+    // one release, then a relaxed flag store (a release store would write the
+    // L2 back a second time); the wait keeps the flag behind the write-back
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
