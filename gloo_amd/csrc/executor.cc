@@ -1692,7 +1692,12 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         // profiles/round2/r2d_rocprof_copy_engines_segments.csv); below that,
         // and over xGMI, hipMemcpyAsync + signal
         const bool bigLocal = autoCopy_ && s.length * es_ >= (16u << 20) && peers_[s.peer].device == ctx_->device();
-        if (kernelCopy_ || bigLocal) {
+        // eager (not captured): hipMemcpyAsync into an IPC mapping is the slow
+        // path of an eager enqueue, and the copy kernel signals without a
+        // write-back since round 3; graph memcpy nodes stay faster
+        // (profiles/round3/r3ag_latency_ab_release_and_copy_engine.jsonl)
+        const bool eagerKernel = autoCopy_ && !graph;
+        if (kernelCopy_ || bigLocal || eagerKernel) {
           const unsigned grid = copySignalGrid(s.length * es_, bigLocal ? 256u : copyBlocksFor(s.peer));
           checkRc(launchCopySignal(dst, src, s.length * es_, sigFlag(s.peer, s.slot),
                                    seqOf(i, r, graph), ticket_ + (size_t)s.peer * GLOO_HIP_NUM_SLOTS + s.slot, epoch,
