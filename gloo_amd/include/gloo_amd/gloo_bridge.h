@@ -171,8 +171,10 @@ class BootstrapContext {
       return 0;
     }
     try {
-      // A gloo::Context on the xGMI transport (gloo_transport.h) has no
-      // unbound buffers for gloo::allgather: exchange through its store.
+      // A gloo::Context on the xGMI transport (gloo_transport.h) already
+      // sits on a library context: exchange through that context's store
+      // rather than moving host records through the transport's own
+      // unbound buffers.
       const int peer = self->context_->rank == 0 ? 1 : 0;
       if (auto* hp = dynamic_cast<transport::hip::Pair*>(self->context_->getPair(peer).get()))
         return hp->hipContext()->allgather(in, out, block);
