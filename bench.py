@@ -423,7 +423,8 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
             # first few mismatches: position, value, expected, this rank's input
             bad_detail = [[int(sample[i]), float(got[i]), float(want_sample[i]), float(x_np[sample[i]])]
                           for i in np.nonzero(badmask)[0][:3]]
-            # timed: steady state (the plan replays as a hipGraph from run 3 on)
+            # timed: steady state (eager enqueue for these 32 MiB messages by default,
+            # graph replay from run 3 on below GLOO_AMD_GRAPH_BYTES or with GLOO_AMD_GRAPH=1)
             times = []
             for _ in range(args.allreduce_iters):
                 dist.barrier()
@@ -443,8 +444,8 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                 wait_s += st["wait_s"]
             # steady state with device stamps: each reduce kernel records its
             # first-workgroup start / last-workgroup end on the GPU clock, so
-            # the runs stay graph-replayed (the per-GPU reduce
-            # rate while the exchange runs)
+            # the runs keep their launch mode, graph replay included (SURVEY
+            # 8(e): the per-GPU reduce rate while the exchange runs)
             a.set_profiling(2)
             st_s = st_b = 0.0
             st_graph = []
@@ -485,9 +486,9 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                 "reduce_kernel_gib_s_per_gpu": [round(g["stamp_b"] / g["stamp_s"] / GIB, 1) if g["stamp_s"] > 0
                                                 else None for g in gathered],
                 "reduce_kernel_timing": ("device stamps inside the reduce kernels (first workgroup start to last "
-                                         "workgroup end), %d graph-replayed runs per rank%s" %
-                                         (args.allreduce_iters, "" if all(g["stamp_graph"] for g in gathered)
-                                          else " (NOT all replayed)")),
+                                         "workgroup end), %d %s runs per rank" %
+                                         (args.allreduce_iters, "graph-replayed" if all(g["stamp_graph"] for g in gathered)
+                                          else "eagerly enqueued (the default above GLOO_AMD_GRAPH_BYTES)")),
                 "host_wait_ms_per_run_max_profiled": max(g["wait_ms_per_run"] for g in gathered),
                 "verified": bool(all(g["first_run_ok"] for g in gathered) and
                                  len({g["digest"] for g in gathered}) == 1),
@@ -916,7 +917,7 @@ def main():
 
         def efficiency(xr):
             """each GPU's reduce-kernel GiB/s while the config-3
-            exchange runs (device stamps, graph replay) over the same GPU's
+            exchange runs (device stamps, steady-state runs) over the same GPU's
             config-2 kernel GiB/s measured above in this run."""
             per = xr.get("reduce_kernel_gib_s_per_gpu") or []
             one = [alg_bytes / (k / 1e3) / GIB for k in per_rank_kernel_ms]
@@ -928,7 +929,7 @@ def main():
                     "reduce_gib_s_during_allreduce": [round(p, 1) for p in per],
                     "one_gpu_kernel_gib_s": [round(o, 1) for o in one],
                     "how": ("min over ranks of (config-3 mesh allreduce reduce-kernel GiB/s, device stamps over "
-                            "graph-replayed runs) / (the same GPU's config-2 64 MiB kernel GiB/s in this run)"),
+                            "steady-state runs) / (the same GPU's config-2 64 MiB kernel GiB/s in this run)"),
                     "data_path": xr.get("data_path")}
 
         def fire():

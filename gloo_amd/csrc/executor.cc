@@ -179,6 +179,16 @@ size_t fuseBytes() {
   return v;
 }
 
+// Largest message below which GLOO_AMD_GRAPH=auto replays a plan as a
+// hipGraph (executor constructor); larger plans are enqueued eagerly.
+size_t graphBytes() {
+  static const size_t v = [] {
+    const char* e = std::getenv("GLOO_AMD_GRAPH_BYTES");
+    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)(4u << 20);
+  }();
+  return v;
+}
+
 // Largest message of a plan the one-launch interpreter runs (0: never).
 size_t interpBytes() {
   static const size_t v = [] {
@@ -995,18 +1005,26 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     // (a plain hipMemset goes to the null stream, which a non-blocking
     // stream does not wait for)
     GLOO_AMD_HIP_CHECK(hipMemsetAsync(ticket_, 0, tickets, stream_));
-    // Graph replay pays off once a plan has steps that are not fused
-    // one-workgroup launches (measured); "1" / "0" force it.
+    // Graph replay pays off where the host is the bottleneck: a plan with
+    // steps that are not fused one-workgroup launches, whose messages are
+    // small.  From GLOO_AMD_GRAPH_BYTES (default 4 MiB) per message the
+    // device is the bottleneck, the host's eager enqueue stays ahead of it,
+    // and eager enqueue measured 7-13 % faster than replay (HD 16 and 64 MiB
+    // per rank, 2 and 4 ranks: DESIGN.md §4, profiles/round3/r3ah_*, r3ak_*).
+    // "1" / "0" force it.
     const char* gm = std::getenv("GLOO_AMD_GRAPH");
     const std::string gmode = gm ? gm : "auto";
     bool unfused = fuseBytes() == 0 || custom_;
-    for (const Step& s : plan_.steps)
+    size_t maxMsg = 0;
+    for (const Step& s : plan_.steps) {
       if ((s.kind == GLOO_HIP_STEP_SEND || s.kind == GLOO_HIP_STEP_REDUCE || s.kind == GLOO_HIP_STEP_COPY ||
            s.kind == GLOO_HIP_STEP_LOCAL_REDUCE || s.kind == GLOO_HIP_STEP_LOCAL_BCAST ||
            s.kind == GLOO_HIP_STEP_FOLD) &&
           s.length * es_ > fuseBytes())
         unfused = true;
-    graphMode_ = gmode == "1" || (gmode == "auto" && unfused);
+      maxMsg = std::max(maxMsg, (size_t)s.length * es_);
+    }
+    graphMode_ = gmode == "1" || (gmode == "auto" && unfused && maxMsg < graphBytes());
     if (interpMode_) GLOO_AMD_HIP_ALLOC(hipMalloc(&interpSteps_, kInterpMaxSteps * sizeof(InterpStep)));
     if (graphMode_) {
       GLOO_AMD_HIP_ALLOC(hipMalloc(&epoch_, sizeof(uint64_t)));

@@ -126,17 +126,20 @@ CONFIG3 = "ring_chunked/sum/f32/P8/n67108864"
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("env", [{}, {"GLOO_AMD_RING_MESH": "0"}, {"GLOO_AMD_COPY": "memcpy"},
+@pytest.mark.parametrize("env", [{}, {"GLOO_AMD_RING_MESH": "0", "GLOO_AMD_GRAPH": "1"},
+                                 {"GLOO_AMD_COPY": "memcpy", "GLOO_AMD_GRAPH": "1"},
                                  {"GLOO_AMD_RING_MESH": "0", "GLOO_AMD_COPY": "kernel"}],
-                         ids=["mesh", "ring_route", "mesh_memcpy", "ring_route_kernel_copy"])
+                         ids=["mesh", "ring_route_graph", "mesh_memcpy_graph", "ring_route_kernel_copy"])
 def test_config3_full_size(torch, env):
     """BASELINE config 3 at its configured size: 8 ranks x 256 MiB fp32,
     ring-chunked, every rank's buffer byte for byte the reference's output
     (gloo/allreduce_ring_chunked.h:102-158) in each of three runs."""
     res = run_processes([CONFIG3], 8, env)
     check(res, [CONFIG3])
-    # run 2 captures the plan and run 3 replays it (device signalling)
-    assert all(r[CONFIG3][2]["mode"]["graph"] for r in res), [r[CONFIG3][2]["mode"] for r in res]
+    # GLOO_AMD_GRAPH=1: run 2 captures the plan and run 3 replays it; by
+    # default its 32 MiB messages are enqueued eagerly (GLOO_AMD_GRAPH_BYTES)
+    want_graph = env.get("GLOO_AMD_GRAPH") == "1"
+    assert all(r[CONFIG3][2]["mode"]["graph"] == want_graph for r in res), [r[CONFIG3][2]["mode"] for r in res]
 
 
 HD = ["halving_doubling/sum/f32/P8/n4194304", "halving_doubling/sum/f32/P8/n5000011",

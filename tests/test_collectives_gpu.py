@@ -869,7 +869,8 @@ def test_device_stamps_keep_graph_replay(torch):
     with tempfile.TemporaryDirectory() as d:
         w = os.path.join(d, "w.py")
         open(w, "w").write(STAMP_WORKER)
-        e = dict(os.environ, GLOO_AMD_ROOT=ROOT)
+        # 8 MiB messages run eagerly by default (GLOO_AMD_GRAPH_BYTES): force replay
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_GRAPH="1")
         procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s")], env=e,
                                   stdout=subprocess.PIPE, text=True) for r in range(P)]
         outs = [p.communicate(timeout=240)[0] for p in procs]
