@@ -893,3 +893,50 @@ def test_device_stamps_keep_graph_replay(torch):
         # read from the Infinity Cache, but no faster than 20 TB/s
         assert 0 < ev_s and 0 < st_s <= 1.5 * ev_s, (ev_s, st_s)
         assert st[-1]["reduce_bytes"] / st_s < 20e12, (st_s, st[-1]["reduce_bytes"])
+
+
+POLICY_WORKER = r'''
+import os, sys, json
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, size, store, algo, n = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5])
+torch.cuda.set_device(0)
+buf = torch.empty(n, device="cuda:0")
+ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=60000)
+a = gloo_amd.Algorithm(ctx, algo, "sum", "f32", [buf.data_ptr()], n)
+out = []
+for it in range(4):
+    buf.fill_(float(rank + 1)); torch.cuda.synchronize()
+    a.run(); torch.cuda.synchronize()
+    out.append({"ok": bool((buf == size * (size + 1) / 2).all()), **a.mode()})
+a.close(); ctx.close()
+print("RESULT" + json.dumps(out), flush=True)
+'''
+
+
+@pytest.mark.parametrize("algo,env,graph", [
+    ("halving_doubling", {}, False),                                    # 8 MiB messages: eager enqueue
+    ("halving_doubling", {"GLOO_AMD_GRAPH_BYTES": str(1 << 30)}, True),  # threshold raised: replay
+    ("ring_chunked", {}, False),
+    ("ring_chunked", {"GLOO_AMD_GRAPH": "1"}, True),
+])
+def test_processes_launch_mode_policy(torch, algo, env, graph):
+    """GLOO_AMD_GRAPH=auto replays plans whose messages are below
+    GLOO_AMD_GRAPH_BYTES (4 MiB) and enqueues larger ones eagerly (executor.cc
+    graphBytes); either way the mesh owners fold and forward in one launch.
+    16 MiB per rank, 2 rank processes, four runs, exact closed form."""
+    P, n = 2, 1 << 22
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(POLICY_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), algo, str(n)],
+                                  env=e, stdout=subprocess.PIPE, text=True) for r in range(P)]
+        outs = [p.communicate(timeout=240)[0] for p in procs]
+        assert [p.returncode for p in procs] == [0] * P
+    for o in outs:
+        res = json.loads(o.split("RESULT", 1)[1])
+        assert all(x["ok"] for x in res), res
+        assert not any(x["interp"] for x in res), res
+        assert [x["graph"] for x in res[2:]] == [graph, graph], res
+        assert res[-1]["fold_send"], res
