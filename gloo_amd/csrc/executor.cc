@@ -1818,7 +1818,8 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         const int mode = s.flags & GLOO_HIP_FOLD_TREE ? 2 : s.flags & GLOO_HIP_FOLD_REVERSE ? 1 : 0;
         // Fold + forward: the SENDs right after a fold that ship its result
         // unchanged (a mesh owner's return of its finished range) ride in the
-        // fold's own pass, and its last workgroup signals them.  Device
+        // fold's own pass, and its last workgroup signals them (and the
+        // NOTIFY credits that follow).  Device
         // signalling only; off while the reduce kernels are being timed, so
         // events and stamps keep measuring a pure fold.
         if (foldSend_ && deviceSignal_ && !custom_ && !profiling_ && !stamping_ && s.length > 0 &&
@@ -1836,7 +1837,14 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
           }
           // every SEND of the run must be taken, or the rest would still
           // re-read the result; a partial run stays unfused
-          if (nf > 0 && (j == steps.size() || steps[j].kind != GLOO_HIP_STEP_SEND)) {
+          const bool sendsTaken = j == steps.size() || steps[j].kind != GLOO_HIP_STEP_SEND;
+          // credits right after (a reduce-scatter owner's NOTIFYs: the fold has
+          // consumed the senders' inboxes) go out from the same last workgroup
+          // as data-free entries, once every read of the fold is complete
+          if (sendsTaken)
+            for (; j < steps.size() && nf < kMaxCopyEntries && steps[j].kind == GLOO_HIP_STEP_NOTIFY; j++)
+              fwd[nf++] = FwdDesc{nullptr, sigFlag(steps[j].peer, steps[j].slot), seqOf(j, r, graph)};
+          if (nf > 0 && sendsTaken) {
             const Step& t0 = steps[i + 1];
             checkRc(launchFoldSend(op_, dtype_, fdst, foldSrcs.data(), (int)foldSrcs.size(), s.length, mode, fwd,
                                    nf, ticket_ + (size_t)t0.peer * GLOO_HIP_NUM_SLOTS + t0.slot, epoch, stream_),

@@ -935,7 +935,7 @@ inline size_t ceil_div(size_t a, size_t b) { return (a + b - 1) / b; }
 // ---------------------------------------------------------------------------
 struct FwdList {
   int n;
-  char* dst[kMaxCopyEntries];       // any element-aligned address
+  char* dst[kMaxCopyEntries];       // any element-aligned address; nullptr: a credit (flag only)
   uint64_t* flag[kMaxCopyEntries];  // nullptr: no arrival flag for this entry
   Seq seq[kMaxCopyEntries];
   unsigned* ticket;                 // zero between launches; nullptr: no signals
@@ -962,7 +962,8 @@ __global__ __launch_bounds__(kVecBlock) void fold_send_kernel(typename Tr::Stora
                       : mode == 1 ? fold_elem<Tr, OP, 1>(srcs, k, i)
                                   : fold_elem<Tr, OP, 0>(srcs, k, i);
         dst[i] = acc;
-        for (int r = 0; r < F.n; r++) reinterpret_cast<S*>(F.dst[r])[i] = acc;
+        for (int r = 0; r < F.n; r++)
+          if (F.dst[r]) reinterpret_cast<S*>(F.dst[r])[i] = acc;
       }
     }
   }
@@ -979,6 +980,7 @@ __global__ __launch_bounds__(kVecBlock) void fold_send_kernel(typename Tr::Stora
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rd, lane_off + u * BLOCK * 16, acc[u]);
     for (int r = 0; r < F.n; r++) {
+      if (!F.dst[r]) continue;  // a credit: no data
       // a forward destination may sit at another residue mod 16 B than dst
       // (ragged inbox regions): its misalignment rides in soffset, as a
       // relatively misaligned source's does
@@ -1317,7 +1319,8 @@ int launchFoldSend(int op, int dtype, void* dst, const void* const* srcs, int k,
   F.ticket = ticket;
   F.lean = fwdLean();
   for (int r = 0; r < nf; r++) {
-    if (!fwd[r].dst || (uintptr_t)fwd[r].dst % es)
+    if (!fwd[r].dst && !fwd[r].flag) return set_error(GLOO_HIP_EINVAL_ARG, "forward entry with neither data nor flag");
+    if ((uintptr_t)fwd[r].dst % es)
       return set_error(GLOO_HIP_EINVAL_PTR, "forward destination not aligned to the element size");
     if (fwd[r].flag && !ticket) return set_error(GLOO_HIP_EINVAL_ARG, "forward flag without a ticket counter");
     F.dst[r] = static_cast<char*>(fwd[r].dst);

@@ -159,7 +159,9 @@ int launchFold(int op, int dtype, void* dst, const void* const* srcs, int k, siz
 // result tile also stored to every fwd[r].dst (peers' inboxes; any
 // element-aligned address) in the same pass; the workgroup taking the launch's
 // last ticket publishes every non-null fwd[r].flag = seq (epoch-scaled, as
-// launchCopySignal).  Built-in ops only.  Returns a gloo_hip status.
+// launchCopySignal).  An entry with dst == nullptr is a credit: its flag is
+// published once every read of the fold is complete, and no data moves.
+// Built-in ops only.  Returns a gloo_hip status.
 struct FwdDesc {
   void* dst;
   uint64_t* flag;

@@ -562,6 +562,9 @@ def test_processes_graph_replay(torch, golden_sched, case, env, graph):
     ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_FWD_RELEASE": "each"}, True),
     ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_FOLD_SEND": "0"}, False),
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_MESH": "0"}, False),  # no FOLD
+    # reduce-scatter owners: a fold and its credits (NOTIFY) in one launch
+    ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_GRAPH": "1"}, True),
+    ("reduce_scatter/max/bf16/P8/n4096", {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_FUSE_BYTES": "0"}, True),
 ])
 def test_processes_fold_send(torch, golden_sched, case, env, fused):
     """Fold + forward: a mesh owner's fold stores its finished range into
@@ -585,8 +588,12 @@ def test_processes_fold_send(torch, golden_sched, case, env, fused):
         ys = [[np.load(os.path.join(d, f"o{r}.{it}.npy")) for it in range(runs)] for r in range(P)]
     want = golden_sched[case + "/out"]
     for it in range(runs):
-        for r in range(P):
-            assert same_bytes(ys[r][it], want), (r, it)
+        if algo == "reduce_scatter":
+            recv = golden_sched[case + "/recv"]
+            assert same_bytes(np.concatenate([ys[r][it][:recv[r]] for r in range(P)]), want), it
+        else:
+            for r in range(P):
+                assert same_bytes(ys[r][it], want), (r, it)
     last = []
     for r in range(P):
         modes = json.loads(outs[r].split("MODES", 1)[1])
