@@ -206,7 +206,9 @@ def host_staged(torch, hip, n, dev, iters=20):
       zero_copy_src  the accumulator stays in HBM and the kernel reads the
                  host chunk in place (the HOST-workspace allreduce's reduce);
       zero_copy_both the kernel reads both operands from host memory and
-                 writes the result back there.
+                 writes the result back there;
+      library_default gloo_hip_reduce_staged with piece 0: zero-copy when both
+                 host buffers are mapped (they are here), else 16 MiB pieces.
     GiB/s is algorithmic (3 * n * 4 B per reduction)."""
     import ctypes
     h_dst = torch.empty(n, dtype=torch.float32, pin_memory=True).uniform_(-1, 1)
@@ -256,7 +258,8 @@ def host_staged(torch, hip, n, dev, iters=20):
     for name, fn in (("serial", serial), ("pipelined_4MiB", pipelined(1 << 20)),
                      ("pipelined_8MiB", pipelined(1 << 21)), ("pipelined_16MiB", pipelined(1 << 22)),
                      ("pipelined_32MiB", pipelined(1 << 23)),
-                     ("zero_copy_src", zc_src), ("zero_copy_both", zc_both)):
+                     ("zero_copy_src", zc_src), ("zero_copy_both", zc_both),
+                     ("library_default", pipelined(0))):
         dt = timed(fn)
         out[name] = {"gib_s_alg": round(3.0 * n * 4 / dt / GIB, 2), "ms_per_chunk": round(dt * 1e3, 3)}
     best = min((k for k in out if k.startswith("pipelined")), key=lambda k: out[k]["ms_per_chunk"])
@@ -267,6 +270,11 @@ def host_staged(torch, hip, n, dev, iters=20):
     pipelined(1 << 21)()
     torch.cuda.synchronize(dev)
     out["pipelined_verified"] = bool(torch.equal(h_dst, a0 + h_src))
+    # gloo_hip_reduce_staged with piece 0: zero-copy on these mapped buffers
+    h_dst.copy_(a0)
+    pipelined(0)()
+    torch.cuda.synchronize(dev)
+    out["library_default_verified"] = bool(torch.equal(h_dst, a0 + h_src))
     # the product check: the zero-copy kernel reads host memory correctly
     ref = d_dst.clone()
     d_src.copy_(h_src)

@@ -14,6 +14,14 @@
 // D2H directions run at the same time on separate DMA engines, and the
 // whole chunk costs about max(H2D bytes, D2H bytes) / link rate instead of
 // their sum.  Streams and events are per thread and device, created once.
+//
+// Zero-copy (piece_elems == 0, both host buffers pinned and mapped into the
+// device's address space): ONE kernel reads both operands over PCIe and
+// writes the result back in place, with no staging copies.  The same 192 MiB
+// cross the link, but as one stream of 16-B accesses: a 64 MiB fp32 chunk
+// takes 2.54-2.59 ms against 2.96-3.01 ms pipelined in 16 MiB pieces
+// (profiles/round3/r3aa_/r3ai_bench_n1*.json host_staged).  A buffer that is
+// pinned but not mapped, or an explicit piece size, keeps the pipeline.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -68,8 +76,17 @@ extern "C" int gloo_hip_reduce_staged(int op, int dtype, void* host_dst, const v
     if (!host_dst || !host_src || !dev_dst || !dev_src) return setError(GLOO_HIP_EINVAL_PTR, "null buffer pointer");
     int device = 0;
     GLOO_AMD_HIP_CHECK(hipGetDevice(&device));
-    StagingStreams& st = streamsFor(device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (piece_elems == 0) {
+      void* mdst = nullptr;
+      void* msrc = nullptr;
+      const bool mapped = hipHostGetDevicePointer(&mdst, host_dst, 0) == hipSuccess &&
+                          hipHostGetDevicePointer(&msrc, const_cast<void*>(host_src), 0) == hipSuccess &&
+                          mdst && msrc;
+      (void)hipGetLastError();  // a buffer that is not mapped is not an error here
+      if (mapped) return gloo_hip_reduce(op, dtype, mdst, msrc, n, s);
+    }
+    StagingStreams& st = streamsFor(device);
     // default: 16 MiB pieces (one MI355X: a 64 MiB fp32 chunk took 3.05 ms
     // in 16 MiB pieces against 5.2-5.8 ms in 4-8 MiB ones and 3.64 ms
     // unpipelined; profiles/round2/r2c_bench_n1.json host_staged)

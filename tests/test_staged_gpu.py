@@ -19,12 +19,14 @@ def torch():
 
 
 @pytest.mark.parametrize("dtype,op,n,piece", [
-    ("f32", "sum", 1 << 20, 0),            # default: n / 8
+    ("f32", "sum", 1 << 20, 0),            # default: zero-copy (torch pins mapped memory)
     ("f32", "sum", 1_000_003, 65_537),     # ragged pieces
     ("f32", "max", 4099, 1 << 20),         # one piece
     ("bf16", "product", 300_007, 50_000),
     ("f16", "min", 123_457, 10_000),
     ("i64", "sum", 77_777, 4096),
+    ("bf16", "max", 300_007, 0),           # zero-copy, 16-bit, ragged
+    ("i64", "product", 77_777, 0),
 ])
 def test_staged_matches_oracle(torch, dtype, op, n, piece):
     import gloo_amd
