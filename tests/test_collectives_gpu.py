@@ -947,3 +947,58 @@ def test_processes_launch_mode_policy(torch, algo, env, graph):
         assert not any(x["interp"] for x in res), res
         assert [x["graph"] for x in res[2:]] == [graph, graph], res
         assert res[-1]["fold_send"], res
+
+
+BYTES_WORKER = r'''
+import hashlib, os, sys, json
+import numpy as np
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, size, store, algo, dtype, n = (int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5],
+                                     int(sys.argv[6]))
+npt = np.uint8 if dtype == "u8" else np.int8
+x = np.random.default_rng([11, rank]).integers(0, 256, n, dtype=np.uint8).view(npt)
+torch.cuda.set_device(0)
+src = torch.from_numpy(x.view(np.uint8).copy()).to("cuda:0")
+buf = torch.empty_like(src)
+ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=60000)
+a = gloo_amd.Algorithm(ctx, algo, "sum", dtype, [buf.data_ptr()], n)
+outs = []
+for it in range(3):
+    buf.copy_(src); torch.cuda.synchronize()
+    a.run(); torch.cuda.synchronize()
+    outs.append(hashlib.sha256(buf.cpu().numpy().tobytes()).hexdigest())
+np.save(sys.argv[7], buf.cpu().numpy())
+print("RESULT" + json.dumps({"mode": a.mode(), "runs": outs}), flush=True)
+a.close(); ctx.close()
+'''
+
+
+@pytest.mark.parametrize("algo,dtype,P,n,env", [
+    ("ring_chunked", "u8", 3, 100_003, {}),                          # ragged byte offsets: misaligned forwards
+    ("halving_doubling", "i8", 5, 77_777, {"GLOO_AMD_INTERP": "0"}),  # pairwise temporaries, eager/graph
+    ("halving_doubling", "u8", 8, 1_000_003, {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_INTERP": "0"}),
+    ("ring_chunked", "i8", 4, 4_000_037, {}),                        # 1 MiB messages, graph replay
+])
+def test_processes_byte_sums_any_offset(torch, algo, dtype, P, n, env):
+    """1-byte elements at ragged counts put every chunk, fold destination and
+    forwarded range at an arbitrary byte offset.  Integer sums wrap and are
+    associative, so every rank must hold the element-wise sum mod 256 of all
+    inputs whatever the fold order; three runs each."""
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(BYTES_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), algo, dtype,
+                                   str(n), os.path.join(d, f"o{r}.npy")], env=e, stdout=subprocess.PIPE, text=True)
+                 for r in range(P)]
+        outs = [p.communicate(timeout=240)[0] for p in procs]
+        assert [p.returncode for p in procs] == [0] * P
+        ys = [np.load(os.path.join(d, f"o{r}.npy")) for r in range(P)]
+    want = np.zeros(n, dtype=np.uint8)
+    for r in range(P):
+        want += np.random.default_rng([11, r]).integers(0, 256, n, dtype=np.uint8)
+    for r in range(P):
+        assert (ys[r].view(np.uint8) == want).all(), r
+        res = json.loads(outs[r].split("RESULT", 1)[1])
+        assert len(set(res["runs"])) == 1, res  # every run gives the same bytes
