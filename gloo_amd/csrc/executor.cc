@@ -1708,7 +1708,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         // HBM -> HBM faster than the blit engine from 16 MiB up (one MI355X:
         // 8.1 vs 9.7 us at 16 MiB, 22.0 vs 26.0 us at 64 MiB kernel time,
         // profiles/round2/r2d_rocprof_copy_engines_segments.csv); below that,
-        // and over xGMI, hipMemcpyAsync + signal
+        // and over xGMI, hipMemcpyAsync + signal inside a captured graph
         const bool bigLocal = autoCopy_ && s.length * es_ >= (16u << 20) && peers_[s.peer].device == ctx_->device();
         // eager (not captured): hipMemcpyAsync into an IPC mapping is the slow
         // path of an eager enqueue, and the copy kernel signals without a
@@ -1818,10 +1818,10 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         const int mode = s.flags & GLOO_HIP_FOLD_TREE ? 2 : s.flags & GLOO_HIP_FOLD_REVERSE ? 1 : 0;
         // Fold + forward: the SENDs right after a fold that ship its result
         // unchanged (a mesh owner's return of its finished range) ride in the
-        // fold's own pass, and its last workgroup signals them (and the
-        // NOTIFY credits that follow).  Device
-        // signalling only; off while the reduce kernels are being timed, so
-        // events and stamps keep measuring a pure fold.
+        // fold's own pass, and its last workgroup signals them and the NOTIFY
+        // credits that follow.  Device signalling only; off while the reduce
+        // kernels are being timed, so events and stamps keep measuring a pure
+        // fold.
         if (foldSend_ && deviceSignal_ && !custom_ && !profiling_ && !stamping_ && s.length > 0 &&
             !(s.flags & GLOO_HIP_DST_ARENA)) {
           char* fdst = userPtr(0) + s.dst_off * es_;
