@@ -179,8 +179,8 @@ size_t fuseBytes() {
   return v;
 }
 
-// Largest message below which GLOO_AMD_GRAPH=auto replays a plan as a
-// hipGraph (executor constructor); larger plans are enqueued eagerly.
+// Largest message below which GLOO_AMD_GRAPH=auto replays a mesh plan as a
+// hipGraph (executor constructor); larger mesh plans are enqueued eagerly.
 size_t graphBytes() {
   static const size_t v = [] {
     const char* e = std::getenv("GLOO_AMD_GRAPH_BYTES");
@@ -1006,12 +1006,14 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     // stream does not wait for)
     GLOO_AMD_HIP_CHECK(hipMemsetAsync(ticket_, 0, tickets, stream_));
     // Graph replay pays off where the host is the bottleneck: a plan with
-    // steps that are not fused one-workgroup launches, whose messages are
-    // small.  From GLOO_AMD_GRAPH_BYTES (default 4 MiB) per message the
-    // device is the bottleneck, the host's eager enqueue stays ahead of it,
-    // and eager enqueue measured 7-13 % faster than replay (HD 16 and 64 MiB
-    // per rank, 2 and 4 ranks: DESIGN.md §4, profiles/round3/r3ah_*, r3ak_*).
-    // "1" / "0" force it.
+    // steps that are not fused one-workgroup launches.  A mesh plan (a few
+    // launches per call) whose messages reach GLOO_AMD_GRAPH_BYTES (default
+    // 4 MiB) is device-bound instead: the host's eager enqueue stays ahead,
+    // and eager measured 7-13 % faster than replay (HD 16 and 64 MiB per
+    // rank, 2 and 4 ranks: DESIGN.md §4, profiles/round3/r3ah_*, r3ak_*).
+    // The reference routes keep replay: their per-hop credit handshakes make
+    // many launches per call, and eager lost there (HD 16 MiB per rank, 4
+    // ranks: 149 vs 122 us, r3ax_*).  "1" / "0" force it.
     const char* gm = std::getenv("GLOO_AMD_GRAPH");
     const std::string gmode = gm ? gm : "auto";
     bool unfused = fuseBytes() == 0 || custom_;
@@ -1024,7 +1026,8 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
         unfused = true;
       maxMsg = std::max(maxMsg, (size_t)s.length * es_);
     }
-    graphMode_ = gmode == "1" || (gmode == "auto" && unfused && maxMsg < graphBytes());
+    const bool meshPlan = (planAlgo_ & GLOO_HIP_ALGO_MESH) || planAlgo_ == GLOO_HIP_ALGO_RING_CHUNKED_MESH;
+    graphMode_ = gmode == "1" || (gmode == "auto" && unfused && !(meshPlan && maxMsg >= graphBytes()));
     if (interpMode_) GLOO_AMD_HIP_ALLOC(hipMalloc(&interpSteps_, kInterpMaxSteps * sizeof(InterpStep)));
     if (graphMode_) {
       GLOO_AMD_HIP_ALLOC(hipMalloc(&epoch_, sizeof(uint64_t)));

@@ -27,8 +27,8 @@
 // overrides the choice.
 //
 // hipGraph replay (device signalling; GLOO_AMD_GRAPH=auto, the default, for
-// plans with unfused steps whose messages are below GLOO_AMD_GRAPH_BYTES;
-// =1 always): once a plan has run with the same buffers, the next run() captures the whole
+// plans with unfused steps, except mesh plans with messages of
+// GLOO_AMD_GRAPH_BYTES or more; =1 always): once a plan has run with the same buffers, the next run() captures the whole
 // enqueue — epoch bump, waits, copies, reductions, signals — into a hipGraph
 // and every later run() is ONE hipGraphLaunch.  Sequence numbers are
 // replayable (signal.h: base + epoch * perRun with a device-side run epoch),

@@ -136,9 +136,10 @@ def test_config3_full_size(torch, env):
     (gloo/allreduce_ring_chunked.h:102-158) in each of three runs."""
     res = run_processes([CONFIG3], 8, env)
     check(res, [CONFIG3])
-    # GLOO_AMD_GRAPH=1: run 2 captures the plan and run 3 replays it; by
-    # default its 32 MiB messages are enqueued eagerly (GLOO_AMD_GRAPH_BYTES)
-    want_graph = env.get("GLOO_AMD_GRAPH") == "1"
+    # GLOO_AMD_GRAPH=1, or the reference route: run 2 captures the plan and
+    # run 3 replays it; the mesh plan's 32 MiB messages are enqueued eagerly
+    # by default (GLOO_AMD_GRAPH_BYTES)
+    want_graph = env.get("GLOO_AMD_GRAPH") == "1" or env.get("GLOO_AMD_RING_MESH") == "0"
     assert all(r[CONFIG3][2]["mode"]["graph"] == want_graph for r in res), [r[CONFIG3][2]["mode"] for r in res]
 
 

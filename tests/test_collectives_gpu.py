@@ -926,11 +926,12 @@ print("RESULT" + json.dumps(out), flush=True)
     ("halving_doubling", {"GLOO_AMD_GRAPH_BYTES": str(1 << 30)}, True),  # threshold raised: replay
     ("ring_chunked", {}, False),
     ("ring_chunked", {"GLOO_AMD_GRAPH": "1"}, True),
+    ("halving_doubling", {"GLOO_AMD_MESH": "0"}, True),                 # reference route: replay
 ])
 def test_processes_launch_mode_policy(torch, algo, env, graph):
-    """GLOO_AMD_GRAPH=auto replays plans whose messages are below
-    GLOO_AMD_GRAPH_BYTES (4 MiB) and enqueues larger ones eagerly (executor.cc
-    graphBytes); either way the mesh owners fold and forward in one launch.
+    """GLOO_AMD_GRAPH=auto replays plans, except mesh plans whose messages
+    reach GLOO_AMD_GRAPH_BYTES (4 MiB), which it enqueues eagerly (executor.cc
+    graphBytes); the mesh owners fold and forward in one launch either way.
     16 MiB per rank, 2 rank processes, four runs, exact closed form."""
     P, n = 2, 1 << 22
     with tempfile.TemporaryDirectory() as d:
@@ -946,7 +947,7 @@ def test_processes_launch_mode_policy(torch, algo, env, graph):
         assert all(x["ok"] for x in res), res
         assert not any(x["interp"] for x in res), res
         assert [x["graph"] for x in res[2:]] == [graph, graph], res
-        assert res[-1]["fold_send"], res
+        assert res[-1]["fold_send"] == (env.get("GLOO_AMD_MESH") != "0"), res
 
 
 BYTES_WORKER = r'''
