@@ -66,6 +66,8 @@ def parse():
                    help="N>1 config-4 sweep: minimum seconds per timed batch (gloo/benchmark default 2 s)")
     p.add_argument("--quick", action="store_true",
                    help="N>1: config 3 + one variant, short HD sweep, RS at 16 Mi (rehearsals)")
+    p.add_argument("--watchdog-seconds", type=float, default=300.0,
+                   help="N>1: the xGMI section's time limit; on expiry the line is printed and the job exits 3")
     return p.parse_args()
 
 
@@ -411,8 +413,8 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
 
     want_sample = expected_at_sample()
 
-    def ring_once(engine, workspace="device", mesh="1"):
-        progress(f"config 3: ring_chunked engine={engine} workspace={workspace} mesh={mesh}")
+    def ring_once(engine, workspace="device", mesh="1", extra_env=None):
+        progress(f"config 3: ring_chunked engine={engine} workspace={workspace} mesh={mesh} {extra_env or ''}")
 
         url = store_url("ring_%s_%s_%s" % (engine, workspace, mesh))  # taken first: every rank, same order
 
@@ -465,6 +467,9 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                     st_s += st["reduce_s"]
                     st_b += st["reduce_bytes"]
                     st_graph.append(a.mode()["graph"])
+            # fold + forward is off under event profiling and on (if the knob
+            # allows) under stamps: mode() reports whether any run fused
+            st_fused = a.mode()["fold_send"]
             a.set_profiling(0)
             torch.cuda.synchronize(dev)
             dig = hashlib.sha256(buf.cpu().numpy().view(np.uint8).tobytes()).hexdigest()
@@ -473,9 +478,10 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
             return {"ms": [round(t * 1e3, 3) for t in times], "reduce_s": red_s, "reduce_b": red_b,
                     "wait_ms_per_run": round(wait_s / 3 * 1e3, 3), "first_run_ok": ok_first,
                     "first_run_bad_samples": bad_first, "first_run_bad_detail": bad_detail, "digest": dig,
-                    "graph": graphed, "stamp_s": st_s, "stamp_b": st_b, "stamp_graph": all(st_graph)}
+                    "graph": graphed, "stamp_s": st_s, "stamp_b": st_b, "stamp_graph": all(st_graph),
+                    "stamp_fused": bool(st_fused)}
         try:
-            res = with_env({"GLOO_AMD_COPY": engine, "GLOO_AMD_RING_MESH": mesh}, body)
+            res = with_env(dict({"GLOO_AMD_COPY": engine, "GLOO_AMD_RING_MESH": mesh}, **(extra_env or {})), body)
         except Exception as e:  # noqa: BLE001
             res = {"error": repr(e)}
         gathered = gather(res)
@@ -486,16 +492,31 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         ms = sorted(max(g["ms"][i] for g in gathered) for i in range(args.allreduce_iters))
         t = ms[len(ms) // 2] / 1e3
         per_gpu = [g["reduce_b"] / g["reduce_s"] / GIB for g in gathered if g["reduce_s"] > 0]
+        fused = all(g["stamp_fused"] for g in gathered)
+        busbw = 2 * (world - 1) / world * n * 4 / t
+        links = {}
+        if link.get("bytes_per_s"):
+            B = link["bytes_per_s"]
+            # ring: every byte crosses one link per hop, 2(P-1) hops of S/P;
+            # mesh: each link carries S/P per phase, two phases, links at once
+            links = {"busbw_frac_of_link": round(busbw / B, 4),
+                     "ring_link_bound_ms": round(2 * (world - 1) / world * n * 4 / B * 1e3, 3),
+                     "mesh_link_bound_ms": round(2 * n * 4 / world / B * 1e3, 3),
+                     "frac_of_mesh_link_bound": round(2 * n * 4 / world / B / t, 4)}
         return {"plan": "mesh" if mesh == "1" and world <= 8 else "ring", "copy_engine": engine,
                 "workspace": workspace, "graph": all(g["graph"] for g in gathered),
                 "ms_p50": round(t * 1e3, 3), "algbw_gib_s": round(n * 4 / t / GIB, 2),
-                "busbw_gib_s": round(2 * (world - 1) / world * n * 4 / t / GIB, 2),
+                "busbw_gib_s": round(busbw / GIB, 2), **links,
+                "schedule": ("%s%s" % ("mesh" if mesh == "1" and world <= 8 else "ring",
+                                       ", fold + forward fused" if fused else ", unfused (fold, then sends)")),
                 "reduce_kernel_gib_s_per_gpu_eager_events": [round(x, 1) for x in per_gpu],
                 "reduce_kernel_gib_s_per_gpu": [round(g["stamp_b"] / g["stamp_s"] / GIB, 1) if g["stamp_s"] > 0
                                                 else None for g in gathered],
                 "reduce_kernel_timing": ("device stamps inside the reduce kernels (first workgroup start to last "
-                                         "workgroup end), %d %s runs per rank" %
-                                         (args.allreduce_iters, "graph-replayed" if all(g["stamp_graph"] for g in gathered)
+                                         "workgroup end%s), %d %s runs per rank" %
+                                         (", forward stores included: the fused fold + forward launch as it ships"
+                                          if fused else "",
+                                          args.allreduce_iters, "graph-replayed" if all(g["stamp_graph"] for g in gathered)
                                           else "eagerly enqueued (the default above GLOO_AMD_GRAPH_BYTES)")),
                 "host_wait_ms_per_run_max_profiled": max(g["wait_ms_per_run"] for g in gathered),
                 "verified": bool(all(g["first_run_ok"] for g in gathered) and
@@ -506,9 +527,15 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                 "verify": "run 1 vs the reference ring fold at 4096 sampled positions on every rank, "
                           "bit-exact; after the last run every rank's 256 MiB digest equal"}
 
+    ngpu = torch.cuda.device_count()
+    # B_link for the link-bound fractions: one peer copy GPU 0 -> GPU 1 over
+    # its direct xGMI link, measured by rank 0 while the others wait
+    link = one_link_bandwidth(torch, dist, rank, n * 4) if ngpu >= 2 and ngpu >= world else \
+        {"bytes_per_s": None, "why": f"{world} ranks on {ngpu} GPU(s): no link to measure"}
+    partial["link"] = {k: (round(v / 1e9, 2) if k == "bytes_per_s" and v else v) for k, v in link.items()}
+    partial["link"]["unit"] = "GB/s (bytes_per_s / 1e9)"
     # default: the mesh plan (batched sends = one multi-destination copy kernel)
     ring = ring_once("auto")
-    ngpu = torch.cuda.device_count()
     partial["config"] = "allreduce_ring_chunked fp32 sum, %d ranks, %d MiB/rank" % (world, args.allreduce_mib)
     partial["data_path"] = "xGMI peer copies" if ngpu >= world else f"{world} ranks on {ngpu} GPU(s)"
     partial.update(ring)
@@ -516,6 +543,9 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         return dict(partial)
     variants = {}
     partial["variants"] = variants
+    # SURVEY 8(e)'s efficiency on the unfused mesh (a pure fold kernel between
+    # the sends), beside the default fused schedule above
+    variants["mesh_unfused"] = ring_once("auto", extra_env={"GLOO_AMD_FOLD_SEND": "0"})
     specs = {"ring_memcpy": ("memcpy", "device", "0"), "ring_kernel": ("kernel", "device", "0"),
              "mesh_memcpy_forked": ("memcpy", "device", "1"), "mesh_host_workspace": ("auto", "host", "1")}
     chosen = (args.config3_variants.split(",") if args.config3_variants
@@ -730,6 +760,36 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     return dict(partial)
 
 
+def one_link_bandwidth(torch, dist, rank, nbytes):
+    """One-peer copy GPU 0 -> GPU 1 (hipMemcpyPeerAsync over the direct xGMI
+    link), best of 5 timed with events on GPU 0, by rank 0 alone; every rank
+    joins the barriers.  Returns {"bytes_per_s", "how"}."""
+    res = [None]
+    dist.barrier()
+    if rank == 0:
+        try:
+            src = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+            dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda:1")
+            best = None
+            for _ in range(6):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                dst.copy_(src, non_blocking=True)
+                e1.record()
+                torch.cuda.synchronize("cuda:0")
+                torch.cuda.synchronize("cuda:1")
+                ms = e0.elapsed_time(e1)
+                best = ms if best is None else min(best, ms)
+            res[0] = {"bytes_per_s": nbytes / (best / 1e3), "bytes": nbytes,
+                      "how": "torch copy cuda:0 -> cuda:1 (one xGMI link), best of 6, events on GPU 0"}
+            del src, dst
+            torch.cuda.empty_cache()
+        except Exception as e:  # noqa: BLE001
+            res[0] = {"bytes_per_s": None, "why": repr(e)}
+    dist.broadcast_object_list(res, src=0)
+    return res[0]
+
+
 class HipEvent:
     """A timing event of the HIP runtime torch has loaded (same soname),
     created with hipEventDisableSystemFence (hip_runtime_api.h): recorded
@@ -923,7 +983,7 @@ def main():
         # the section marked as timed out, and the process exits.
         partial = {}
 
-        def efficiency(xr):
+        def efficiency_of(xr, data_path):
             """each GPU's reduce-kernel GiB/s while the config-3
             exchange runs (device stamps, steady-state runs) over the same GPU's
             config-2 kernel GiB/s measured above in this run."""
@@ -931,24 +991,40 @@ def main():
             one = [alg_bytes / (k / 1e3) / GIB for k in per_rank_kernel_ms]
             eff = [p / o for p, o in zip(per, one) if p]
             if len(eff) != world:
-                return {"value": None, "why": xr.get("error", "no stamped reduce timing from every rank")}
+                return {"value": None, "why": xr.get("error", "no stamped reduce timing from every rank"),
+                        "data_path": data_path}
             return {"value": round(min(eff), 4), "mean": round(sum(eff) / len(eff), 4),
                     "per_rank": [round(e, 4) for e in eff],
                     "reduce_gib_s_during_allreduce": [round(p, 1) for p in per],
                     "one_gpu_kernel_gib_s": [round(o, 1) for o in one],
+                    "schedule": xr.get("schedule"),
                     "how": ("min over ranks of (config-3 mesh allreduce reduce-kernel GiB/s, device stamps over "
-                            "steady-state runs) / (the same GPU's config-2 64 MiB kernel GiB/s in this run)"),
-                    "data_path": xr.get("data_path")}
+                            "steady-state runs, bytes = the fold's (P + 1) reads and writes) / (the same GPU's "
+                            "config-2 64 MiB kernel GiB/s in this run)"),
+                    "data_path": data_path}
+
+        def efficiency(xr):
+            """Twice: SURVEY 8(e)'s definition on the unfused mesh (a pure
+            fold kernel), and the default schedule as it ships (fold and
+            forward in one launch, its forward stores inside the stamps)."""
+            base = xr.get("data_path") or partial.get("data_path")
+            unf = (xr.get("variants") or {}).get("mesh_unfused") or {}
+            res = efficiency_of(unf, f"{base}; unfused mesh: fold kernel, then the sends (GLOO_AMD_FOLD_SEND=0)")
+            res["fused_default"] = efficiency_of(
+                xr, f"{base}; default schedule: {xr.get('schedule', 'mesh')}")
+            return res
 
         def fire():
             if rank == 0:
-                out["xgmi_allreduce"] = dict(partial, error="watchdog: section exceeded 300 s")
+                out["xgmi_allreduce"] = dict(partial, error="watchdog: section exceeded %g s" % args.watchdog_seconds)
                 out["per_gpu_efficiency"] = efficiency(partial)
+                out["value_note"] = "the N>1 section timed out: the job exits 3 after this line"
                 print(json.dumps(out), flush=True)
-            os._exit(0)
+            # a hung section must show in the driver's record: non-zero exit
+            os._exit(3)
 
         progress("N>1 sections")
-        wd = arm_watchdog(300, fire)
+        wd = arm_watchdog(args.watchdog_seconds, fire)
         xr = xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial)
         wd.cancel()
         if rank == 0:

@@ -270,6 +270,62 @@ EXPORTED = EXPORTED + ("gloo_hip_context_create_kv", "gloo_hip_transport_create"
 WORKSPACES = {"device": 0, "host": 1}
 
 
+def _bind_transport(L):
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.gloo_hip_transport_create.argtypes = [vp, vp, ctypes.POINTER(vp)]
+    L.gloo_hip_transport_destroy.argtypes = [vp]
+    L.gloo_hip_buffer_create.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, sz, ctypes.c_int, ctypes.POINTER(vp)]
+    L.gloo_hip_buffer_destroy.argtypes = [vp]
+    L.gloo_hip_buffer_send.argtypes = [vp, sz, sz, sz]
+    L.gloo_hip_buffer_wait_recv.argtypes = [vp]
+    L.gloo_hip_buffer_wait_send.argtypes = [vp]
+
+
+_bind_transport(lib)
+
+
+class Transport:
+    """The xGMI transport's bound buffers (gloo::transport::Pair /
+    Buffer, gloo/transport/pair.h:33-41, buffer.h:26-34) over a Context:
+    construction is collective.  Receive buffers in device memory are written
+    in place by the peer (HIP IPC across processes); host memory across
+    processes travels in payload records of at most 40 bytes per message."""
+
+    def __init__(self, ctx, stream=0):
+        h = ctypes.c_void_p()
+        _check(lib.gloo_hip_transport_create(ctx._h, stream or None, ctypes.byref(h)))
+        self._h = h
+
+    def buffer(self, peer, slot, ptr, size, send):
+        return TransportBuffer(self, peer, slot, ptr, size, send)
+
+    def close(self):
+        if self._h:
+            _check(lib.gloo_hip_transport_destroy(self._h))
+            self._h = None
+
+
+class TransportBuffer:
+    def __init__(self, t, peer, slot, ptr, size, send):
+        h = ctypes.c_void_p()
+        _check(lib.gloo_hip_buffer_create(t._h, peer, slot, ptr or None, size, 1 if send else 0, ctypes.byref(h)))
+        self._h = h
+
+    def send(self, offset=0, length=None, roffset=0):
+        _check(lib.gloo_hip_buffer_send(self._h, offset, length if length is not None else 0, roffset))
+
+    def wait_recv(self):
+        _check(lib.gloo_hip_buffer_wait_recv(self._h))
+
+    def wait_send(self):
+        _check(lib.gloo_hip_buffer_wait_send(self._h))
+
+    def close(self):
+        if self._h:
+            _check(lib.gloo_hip_buffer_destroy(self._h))
+            self._h = None
+
+
 def ipc_stats():
     """This process's IPC slab pool (gloo_amd/include/gloo_amd/ipc.h): slabs
     exported (never freed while the process lives) and their bytes, slabs free
@@ -410,7 +466,7 @@ class AllreduceOptions(ctypes.Structure):
 
 
 lib.gloo_hip_allreduce.argtypes = [ctypes.c_void_p, ctypes.POINTER(AllreduceOptions)]
-EXPORTED = EXPORTED + ("gloo_hip_allreduce", "gloo_hip_plan_ex")
+EXPORTED = EXPORTED + ("gloo_hip_allreduce", "gloo_hip_plan_ex", "gloo_hip_arena_slabs")
 
 
 ALLREDUCE_ALGORITHMS = {"ring": 1, "bcube": 2}  # AllreduceOptions::Algorithm (gloo/allreduce.h:38-42)

@@ -151,6 +151,12 @@ int gloo_hip_algorithm_create_streams(gloo_hip_context_t ctx, int algo, int op, 
     }
     std::vector<hipStream_t> ss;
     for (int i = 0; i < nstreams; i++) ss.push_back(static_cast<hipStream_t>(streams[i]));
+    // Validated before the collective construction: a refusal after it would
+    // run the executor's release() on this rank alone, and the peers would
+    // wait at its barrier until the context timeout.
+    for (hipStream_t t : ss)
+      GLOO_AMD_ENFORCE(t != nullptr || ss.size() == 1, "null stream in a list of ", ss.size(),
+                       " (one stream per pointer)");
     auto a = std::make_unique<gloo_hip_algorithm>();
     a->exec = gloo_amd::PlanExecutor::create(ctx->ctx, algo, op, dtype, std::vector<void*>(ptrs, ptrs + nptrs), count,
                                              re, ss.empty() ? nullptr : ss[0], std::vector<void*>{}, 0, workspace);

@@ -22,12 +22,25 @@
 
 #include "gloo_amd.h"
 #include "gloo_amd/common.h"
+#include "gloo_amd/errors.h"
 #include "gloo_amd/ipc.h"
 #include "gloo_amd/signal.h"
 
 namespace gloo_amd {
 
 namespace {
+
+// A cross-process inbox arena larger than kSegMax is split into slabs.
+// Importing a block of 2^31 bytes or more hangs in hipIpcOpenMemHandle on
+// ROCm 7 / MI355X (profiles/round3/r3t_*, r3u_*), and the pool's size classes
+// above 1 GiB are multiples of 256 MiB (ipc.cc), so 1.75 GiB is the largest
+// class an import may map.  Every range a step or a peer's message touches
+// lies inside one slab (arenaSegments), so pointers into the arena are
+// resolved per range and no kernel ever sees a slab boundary.
+constexpr int kMaxArenaSegs = 16;
+constexpr size_t kSegMax = size_t(7) << 28;     // 1.75 GiB
+constexpr size_t kSegTarget = size_t(1) << 30;  // accesses are packed into slabs of about 1 GiB
+constexpr size_t kSegAlign = 256;               // a logical offset keeps its residue mod 256 B in its slab
 
 struct ArenaRecord {
   int32_t pid;
@@ -48,6 +61,17 @@ struct ArenaRecord {
   uint64_t mailboxBytes;
   uint64_t slabBytes;        // size class of the arena's pool slab (ipc.h): what an import maps
   uint64_t mailboxSlabBytes; // likewise for the mailbox's slab
+  // > 0: the arena is nseg pool slabs, none of 2 GiB or more (arenaSegments);
+  // `ptr`, `handle`, `nonce` and `slabBytes` above are then unused
+  int32_t nseg;
+  int32_t pad;
+  struct Seg {
+    uint64_t start, end;  // the logical arena bytes [start, end) it holds
+    uint64_t ptr;         // the slab; logical `start` sits at ptr + (start % kSegAlign)
+    uint64_t slabBytes;
+    uint64_t nonce;       // written at the slab's first word, checked by every importer
+    hipIpcMemHandle_t handle;
+  } seg[kMaxArenaSegs];
 };
 
 // A value no earlier arena of this process or its peers is likely to hold.
@@ -474,9 +498,94 @@ Plan planFor(int algo, int rank, int size, size_t count, int nin, int nout, size
 
 // The text of a failed import check (tests and tools look for it).
 constexpr const char* kStaleImport = "does not show its contents";
-// Largest inbox arena shared between processes (see the constructor).
-constexpr size_t kMaxIpcArena = (size_t(2) << 30) - (size_t(2) << 20);
+
+// The slabs of a segmented arena (kSegMax): the byte ranges of the arena
+// every step of `p` reads or writes — its inbox regions (DECL_RECV, which
+// bound every peer's message), the REDUCE inboxes and the arena operands of
+// copies, sends and folds — merged where they overlap into atoms, and the
+// atoms packed in order into slabs of at most kSegTarget bytes (an atom
+// larger than that gets a slab of its own, up to kSegMax).  An atom above
+// kSegMax, or more than kMaxArenaSegs slabs, is refused.
+std::vector<std::pair<size_t, size_t>> arenaSegments(const Plan& p, size_t es) {
+  std::vector<std::pair<size_t, size_t>> iv;
+  auto add = [&](uint64_t off, uint64_t len) {
+    if (len) iv.push_back({(size_t)off * es, (size_t)(off + len) * es});
+  };
+  for (const Step& s : p.steps) {
+    if (s.kind == GLOO_HIP_STEP_DECL_RECV) {
+      add(s.dst_off, s.length);
+    } else if (s.kind == GLOO_HIP_STEP_REDUCE) {
+      add(s.src_off, s.length);
+    } else {
+      if (s.flags & GLOO_HIP_SRC_ARENA) add(s.src_off, s.length);
+      if (s.flags & GLOO_HIP_DST_ARENA) add(s.dst_off, s.length);
+    }
+  }
+  std::sort(iv.begin(), iv.end());
+  std::vector<std::pair<size_t, size_t>> atoms;
+  for (const auto& x : iv) {
+    if (!atoms.empty() && x.first < atoms.back().second) {
+      atoms.back().second = std::max(atoms.back().second, x.second);
+    } else {
+      atoms.push_back(x);
+    }
+  }
+  std::vector<std::pair<size_t, size_t>> segs;
+  for (const auto& a : atoms) {
+    GLOO_AMD_ENFORCE(a.second - a.first <= kSegMax, "one inbox region of ", a.second - a.first,
+                     " B would be shared between processes; HIP IPC imports of 2 GiB and more hang on this "
+                     "platform, so a message may span at most ", kSegMax,
+                     " B: split the call, or run the ranks as threads of one process");
+    if (!segs.empty() && a.second - segs.back().first <= kSegTarget) {
+      segs.back().second = a.second;
+    } else {
+      segs.push_back(a);
+    }
+  }
+  GLOO_AMD_ENFORCE(segs.size() <= (size_t)kMaxArenaSegs, "an inbox arena of ", segs.size(),
+                   " slabs (at most ", kMaxArenaSegs, "): split the call");
+  return segs;
+}
 }  // namespace
+
+}  // namespace gloo_amd
+
+// Test and tooling hook (include/gloo_amd.h): the slabs a rank's inbox arena
+// is split into when other processes map it (executor.cc kSegMax); 0 slabs
+// when it stays one block.
+extern "C" int gloo_hip_arena_slabs(int algo, int rank, int size, size_t count, int ninputs, int noutputs,
+                                    size_t elem_size, size_t max_segment_bytes, const int* recv_elems,
+                                    uint64_t* ranges, size_t capacity, size_t* nslabs) {
+  using namespace gloo_amd;
+  try {
+    GLOO_AMD_ENFORCE(nslabs && size >= 1 && rank >= 0 && rank < size && elem_size > 0, "bad arguments");
+    std::vector<int> re;
+    if (recv_elems) re.assign(recv_elems, recv_elems + size);
+    const Plan p = planFor(algo, rank, size, count, ninputs, noutputs, elem_size, max_segment_bytes, re);
+    constexpr size_t kArenaGranule = 2u << 20;
+    const size_t bytes = (std::max<size_t>(256, p.arena * elem_size) + kArenaGranule - 1) / kArenaGranule * kArenaGranule;
+    std::vector<std::pair<size_t, size_t>> segs;
+    if (bytes > kSegMax) segs = arenaSegments(p, elem_size);
+    *nslabs = segs.size();
+    for (size_t k = 0; ranges && k < segs.size() && k < capacity; k++) {
+      ranges[2 * k] = segs[k].first;
+      ranges[2 * k + 1] = segs[k].second;
+    }
+    return GLOO_HIP_OK;
+  } catch (const std::exception& e) {
+    return gloo_amd::setError(GLOO_HIP_EINVAL_ARG, e.what());
+  }
+}
+
+namespace gloo_amd {
+
+char* PlanExecutor::segAt(const std::vector<ArenaSeg>& segs, char* base, size_t off, size_t bytes) {
+  if (segs.empty()) return base + off;
+  for (const ArenaSeg& g : segs)
+    if (g.start <= off && off + bytes <= g.end) return g.ptr + (off - g.start);
+  GLOO_AMD_ENFORCE(bytes == 0, "arena range [", off, ", +", bytes, ") crosses a slab boundary");
+  return segs.front().ptr;  // an empty message: never dereferenced
+}
 
 void PlanExecutor::setBuffers(const std::vector<void*>& inputs, const std::vector<void*>& outputs) {
   GLOO_AMD_ENFORCE(inputs.size() == inputs_.size() && outputs.size() == ptrs_.size(),
@@ -675,11 +784,16 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     where = ctx_->allgather(strcat_("inst", inst_, "/where"), blob);
   }
   GLOO_AMD_TRACE_PHASE("where exchanged");
-  // Inbox arenas other processes map must stay below 2 GiB: importing a
-  // block of 2 GiB or more hangs in hipIpcOpenMemHandle on ROCm 7 / MI355X
-  // (profiles/round3/r3t_*, r3u_*; 1.5 GiB imports work).  Every rank
-  // decides from the same data (all ranks' plans, all ranks' pids), so all
-  // refuse together rather than some waiting at the next exchange.
+  // Inbox arenas other processes map: no imported block may reach 2 GiB
+  // (importing one hangs in hipIpcOpenMemHandle on ROCm 7 / MI355X,
+  // profiles/round3/r3t_*, r3u_*), so an arena above kSegMax becomes several
+  // slabs (arenaSegments).  Every rank checks every rank's plan (the same
+  // data everywhere), so a layout that cannot be split is refused by all
+  // ranks together rather than some waiting at the next exchange.
+  constexpr size_t kArenaGranule = 2u << 20;
+  auto arenaBytesOf = [&](const Plan& p) {
+    return (std::max<size_t>(256, p.arena * es_) + kArenaGranule - 1) / kArenaGranule * kArenaGranule;
+  };
   {
     bool anyCross = false;
     for (int r = 0; r < P; r++) {
@@ -690,16 +804,13 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     }
     const char* hm = std::getenv("GLOO_AMD_ARENA");
     const bool host = workspace == GLOO_HIP_WORKSPACE_HOST || (hm && std::string(hm) == "host");
-    if (anyCross && !host) {
-      size_t maxArena = 0;
-      for (int r = 0; r < P; r++)
-        maxArena = std::max(maxArena, (size_t)planFor(planAlgo_, r, P, count_, (int)inputs_.size(),
-                                                      (int)ptrs_.size(), es_, maxSegmentBytes_, recvElems_).arena * es_);
-      GLOO_AMD_ENFORCE(maxArena < kMaxIpcArena, "an inbox arena of ", maxArena, " B (", count_, " elements of ", es_,
-                       " B) would be shared between processes; HIP IPC imports of 2 GiB and more hang on this "
-                       "platform: split the call into pieces of at most ", kMaxIpcArena / 2 / es_,
-                       " elements, or run the ranks as threads of one process");
-    }
+    if (anyCross && !host)
+      for (int r = 0; r < P; r++) {
+        const Plan pr = r == me ? plan_
+                                : planFor(planAlgo_, r, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_,
+                                          maxSegmentBytes_, recvElems_);
+        if (arenaBytesOf(pr) > kSegMax) (void)arenaSegments(pr, es_);
+      }
   }
   peers_.resize(P);
   bool sharesDeviceInProcess = false, crossSender = false;
@@ -738,12 +849,23 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   // address a peer has imported always maps these pages (a freed and
   // re-exported block of the same size at the same address was imported as
   // the OLD block's pages: DESIGN.md §4, profiles/round3/r3b_*).
-  constexpr size_t kArenaGranule = 2u << 20;
-  const size_t arenaBytes = (std::max<size_t>(256, plan_.arena * es_) + kArenaGranule - 1) / kArenaGranule * kArenaGranule;
+  const size_t arenaBytes = arenaBytesOf(plan_);
   arenaBytes_ = arenaBytes;
   if (hostArena_) {
     arenaShm_ = HostShm::create(arenaBytes);
     arena_ = static_cast<char*>(arenaShm_->dev);
+  } else if (crossProcess_ && arenaBytes > kSegMax) {
+    // several slabs, each below 2 GiB; the ranges of the plan never straddle two
+    for (const auto& g : arenaSegments(plan_, es_)) {
+      ArenaSeg a;
+      a.start = g.first;
+      a.end = g.second;
+      GLOO_AMD_TRACE_PHASE("acquiring a slab for arena bytes [", a.start, ", ", a.end, ") fine=", fineArena_);
+      a.slab = ipc::acquire(ctx_->device(), a.end - a.start + a.start % kSegAlign, fineArena_);
+      arenaSegs_.push_back(a);  // released with the executor even if a later acquire fails
+      arenaSegs_.back().ptr = a.slab->ptr + a.start % kSegAlign;
+    }
+    arena_ = arenaSegs_.front().ptr;  // non-null; every access goes through arenaAt
   } else if (crossProcess_) {
     GLOO_AMD_TRACE_PHASE("acquiring a slab of ", arenaBytes, " B fine=", fineArena_);
     arenaSlab_ = ipc::acquire(ctx_->device(), arenaBytes, fineArena_);
@@ -825,7 +947,21 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   rec.ptr = reinterpret_cast<uint64_t>(arena_);
   rec.bytes = arenaBytes;
   rec.deviceSignal = deviceSignal_ ? 1 : 0;
-  if (!hostArena_) {
+  if (!arenaSegs_.empty()) {
+    rec.nseg = (int32_t)arenaSegs_.size();
+    for (size_t k = 0; k < arenaSegs_.size(); k++) {
+      const ArenaSeg& a = arenaSegs_[k];
+      ArenaRecord::Seg& g = rec.seg[k];
+      g.start = a.start;
+      g.end = a.end;
+      g.ptr = reinterpret_cast<uint64_t>(a.slab->ptr);
+      g.slabBytes = a.slab->bytes;
+      g.handle = a.slab->handle;
+      g.nonce = arenaNonce();
+      GLOO_AMD_HIP_CHECK(hipMemcpyAsync(a.slab->ptr, &g.nonce, sizeof(g.nonce), hipMemcpyHostToDevice, stream_));
+    }
+    GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+  } else if (!hostArena_) {
     // the first 8 bytes of the arena carry a nonce until the first message
     // lands; a peer that maps the arena over IPC reads it back (below)
     rec.nonce = arenaNonce();
@@ -910,7 +1046,38 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       }
     }
     if (!sendPeers.count(peer)) continue;
-    if (pr.host && pr.pid != ctx_->pid()) {
+    GLOO_AMD_ENFORCE(pr.nseg >= 0 && pr.nseg <= kMaxArenaSegs, "bad arena record from rank ", peer);
+    if (pr.nseg > 0) {
+      // a segmented arena: every slab mapped (or, in this process, used) on
+      // its own and checked by its nonce
+      for (int k = 0; k < pr.nseg; k++) {
+        const ArenaRecord::Seg& g = pr.seg[k];
+        char* base = reinterpret_cast<char*>(g.ptr);
+        const size_t need = g.end - g.start + g.start % kSegAlign;
+        if (pr.pid != ctx_->pid()) {
+          GLOO_AMD_TRACE_PHASE("importing rank ", peer, "'s arena slab ", k, " ", (void*)g.ptr, " (", g.slabBytes, " B)");
+          base = static_cast<char*>(ipc::import(pr.pid, pr.incarnation, g.ptr, std::max<uint64_t>(need, g.slabBytes),
+                                                g.handle));
+          peers_[peer].ipc = true;
+        } else if (pr.device != ctx_->device()) {
+          hipError_t e = hipDeviceEnablePeerAccess(pr.device, 0);
+          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
+          (void)hipGetLastError();
+        }
+        uint64_t seen = 0;
+        GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, base, sizeof(seen), hipMemcpyDeviceToHost, stream_));
+        GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+        GLOO_AMD_ENFORCE(seen == g.nonce, "rank ", me, ": the mapping of rank ", peer, "'s arena slab ", k, " (",
+                         (void*)g.ptr, ", ", g.slabBytes, " B, in pid ", pr.pid, ", mapped at ", (void*)base, ") ",
+                         kStaleImport, ": read ", seen, ", expected ", g.nonce);
+        ArenaSeg a;
+        a.start = g.start;
+        a.end = g.end;
+        a.ptr = base + g.start % kSegAlign;
+        peers_[peer].segs.push_back(a);
+      }
+      peers_[peer].base = peers_[peer].segs.front().ptr;
+    } else if (pr.host && pr.pid != ctx_->pid()) {
       // another process's host workspace: map the same pages here
       peerShm_.push_back(HostShm::open(std::string(pr.shm), pr.bytes));
       peers_[peer].base = static_cast<char*>(peerShm_.back()->dev);
@@ -1075,8 +1242,11 @@ void PlanExecutor::release() {
     if (ctx_->size > 1) {
       // IPC imports stay mapped (ipc.h: the process-wide import cache);
       // nobody reuses or frees an arena a peer may still write
-      for (auto& p : peers_)
-        if (p.ipc) ipc::unimport(p.base);
+      for (auto& p : peers_) {
+        if (!p.ipc) continue;
+        if (p.segs.empty()) ipc::unimport(p.base);
+        for (const ArenaSeg& a : p.segs) ipc::unimport(a.ptr - a.start % kSegAlign);
+      }
       for (size_t q = 0; q < peerMailbox_.size(); q++)
         if (peerMailboxIpc_[q]) ipc::unimport(peerMailbox_[q]);
       peers_.clear();
@@ -1085,11 +1255,14 @@ void PlanExecutor::release() {
       peerShm_.clear();
       if (arenaShm_) {
         arenaShm_.reset();
+      } else if (!arenaSegs_.empty()) {
+        for (ArenaSeg& a : arenaSegs_) ipc::release(a.slab);  // back to the pool, never freed
       } else if (arenaSlab_) {
         ipc::release(arenaSlab_);  // back to the pool, never freed
       } else if (arena_) {
         GLOO_AMD_HIP_RELEASE(hipFree(arena_));  // never exported
       }
+      arenaSegs_.clear();
       arenaSlab_ = nullptr;
       arena_ = nullptr;
       if (mailboxSlab_) {
@@ -1361,10 +1534,13 @@ void PlanExecutor::buildInterp() {
   };
   // a sliced plan's message sizes were vetted when the ranks agreed on it
   const size_t limit = slices_ > 1 ? SIZE_MAX : interpBytes();
-  auto userOrArena = [&](bool arena) { return arena ? arena_ : userPtr(0); };
+  // a step operand: arena (the slab holding [off, +len)) or user buffer 0
+  auto userOrArena = [&](bool arena, uint64_t off, uint64_t len) -> char* {
+    return arena ? arenaAt(off, len) : userPtr(0) + off * es_;
+  };
   auto sendSrc = [&](const Step& t) -> const char* {
-    const char* base = t.flags & GLOO_HIP_SRC_ARENA ? arena_ : t.flags & GLOO_HIP_FROM_INPUTS ? inPtr(0) : userPtr(0);
-    return base + t.src_off * es_;
+    if (t.flags & GLOO_HIP_SRC_ARENA) return arenaAt(t.src_off, t.length);
+    return (t.flags & GLOO_HIP_FROM_INPUTS ? inPtr(0) : userPtr(0)) + t.src_off * es_;
   };
   std::vector<InterpStep> v;
   auto push = [&](int kind) -> InterpStep& {
@@ -1417,7 +1593,7 @@ void PlanExecutor::buildInterp() {
         break;
       case GLOO_HIP_STEP_SEND: {
         InterpStep& t = push(kInterpSend);
-        t.dst = peers_[s.peer].base + (remoteRegion_.at({s.peer, s.slot}) + s.dst_off) * es_;
+        t.dst = peerAt(s.peer, remoteRegion_.at({s.peer, s.slot}) + s.dst_off, s.length);
         t.src[0] = sendSrc(s);
         t.n = s.length;
         withSeq(t, i, sigFlag(s.peer, s.slot));
@@ -1433,12 +1609,12 @@ void PlanExecutor::buildInterp() {
       case GLOO_HIP_STEP_REDUCE: {  // out = (in | out) op inbox
         const char* a = (s.flags & GLOO_HIP_FROM_INPUTS ? inPtr(0) : static_cast<const char*>(userPtr(0))) +
                         s.dst_off * es_;
-        fold(userPtr(0) + s.dst_off * es_, {a, arena_ + s.src_off * es_}, s.length, 0);
+        fold(userPtr(0) + s.dst_off * es_, {a, arenaAt(s.src_off, s.length)}, s.length, 0);
         break;
       }
       case GLOO_HIP_STEP_COPY:
-        if (!copy(userOrArena(s.flags & GLOO_HIP_DST_ARENA) + s.dst_off * es_,
-                  userOrArena(s.flags & GLOO_HIP_SRC_ARENA) + s.src_off * es_, s.length))
+        if (!copy(userOrArena(s.flags & GLOO_HIP_DST_ARENA, s.dst_off, s.length),
+                  userOrArena(s.flags & GLOO_HIP_SRC_ARENA, s.src_off, s.length), s.length))
           return fail();
         break;
       case GLOO_HIP_STEP_LOCAL_REDUCE:  // as enqueue(): chained folds of <= GLOO_HIP_MAX_SRCS sources
@@ -1474,7 +1650,7 @@ void PlanExecutor::buildInterp() {
         break;
       case GLOO_HIP_STEP_FOLD:
         GLOO_AMD_ENFORCE(!foldSrcs.empty() && foldSrcs.size() <= GLOO_HIP_MAX_SRCS, "bad fold");
-        fold(userOrArena(s.flags & GLOO_HIP_DST_ARENA) + s.dst_off * es_, foldSrcs, s.length,
+        fold(userOrArena(s.flags & GLOO_HIP_DST_ARENA, s.dst_off, s.length), foldSrcs, s.length,
              s.flags & GLOO_HIP_FOLD_TREE ? 2 : s.flags & GLOO_HIP_FOLD_REVERSE ? 1 : 0);
         foldSrcs.clear();
         break;
@@ -1526,17 +1702,19 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
   // hop costs dispatches, not bytes.  Off while profiling reduce kernels.
   const size_t kFuseBytes = fuseBytes();
   const bool fuse = deviceSignal_ && !profiling_ && kFuseBytes > 0 && !custom_;
-  auto userOrArena = [&](bool arena) { return arena ? arena_ : userPtr(0); };
+  // a step operand: arena (the slab holding [off, +len)) or user buffer 0
+  auto userOrArena = [&](bool arena, uint64_t off, uint64_t len) -> char* {
+    return arena ? arenaAt(off, len) : userPtr(0) + off * es_;
+  };
   // a SEND's source: the arena, input 0 (gloo::reduce's first segments) or output 0
   auto sendSrc = [&](const Step& t) -> const char* {
-    const char* base = t.flags & GLOO_HIP_SRC_ARENA ? arena_
-                       : t.flags & GLOO_HIP_FROM_INPUTS ? static_cast<const char*>(inputs_.at(0))
-                                                        : userPtr(0);
-    return base + t.src_off * es_;
+    if (t.flags & GLOO_HIP_SRC_ARENA) return arenaAt(t.src_off, t.length);
+    return (t.flags & GLOO_HIP_FROM_INPUTS ? static_cast<const char*>(inputs_.at(0)) : userPtr(0)) +
+           t.src_off * es_;
   };
   const std::vector<Step>& steps = plan_.steps;
   auto sendDst = [&](const Step& t) {
-    return peers_[t.peer].base + (remoteRegion_[{t.peer, t.slot}] + t.dst_off) * es_;
+    return peerAt(t.peer, remoteRegion_[{t.peer, t.slot}] + t.dst_off, t.length);
   };
   auto isWaitKind = [](int k) { return k == GLOO_HIP_STEP_WAIT_RECV || k == GLOO_HIP_STEP_WAIT_NOTIFY; };
   std::vector<const void*> foldSrcs;
@@ -1613,8 +1791,8 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
       std::vector<size_t> lens;
       for (; j < steps.size() && steps[j].kind == GLOO_HIP_STEP_COPY && ops.size() < (size_t)kMaxCopyEntries; j++) {
         const Step& t = steps[j];
-        ops.push_back({userOrArena(t.flags & GLOO_HIP_DST_ARENA) + t.dst_off * es_,
-                       userOrArena(t.flags & GLOO_HIP_SRC_ARENA) + t.src_off * es_});
+        ops.push_back({userOrArena(t.flags & GLOO_HIP_DST_ARENA, t.dst_off, t.length),
+                       userOrArena(t.flags & GLOO_HIP_SRC_ARENA, t.src_off, t.length)});
         lens.push_back(t.length * es_);
       }
       bool disjoint = true;
@@ -1663,12 +1841,12 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         if (t->kind == GLOO_HIP_STEP_REDUCE) {
           op = op_;
           dst = userPtr(0) + t->dst_off * es_;
-          src = arena_ + t->src_off * es_;
+          src = arenaAt(t->src_off, t->length);
         } else if (t->kind == GLOO_HIP_STEP_COPY) {
-          dst = userOrArena(t->flags & GLOO_HIP_DST_ARENA) + t->dst_off * es_;
-          src = userOrArena(t->flags & GLOO_HIP_SRC_ARENA) + t->src_off * es_;
+          dst = userOrArena(t->flags & GLOO_HIP_DST_ARENA, t->dst_off, t->length);
+          src = userOrArena(t->flags & GLOO_HIP_SRC_ARENA, t->src_off, t->length);
         } else {
-          dst = peers_[t->peer].base + (remoteRegion_[{t->peer, t->slot}] + t->dst_off) * es_;
+          dst = peerAt(t->peer, remoteRegion_[{t->peer, t->slot}] + t->dst_off, t->length);
           src = sendSrc(*t);
         }
         const size_t bytes = t->length * es_;
@@ -1704,7 +1882,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
       case GLOO_HIP_STEP_DECL_RECV:
         break;
       case GLOO_HIP_STEP_SEND: {
-        char* dst = peers_[s.peer].base + (remoteRegion_[{s.peer, s.slot}] + s.dst_off) * es_;
+        char* dst = peerAt(s.peer, remoteRegion_[{s.peer, s.slot}] + s.dst_off, s.length);
         const char* src = sendSrc(s);
         // GLOO_AMD_COPY=auto: a lone SEND of >= 16 MiB to a rank on this
         // same GPU goes to the copy kernel with 256 workgroups, which moves
@@ -1746,10 +1924,10 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         if (s.flags & GLOO_HIP_FROM_INPUTS) {  // out = in op inbox (gloo/reduce.cc:180-184)
           checkRc(gloo_hip_reduce3(op_, dtype_, userPtr(0) + s.dst_off * es_,
                                    static_cast<const char*>(inputs_.at(0)) + s.dst_off * es_,
-                                   arena_ + s.src_off * es_, s.length, stream_),
+                                   arenaAt(s.src_off, s.length), s.length, stream_),
                   "gloo_hip_reduce3");
         } else {
-          checkRc(gloo_hip_reduce(op_, dtype_, userPtr(0) + s.dst_off * es_, arena_ + s.src_off * es_, s.length,
+          checkRc(gloo_hip_reduce(op_, dtype_, userPtr(0) + s.dst_off * es_, arenaAt(s.src_off, s.length), s.length,
                                   stream_),
                   "gloo_hip_reduce");
         }
@@ -1761,8 +1939,8 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         break;
       }
       case GLOO_HIP_STEP_COPY: {
-        char* dst = (s.flags & GLOO_HIP_DST_ARENA ? arena_ : userPtr(0)) + s.dst_off * es_;
-        const char* src = (s.flags & GLOO_HIP_SRC_ARENA ? arena_ : userPtr(0)) + s.src_off * es_;
+        char* dst = userOrArena(s.flags & GLOO_HIP_DST_ARENA, s.dst_off, s.length);
+        const char* src = userOrArena(s.flags & GLOO_HIP_SRC_ARENA, s.src_off, s.length);
         deviceMove(dst, src, s.length * es_, stream_);
         break;
       }
@@ -1823,9 +2001,11 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         // unchanged (a mesh owner's return of its finished range) ride in the
         // fold's own pass, and its last workgroup signals them and the NOTIFY
         // credits that follow.  Device signalling only; off while the reduce
-        // kernels are being timed, so events and stamps keep measuring a pure
-        // fold.
-        if (foldSend_ && deviceSignal_ && !custom_ && !profiling_ && !stamping_ && s.length > 0 &&
+        // kernels are timed with events (they need a pure fold between two
+        // markers).  Device stamps time the fused launch itself, forward
+        // stores included (stamp_end waits for them), so what ships is what
+        // is measured; the slot's bytes stay the fold's (k + 1) * n * s.
+        if (foldSend_ && deviceSignal_ && !custom_ && !profiling_ && s.length > 0 &&
             !(s.flags & GLOO_HIP_DST_ARENA)) {
           char* fdst = userPtr(0) + s.dst_off * es_;
           FwdDesc fwd[kMaxCopyEntries];
@@ -1849,6 +2029,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
               fwd[nf++] = FwdDesc{nullptr, sigFlag(steps[j].peer, steps[j].slot), seqOf(j, r, graph)};
           if (nf > 0 && sendsTaken) {
             const Step& t0 = steps[i + 1];
+            StampScope stamp(slotOf(i));
             checkRc(launchFoldSend(op_, dtype_, fdst, foldSrcs.data(), (int)foldSrcs.size(), s.length, mode, fwd,
                                    nf, ticket_ + (size_t)t0.peer * GLOO_HIP_NUM_SLOTS + t0.slot, epoch, stream_),
                     "fold+forward");
@@ -1860,7 +2041,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         }
         {
           StampScope stamp(slotOf(i));
-          checkRc(launchFold(op_, dtype_, userOrArena(s.flags & GLOO_HIP_DST_ARENA) + s.dst_off * es_,
+          checkRc(launchFold(op_, dtype_, userOrArena(s.flags & GLOO_HIP_DST_ARENA, s.dst_off, s.length),
                              foldSrcs.data(), (int)foldSrcs.size(), s.length, mode, stream_),
                   "fold");
         }

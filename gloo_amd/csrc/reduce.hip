@@ -92,6 +92,13 @@ using TrF64 = FloatTraits<double>;
 // followed by the f16 rounding equals one correctly rounded f16 result for
 // + and * because 24 >= 2*11+2, so this matches F16C (gloo/math.cc:17-97)
 // and CUDA __float2half(__half2float(a) op __half2float(b)) (cuda.cu:301-318).
+//
+// NaN results carry the reference's bits, not the convert's: the F16C body as
+// the reference builds it (g++, -mf16c) returns the second operand's NaN
+// quietened, else the first's, else x86's default NaN 0xFE00 for an invalid
+// operation (inf - inf, 0 * inf).  Probed on oracle/_ref, pinned by
+// tests/golden/math_golden.npz "f16_nan/*".  One compare + two selects on the
+// rare path's condition; they hide under the memory stream.
 struct TrF16 {
   using Storage = uint16_t;
   __device__ static __forceinline__ float widen(uint16_t x) {
@@ -100,11 +107,17 @@ struct TrF16 {
   __device__ static __forceinline__ uint16_t narrow(float f) {
     return __builtin_bit_cast(uint16_t, (_Float16)f);
   }
+  __device__ static __forceinline__ bool is_nan(uint16_t x) { return (x & 0x7FFFu) > 0x7C00u; }
+  __device__ static __forceinline__ uint16_t nan_of(uint16_t a, uint16_t b) {
+    return is_nan(b) ? (uint16_t)(b | 0x0200u) : is_nan(a) ? (uint16_t)(a | 0x0200u) : (uint16_t)0xFE00u;
+  }
   __device__ static __forceinline__ uint16_t sum(uint16_t a, uint16_t b) {
-    return narrow(widen(a) + widen(b));
+    const float r = widen(a) + widen(b);
+    return r != r ? nan_of(a, b) : narrow(r);
   }
   __device__ static __forceinline__ uint16_t product(uint16_t a, uint16_t b) {
-    return narrow(widen(a) * widen(b));
+    const float r = widen(a) * widen(b);
+    return r != r ? nan_of(a, b) : narrow(r);
   }
   __device__ static __forceinline__ uint16_t max(uint16_t a, uint16_t b) {
     return (widen(a) < widen(b)) ? b : a;
@@ -115,14 +128,17 @@ struct TrF16 {
 };
 
 // bfloat16 held as raw bits (c10::BFloat16 semantics: widen by <<16, op in
-// f32, round-to-nearest-even back; v_cvt_pk_bf16_f32 on gfx950).
+// f32, round-to-nearest-even back; v_cvt_pk_bf16_f32 on gfx950).  c10's
+// round_to_nearest_even returns the canonical 0x7FC0 for every NaN
+// (torch/headeronly/util/BFloat16.h:100-108), where the convert keeps sign
+// and payload: one compare + select restores the reference's bits.
 struct TrBF16 {
   using Storage = uint16_t;
   __device__ static __forceinline__ float widen(uint16_t x) {
     return __builtin_bit_cast(float, (uint32_t)x << 16);
   }
   __device__ static __forceinline__ uint16_t narrow(float f) {
-    return __builtin_bit_cast(uint16_t, (__bf16)f);
+    return f != f ? (uint16_t)0x7FC0u : __builtin_bit_cast(uint16_t, (__bf16)f);
   }
   __device__ static __forceinline__ uint16_t sum(uint16_t a, uint16_t b) {
     return narrow(widen(a) + widen(b));

@@ -9,6 +9,7 @@
 #include <chrono>
 #include <cstring>
 #include <limits>
+#include <memory>
 #include <random>
 #include <string>
 #include <thread>
@@ -31,11 +32,15 @@ struct RecvRecord {
   int32_t host;     // host memory: written directly within one process, as payload words across processes
   int32_t channel;  // this buffer's channel of the transport block
   int32_t pad;
+  uint64_t alloc;   // bytes of the device allocation an import would map
   hipIpcMemHandle_t handle;
 };
 
-// Channel::len of a message carried in the payload words.
-constexpr uint32_t kPayloadFlag = 0x80000000u;
+// An IPC import maps the exporter's whole allocation, and importing a block
+// of 2^31 bytes or more hangs in hipIpcOpenMemHandle on ROCm 7 / MI355X
+// (profiles/round3/r3t_*, r3u_*): a receive buffer inside such an allocation
+// is refused to a peer process before any import is attempted.
+constexpr uint64_t kMaxImportBytes = uint64_t(1) << 31;
 
 std::string recordKey(uint64_t inst, int sender, int receiver, uint64_t slot) {
   return strcat_("gloo_amd/xgmi/", inst, "/", sender, "->", receiver, "/", slot);
@@ -53,19 +58,43 @@ bool isDevice(const void* p) {
 void bump(void* p) { static_cast<std::atomic<uint64_t>*>(p)->fetch_add(1, std::memory_order_acq_rel); }
 
 // A message for a host receive buffer in another process: its bytes go into
-// the channel's payload words, then the arrival is published.
+// the payload record of its arrival number, then the arrival is published.
+// Runs as a stream host function; a record still holding an unconsumed
+// message (kPayloadRing sends ahead of the receiver's waits) is waited for,
+// up to the context timeout, after which the message is dropped and
+// `failed` is set for the sending thread to raise.
 struct PayloadSend {
-  Device::Channel* ch;
-  const char* src;  // read when the stream reaches this point
+  Device* dev;
+  int src, dst, idx;
+  const char* bytes;  // read when the stream reaches this point
   uint32_t off, len;
+  std::chrono::milliseconds timeout;
+  std::atomic<int>* failed;
 };
 void payloadSend(void* p) {
-  auto* s = static_cast<PayloadSend*>(p);
-  if (s->len) std::memcpy(s->ch->payload, s->src, s->len);
-  s->ch->off = s->off;
-  s->ch->len = kPayloadFlag | s->len;
-  s->ch->count.fetch_add(1, std::memory_order_acq_rel);
-  delete s;
+  std::unique_ptr<PayloadSend> s(static_cast<PayloadSend*>(p));
+  Device::Channel& ch = s->dev->channel(s->src, s->dst, s->idx);
+  const uint64_t k = ch.count.load(std::memory_order_acquire) + 1;
+  Device::PayloadRecord& rec = s->dev->payloadRecord(s->src, s->dst, s->idx, k);
+  const auto deadline = std::chrono::steady_clock::now() + s->timeout;
+  for (uint64_t i = 0;; i++) {
+    const uint64_t seq = rec.seq.load(std::memory_order_acquire);
+    if (seq == 0 || rec.ack.load(std::memory_order_acquire) == seq) break;
+    if (std::chrono::steady_clock::now() > deadline) {
+      s->failed->store(1, std::memory_order_release);
+      return;
+    }
+    if (i < 4096) {
+      __builtin_ia32_pause();
+    } else {
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
+  if (s->len) std::memcpy(rec.payload, s->bytes, s->len);
+  rec.off = s->off;
+  rec.len = s->len;
+  rec.seq.store(k, std::memory_order_release);
+  ch.count.fetch_add(1, std::memory_order_acq_rel);
 }
 
 // Polls `done` with back-off until it holds, `abort` is set (returns false)
@@ -108,6 +137,7 @@ class SendBuffer : public Buffer {
   void send(size_t offset, size_t length, size_t roffset) override {
     Context& ctx = *dev_->context();
     GLOO_AMD_HIP_CHECK(hipSetDevice(ctx.device()));
+    raiseIfFailed();
     resolve();
     GLOO_AMD_ENFORCE(offset + length <= size_, "send of [", offset, ", +", length, ") beyond a ", size_,
                      "-byte send buffer");
@@ -124,8 +154,9 @@ class SendBuffer : public Buffer {
         GLOO_AMD_HIP_CHECK(hipMemcpyAsync(staging_, src, length, hipMemcpyDeviceToHost, s));
         src = staging_;
       }
-      GLOO_AMD_HIP_CHECK(hipLaunchHostFunc(
-          s, payloadSend, new PayloadSend{channel_, src, (uint32_t)roffset, (uint32_t)length}));
+      GLOO_AMD_HIP_CHECK(hipLaunchHostFunc(s, payloadSend,
+                                           new PayloadSend{dev_, ctx.rank, peer_, channelIdx_, src, (uint32_t)roffset,
+                                                           (uint32_t)length, ctx.timeout(), &failed_}));
     } else {
       if (length) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(remote_ + roffset, ptr_ + offset, length, hipMemcpyDefault, s));
       // stream-ordered: the arrival is published only once the bytes landed
@@ -134,9 +165,18 @@ class SendBuffer : public Buffer {
     GLOO_AMD_HIP_CHECK(hipEventRecord(sent_, s));
   }
   void waitRecv() override { throw EnforceNotMet("waitRecv on a send buffer"); }
-  void waitSend() override { GLOO_AMD_HIP_CHECK(hipEventSynchronize(sent_)); }
+  void waitSend() override {
+    GLOO_AMD_HIP_CHECK(hipEventSynchronize(sent_));
+    raiseIfFailed();
+  }
 
  private:
+  void raiseIfFailed() {
+    if (failed_.exchange(0, std::memory_order_acq_rel))
+      throw IoException(strcat_("Timed out waiting for rank ", peer_, " to consume ", kPayloadRing,
+                                " earlier messages (slot ", slot_, "); a message was dropped"));
+  }
+
   // The peer's receive buffer of this slot (published when it was created).
   void resolve() {
     if (resolved_) return;
@@ -146,6 +186,7 @@ class SendBuffer : public Buffer {
     RecvRecord r;
     std::memcpy(&r, v.data(), sizeof(r));
     peerSize_ = r.size;
+    channelIdx_ = r.channel;
     channel_ = &dev_->channel(ctx.rank, peer_, r.channel);
     if (r.size == 0) {
       remote_ = nullptr;  // a notification buffer: arrivals only
@@ -159,6 +200,10 @@ class SendBuffer : public Buffer {
     } else if (r.host) {
       payload_ = true;  // host memory of another process: payload words
     } else {
+      GLOO_AMD_ENFORCE(r.alloc < kMaxImportBytes, "rank ", peer_, "'s receive buffer (slot ", slot_,
+                       ") lies in a device allocation of ", r.alloc, " B; HIP IPC imports of 2 GiB and more hang "
+                       "on this platform, so a peer process cannot write into it: allocate receive buffers below ",
+                       kMaxImportBytes, " B, or run the ranks as threads of one process");
       GLOO_AMD_ENFORCE(r.ipc, "rank ", peer_, "'s receive buffer is not IPC-exportable");
       // The caller's memory cannot come from the IPC slab pool (ipc.h);
       // this import is used by eager copies only, never captured into a
@@ -188,8 +233,10 @@ class SendBuffer : public Buffer {
   void* opened_ = nullptr;
   char* staging_ = nullptr;
   size_t peerSize_ = 0;
+  int channelIdx_ = -1;
   Device::Channel* channel_ = nullptr;
   hipEvent_t sent_ = nullptr;
+  std::atomic<int> failed_{0};
 };
 
 class RecvBuffer : public Buffer {
@@ -218,9 +265,11 @@ class RecvBuffer : public Buffer {
             hipIpcGetMemHandle(&r.handle, base) == hipSuccess) {
           r.ipc = 1;
           r.offset = (uint64_t)(ptr_ - static_cast<char*>(base));
+          r.alloc = allocSize;
         }
       } else {
         r.host = 1;
+        host_ = true;
       }
       (void)hipGetLastError();
     }
@@ -240,17 +289,22 @@ class RecvBuffer : public Buffer {
     const uint64_t target = baseline_ + ++received_;
     pollUntil([&] { return (int64_t)(channel_->count.load(std::memory_order_acquire) - target) >= 0; }, nullptr,
               ctx.timeout(), strcat_("waiting for rank ", peer_, " (slot ", slot_, ") on rank ", ctx.rank));
-    const uint32_t len = channel_->len;
-    if (len & kPayloadFlag) {  // carried in the payload words (host buffer, sender in another process)
-      const uint32_t n = len & ~kPayloadFlag;
-      GLOO_AMD_ENFORCE(channel_->off + n <= size_, "payload beyond the receive buffer");
-      if (n) std::memcpy(ptr_ + channel_->off, channel_->payload, n);
-    }
+    if (!host_) return;  // device memory: always written in place
+    // A host buffer's sender in another process carries the bytes in the
+    // payload record tagged with this arrival; one in this process wrote
+    // them in place (no record carries this arrival number then).
+    Device::PayloadRecord& rec = dev_->payloadRecord(peer_, ctx.rank, idx_, target);
+    if (rec.seq.load(std::memory_order_acquire) != target) return;
+    GLOO_AMD_ENFORCE((size_t)rec.off + rec.len <= size_, "payload of ", rec.len, " B at ", rec.off,
+                     " beyond the ", size_, "-byte receive buffer");
+    if (rec.len) std::memcpy(ptr_ + rec.off, rec.payload, rec.len);
+    rec.ack.store(target, std::memory_order_release);
   }
 
  private:
   Device* dev_;
   int peer_;
+  bool host_ = false;
   int idx_ = -1;
   Device::Channel* channel_ = nullptr;
   uint64_t baseline_ = 0, received_ = 0;
@@ -270,7 +324,8 @@ Device::Device(std::shared_ptr<Context> ctx, hipStream_t stream) : ctx_(std::mov
     ownStream_ = true;
   }
   const size_t P = (size_t)ctx_->size;
-  blockBytes_ = 4096 + P * P * kChannels * sizeof(Channel) + P * P * kAnnouncements * sizeof(Announcement) + P * 64;
+  blockBytes_ = 4096 + P * P * kChannels * sizeof(Channel) + P * P * kAnnouncements * sizeof(Announcement) + P * 64 +
+                P * P * kChannels * kPayloadRing * sizeof(PayloadRecord);
   blockBytes_ = (blockBytes_ + 4095) / 4096 * 4096;
   std::string name;
   if (ctx_->rank == 0) {
@@ -353,6 +408,14 @@ std::atomic<uint64_t>& Device::orderCounter(int dst) {
   char* p = static_cast<char*>(block_) + 4096 + P * P * kChannels * sizeof(Channel) +
             P * P * kAnnouncements * sizeof(Announcement) + (size_t)dst * 64;
   return *reinterpret_cast<std::atomic<uint64_t>*>(p);
+}
+
+Device::PayloadRecord& Device::payloadRecord(int src, int dst, int idx, uint64_t k) {
+  const size_t P = (size_t)ctx_->size;
+  GLOO_AMD_ENFORCE(idx >= 0 && idx < kChannels, "bad channel ", idx);
+  auto* base = reinterpret_cast<PayloadRecord*>(static_cast<char*>(block_) + 4096 + P * P * kChannels * sizeof(Channel) +
+                                                P * P * kAnnouncements * sizeof(Announcement) + P * 64);
+  return base[(((size_t)src * P + (size_t)dst) * kChannels + (size_t)idx) * kPayloadRing + (size_t)(k % kPayloadRing)];
 }
 
 int Device::allocChannel(int src) {

@@ -142,14 +142,31 @@ class PlanExecutor {
   // last-workgroup end on the GPU's constant clock, which also works inside a
   // replayed hipGraph (events around the steps would force eager runs).
   // After each run the same accessors report the summed kernel durations.
+  // A fused fold + forward launch is stamped as it ships (its forward stores
+  // inside the span); its bytes count as the fold's.
   void setStamping(bool on);
   double lastReduceSeconds() const { return reduceSeconds_; }
   double lastReduceBytes() const { return reduceBytes_; }
   size_t lastReduceCount() const { return reduceCount_; }
 
  private:
+  // One slab of a segmented inbox arena: logical arena bytes [start, end),
+  // with logical `start` at ptr (executor.cc kSegMax).
+  struct ArenaSeg {
+    size_t start = 0, end = 0;
+    char* ptr = nullptr;
+    ipc::Slab* slab = nullptr;  // own arena only
+  };
+  // The address of logical arena byte `off` of a range of `bytes`: base + off
+  // for a one-block arena, else inside the slab that holds the whole range.
+  static char* segAt(const std::vector<ArenaSeg>& segs, char* base, size_t off, size_t bytes);
+  char* arenaAt(uint64_t elems, uint64_t len) const { return segAt(arenaSegs_, arena_, elems * es_, len * es_); }
+  char* peerAt(int peer, uint64_t elems, uint64_t len) const {
+    return segAt(peers_[peer].segs, peers_[peer].base, elems * es_, len * es_);
+  }
   struct Peer {
     char* base = nullptr;
+    std::vector<ArenaSeg> segs;  // its arena's slabs (empty: one block at base)
     bool ipc = false;
     int pid = -1;
     int device = -1;
@@ -197,6 +214,7 @@ class PlanExecutor {
   char* arena_ = nullptr;       // device-visible address of this rank's inboxes
   bool crossProcess_ = false;   // a plan peer lives in another process: arena and mailbox are IPC pool slabs
   ipc::Slab* arenaSlab_ = nullptr;
+  std::vector<ArenaSeg> arenaSegs_;  // a segmented arena's slabs (empty: one block at arena_)
   ipc::Slab* mailboxSlab_ = nullptr;
   size_t arenaBytes_ = 0;       // its allocated size (whole 2 MiB granules)
   bool hostArena_ = false;      // inboxes in shared pinned host memory (HOST workspace)

@@ -8,8 +8,8 @@
 //   Pair::createRecvBuffer(slot, ptr, size)   registers memory the peer writes
 //        into: DEVICE memory is exported (HIP IPC across processes, the raw
 //        pointer within one); HOST memory is written directly within one
-//        process, and across processes carried in the channel's payload
-//        words (at most kPayloadBytes: the reference's notification buffers,
+//        process, and across processes carried in payload records (at most
+//        kPayloadBytes per message: the reference's notification buffers,
 //        &dummy_ / sizeof(dummy_), gloo/cuda_allreduce_ring_chunked.cc:119-123);
 //   Pair::createSendBuffer(slot, ptr, size)   a local buffer; on its first send
 //        it resolves the peer's receive buffer of the same slot;
@@ -22,11 +22,19 @@
 //        IoException, as gloo/transport/tcp/buffer.cc:67-73);
 //   Buffer::waitSend()                        blocks until the last send's copy
 //        out of this buffer has completed.
-// Every receive buffer owns one channel (arrival counter + payload words) of
-// the transport block, allocated by the receiver per (sender, slot) and
+// Every receive buffer owns one channel (an arrival counter, plus a ring of
+// kPayloadRing payload records) of the transport block, allocated by the
+// receiver per (sender, slot) and
 // published with its record, so any number of slots may be live — as many
 // as kChannels per (sender, receiver) at once — and Gloo's ever-increasing
-// context->nextSlot() values never collide.
+// context->nextSlot() values never collide.  A payload message k (the k-th
+// arrival of its channel) lands in record k % kPayloadRing, tagged with k;
+// the receiver copies it out in the waitRecv that expects arrival k and
+// acknowledges it, and the sender reuses a record only once its last message
+// was acknowledged (waiting, bounded by the context timeout, when
+// kPayloadRing messages are unconsumed).  So a second send before the
+// receiver's wait keeps both messages, as the reference's direct writes do,
+// and a device receive buffer reusing the channel never reads a payload.
 //
 // Unbound buffers (the new-style collectives, gloo/allreduce.cc,
 // gloo/allgather.cc, gloo/reduce.cc): two-sided send / recv matched per
@@ -70,7 +78,8 @@ class Pair;
 
 constexpr int kChannels = 128;       // live receive buffers per (sender, receiver)
 constexpr int kAnnouncements = 128;  // unbound messages in flight per (sender, receiver)
-constexpr size_t kPayloadBytes = 48;
+constexpr size_t kPayloadBytes = 40;
+constexpr int kPayloadRing = 4;       // payload messages in flight per channel
 
 // One per rank: the transport device over a connected gloo_amd::Context.
 // Construction is collective (every rank, in the same order as its
@@ -94,11 +103,19 @@ class Device {
 
   struct Channel {
     std::atomic<uint64_t> count;  // arrivals
-    uint32_t off, len;            // the last payload's place in the receive buffer
-    char payload[kPayloadBytes];
+    uint64_t pad[7];
   };
   static_assert(sizeof(Channel) == 64, "one line per channel");
+  struct PayloadRecord {
+    std::atomic<uint64_t> seq;  // the arrival number of the message it holds (0: never used)
+    std::atomic<uint64_t> ack;  // the arrival number the receiver consumed from it
+    uint32_t off, len;          // the message's place in the receive buffer
+    char payload[kPayloadBytes];
+  };
+  static_assert(sizeof(PayloadRecord) == 64, "one line per record");
   Channel& channel(int src, int dst, int idx);
+  // The record arrival `k` of channel (src -> dst, idx) uses.
+  PayloadRecord& payloadRecord(int src, int dst, int idx, uint64_t k);
   int allocChannel(int src);  // receiver side: a free channel of (src -> me)
   void freeChannel(int src, int idx);
 

@@ -115,7 +115,21 @@ DEF_INT(red_u64, uint64_t, uint64_t)
 DEF_FLT(red_f32, float)
 DEF_FLT(red_f64, double)
 
-#define DEF_HALF(NAME, WIDEN, NARROW)                                           \
+/* A NaN result of a 16-bit SUM / PRODUCT, stated explicitly rather than left
+ * to the host's SSE NaN propagation:
+ *  - fp16, the F16C body as the reference builds it (g++ -O3 -mavx -mf16c,
+ *    gloo/math.cc:22-36): the second operand's NaN quietened, else the
+ *    first's, else x86's default NaN 0xFE00 (inf - inf, 0 * inf).  Probed on
+ *    oracle/_ref over every pair of signed payloads (oracle/gen_golden.py
+ *    "f16_nan");
+ *  - bf16: c10's round_to_nearest_even returns 0x7FC0 for any NaN. */
+static inline int f16_nan(uint16_t x) { return (x & 0x7fff) > 0x7c00; }
+static inline uint16_t nan_f16(uint16_t x, uint16_t y) {
+  return f16_nan(y) ? (uint16_t)(y | 0x200) : f16_nan(x) ? (uint16_t)(x | 0x200) : 0xFE00;
+}
+static inline uint16_t nan_bf16(uint16_t x, uint16_t y) { (void)x; (void)y; return 0x7FC0; }
+
+#define DEF_HALF(NAME, WIDEN, NARROW, NANOF)                                    \
   static void NAME(int op, uint16_t* c, const uint16_t* a, const uint16_t* b,   \
                    size_t n) {                                                  \
     size_t i;                                                                   \
@@ -123,15 +137,17 @@ DEF_FLT(red_f64, double)
       const uint16_t x = a[i], y = b[i];                                        \
       const float fx = WIDEN(x), fy = WIDEN(y);                                 \
       uint16_t r;                                                               \
-      if (op == SUM) r = NARROW(fx + fy);                                       \
-      else if (op == PRODUCT) r = NARROW(fx * fy);                              \
-      else if (op == MAX) r = (fx < fy) ? y : x;                                \
+      float f;                                                                  \
+      if (op == SUM || op == PRODUCT) {                                         \
+        f = op == SUM ? fx + fy : fx * fy;                                      \
+        r = f != f ? NANOF(x, y) : NARROW(f);                                   \
+      } else if (op == MAX) r = (fx < fy) ? y : x;                              \
       else r = (fy < fx) ? y : x;                                               \
       c[i] = r;                                                                 \
     }                                                                           \
   }
-DEF_HALF(red_f16, oracle_f16_to_f32, oracle_f32_to_f16)
-DEF_HALF(red_bf16, oracle_bf16_to_f32, oracle_f32_to_bf16)
+DEF_HALF(red_f16, oracle_f16_to_f32, oracle_f32_to_f16, nan_f16)
+DEF_HALF(red_bf16, oracle_bf16_to_f32, oracle_f32_to_bf16, nan_bf16)
 
 int oracle_reduce3(int op, int dtype, void* c, const void* a, const void* b, size_t n) {
   if (op < SUM || op > MIN) return -1;

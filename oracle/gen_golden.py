@@ -77,8 +77,33 @@ def gen_math():
     c = np.empty_like(a)
     oracle.ref().ref_reduce3_f16_scalar(1, c.ctypes.data, a.ctypes.data, b.ctypes.data, 1)
     out["f16_scalar_defect/a"], out["f16_scalar_defect/b"], out["f16_scalar_defect/sum"] = a, b, c
+    out.update(nan_pairs())
     np.savez_compressed(os.path.join(OUT, "math_golden.npz"), **out)
     print("math_golden.npz:", len(out), "arrays")
+
+
+def nan_pairs():
+    """Every ordered pair of 16-bit NaNs (signed, quiet and signalling payloads)
+    and specials, for the NaN bits of SUM / PRODUCT: the F16C body keeps the
+    second operand's payload, else the first's, else emits 0xFE00; c10's bf16
+    emits 0x7FC0.  The length is a multiple of 8, so every element goes through
+    the F16C body (gloo/math.cc:27-32), none through the scalar leftovers."""
+    f16 = [0x7E00, 0xFE00, 0x7C01, 0x7D55, 0xFD55, 0x7FFF, 0xFC01, 0x3C00, 0x7C00, 0xFC00,
+           0x0000, 0x8000, 0x0001, 0x7BFF]
+    bf16 = [0x7FC0, 0xFFC0, 0x7F81, 0x7FD5, 0xFFD5, 0x7FFF, 0xFF81, 0x3F80, 0x7F80, 0xFF80,
+            0x0000, 0x8000, 0x0001, 0x7F7F]
+    out = {}
+    for dtype, vals in (("f16", f16), ("bf16", bf16)):
+        v = np.array(vals, dtype=np.uint16)
+        a = np.repeat(v, len(v))
+        b = np.tile(v, len(v))
+        pad = (-len(a)) % 8
+        a = np.concatenate([a, np.full(pad, v[-1], np.uint16)])
+        b = np.concatenate([b, np.full(pad, v[-1], np.uint16)])
+        out[f"{dtype}_nan/a"], out[f"{dtype}_nan/b"] = a, b
+        for op in oracle.OPS:
+            out[f"{dtype}_nan/{op}"] = oracle.ref_reduce3(op, dtype, a, b)
+    return out
 
 
 def ref_allreduce(algo, op, dtype, inputs):

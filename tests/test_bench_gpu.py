@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def run_bench(variants):
+def run_bench(variants, full=False):
     cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5",
            "--config3-only"]
     if variants:
@@ -32,10 +32,11 @@ def run_bench(variants):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=380, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
-    x = json.loads(line)["xgmi_allreduce"]
+    out = json.loads(line)
+    x = out["xgmi_allreduce"]
     assert x.get("verified") is True, x
     assert x["variants"], x
-    return x["variants"]
+    return out if full else x["variants"]
 
 
 @pytest.fixture(scope="module")
@@ -48,8 +49,30 @@ def gpu():
 
 @pytest.mark.timeout(400)
 def test_config3_variants_in_bench_order_verified(gpu):
-    for name, v in run_bench("").items():
+    out = run_bench("", full=True)
+    for name, v in out["xgmi_allreduce"]["variants"].items():
         assert v.get("verified") is True, (name, v)
+    # SURVEY 8(e) twice: the unfused mesh (a pure fold kernel) and the
+    # default schedule as it ships (fold + forward fused, stamped as one)
+    eff = out["per_gpu_efficiency"]
+    assert eff["value"] and "unfused" in eff["data_path"], eff
+    assert eff["fused_default"]["value"] and "fused" in eff["fused_default"]["data_path"], eff
+    assert "fold + forward fused" in out["xgmi_allreduce"]["schedule"], out["xgmi_allreduce"]
+    assert "unfused" in out["xgmi_allreduce"]["variants"]["mesh_unfused"]["schedule"]
+
+
+@pytest.mark.timeout(200)
+def test_watchdog_fire_exits_nonzero(gpu):
+    """A hung N>1 section must show in the driver's record: the watchdog
+    prints the line with the section marked timed out, then the job fails."""
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5",
+           "--config3-only", "--no-cpu", "--no-host-staged", "--watchdog-seconds", "0.5"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=ROOT)
+    assert r.returncode != 0, r.stdout[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    out = json.loads(line)
+    assert "watchdog" in out["xgmi_allreduce"]["error"], out["xgmi_allreduce"]
+    assert out["value"] > 0
 
 
 @pytest.mark.timeout(400)

@@ -861,7 +861,7 @@ for mode in (1, 2):
         st = a.stats()
         md = a.mode()
         out.append({"mode": mode, "it": it, "graph": md["graph"], "graph_error": md["graph_error"],
-                    "ok": bool((buf == size).all()), **st})
+                    "fold_send": md["fold_send"], "ok": bool((buf == size).all()), **st})
 a.close(); ctx.close()
 print("RESULT" + json.dumps(out), flush=True)
 '''
@@ -869,9 +869,10 @@ print("RESULT" + json.dumps(out), flush=True)
 
 def test_device_stamps_keep_graph_replay(torch):
     """Reduce-kernel timing by device stamps (set_profiling(2)): the runs keep
-    their graph replay, report the same algorithmic bytes and reductions as
-    the event mode (the mesh fold: (P + 1) * n/P elements), and kernel
-    seconds no longer than the events' and physically possible."""
+    their graph replay AND the fused fold + forward launch that ships (events
+    need a pure fold, so they run unfused), report the same algorithmic bytes
+    and reductions as the event mode (the mesh fold: (P + 1) * n/P elements),
+    and kernel seconds physically possible."""
     P = 2
     with tempfile.TemporaryDirectory() as d:
         w = os.path.join(d, "w.py")
@@ -889,16 +890,19 @@ def test_device_stamps_keep_graph_replay(torch):
         ev = [x for x in res if x["mode"] == 1]
         st = [x for x in res if x["mode"] == 2]
         assert not any(x["graph"] for x in ev)          # events force eager runs
+        assert not any(x["fold_send"] for x in ev)      # ... and an unfused fold
         assert st[-1]["graph"] and st[-2]["graph"], res  # stamps are captured and replayed
+        assert all(x["fold_send"] for x in st), res     # the shipped fused launch is the one stamped
         for x in ev + st:
             assert x["reduce_bytes"] == (P + 1) * 4 * (n // P), x
             assert x["reductions"] == P - 1, x
         ev_s = min(x["reduce_s"] for x in ev)
         st_s = min(x["reduce_s"] for x in st)
-        # stamps span first-workgroup start to last-workgroup end, so they
-        # never exceed the events around the launch by much; the inbox may be
-        # read from the Infinity Cache, but no faster than 20 TB/s
-        assert 0 < ev_s and 0 < st_s <= 1.5 * ev_s, (ev_s, st_s)
+        # stamps span first-workgroup start to last-workgroup end; the fused
+        # launch also stores the forward (4 streams of n/P against the fold's
+        # 3), so it may take up to ~4/3 of the pure fold plus spread; the
+        # inbox may be read from the Infinity Cache, but no faster than 20 TB/s
+        assert 0 < ev_s and 0 < st_s <= 2.0 * ev_s, (ev_s, st_s)
         assert st[-1]["reduce_bytes"] / st_s < 20e12, (st_s, st[-1]["reduce_bytes"])
 
 

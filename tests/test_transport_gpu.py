@@ -42,3 +42,139 @@ def test_transport_ring_chunked_processes(tmp_path, P, count):
     outs = [p.communicate(timeout=280)[0] for p in procs]
     assert [p.returncode for p in procs] == [0] * P, outs
     assert all(o.startswith("ok") for o in outs), outs
+
+
+# ---- bound buffers between processes, through the Python binding ----------
+
+TRANSPORT_WORKER = r'''
+import ctypes, os, sys, time, json
+import numpy as np
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, store, case = int(sys.argv[1]), sys.argv[2], sys.argv[3]
+torch.cuda.set_device(0)
+ctx = gloo_amd.Context(rank, 2, store, device=0, timeout_ms=20000)
+t = gloo_amd.Transport(ctx)
+out = {}
+def hp(a):
+    return a.ctypes.data
+if case == "reuse":
+    # ADVICE r3: a receive buffer on a channel an earlier HOST buffer of a
+    # peer process used must not act on that buffer's payload record
+    if rank == 1:
+        h = np.zeros(4, np.uint32)
+        rb = t.buffer(0, 1, hp(h), h.nbytes, False)
+        rb.wait_recv()
+        out["host"] = h.tolist()
+        rb.close()
+        d = torch.zeros(4, dtype=torch.int32, device="cuda:0")
+        rb = t.buffer(0, 2, d.data_ptr(), 16, False)   # the same channel, now device memory
+        rb.wait_recv()
+        torch.cuda.synchronize()
+        out["device"] = d.cpu().tolist()
+        rb.close()
+        nb = t.buffer(0, 3, 0, 0, False)               # a notification buffer on it
+        nb.wait_recv()
+        out["notify"] = True
+        nb.close()
+    else:
+        src = np.array([11, 22, 33, 44], np.uint32)
+        sb = t.buffer(1, 1, hp(src), src.nbytes, True)
+        sb.send(0, 16)
+        sb.wait_send()
+        sb.close()
+        dsrc = torch.tensor([5, 6, 7, 8], dtype=torch.int32, device="cuda:0")
+        torch.cuda.synchronize()
+        sb = t.buffer(1, 2, dsrc.data_ptr(), 16, True)
+        sb.send(0, 16)
+        sb.wait_send()
+        sb.close()
+        dummy = np.zeros(1, np.int32)
+        nb = t.buffer(1, 3, hp(dummy), 4, True)
+        nb.send(0, 0)
+        nb.wait_send()
+        nb.close()
+elif case == "burst":
+    # ADVICE r3: sends to a host buffer of another process before the
+    # receiver waits keep every message (more than the payload ring's depth)
+    k = 7
+    if rank == 1:
+        h = np.zeros(k, np.uint32)
+        rb = t.buffer(0, 1, hp(h), h.nbytes, False)
+        time.sleep(1.0)                                 # the sender runs ahead
+        for _ in range(k):
+            rb.wait_recv()
+        out["host"] = h.tolist()
+        rb.close()
+    else:
+        src = np.arange(100, 100 + k, dtype=np.uint32)
+        sb = t.buffer(1, 1, hp(src), src.nbytes, True)
+        for i in range(k):
+            sb.send(4 * i, 4, 4 * i)
+        sb.wait_send()
+        sb.close()
+elif case == "big_alloc":
+    # VERDICT r3 #2: a receive buffer inside an allocation of 2 GiB or more
+    # is refused to a peer process before any import (which would hang)
+    if rank == 1:
+        big = torch.empty(5 << 29, dtype=torch.uint8, device="cuda:0")   # 2.5 GiB
+        rb = t.buffer(0, 1, big.data_ptr() + (1 << 20), 4096, False)
+        ctx_done = gloo_amd.Context(1, 2, store + "_done", device=0, timeout_ms=20000)
+        rb.close()
+        ctx_done.close()
+        del big
+    else:
+        src = torch.ones(1024, dtype=torch.int32, device="cuda:0")
+        sb = t.buffer(1, 1, src.data_ptr(), 4096, True)
+        try:
+            sb.send(0, 4096)
+            out["raised"] = None
+        except gloo_amd.GlooHipError as e:
+            out["raised"] = str(e)
+        ctx_done = gloo_amd.Context(0, 2, store + "_done", device=0, timeout_ms=20000)
+        sb.close()
+        ctx_done.close()
+t.close()
+ctx.close()
+print("RESULT" + json.dumps(out), flush=True)
+'''
+
+
+def run_transport_case(tmp_path, case):
+    pytest.importorskip("torch")
+    import json
+    import sys
+    w = tmp_path / "w.py"
+    w.write_text(TRANSPORT_WORKER)
+    env = dict(os.environ, GLOO_AMD_ROOT=ROOT)
+    procs = [subprocess.Popen([sys.executable, str(w), str(r), "file:" + str(tmp_path / "s"), case], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    res = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=100)
+            assert p.returncode == 0, e[-3000:]
+            res.append(json.loads(o.split("RESULT", 1)[1]))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return res
+
+
+@pytest.mark.timeout(150)
+def test_transport_channel_reuse_after_host_buffer(tmp_path):
+    res = run_transport_case(tmp_path, "reuse")
+    assert res[1] == {"host": [11, 22, 33, 44], "device": [5, 6, 7, 8], "notify": True}, res
+
+
+@pytest.mark.timeout(150)
+def test_transport_host_sends_before_wait_all_kept(tmp_path):
+    res = run_transport_case(tmp_path, "burst")
+    assert res[1]["host"] == list(range(100, 107)), res
+
+
+@pytest.mark.timeout(150)
+def test_transport_refuses_import_of_2gib_allocation(tmp_path):
+    res = run_transport_case(tmp_path, "big_alloc")
+    assert res[0]["raised"] and "2 GiB" in res[0]["raised"], res
