@@ -241,6 +241,7 @@ def _bind_collectives(L):
                                                     ctypes.c_int, ctypes.POINTER(vp)]
     L.gloo_hip_algorithm_set_streams.argtypes = [vp, ctypes.POINTER(vp), ctypes.c_int]
     L.gloo_hip_ipc_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+    L.gloo_hip_ipc_stats_ex.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]
     L.gloo_hip_algorithm_run.argtypes = [vp]
     L.gloo_hip_algorithm_destroy.argtypes = [vp]
     L.gloo_hip_algorithm_wait_seconds.argtypes = [vp]
@@ -257,7 +258,8 @@ EXPORTED = EXPORTED + ("gloo_hip_context_create", "gloo_hip_context_create_ex", 
                        "gloo_hip_algorithm_destroy", "gloo_hip_algorithm_wait_seconds",
                        "gloo_hip_algorithm_set_profiling", "gloo_hip_algorithm_stats",
                        "gloo_hip_algorithm_mode", "gloo_hip_algorithm_create_ws", "gloo_hip_context_mode",
-                       "gloo_hip_algorithm_create_streams", "gloo_hip_algorithm_set_streams", "gloo_hip_ipc_stats")
+                       "gloo_hip_algorithm_create_streams", "gloo_hip_algorithm_set_streams", "gloo_hip_ipc_stats",
+                       "gloo_hip_ipc_stats_ex", "gloo_hip_ipc_trim")
 # the xGMI transport's bound buffers (gloo_amd/include/gloo_amd/gloo_transport.h)
 EXPORTED = EXPORTED + ("gloo_hip_context_create_kv", "gloo_hip_transport_create", "gloo_hip_transport_destroy",
                        "gloo_hip_buffer_create", "gloo_hip_buffer_destroy", "gloo_hip_buffer_send",
@@ -328,12 +330,21 @@ class TransportBuffer:
 
 def ipc_stats():
     """This process's IPC slab pool (gloo_amd/include/gloo_amd/ipc.h): slabs
-    exported (never freed while the process lives) and their bytes, slabs free
-    for reuse, peer slabs mapped, hipIpcOpenMemHandle calls made."""
-    out = (ctypes.c_uint64 * 5)()
-    _check(lib.gloo_hip_ipc_stats(out))
+    exported and their bytes, slabs free for reuse, peer slabs mapped,
+    hipIpcOpenMemHandle calls made; trims, bytes they freed, mappings they
+    closed, retired addresses, allocations parked at one, and the ceiling
+    (GLOO_AMD_IPC_POOL_MAX)."""
+    out = (ctypes.c_uint64 * 11)()
+    _check(lib.gloo_hip_ipc_stats_ex(out, 11))
     return {"slabs": out[0], "slab_bytes": out[1], "free": out[2], "peer_slabs_mapped": out[3],
-            "ipc_opens": out[4]}
+            "ipc_opens": out[4], "trims": out[5], "trimmed_bytes": out[6], "mappings_closed": out[7],
+            "retired_addresses": out[8], "parked_allocations": out[9], "pool_max_bytes": out[10]}
+
+
+def ipc_trim():
+    """Frees the pooled slabs no executor holds and closes the peer mappings
+    no executor holds (local, safe while peers live; ipc.h)."""
+    _check(lib.gloo_hip_ipc_trim())
 
 
 def _mode_dict(out):

@@ -113,6 +113,10 @@ int gloo_hip_context_destroy(gloo_hip_context_t ctx) {
   return guarded([&] {
     if (ctx) ctx->cache.clear();  // executors tear down before the context
     delete ctx;
+    // slabs acquired while others were in use may have taken the pool past
+    // its ceiling: give back what no executor holds (ipc.h)
+    const gloo_amd::ipc::Stats st = gloo_amd::ipc::stats();
+    if (st.free && st.slabBytes > st.max) gloo_amd::ipc::trim();
   });
 }
 
@@ -182,15 +186,21 @@ int gloo_hip_algorithm_create(gloo_hip_context_t ctx, int algo, int op, int dtyp
 }
 
 int gloo_hip_ipc_stats(uint64_t* out) {
+  return gloo_hip_ipc_stats_ex(out, 5);
+}
+
+int gloo_hip_ipc_stats_ex(uint64_t* out, size_t n) {
   return guarded([&] {
     GLOO_AMD_ENFORCE(out, "null argument");
     const gloo_amd::ipc::Stats st = gloo_amd::ipc::stats();
-    out[0] = st.slabs;
-    out[1] = st.slabBytes;
-    out[2] = st.free;
-    out[3] = st.imports;
-    out[4] = st.opens;
+    const uint64_t v[] = {st.slabs, st.slabBytes, st.free,    st.imports, st.opens, st.trims,
+                          st.trimmedBytes, st.closes, st.retired, st.parked, st.max};
+    for (size_t i = 0; i < n && i < sizeof(v) / sizeof(v[0]); i++) out[i] = v[i];
   });
+}
+
+int gloo_hip_ipc_trim(void) {
+  return guarded([&] { gloo_amd::ipc::trim(); });
 }
 
 int gloo_hip_algorithm_run(gloo_hip_algorithm_t a) {

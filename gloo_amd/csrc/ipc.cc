@@ -9,6 +9,7 @@
 #include <memory>
 #include <mutex>
 #include <random>
+#include <set>
 #include <tuple>
 #include <vector>
 
@@ -38,20 +39,80 @@ size_t sizeClass(size_t bytes) {
 
 struct Pool {
   std::mutex m;
-  std::vector<std::unique_ptr<Slab>> slabs;  // every slab ever exported (never freed)
+  std::vector<std::unique_ptr<Slab>> slabs;  // every live exported slab (freed only by a trim)
   std::vector<Slab*> free;
+  std::set<std::pair<int, uintptr_t>> retired;  // (device, address) of every slab a trim freed
   struct Mapping {
     uint64_t incarnation;
     void* ptr;
     size_t bytes;
+    size_t users;  // executors holding it (import / unimport)
   };
   std::map<std::pair<int, uint64_t>, Mapping> imports;  // (pid, exporter address)
-  size_t opens = 0;
+  size_t opens = 0, trims = 0, trimmedBytes = 0, closes = 0, parked = 0;
   static Pool& get() {
     static Pool* p = new Pool();  // never destroyed: process exit releases device memory
     return *p;
   }
 };
+
+// GLOO_AMD_IPC_POOL_MAX: bytes of exported slabs per process (suffix K, M
+// or G); an acquire that would pass it trims first.  Default 16 GiB.
+size_t poolMax() {
+  static const size_t v = [] {
+    const char* e = std::getenv("GLOO_AMD_IPC_POOL_MAX");
+    if (!e || !*e) return size_t(16) << 30;
+    char* end = nullptr;
+    const double x = std::strtod(e, &end);
+    size_t mul = 1;
+    if (end && (*end == 'K' || *end == 'k')) mul = size_t(1) << 10;
+    if (end && (*end == 'M' || *end == 'm')) mul = size_t(1) << 20;
+    if (end && (*end == 'G' || *end == 'g')) mul = size_t(1) << 30;
+    return (size_t)(x * (double)mul);
+  }();
+  return v;
+}
+
+// Frees every free-listed slab and closes every import no executor holds;
+// p.m held.  Safe without the peers: a slab is free-listed only after its
+// executor's collective tear-down barrier (no peer writes it any more), its
+// address is retired so no later slab of this process is exported there (a
+// byte-identical handle always means the same pages, the invariant of the
+// pool), and a peer's mapping of it keeps the pages alive until that peer
+// trims in turn, never letting it see other memory.
+void trimLocked(Pool& p) {
+  for (Slab* s : p.free) {
+    for (size_t i = 0; i < p.slabs.size(); i++)
+      if (p.slabs[i].get() == s) {
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(s->device);
+        GLOO_AMD_HIP_RELEASE(hipFree(s->ptr));
+        if (prev >= 0) (void)hipSetDevice(prev);
+        p.retired.insert({s->device, reinterpret_cast<uintptr_t>(s->ptr)});
+        p.trimmedBytes += s->bytes;
+        p.slabs.erase(p.slabs.begin() + (long)i);
+        break;
+      }
+  }
+  p.free.clear();
+  for (auto it = p.imports.begin(); it != p.imports.end();) {
+    if (it->second.users == 0) {
+      GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(it->second.ptr));
+      p.closes++;
+      it = p.imports.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  p.trims++;
+}
+
+size_t slabBytesLocked(const Pool& p) {
+  size_t b = 0;
+  for (const auto& x : p.slabs) b += x->bytes;
+  return b;
+}
 
 // Bytes the runtime maps from `m` to the end of its allocation (the
 // exporter's whole slab), or 0 when it keeps no record.
@@ -94,6 +155,8 @@ Slab* acquire(int device, size_t bytes, bool fine) {
       return s;
     }
   }
+  // the pool's ceiling: free what no executor uses before growing past it
+  if (poolEnabled() && !p.free.empty() && slabBytesLocked(p) + want > poolMax()) trimLocked(p);
   auto s = std::make_unique<Slab>();
   s->bytes = want;
   s->device = device;
@@ -101,12 +164,28 @@ Slab* acquire(int device, size_t bytes, bool fine) {
   int prev = -1;
   GLOO_AMD_HIP_CHECK(hipGetDevice(&prev));
   GLOO_AMD_HIP_CHECK(hipSetDevice(device));
+  // Never export at a retired address: park such a block (allocated, not
+  // exported) and allocate again, then free the parked blocks.
+  std::vector<void*> parked;
   void* ptr = nullptr;
-  if (fine) {
-    GLOO_AMD_HIP_ALLOC(hipExtMallocWithFlags(&ptr, want, hipDeviceMallocFinegrained));
-  } else {
-    GLOO_AMD_HIP_ALLOC(hipMalloc(&ptr, want));
+  for (;;) {
+    ptr = nullptr;
+    hipError_t e = fine ? hipExtMallocWithFlags(&ptr, want, hipDeviceMallocFinegrained) : hipMalloc(&ptr, want);
+    if (e != hipSuccess) {
+      for (void* q : parked) (void)hipFree(q);
+      (void)hipSetDevice(prev);
+      GLOO_AMD_HIP_ALLOC(e);
+    }
+    if (!p.retired.count({device, reinterpret_cast<uintptr_t>(ptr)})) break;
+    parked.push_back(ptr);
+    p.parked++;
+    if (parked.size() > 64) {
+      for (void* q : parked) (void)hipFree(q);
+      (void)hipSetDevice(prev);
+      GLOO_AMD_ENFORCE(false, "IPC pool: the allocator keeps returning retired addresses");
+    }
   }
+  for (void* q : parked) GLOO_AMD_HIP_RELEASE(hipFree(q));
   s->ptr = static_cast<char*>(ptr);
   const hipError_t e = hipIpcGetMemHandle(&s->handle, ptr);
   if (e != hipSuccess) {
@@ -137,15 +216,23 @@ void release(Slab* s) {
 }
 
 void unimport(void* mapped) {
-  if (poolEnabled() || !mapped) return;  // mappings of pool slabs are kept
+  if (!mapped) return;
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
   for (auto it = p.imports.begin(); it != p.imports.end(); ++it)
     if (it->second.ptr == mapped) {
+      if (it->second.users) it->second.users--;
+      if (poolEnabled()) return;  // mappings of pool slabs are kept until a trim
       GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(mapped));
       p.imports.erase(it);
       return;
     }
+}
+
+void trim() {
+  Pool& p = Pool::get();
+  std::lock_guard<std::mutex> lk(p.m);
+  trimLocked(p);
 }
 
 void* import(int pid, uint64_t inc, uint64_t ptr, size_t bytes, const hipIpcMemHandle_t& handle) {
@@ -158,6 +245,7 @@ void* import(int pid, uint64_t inc, uint64_t ptr, size_t bytes, const hipIpcMemH
       if (it->second.bytes < bytes) it->second.bytes = std::max(it->second.bytes, mappedSpan(it->second.ptr));
       GLOO_AMD_ENFORCE(it->second.bytes >= bytes, "slab of pid ", pid, " at ", (void*)ptr, " imported at ",
                        it->second.bytes, " B, now published at ", bytes, " B");
+      it->second.users++;
       return it->second.ptr;
     }
     // a new process reusing a dead one's pid: its mapping is of no use
@@ -170,7 +258,7 @@ void* import(int pid, uint64_t inc, uint64_t ptr, size_t bytes, const hipIpcMemH
   // The mapping spans the exporter's whole slab (its size class), not just
   // the bytes this first importer asked for: a later use of the same slab
   // (a mailbox slab reused as an arena) may publish more of it.
-  p.imports[key] = {inc, m, std::max(bytes, mappedSpan(m))};
+  p.imports[key] = {inc, m, std::max(bytes, mappedSpan(m)), 1};
   return m;
 }
 
@@ -183,6 +271,12 @@ Stats stats() {
   s.free = p.free.size();
   s.imports = p.imports.size();
   s.opens = p.opens;
+  s.trims = p.trims;
+  s.trimmedBytes = p.trimmedBytes;
+  s.closes = p.closes;
+  s.retired = p.retired.size();
+  s.parked = p.parked;
+  s.max = poolMax();
   return s;
 }
 

@@ -11,11 +11,15 @@
 // process lives.  So:
 //
 //   Exporter side: every block that another process maps is a Slab from a
-//   process-wide pool.  A slab is allocated and exported ONCE and never freed
-//   while the process lives; an executor that no longer needs it returns it
-//   to the pool, and the next executor needing that size class on that device
-//   reuses it.  An address a peer has imported therefore always maps the
-//   same pages, and a byte-identical handle always means the same memory.
+//   process-wide pool.  A slab is allocated and exported ONCE; an executor
+//   that no longer needs it returns it to the pool, and the next executor
+//   needing that size class on that device reuses it.  A trim (trim(), or
+//   an acquire that would take the pool past GLOO_AMD_IPC_POOL_MAX, default
+//   16 GiB) frees the free-listed slabs and RETIRES their addresses: no later
+//   slab of this process is ever exported at a retired address (acquire
+//   parks such an allocation and allocates again).  So an address a peer
+//   has imported always maps the same pages, and a byte-identical handle
+//   always means the same memory, with or without trims.
 //   Size classes are powers of two of 2 MiB granules up to 1 GiB, then
 //   multiples of 256 MiB (a 1.5 GiB arena must not become a 2 GiB slab:
 //   importing blocks of 2 GiB or more hangs on this platform, so the
@@ -23,8 +27,10 @@
 //   at most about twice the largest set of simultaneously live arenas.
 //
 //   Importer side: a mapping is opened once per (exporter pid, exporter
-//   incarnation, exporter address) and kept — never closed while the
-//   importer lives (the exporter never frees it, so it never goes stale).
+//   incarnation, exporter address) and kept, counted by the executors that
+//   hold it; a trim closes the mappings no executor holds (a later import
+//   of the same slab opens it afresh, which is safe because the exporter
+//   never re-exports that address for other pages).
 //   The incarnation (a random word per process) tells a new process that
 //   reuses a dead one's pid apart; its old mappings are closed first.
 //
@@ -59,15 +65,19 @@ void release(Slab* s);
 
 // The mapping of a peer process's slab (opened once, kept).
 void* import(int pid, uint64_t incarnation, uint64_t ptr, size_t bytes, const hipIpcMemHandle_t& handle);
-// A no-op with the pool on.  GLOO_AMD_IPC_POOL=0 (diagnosis only) restores
-// the behaviour the pool replaced: release() frees the slab at once and
-// unimport() closes the mapping (tools/ipc_bisect.sh reproduces the stale
-// import with it).
+// Drops an executor's hold on a mapping (kept until a trim).
+// GLOO_AMD_IPC_POOL=0 (diagnosis only) restores the behaviour the pool
+// replaced: release() frees the slab at once and unimport() closes the
+// mapping (tools/ipc_bisect.sh reproduces the stale import with it).
 void unimport(void* mapped);
 bool poolEnabled();
+// Frees every free-listed slab (retiring its address) and closes every
+// mapping no executor holds.  Local: needs no peer (see above).
+void trim();
 
 struct Stats {
   size_t slabs = 0, slabBytes = 0, free = 0, imports = 0, opens = 0;
+  size_t trims = 0, trimmedBytes = 0, closes = 0, retired = 0, parked = 0, max = 0;
 };
 Stats stats();
 

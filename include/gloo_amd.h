@@ -362,10 +362,19 @@ int gloo_hip_algorithm_run(gloo_hip_algorithm_t algo);
 
 /* This process's IPC slab pool (gloo_amd/include/gloo_amd/ipc.h; no
  * reference counterpart, for tests and tools): out5[0] = slabs exported
- * (never freed while the process lives), [1] = their bytes, [2] = slabs
- * free for reuse, [3] = peer slabs mapped, [4] = hipIpcOpenMemHandle calls
- * made (each peer slab is opened once and kept). */
+ * (freed only by a trim), [1] = their bytes, [2] = slabs free for reuse,
+ * [3] = peer slabs mapped, [4] = hipIpcOpenMemHandle calls made (a peer
+ * slab is opened once and kept until a trim finds no executor holding it). */
 int gloo_hip_ipc_stats(uint64_t* out5);
+/* The same, up to 11 words: + trims, bytes trimmed, imports closed, retired
+ * addresses, allocations parked at a retired address, the pool's ceiling
+ * (GLOO_AMD_IPC_POOL_MAX, default 16 GiB; an acquire that would pass it
+ * first frees the slabs no executor holds). */
+int gloo_hip_ipc_stats_ex(uint64_t* out, size_t n);
+/* Frees every pooled slab no executor holds (retiring its address, so no
+ * later slab is exported there) and closes every peer mapping no executor
+ * holds.  Local to the process; safe while peers live. */
+int gloo_hip_ipc_trim(void);
 int gloo_hip_algorithm_destroy(gloo_hip_algorithm_t algo);
 /* Host seconds the last run() spent blocked waiting for peers. */
 double gloo_hip_algorithm_wait_seconds(gloo_hip_algorithm_t algo);
