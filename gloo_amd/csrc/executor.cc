@@ -713,6 +713,15 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   if (mesh && (algo_ == GLOO_HIP_ALGO_HALVING_DOUBLING || algo_ == GLOO_HIP_ALGO_REDUCE_SCATTER ||
                isNewStyle(algo_)))
     planAlgo_ = algo_ | GLOO_HIP_ALGO_MESH;
+  // Ring-chunked on its ring route (the mesh off, or P > 8): three inboxes
+  // per channel, so each round reduces and forwards in one pass (plan.cc
+  // planRingChunkedPipe; the reference's bytes).  GLOO_AMD_RING_PIPE=0 keeps
+  // the reference's literal two-inbox order.  A custom op keeps it too: it
+  // is called as the reference calls it, on the reference's steps.
+  if (planAlgo_ == GLOO_HIP_ALGO_RING_CHUNKED && !custom_) {
+    const char* rp = std::getenv("GLOO_AMD_RING_PIPE");
+    if (!(rp && rp[0] == '0')) planAlgo_ = GLOO_HIP_ALGO_RING_CHUNKED_PIPE;
+  }
   plan_ = planFor(planAlgo_, me, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_, maxSegmentBytes_,
                   recvElems_);
   GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));

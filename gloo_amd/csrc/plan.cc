@@ -209,6 +209,100 @@ Plan planRingChunked(int rank, int size, uint64_t count, int nptrs) {
 }
 
 // ---------------------------------------------------------------------------
+// AllreduceRingChunked's own ring route, pipelined: the reference's chunks,
+// hops, association and operand order (so its bytes), with each round's
+// reduce and the send of its result in ONE pass.
+//
+// In the reference a round is wait(left) -> reduce -> notify(left) ->
+// wait(right's credit) -> send (:141-157): the send re-reads the reduced
+// chunk after a kernel boundary, and a pass that reduced and forwarded at
+// once would have to wait for the right's credit first.  With the
+// reference's two inboxes that order deadlocks (the credit a round waits
+// for is the right's credit of the SAME round, tests/test_fold_forward_plan.py).
+// With THREE inboxes per channel it cannot: message m goes to the right's
+// inbox m % 3 and waits only for the right's credit of message m - 3, which
+// the right sends one round earlier, so no credit chain wraps around the
+// ring.  Each round is then
+//     WAIT_RECV(left) [WAIT_NOTIFY(right)] FOLD(local, inbox) SEND(right) NOTIFY(left)
+// and the executor runs FOLD + SEND + NOTIFY as one fold_send launch: every
+// tile is reduced, stored locally and into the right's inbox in the same
+// pass, and the last workgroup publishes the arrival and the credit.  The
+// allgather rounds are the same with a one-source FOLD (a copy).  Every
+// consumed message is credited (M per run), the first three sends of a run
+// wait for nothing, and the run ends waiting for the credits of its last
+// three messages (the reference's trailing notify/wait pair, :205-206), so
+// runs need no other barrier.  Messages of a run: M = 2 + (2P - 2) + (2P - 4).
+// ---------------------------------------------------------------------------
+Plan planRingChunkedPipe(int rank, int size, uint64_t count, int nptrs) {
+  Plan p;
+  if (count == 0) return p;
+  const uint64_t chunks = 2ull * size;
+  const uint64_t chunkSize = std::max<uint64_t>(256, (count + chunks - 1) / chunks);
+  const int left = (size + rank - 1) % size, right = (rank + 1) % size;
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, 0, 0, 0, count));
+  if (size == 1) {
+    if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count));
+    return p;
+  }
+  static const int kSlot[3] = {0, 1, 3};  // data slots; GLOO_HIP_SLOT_NOTIFY (2) carries the credits
+  p.arena = 3 * chunkSize;
+  for (int i = 0; i < 3; i++)
+    p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, left, kSlot[i], 0, i * chunkSize, 0, chunkSize));
+  auto span = [&](uint64_t chunkOffset, uint64_t& offset, uint64_t& length) {
+    offset = chunkOffset * chunkSize;
+    length = chunkSize;
+    if (offset + length > count) length = offset < count ? count - offset : 0;
+  };
+  uint64_t sent = 0, consumed = 0;
+  // SEND of chunk `co` (:215-236, the 1-element dummy for an empty chunk),
+  // after the right's credit of message sent - 3
+  auto send = [&](uint64_t co) {
+    uint64_t offset = (co % chunks) * chunkSize, length = chunkSize;
+    if (offset + length <= count) {
+    } else if (offset < count) {
+      length = count - offset;
+    } else {
+      offset = 0;
+      length = 1;
+    }
+    p.steps.push_back(mk(GLOO_HIP_STEP_SEND, right, kSlot[sent % 3], 0, 0, offset, length));
+    sent++;
+  };
+  auto credit = [&] {
+    if (sent >= 3) p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, right, GLOO_HIP_SLOT_NOTIFY));
+  };
+  auto chunkAt = [&](uint64_t round) {
+    return (uint64_t)((2 * (uint64_t)rank) - (round & ~1ull) + (round & 1ull) + chunks) % chunks;
+  };
+  // one round: take the next message from the left into chunk co (reduce:
+  // local op incoming, or copy), then forward the result (forward = false:
+  // the last allgather rounds send nothing)
+  auto round = [&](uint64_t co, bool reduce, bool forward) {
+    uint64_t offset, length;
+    span(co, offset, length);
+    const int in = kSlot[consumed % 3];
+    const uint64_t inOff = (consumed % 3) * chunkSize;
+    consumed++;
+    p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, left, in));
+    if (forward) credit();
+    if (length > 0) {
+      if (reduce) p.steps.push_back(mk(GLOO_HIP_STEP_FOLD_SRC, -1, 0, 0, 0, offset, length));
+      p.steps.push_back(mk(GLOO_HIP_STEP_FOLD_SRC, -1, 0, GLOO_HIP_SRC_ARENA, 0, inOff, length));
+      p.steps.push_back(mk(GLOO_HIP_STEP_FOLD, -1, 0, 0, offset, 0, length));
+    }
+    if (forward) send(co);
+    p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, left, GLOO_HIP_SLOT_NOTIFY));
+  };
+  send(2 * rank);                                           // :102-103
+  send(2 * rank + 1);
+  for (uint64_t r = 2; r < chunks; r++) round(chunkAt(r), true, true);            // :106-158
+  for (uint64_t r = 0; r < chunks - 2; r++) round(chunkAt(r), false, r < chunks - 4);  // :163-200
+  for (int i = 0; i < 3; i++) p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, right, GLOO_HIP_SLOT_NOTIFY));
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count));
+  return p;
+}
+
+// ---------------------------------------------------------------------------
 // AllreduceRingChunked's result, mesh data movement.
 //
 // In the ring (planRingChunked above) the chunk pair q = {2q, 2q+1} starts
@@ -982,6 +1076,7 @@ Plan makePlan(int algo, int rank, int size, uint64_t count, int nptrs, const std
   switch (algo) {
     case GLOO_HIP_ALGO_RING_CHUNKED: return planRingChunked(rank, size, count, nptrs);
     case GLOO_HIP_ALGO_RING_CHUNKED_MESH: return planRingChunkedMesh(rank, size, count, nptrs);
+    case GLOO_HIP_ALGO_RING_CHUNKED_PIPE: return planRingChunkedPipe(rank, size, count, nptrs);
     case GLOO_HIP_ALGO_HALVING_DOUBLING: return planHalvingDoubling(rank, size, count, nptrs);
     case GLOO_HIP_ALGO_RING: return planRing(rank, size, count, nptrs);
     case GLOO_HIP_ALGO_LOCAL: return planLocal(rank, size, count, nptrs);

@@ -183,6 +183,12 @@ typedef enum {
   GLOO_HIP_ALGO_REDUCE = 8,           /* new-style gloo::reduce(opts)
                                          (gloo/reduce.cc:21-247); the root is
                                          recv_elems[0] in gloo_hip_plan*      */
+  /* AllreduceRingChunked's own ring route (its hops, association and bytes)
+   * with three inboxes per channel, so that each round's reduce and the send
+   * of its result run as one pass (plan.cc planRingChunkedPipe).  RING_CHUNKED
+   * executes as this plan where it keeps the ring route (no mesh) unless
+   * GLOO_AMD_RING_PIPE=0. */
+  GLOO_HIP_ALGO_RING_CHUNKED_PIPE = 9,
 } gloo_hip_algo_t;
 
 /* algo | GLOO_HIP_ALGO_MESH: the algorithm's result with mesh data movement,
