@@ -39,6 +39,7 @@ for n in sizes:
     for it in range(2):
         if it:
             buf.copy_(((torch.arange(n, device="cuda:0", dtype=torch.int64) * 7 + rank) % 4096).float())
+            torch.cuda.synchronize()  # the executor runs on its own stream
         a.run()
         torch.cuda.synchronize()
         ok.append(bool((buf == want).all()))

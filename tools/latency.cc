@@ -8,6 +8,7 @@
 // Build: hipcc --offload-arch=gfx950 -O2 -std=c++17 -Iinclude -Igloo_amd/include tools/latency.cc \
 //        -o tools/latency -Lgloo_amd -lgloo_amd -Wl,-rpath,'$ORIGIN/../gloo_amd'
 // Prints one JSON line per rank with p50 / p90 of both, in microseconds.
+// LATENCY_ALGO=ring_chunked runs HipAllreduceRingChunked<float> instead.
 //
 //   latency <rank> <size> <store-url> [count=256] [iters=2000]
 #include <hip/hip_runtime.h>
@@ -16,6 +17,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -44,7 +46,14 @@ int main(int argc, char** argv) {
   (void)hipMemset(d, 0, count * sizeof(float));
   hipStream_t s;
   (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-  gloo_amd::HipAllreduceHalvingDoubling<float> algo(ctx, {d}, count, {s});
+  const char* la = std::getenv("LATENCY_ALGO");
+  const std::string algoName = la ? la : "halving_doubling";
+  std::unique_ptr<gloo_amd::Algorithm> algop;
+  if (algoName == "ring_chunked")
+    algop.reset(new gloo_amd::HipAllreduceRingChunked<float>(ctx, {d}, count, {s}));
+  else
+    algop.reset(new gloo_amd::HipAllreduceHalvingDoubling<float>(ctx, {d}, count, {s}));
+  gloo_amd::Algorithm& algo = *algop;
   for (int i = 0; i < 50; i++) {
     algo.run();
     (void)hipStreamSynchronize(s);
@@ -72,9 +81,9 @@ int main(int argc, char** argv) {
     return v[(size_t)(q * (v.size() - 1))];
   };
   const char* g = std::getenv("LATENCY_LABEL");
-  std::printf("{\"rank\": %d, \"size\": %d, \"count\": %d, \"mode\": \"%s\", \"enqueue_us_p50\": %.2f, "
+  std::printf("{\"rank\": %d, \"size\": %d, \"algo\": \"%s\", \"count\": %d, \"mode\": \"%s\", \"enqueue_us_p50\": %.2f, "
               "\"enqueue_us_p90\": %.2f, \"total_us_p50\": %.2f, \"total_us_p90\": %.2f, \"nop_launch_sync_us_p50\": %.2f}\n",
-              rank, size, count, g ? g : "auto", pct(enq, 0.5), pct(enq, 0.9), pct(tot, 0.5), pct(tot, 0.9),
+              rank, size, algoName.c_str(), count, g ? g : "auto", pct(enq, 0.5), pct(enq, 0.9), pct(tot, 0.5), pct(tot, 0.9),
               pct(nop, 0.5));
   (void)hipFree(d);
   return 0;
