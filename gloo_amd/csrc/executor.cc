@@ -61,18 +61,29 @@ struct ArenaRecord {
   uint64_t mailboxBytes;
   uint64_t slabBytes;        // size class of the arena's pool slab (ipc.h): what an import maps
   uint64_t mailboxSlabBytes; // likewise for the mailbox's slab
-  // > 0: the arena is nseg pool slabs, none of 2 GiB or more (arenaSegments);
+  // > 0: the arena is nseg pool slabs, none of 2 GiB or more (arenaSegments),
+  // described by the nseg ArenaSeg records that follow this one in the blob;
   // `ptr`, `handle`, `nonce` and `slabBytes` above are then unused
   int32_t nseg;
   int32_t pad;
-  struct Seg {
-    uint64_t start, end;  // the logical arena bytes [start, end) it holds
-    uint64_t ptr;         // the slab; logical `start` sits at ptr + (start % kSegAlign)
-    uint64_t slabBytes;
-    uint64_t nonce;       // written at the slab's first word, checked by every importer
-    hipIpcMemHandle_t handle;
-  } seg[kMaxArenaSegs];
 };
+struct ArenaSegRecord {
+  uint64_t start, end;  // the logical arena bytes [start, end) it holds
+  uint64_t ptr;         // the slab; logical `start` sits at ptr + (start % kSegAlign)
+  uint64_t slabBytes;
+  uint64_t nonce;       // written at the slab's first word, checked by every importer
+  hipIpcMemHandle_t handle;
+};
+// A peer's arena record and its slab records, checked for shape.
+void parseArena(const std::vector<char>& v, int peer, ArenaRecord* r, std::vector<ArenaSegRecord>* segs) {
+  GLOO_AMD_ENFORCE(v.size() >= sizeof(ArenaRecord), "bad arena record from rank ", peer);
+  std::memcpy(r, v.data(), sizeof(*r));
+  GLOO_AMD_ENFORCE(r->nseg >= 0 && r->nseg <= kMaxArenaSegs &&
+                       v.size() == sizeof(ArenaRecord) + (size_t)r->nseg * sizeof(ArenaSegRecord),
+                   "bad arena record from rank ", peer);
+  segs->resize((size_t)r->nseg);
+  if (r->nseg) std::memcpy(segs->data(), v.data() + sizeof(ArenaRecord), segs->size() * sizeof(ArenaSegRecord));
+}
 
 // A value no earlier arena of this process or its peers is likely to hold.
 uint64_t arenaNonce() {
@@ -956,11 +967,13 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   rec.ptr = reinterpret_cast<uint64_t>(arena_);
   rec.bytes = arenaBytes;
   rec.deviceSignal = deviceSignal_ ? 1 : 0;
+  std::vector<ArenaSegRecord> segRecs(arenaSegs_.size());
   if (!arenaSegs_.empty()) {
     rec.nseg = (int32_t)arenaSegs_.size();
     for (size_t k = 0; k < arenaSegs_.size(); k++) {
       const ArenaSeg& a = arenaSegs_[k];
-      ArenaRecord::Seg& g = rec.seg[k];
+      ArenaSegRecord& g = segRecs[k];
+      std::memset(&g, 0, sizeof(g));
       g.start = a.start;
       g.end = a.end;
       g.ptr = reinterpret_cast<uint64_t>(a.slab->ptr);
@@ -1007,8 +1020,9 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   } else if (arenaSlab_) {
     rec.handle = arenaSlab_->handle;  // exported once, when the pool allocated the slab
   }
-  std::vector<char> blob(sizeof(rec));
+  std::vector<char> blob(sizeof(rec) + segRecs.size() * sizeof(ArenaSegRecord));
   std::memcpy(blob.data(), &rec, sizeof(rec));
+  if (!segRecs.empty()) std::memcpy(blob.data() + sizeof(rec), segRecs.data(), segRecs.size() * sizeof(ArenaSegRecord));
   GLOO_AMD_TRACE_PHASE("exchanging arena records");
   const std::vector<std::vector<char>> arenas = ctx_->allgather(strcat_("inst", inst_, "/arena"), blob);
   GLOO_AMD_TRACE_PHASE("arena records exchanged");
@@ -1028,10 +1042,9 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   peerMailbox_.assign(P, nullptr);
   peerMailboxIpc_.assign(P, false);
   for (int peer : planPeers) {
-    const std::vector<char>& v = arenas.at(peer);
-    GLOO_AMD_ENFORCE(v.size() == sizeof(ArenaRecord), "bad arena record from rank ", peer);
     ArenaRecord pr;
-    std::memcpy(&pr, v.data(), sizeof(pr));
+    std::vector<ArenaSegRecord> prSegs;
+    parseArena(arenas.at(peer), peer, &pr, &prSegs);
     if (mailbox_ && pr.deviceSignal && pr.hasMailbox) {
       if (pr.pid == ctx_->pid()) {
         peerMailbox_[peer] = reinterpret_cast<uint64_t*>(pr.mailboxPtr);
@@ -1055,12 +1068,11 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       }
     }
     if (!sendPeers.count(peer)) continue;
-    GLOO_AMD_ENFORCE(pr.nseg >= 0 && pr.nseg <= kMaxArenaSegs, "bad arena record from rank ", peer);
     if (pr.nseg > 0) {
       // a segmented arena: every slab mapped (or, in this process, used) on
       // its own and checked by its nonce
       for (int k = 0; k < pr.nseg; k++) {
-        const ArenaRecord::Seg& g = pr.seg[k];
+        const ArenaSegRecord& g = prSegs[(size_t)k];
         char* base = reinterpret_cast<char*>(g.ptr);
         const size_t need = g.end - g.start + g.start % kSegAlign;
         if (pr.pid != ctx_->pid()) {
@@ -1146,10 +1158,9 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   int32_t agreed = proposal;
   for (int r = 0; r < P && agreed > 1; r++) {
     if (r == me) continue;
-    const std::vector<char>& v = arenas.at(r);
-    GLOO_AMD_ENFORCE(v.size() == sizeof(ArenaRecord), "bad arena record from rank ", r);
     ArenaRecord pr;
-    std::memcpy(&pr, v.data(), sizeof(pr));
+    std::vector<ArenaSegRecord> prSegs;
+    parseArena(arenas.at(r), r, &pr, &prSegs);
     agreed = std::min(agreed, pr.interpSlices);
   }
   slices_ = agreed > 1 ? agreed : 1;

@@ -36,7 +36,7 @@ class Store {
 class CallbackStore : public Store {
  public:
   using Fn = int (*)(void* user, const void* in, void* out, size_t block);
-  static constexpr size_t kBlock = 1024;
+  static constexpr size_t kBlock = 4096;  // a segmented arena record is up to ~2 KiB (executor.cc)
   CallbackStore(Fn fn, void* user) : fn_(fn), user_(user) {}
   void set(const std::string& key, const std::vector<char>& data) override;
   std::vector<char> get(const std::string& key, std::chrono::milliseconds timeout) override;

@@ -58,19 +58,20 @@ def test_ipc_pool_bounded_with_trims():
     with tempfile.TemporaryDirectory() as d:
         w = os.path.join(d, "w.py")
         open(w, "w").write(WORKER)
-        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_IPC_POOL_MAX=str(cap))
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_IPC_POOL_MAX=str(cap), GLOO_AMD_TRACE="1")
         procs = [subprocess.Popen([sys.executable, w, str(r), "file:" + os.path.join(d, "s")], env=e,
                                   stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
-        res = []
+        outs = []
         try:
             for p in procs:
-                o, err = p.communicate(timeout=280)
-                assert p.returncode == 0, err[-3000:]
-                res.append(json.loads(o.split("RESULT", 1)[1]))
+                outs.append(p.communicate(timeout=280))
         finally:
             for p in procs:
                 if p.poll() is None:
                     p.kill()
+        assert [p.returncode for p in procs] == [0, 0], "\n".join(f"rank {r}: {e[-2500:]}"
+                                                              for r, (o, e) in enumerate(outs))
+        res = [json.loads(o.split("RESULT", 1)[1]) for o, e in outs]
     for r in res:
         for s in r["steps"]:
             assert s["ok"] == [True, True], s
