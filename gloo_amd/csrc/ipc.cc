@@ -81,6 +81,17 @@ size_t poolMax() {
 // pool), and a peer's mapping of it keeps the pages alive until that peer
 // trims in turn, never letting it see other memory.
 void trimLocked(Pool& p) {
+  // this process's unused mappings of peer slabs first (a peer freeing its
+  // slab never waits for them, but they hold its pages)
+  for (auto it = p.imports.begin(); it != p.imports.end();) {
+    if (it->second.users == 0) {
+      GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(it->second.ptr));
+      p.closes++;
+      it = p.imports.erase(it);
+    } else {
+      ++it;
+    }
+  }
   for (Slab* s : p.free) {
     for (size_t i = 0; i < p.slabs.size(); i++)
       if (p.slabs[i].get() == s) {
@@ -96,15 +107,6 @@ void trimLocked(Pool& p) {
       }
   }
   p.free.clear();
-  for (auto it = p.imports.begin(); it != p.imports.end();) {
-    if (it->second.users == 0) {
-      GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(it->second.ptr));
-      p.closes++;
-      it = p.imports.erase(it);
-    } else {
-      ++it;
-    }
-  }
   p.trims++;
 }
 

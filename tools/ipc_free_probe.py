@@ -20,8 +20,16 @@ import time
 HIP = "libamdhip64.so.7"
 
 
+class Handle(ctypes.Structure):
+    _fields_ = [("reserved", ctypes.c_char * 64)]
+
+
 def rt():
     L = ctypes.CDLL(HIP)
+    L.hipIpcGetMemHandle.argtypes = [ctypes.POINTER(Handle), ctypes.c_void_p]
+    L.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(ctypes.c_void_p), Handle, ctypes.c_uint]
+    L.hipIpcCloseMemHandle.argtypes = [ctypes.c_void_p]
+    L.hipFree.argtypes = [ctypes.c_void_p]
     return L
 
 
@@ -39,9 +47,11 @@ def exporter(d):
     L.hipSetDevice(0)
     p = ctypes.c_void_p()
     assert L.hipMalloc(ctypes.byref(p), ctypes.c_size_t(64 << 20)) == 0
-    h = (ctypes.c_char * 64)()
-    assert L.hipIpcGetMemHandle(h, p) == 0
-    open(os.path.join(d, "handle.tmp"), "wb").write(bytes(h))
+    L.hipMemset(p, 0xAA, ctypes.c_size_t(64 << 20))
+    L.hipDeviceSynchronize()
+    h = Handle()
+    assert L.hipIpcGetMemHandle(ctypes.byref(h), p) == 0
+    open(os.path.join(d, "handle.tmp"), "wb").write(bytes(h.reserved))
     os.rename(os.path.join(d, "handle.tmp"), os.path.join(d, "handle"))
     assert wait_file(os.path.join(d, "imported"), 60)
     stop = [False]
@@ -59,11 +69,15 @@ def exporter(d):
     t_free = time.time() - t0
     q = ctypes.c_void_p()
     assert L.hipMalloc(ctypes.byref(q), ctypes.c_size_t(64 << 20)) == 0
-    h2 = (ctypes.c_char * 64)()
-    L.hipIpcGetMemHandle(h2, q)
+    L.hipMemset(q, 0x55, ctypes.c_size_t(64 << 20))
+    L.hipDeviceSynchronize()
+    h2 = Handle()
+    L.hipIpcGetMemHandle(ctypes.byref(h2), q)
+    open(os.path.join(d, "handle2.tmp"), "wb").write(bytes(h2.reserved))
+    os.rename(os.path.join(d, "handle2.tmp"), os.path.join(d, "handle2"))
     print(json.dumps({"exporter": "freed", "hipFree_rc": rc, "hipFree_s": round(t_free, 4),
                       "old": hex(p.value), "new": hex(q.value), "same_address": p.value == q.value,
-                      "same_handle": bytes(h) == bytes(h2)}), flush=True)
+                      "same_handle": bytes(h.reserved) == bytes(h2.reserved)}), flush=True)
     open(os.path.join(d, "freed"), "w").write("1")
     wait_file(os.path.join(d, "closed"), 60)
     L.hipFree(q)
@@ -73,11 +87,25 @@ def importer(d):
     L = rt()
     L.hipSetDevice(0)
     assert wait_file(os.path.join(d, "handle"), 60)
-    h = (ctypes.c_char * 64).from_buffer_copy(open(os.path.join(d, "handle"), "rb").read())
+    h = Handle.from_buffer_copy(open(os.path.join(d, "handle"), "rb").read())
     m = ctypes.c_void_p()
-    rc = L.hipIpcOpenMemHandle(ctypes.byref(m), h, ctypes.c_uint(1))
+    rc = L.hipIpcOpenMemHandle(ctypes.byref(m), h, 1)
     open(os.path.join(d, "imported"), "w").write("1")
-    ok = wait_file(os.path.join(d, "freed"), 30)
+    ok = wait_file(os.path.join(d, "freed"), 12)
+    # while the first mapping is still open: the exporter's new block at the
+    # same address, through its own (different?) handle
+    seen = ctypes.c_uint64(0)
+    rc3 = rc4 = None
+    if ok and wait_file(os.path.join(d, "handle2"), 5):
+        h2 = Handle.from_buffer_copy(open(os.path.join(d, "handle2"), "rb").read())
+        m2 = ctypes.c_void_p()
+        rc3 = L.hipIpcOpenMemHandle(ctypes.byref(m2), h2, 1)
+        if rc3 == 0:
+            L.hipMemcpy(ctypes.byref(seen), m2, ctypes.c_size_t(8), 2)
+            rc4 = L.hipIpcCloseMemHandle(m2)
+        print(json.dumps({"importer": "second import", "open_rc": rc3, "first_word": hex(seen.value),
+                          "same_mapping_as_first": m2.value == m.value if rc3 == 0 else None,
+                          "close_rc": rc4}), flush=True)
     t0 = time.time()
     rc2 = L.hipIpcCloseMemHandle(m)
     print(json.dumps({"importer": "closed", "open_rc": rc, "close_rc": rc2, "close_s": round(time.time() - t0, 4),
