@@ -341,10 +341,12 @@ def ipc_stats():
             "retired_addresses": out[8], "parked_allocations": out[9], "pool_max_bytes": out[10]}
 
 
-def ipc_trim():
-    """Frees the pooled slabs no executor holds and closes the peer mappings
-    no executor holds (local, safe while peers live; ipc.h)."""
-    _check(lib.gloo_hip_ipc_trim())
+def ipc_trim(ctx=None):
+    """Collective over ctx's ranks: close the peer mappings no executor
+    holds, barrier, free the pooled slabs no executor holds (ipc.h).
+    ctx=None: this process alone (its peers are gone)."""
+    lib.gloo_hip_ipc_trim.argtypes = [ctypes.c_void_p]
+    _check(lib.gloo_hip_ipc_trim(ctx._h if ctx is not None else None))
 
 
 def _mode_dict(out):

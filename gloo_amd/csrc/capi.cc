@@ -113,10 +113,10 @@ int gloo_hip_context_destroy(gloo_hip_context_t ctx) {
   return guarded([&] {
     if (ctx) ctx->cache.clear();  // executors tear down before the context
     delete ctx;
-    // slabs acquired while others were in use may have taken the pool past
-    // its ceiling: give back what no executor holds (ipc.h)
-    const gloo_amd::ipc::Stats st = gloo_amd::ipc::stats();
-    if (st.free && st.slabBytes > st.max) gloo_amd::ipc::trim();
+    // over the IPC pool's ceiling: drop this process's unused mappings of
+    // peer slabs (local and safe; the slabs themselves are freed by the next
+    // collective trim, ipc.h)
+    if (gloo_amd::ipc::overCeiling(0)) gloo_amd::ipc::closeUnusedImports();
   });
 }
 
@@ -199,8 +199,16 @@ int gloo_hip_ipc_stats_ex(uint64_t* out, size_t n) {
   });
 }
 
-int gloo_hip_ipc_trim(void) {
-  return guarded([&] { gloo_amd::ipc::trim(); });
+int gloo_hip_ipc_trim(gloo_hip_context_t ctx) {
+  return guarded([&] {
+    if (!ctx || ctx->ctx->size == 1) {
+      gloo_amd::ipc::trim();  // no peers to wait for
+      return;
+    }
+    gloo_amd::ipc::closeUnusedImports();
+    ctx->ctx->barrier("ipc-trim");
+    gloo_amd::ipc::freeUnusedSlabs();
+  });
 }
 
 int gloo_hip_algorithm_run(gloo_hip_algorithm_t a) {

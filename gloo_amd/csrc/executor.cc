@@ -796,30 +796,50 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     if (s.kind == GLOO_HIP_STEP_SEND) sendPeers.insert(s.peer);
     if (s.kind == GLOO_HIP_STEP_DECL_RECV) recvPeers.insert(s.peer);
   }
+  constexpr size_t kArenaGranule = 2u << 20;
+  auto arenaBytesOf = [&](const Plan& p) {
+    return (std::max<size_t>(256, p.arena * es_) + kArenaGranule - 1) / kArenaGranule * kArenaGranule;
+  };
+  // (pid, device, whether this rank's IPC pool would pass its ceiling with
+  // this executor's slabs)
   std::vector<std::vector<char>> where;
   {
-    int32_t hello[2] = {ctx_->pid(), ctx_->device()};
+    int32_t hello[3] = {ctx_->pid(), ctx_->device(), ipc::overCeiling(arenaBytesOf(plan_) + (2u << 20)) ? 1 : 0};
     std::vector<char> blob(sizeof(hello));
     std::memcpy(blob.data(), hello, sizeof(hello));
     where = ctx_->allgather(strcat_("inst", inst_, "/where"), blob);
   }
   GLOO_AMD_TRACE_PHASE("where exchanged");
+  // The IPC pool's ceiling (ipc.h): when any rank would pass it, every rank
+  // closes the mappings no executor holds, and once all have (a peer's
+  // slab freed while still mapped breaks the next export over its memory)
+  // frees its unused slabs, before any slab of this executor is acquired.
+  {
+    bool trim = false;
+    for (int r = 0; r < P; r++) {
+      int32_t w[3];
+      GLOO_AMD_ENFORCE(where.at(r).size() == sizeof(w), "bad record from rank ", r);
+      std::memcpy(w, where[r].data(), sizeof(w));
+      trim = trim || w[2] != 0;
+    }
+    if (trim) {
+      GLOO_AMD_TRACE_PHASE("trimming the IPC pool");
+      ipc::closeUnusedImports();
+      ctx_->barrier(strcat_("inst", inst_, "/ipc-trim"));
+      ipc::freeUnusedSlabs();
+    }
+  }
   // Inbox arenas other processes map: no imported block may reach 2 GiB
   // (importing one hangs in hipIpcOpenMemHandle on ROCm 7 / MI355X,
   // profiles/round3/r3t_*, r3u_*), so an arena above kSegMax becomes several
   // slabs (arenaSegments).  Every rank checks every rank's plan (the same
   // data everywhere), so a layout that cannot be split is refused by all
   // ranks together rather than some waiting at the next exchange.
-  constexpr size_t kArenaGranule = 2u << 20;
-  auto arenaBytesOf = [&](const Plan& p) {
-    return (std::max<size_t>(256, p.arena * es_) + kArenaGranule - 1) / kArenaGranule * kArenaGranule;
-  };
   {
     bool anyCross = false;
     for (int r = 0; r < P; r++) {
-      int32_t w[2];
-      GLOO_AMD_ENFORCE(where.at(r).size() == sizeof(w), "bad record from rank ", r);
-      std::memcpy(w, where[r].data(), sizeof(w));
+      int32_t w[3];
+      std::memcpy(w, where.at(r).data(), sizeof(w));
       if (w[0] != ctx_->pid()) anyCross = true;
     }
     const char* hm = std::getenv("GLOO_AMD_ARENA");
@@ -836,8 +856,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   bool sharesDeviceInProcess = false, crossSender = false;
   for (int peer : planPeers) {
     const std::vector<char>& v = where.at(peer);
-    GLOO_AMD_ENFORCE(v.size() == 2 * sizeof(int32_t), "bad record from rank ", peer);
-    int32_t w[2];
+    int32_t w[3];
     std::memcpy(w, v.data(), sizeof(w));
     peers_[peer].pid = w[0];
     peers_[peer].device = w[1];

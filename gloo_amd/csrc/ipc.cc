@@ -73,16 +73,8 @@ size_t poolMax() {
   return v;
 }
 
-// Frees every free-listed slab and closes every import no executor holds;
-// p.m held.  Safe without the peers: a slab is free-listed only after its
-// executor's collective tear-down barrier (no peer writes it any more), its
-// address is retired so no later slab of this process is exported there (a
-// byte-identical handle always means the same pages, the invariant of the
-// pool), and a peer's mapping of it keeps the pages alive until that peer
-// trims in turn, never letting it see other memory.
-void trimLocked(Pool& p) {
-  // this process's unused mappings of peer slabs first (a peer freeing its
-  // slab never waits for them, but they hold its pages)
+// Closes every mapping of a peer slab that no executor holds; p.m held.
+void closeUnusedLocked(Pool& p) {
   for (auto it = p.imports.begin(); it != p.imports.end();) {
     if (it->second.users == 0) {
       GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(it->second.ptr));
@@ -92,6 +84,17 @@ void trimLocked(Pool& p) {
       ++it;
     }
   }
+}
+
+// Frees every free-listed slab and retires its address; p.m held.  A slab is
+// free-listed only after its executor's collective tear-down barrier (no
+// peer writes it any more); the address is retired so that no later slab of
+// this process is exported there, and a byte-identical handle keeps meaning
+// the same pages.  Freeing a slab a peer still maps is not safe on ROCm 7:
+// the next export of memory allocated over it can fail ("invalid argument",
+// profiles/round4/r4d_*), so callers free only after every peer has closed
+// its unused mappings (trimCollective, executor.cc).
+void freeUnusedLocked(Pool& p) {
   for (Slab* s : p.free) {
     for (size_t i = 0; i < p.slabs.size(); i++)
       if (p.slabs[i].get() == s) {
@@ -157,8 +160,6 @@ Slab* acquire(int device, size_t bytes, bool fine) {
       return s;
     }
   }
-  // the pool's ceiling: free what no executor uses before growing past it
-  if (poolEnabled() && !p.free.empty() && slabBytesLocked(p) + want > poolMax()) trimLocked(p);
   auto s = std::make_unique<Slab>();
   s->bytes = want;
   s->device = device;
@@ -191,6 +192,7 @@ Slab* acquire(int device, size_t bytes, bool fine) {
   s->ptr = static_cast<char*>(ptr);
   const hipError_t e = hipIpcGetMemHandle(&s->handle, ptr);
   if (e != hipSuccess) {
+    (void)hipGetLastError();
     (void)hipFree(ptr);  // never exported: safe to free
     (void)hipSetDevice(prev);
     GLOO_AMD_HIP_ALLOC(e);
@@ -231,10 +233,22 @@ void unimport(void* mapped) {
     }
 }
 
-void trim() {
+void closeUnusedImports() {
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
-  trimLocked(p);
+  closeUnusedLocked(p);
+}
+
+void freeUnusedSlabs() {
+  Pool& p = Pool::get();
+  std::lock_guard<std::mutex> lk(p.m);
+  freeUnusedLocked(p);
+}
+
+bool overCeiling(size_t more) {
+  Pool& p = Pool::get();
+  std::lock_guard<std::mutex> lk(p.m);
+  return poolEnabled() && !p.free.empty() && slabBytesLocked(p) + more > poolMax();
 }
 
 void* import(int pid, uint64_t inc, uint64_t ptr, size_t bytes, const hipIpcMemHandle_t& handle) {

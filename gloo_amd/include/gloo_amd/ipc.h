@@ -13,13 +13,18 @@
 //   Exporter side: every block that another process maps is a Slab from a
 //   process-wide pool.  A slab is allocated and exported ONCE; an executor
 //   that no longer needs it returns it to the pool, and the next executor
-//   needing that size class on that device reuses it.  A trim (trim(), or
-//   an acquire that would take the pool past GLOO_AMD_IPC_POOL_MAX, default
-//   16 GiB) frees the free-listed slabs and RETIRES their addresses: no later
-//   slab of this process is ever exported at a retired address (acquire
-//   parks such an allocation and allocates again).  So an address a peer
-//   has imported always maps the same pages, and a byte-identical handle
-//   always means the same memory, with or without trims.
+//   needing that size class on that device reuses it.  A trim frees the
+//   free-listed slabs and RETIRES their addresses: no later slab of this
+//   process is ever exported at a retired address (acquire parks such an
+//   allocation and allocates again).  So an address a peer has imported
+//   always maps the same pages, and a byte-identical handle always means
+//   the same memory, with or without trims.  Trims are collective
+//   (trimCollective in context.h): every rank first closes the mappings no
+//   executor holds, then, after a barrier, frees its unused slabs — ROCm 7
+//   fails the next export of memory allocated over a slab freed while a peer
+//   still mapped it.  They run when a rank's pool would pass
+//   GLOO_AMD_IPC_POOL_MAX (default 16 GiB): at an executor's construction
+//   (before its slabs are acquired) and at a context's destruction.
 //   Size classes are powers of two of 2 MiB granules up to 1 GiB, then
 //   multiples of 256 MiB (a 1.5 GiB arena must not become a 2 GiB slab:
 //   importing blocks of 2 GiB or more hangs on this platform, so the
@@ -71,9 +76,18 @@ void* import(int pid, uint64_t incarnation, uint64_t ptr, size_t bytes, const hi
 // mapping (tools/ipc_bisect.sh reproduces the stale import with it).
 void unimport(void* mapped);
 bool poolEnabled();
-// Frees every free-listed slab (retiring its address) and closes every
-// mapping no executor holds.  Local: needs no peer (see above).
-void trim();
+// The two halves of a trim (above): close this process's mappings no
+// executor holds; free (and retire) its free-listed slabs.
+void closeUnusedImports();
+void freeUnusedSlabs();
+// Whether the pool holds free slabs and would pass its ceiling with `more`
+// bytes of new slabs.
+bool overCeiling(size_t more);
+// Both halves at once, for a process whose peers are gone (gloo_hip_ipc_trim).
+inline void trim() {
+  closeUnusedImports();
+  freeUnusedSlabs();
+}
 
 struct Stats {
   size_t slabs = 0, slabBytes = 0, free = 0, imports = 0, opens = 0;

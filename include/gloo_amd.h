@@ -377,10 +377,13 @@ int gloo_hip_ipc_stats(uint64_t* out5);
  * (GLOO_AMD_IPC_POOL_MAX, default 16 GiB; an acquire that would pass it
  * first frees the slabs no executor holds). */
 int gloo_hip_ipc_stats_ex(uint64_t* out, size_t n);
-/* Frees every pooled slab no executor holds (retiring its address, so no
- * later slab is exported there) and closes every peer mapping no executor
- * holds.  Local to the process; safe while peers live. */
-int gloo_hip_ipc_trim(void);
+/* Collective over ctx (every rank calls it, in the same order as its other
+ * collective calls): each rank closes the peer mappings no executor holds,
+ * then, after a barrier, frees the pooled slabs no executor holds (retiring
+ * their addresses, so no later slab is exported there).  ctx = NULL: this
+ * process alone, for when its peers are gone.  Executor construction runs
+ * the same trim by itself when a rank's pool would pass its ceiling. */
+int gloo_hip_ipc_trim(gloo_hip_context_t ctx);
 int gloo_hip_algorithm_destroy(gloo_hip_algorithm_t algo);
 /* Host seconds the last run() spent blocked waiting for peers. */
 double gloo_hip_algorithm_wait_seconds(gloo_hip_algorithm_t algo);

@@ -4,9 +4,11 @@ Two rank processes build halving-doubling executors (mesh route: their inbox
 arenas are exported slabs) of ten size classes in sequence, then walk back
 down through classes that a trim freed.  With GLOO_AMD_IPC_POOL_MAX = 256 MiB
 the pool never holds more than the ceiling beyond the slabs of the live
-executor, trims happen, their addresses are retired (never exported again
-for other pages), and every run is exact: the closed form of rank r
-contributing (7 i + r) mod 4096 at element i."""
+executor (an executor's construction trims collectively first), trims
+happen, their addresses are retired (never exported again for other pages),
+every run is exact (the closed form of rank r contributing (7 i + r) mod
+4096 at element i), and an explicit collective gloo_hip_ipc_trim leaves no
+slab and no mapping."""
 import json
 import os
 import subprocess
@@ -46,8 +48,11 @@ for n in sizes:
     a.close()
     out.append({"n": n, "ok": ok, "stats": st})
     del buf, want
+final = gloo_amd.ipc_stats()
+gloo_amd.ipc_trim(ctx)   # collective: every unused slab and mapping goes
+trimmed = gloo_amd.ipc_stats()
 ctx.close()
-print("RESULT" + json.dumps({"steps": out, "final": gloo_amd.ipc_stats()}), flush=True)
+print("RESULT" + json.dumps({"steps": out, "final": final, "trimmed": trimmed}), flush=True)
 '''
 
 
@@ -80,4 +85,7 @@ def test_ipc_pool_bounded_with_trims():
             assert s["stats"]["pool_max_bytes"] == cap
         f = r["final"]
         assert f["trims"] >= 1 and f["retired_addresses"] >= 1, f
-        assert f["slab_bytes"] <= cap, f
+        assert f["slab_bytes"] <= cap + 4 * r["steps"][-1]["n"] + (8 << 20), f
+        t = r["trimmed"]
+        assert t["slabs"] == 0 and t["slab_bytes"] == 0 and t["free"] == 0, t
+        assert t["peer_slabs_mapped"] == 0, t

@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
-"""Probe (measurement tool, not product): does hipFree of an IPC-exported
-block block while a peer process still has it mapped?  And may the exporter
-free a block, allocate again, and hand out a NEW handle at that address?
+"""Probe (measurement tool, not product): what the HIP runtime does when an
+IPC-exported block is freed while a peer process still maps it.
 
-  exporter: hipMalloc 64 MiB, export, wait for the importer's mapping,
-            hipFree (timed, watchdog prints every 2 s), allocate again and
-            report the new address, then tell the importer.
-  importer: map, signal, wait for "freed" (at most 30 s), close, report.
+  exporter: A = hipMalloc 1 GiB, export, wait for the importer's mapping;
+            hipFree(A) (timed); B = hipMalloc 512 MiB, export (rc?), report
+            addresses; tell the importer; wait for its close;
+            C = hipMalloc 512 MiB, export (rc?).
+  importer: map A, signal; wait for "freed"; read A's first word through the
+            old mapping; close (timed); signal.
 usage: ipc_free_probe.py  (spawns both; JSON lines on stdout)"""
 import ctypes
 import json
@@ -14,7 +15,6 @@ import os
 import subprocess
 import sys
 import tempfile
-import threading
 import time
 
 HIP = "libamdhip64.so.7"
@@ -30,11 +30,21 @@ def rt():
     L.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(ctypes.c_void_p), Handle, ctypes.c_uint]
     L.hipIpcCloseMemHandle.argtypes = [ctypes.c_void_p]
     L.hipFree.argtypes = [ctypes.c_void_p]
+    L.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    L.hipMemset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
+    L.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
     return L
 
 
-def wait_file(path, limit):
+def put(d, name, data=b"1"):
+    with open(os.path.join(d, name + ".tmp"), "wb") as f:
+        f.write(data)
+    os.rename(os.path.join(d, name + ".tmp"), os.path.join(d, name))
+
+
+def wait_file(d, name, limit):
     t0 = time.time()
+    path = os.path.join(d, name)
     while not os.path.exists(path):
         if time.time() - t0 > limit:
             return False
@@ -42,75 +52,60 @@ def wait_file(path, limit):
     return True
 
 
+def alloc_export(L, nbytes, fill):
+    p = ctypes.c_void_p()
+    rc = L.hipMalloc(ctypes.byref(p), nbytes)
+    if rc:
+        return None, None, rc
+    L.hipMemset(p, fill, nbytes)
+    L.hipDeviceSynchronize()
+    h = Handle()
+    return p, h, L.hipIpcGetMemHandle(ctypes.byref(h), p)
+
+
 def exporter(d):
     L = rt()
     L.hipSetDevice(0)
-    p = ctypes.c_void_p()
-    assert L.hipMalloc(ctypes.byref(p), ctypes.c_size_t(64 << 20)) == 0
-    L.hipMemset(p, 0xAA, ctypes.c_size_t(64 << 20))
-    L.hipDeviceSynchronize()
-    h = Handle()
-    assert L.hipIpcGetMemHandle(ctypes.byref(h), p) == 0
-    open(os.path.join(d, "handle.tmp"), "wb").write(bytes(h.reserved))
-    os.rename(os.path.join(d, "handle.tmp"), os.path.join(d, "handle"))
-    assert wait_file(os.path.join(d, "imported"), 60)
-    stop = [False]
-
-    def dog():
-        t0 = time.time()
-        while not stop[0]:
-            time.sleep(2)
-            if not stop[0]:
-                print(json.dumps({"exporter": "hipFree still blocked", "s": round(time.time() - t0, 1)}), flush=True)
-    threading.Thread(target=dog, daemon=True).start()
+    a, ha, rc = alloc_export(L, 1 << 30, 0xAA)
+    assert rc == 0, rc
+    put(d, "handle", bytes(ha.reserved))
+    assert wait_file(d, "imported", 60)
     t0 = time.time()
-    rc = L.hipFree(p)
-    stop[0] = True
+    rc_free = L.hipFree(a)
     t_free = time.time() - t0
-    q = ctypes.c_void_p()
-    assert L.hipMalloc(ctypes.byref(q), ctypes.c_size_t(64 << 20)) == 0
-    L.hipMemset(q, 0x55, ctypes.c_size_t(64 << 20))
-    L.hipDeviceSynchronize()
-    h2 = Handle()
-    L.hipIpcGetMemHandle(ctypes.byref(h2), q)
-    open(os.path.join(d, "handle2.tmp"), "wb").write(bytes(h2.reserved))
-    os.rename(os.path.join(d, "handle2.tmp"), os.path.join(d, "handle2"))
-    print(json.dumps({"exporter": "freed", "hipFree_rc": rc, "hipFree_s": round(t_free, 4),
-                      "old": hex(p.value), "new": hex(q.value), "same_address": p.value == q.value,
-                      "same_handle": bytes(h.reserved) == bytes(h2.reserved)}), flush=True)
-    open(os.path.join(d, "freed"), "w").write("1")
-    wait_file(os.path.join(d, "closed"), 60)
-    L.hipFree(q)
+    b, hb, rc_b = alloc_export(L, 512 << 20, 0x55)
+    print(json.dumps({"exporter": "freed A while mapped, exported B", "hipFree_rc": rc_free,
+                      "hipFree_s": round(t_free, 4), "A": hex(a.value), "B": hex(b.value) if b else None,
+                      "B_inside_A": bool(b and a.value <= b.value < a.value + (1 << 30)),
+                      "export_B_rc": rc_b}), flush=True)
+    put(d, "freed")
+    assert wait_file(d, "closed", 60)
+    c, hc, rc_c = alloc_export(L, 512 << 20, 0x33)
+    print(json.dumps({"exporter": "after the importer closed A, exported C", "C": hex(c.value) if c else None,
+                      "C_inside_A": bool(c and a.value <= c.value < a.value + (1 << 30)),
+                      "export_C_rc": rc_c}), flush=True)
+    for x in (b, c):
+        if x:
+            L.hipFree(x)
 
 
 def importer(d):
     L = rt()
     L.hipSetDevice(0)
-    assert wait_file(os.path.join(d, "handle"), 60)
+    assert wait_file(d, "handle", 60)
     h = Handle.from_buffer_copy(open(os.path.join(d, "handle"), "rb").read())
     m = ctypes.c_void_p()
     rc = L.hipIpcOpenMemHandle(ctypes.byref(m), h, 1)
-    open(os.path.join(d, "imported"), "w").write("1")
-    ok = wait_file(os.path.join(d, "freed"), 12)
-    # while the first mapping is still open: the exporter's new block at the
-    # same address, through its own (different?) handle
+    put(d, "imported")
+    ok = wait_file(d, "freed", 30)
     seen = ctypes.c_uint64(0)
-    rc3 = rc4 = None
-    if ok and wait_file(os.path.join(d, "handle2"), 5):
-        h2 = Handle.from_buffer_copy(open(os.path.join(d, "handle2"), "rb").read())
-        m2 = ctypes.c_void_p()
-        rc3 = L.hipIpcOpenMemHandle(ctypes.byref(m2), h2, 1)
-        if rc3 == 0:
-            L.hipMemcpy(ctypes.byref(seen), m2, ctypes.c_size_t(8), 2)
-            rc4 = L.hipIpcCloseMemHandle(m2)
-        print(json.dumps({"importer": "second import", "open_rc": rc3, "first_word": hex(seen.value),
-                          "same_mapping_as_first": m2.value == m.value if rc3 == 0 else None,
-                          "close_rc": rc4}), flush=True)
+    rc_read = L.hipMemcpy(ctypes.byref(seen), m, 8, 2) if rc == 0 else None
     t0 = time.time()
-    rc2 = L.hipIpcCloseMemHandle(m)
-    print(json.dumps({"importer": "closed", "open_rc": rc, "close_rc": rc2, "close_s": round(time.time() - t0, 4),
-                      "saw_freed_before_close": ok}), flush=True)
-    open(os.path.join(d, "closed"), "w").write("1")
+    rc2 = L.hipIpcCloseMemHandle(m) if rc == 0 else None
+    print(json.dumps({"importer": "read A after its free, closed", "open_rc": rc, "read_rc": rc_read,
+                      "first_word": hex(seen.value), "close_rc": rc2, "close_s": round(time.time() - t0, 4),
+                      "saw_freed": ok}), flush=True)
+    put(d, "closed")
 
 
 if __name__ == "__main__":
