@@ -1010,8 +1010,15 @@ def main():
             base = xr.get("data_path") or partial.get("data_path")
             unf = (xr.get("variants") or {}).get("mesh_unfused") or {}
             res = efficiency_of(unf, f"{base}; unfused mesh: fold kernel, then the sends (GLOO_AMD_FOLD_SEND=0)")
-            res["fused_default"] = efficiency_of(
-                xr, f"{base}; default schedule: {xr.get('schedule', 'mesh')}")
+            fused = efficiency_of(xr, f"{base}; default schedule: {xr.get('schedule', 'mesh')}")
+            if fused.get("value") and "fused" in (xr.get("schedule") or "") and "unfused" not in xr["schedule"]:
+                # the fused launch also stores each owner's range to its P - 1
+                # peers: (P + 1) fold streams + (P - 1) forward streams
+                k = 2 * world / (world + 1)
+                fused["value_incl_forward_bytes"] = round(fused["value"] * k, 4)
+                fused["forward_note"] = ("value counts the fold's (P + 1) streams only; value_incl_forward_bytes "
+                                         "adds the (P - 1) forward stores the same launch makes (x 2P / (P + 1))")
+            res["fused_default"] = fused
             return res
 
         def fire():
