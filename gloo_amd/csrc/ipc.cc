@@ -41,7 +41,12 @@ struct Pool {
   std::mutex m;
   std::vector<std::unique_ptr<Slab>> slabs;  // every live exported slab (freed only by a trim)
   std::vector<Slab*> free;
-  std::set<std::pair<int, uintptr_t>> retired;  // (device, address) of every slab a trim freed
+  // device -> [start, end) of every slab a trim freed: no later slab may
+  // overlap one (the runtime caches freed blocks and hands out pieces of
+  // them again; an export over such memory failed, and a peer's import of
+  // it showed stale pages, profiles/round4/r4d_*, r4e_*)
+  std::map<int, std::map<uintptr_t, uintptr_t>> retired;
+  size_t retiredCount = 0;
   struct Mapping {
     uint64_t incarnation;
     void* ptr;
@@ -103,7 +108,8 @@ void freeUnusedLocked(Pool& p) {
         (void)hipSetDevice(s->device);
         GLOO_AMD_HIP_RELEASE(hipFree(s->ptr));
         if (prev >= 0) (void)hipSetDevice(prev);
-        p.retired.insert({s->device, reinterpret_cast<uintptr_t>(s->ptr)});
+        p.retired[s->device][reinterpret_cast<uintptr_t>(s->ptr)] = reinterpret_cast<uintptr_t>(s->ptr) + s->bytes;
+        p.retiredCount++;
         p.trimmedBytes += s->bytes;
         p.slabs.erase(p.slabs.begin() + (long)i);
         break;
@@ -111,6 +117,19 @@ void freeUnusedLocked(Pool& p) {
   }
   p.free.clear();
   p.trims++;
+}
+
+bool overlapsRetired(const Pool& p, int device, const void* ptr, size_t bytes) {
+  auto d = p.retired.find(device);
+  if (d == p.retired.end()) return false;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(ptr), b = a + bytes;
+  auto it = d->second.upper_bound(a);  // first range starting after a
+  if (it != d->second.end() && it->first < b) return true;
+  if (it != d->second.begin()) {
+    --it;
+    if (it->second > a) return true;
+  }
+  return false;
 }
 
 size_t slabBytesLocked(const Pool& p) {
@@ -167,10 +186,12 @@ Slab* acquire(int device, size_t bytes, bool fine) {
   int prev = -1;
   GLOO_AMD_HIP_CHECK(hipGetDevice(&prev));
   GLOO_AMD_HIP_CHECK(hipSetDevice(device));
-  // Never export at a retired address: park such a block (allocated, not
-  // exported) and allocate again, then free the parked blocks.
+  // Never export memory overlapping a retired slab, and never keep a block
+  // the runtime refuses to export: park it (allocated, not exported) and
+  // allocate again while it is held, then free the parked blocks.
   std::vector<void*> parked;
   void* ptr = nullptr;
+  hipError_t eh = hipSuccess;
   for (;;) {
     ptr = nullptr;
     hipError_t e = fine ? hipExtMallocWithFlags(&ptr, want, hipDeviceMallocFinegrained) : hipMalloc(&ptr, want);
@@ -179,24 +200,22 @@ Slab* acquire(int device, size_t bytes, bool fine) {
       (void)hipSetDevice(prev);
       GLOO_AMD_HIP_ALLOC(e);
     }
-    if (!p.retired.count({device, reinterpret_cast<uintptr_t>(ptr)})) break;
+    if (!overlapsRetired(p, device, ptr, want)) {
+      eh = hipIpcGetMemHandle(&s->handle, ptr);
+      if (eh == hipSuccess) break;
+      (void)hipGetLastError();
+    }
     parked.push_back(ptr);
     p.parked++;
     if (parked.size() > 64) {
       for (void* q : parked) (void)hipFree(q);
       (void)hipSetDevice(prev);
-      GLOO_AMD_ENFORCE(false, "IPC pool: the allocator keeps returning retired addresses");
+      GLOO_AMD_ENFORCE(false, "IPC pool: no exportable block of ", want, " B after 64 tries (",
+                       eh == hipSuccess ? "retired ranges" : hipGetErrorString(eh), ")");
     }
   }
   for (void* q : parked) GLOO_AMD_HIP_RELEASE(hipFree(q));
   s->ptr = static_cast<char*>(ptr);
-  const hipError_t e = hipIpcGetMemHandle(&s->handle, ptr);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    (void)hipFree(ptr);  // never exported: safe to free
-    (void)hipSetDevice(prev);
-    GLOO_AMD_HIP_ALLOC(e);
-  }
   (void)hipSetDevice(prev);
   p.slabs.push_back(std::move(s));
   return p.slabs.back().get();
@@ -290,7 +309,7 @@ Stats stats() {
   s.trims = p.trims;
   s.trimmedBytes = p.trimmedBytes;
   s.closes = p.closes;
-  s.retired = p.retired.size();
+  s.retired = p.retiredCount;
   s.parked = p.parked;
   s.max = poolMax();
   return s;

@@ -68,7 +68,7 @@ def exporter(d):
     L.hipSetDevice(0)
     a, ha, rc = alloc_export(L, 1 << 30, 0xAA)
     assert rc == 0, rc
-    put(d, "handle", bytes(ha.reserved))
+    put(d, "handle", ctypes.string_at(ctypes.byref(ha), 64))
     assert wait_file(d, "imported", 60)
     t0 = time.time()
     rc_free = L.hipFree(a)
