@@ -1426,9 +1426,12 @@ void PlanExecutor::setStamping(bool on) {
       const Step& s = plan_.steps[i];
       if (s.kind == GLOO_HIP_STEP_FOLD_SRC) srcs++;
       if (s.kind != GLOO_HIP_STEP_REDUCE && s.kind != GLOO_HIP_STEP_FOLD) continue;
-      stampSlotOf_[i] = (int)stampBytes_.size();
-      stampBytes_.push_back((s.kind == GLOO_HIP_STEP_REDUCE ? 3.0 : srcs + 1.0) * s.length * es_);
-      stampCount_.push_back(s.kind == GLOO_HIP_STEP_REDUCE ? 1 : std::max<size_t>(srcs, 1) - 1);
+      // a one-source FOLD is a copy (the pipelined ring's allgather), not a reduction
+      if (s.kind == GLOO_HIP_STEP_REDUCE || srcs >= 2) {
+        stampSlotOf_[i] = (int)stampBytes_.size();
+        stampBytes_.push_back((s.kind == GLOO_HIP_STEP_REDUCE ? 3.0 : srcs + 1.0) * s.length * es_);
+        stampCount_.push_back(s.kind == GLOO_HIP_STEP_REDUCE ? 1 : srcs - 1);
+      }
       if (s.kind == GLOO_HIP_STEP_FOLD) srcs = 0;
     }
     stampSlots_ = (int)stampBytes_.size();
@@ -1764,8 +1767,10 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
     ~StampScope() { setLaunchStamp(prev); }
     uint64_t* prev;
   };
-  auto slotOf = [&](size_t step) {
-    return stamping_ ? stamps_ + (size_t)kStampSlotWords * stampSlotOf_.at(step) : nullptr;
+  auto slotOf = [&](size_t step) -> uint64_t* {
+    if (!stamping_) return nullptr;
+    auto it = stampSlotOf_.find(step);
+    return it == stampSlotOf_.end() ? nullptr : stamps_ + (size_t)kStampSlotWords * it->second;
   };
   for (size_t i = 0; i < steps.size(); i++) {
     const Step& s = steps[i];
@@ -2086,8 +2091,12 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         }
         if (profiling_) {
           GLOO_AMD_HIP_CHECK(hipEventRecord(event(), stream_));
-          reduceBytes_ += (foldSrcs.size() + 1.0) * s.length * es_;
-          reduceCount_ += foldSrcs.size() - 1;
+          if (foldSrcs.size() >= 2) {
+            reduceBytes_ += (foldSrcs.size() + 1.0) * s.length * es_;
+            reduceCount_ += foldSrcs.size() - 1;
+          } else {
+            evUsed_ -= 2;  // a one-source fold is a copy: not a reduce kernel to time
+          }
         }
         foldSrcs.clear();
         break;
