@@ -66,8 +66,11 @@ def parse():
                    help="N>1 config-4 sweep: minimum seconds per timed batch (gloo/benchmark default 2 s)")
     p.add_argument("--quick", action="store_true",
                    help="N>1: config 3 + one variant, short HD sweep, RS at 16 Mi (rehearsals)")
-    p.add_argument("--watchdog-seconds", type=float, default=300.0,
-                   help="N>1: the xGMI section's time limit; on expiry the line is printed and the job exits 3")
+    p.add_argument("--watchdog-seconds", type=float, default=180.0,
+                   help="N>1: the xGMI section may go this long without progress (a hang); then the line is "
+                        "printed and the job exits 3")
+    p.add_argument("--watchdog-total-seconds", type=float, default=1500.0,
+                   help="N>1: the xGMI section's overall limit (same outcome)")
     return p.parse_args()
 
 
@@ -80,9 +83,13 @@ def relaunch_distributed(args):
     return subprocess.call(cmd)
 
 
+_LAST_PROGRESS = [time.time()]
+
+
 def progress(msg):
     """One progress line on stderr (every rank): a long multi-rank run keeps
-    writing, and a stuck section names itself."""
+    writing, and a stuck section names itself.  Also the watchdog's clock."""
+    _LAST_PROGRESS[0] = time.time()
     print(f"[bench r{os.environ.get('RANK', '0')} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
@@ -826,12 +833,29 @@ class HipEvent:
             self.h = ctypes.c_void_p()
 
 
-def arm_watchdog(seconds, on_fire):
-    import threading
-    t = threading.Timer(seconds, on_fire)
-    t.daemon = True
-    t.start()
-    return t
+class Watchdog:
+    """Fires on_fire(reason) once the section has gone `idle_s` without a
+    progress() line (every rank's sections end in a gather, so one hung rank
+    stalls them all) or `total_s` in all; cancel() stops it."""
+
+    def __init__(self, idle_s, total_s, on_fire):
+        import threading
+        self.stop = threading.Event()
+        t0 = time.time()
+        _LAST_PROGRESS[0] = t0
+
+        def loop():
+            while not self.stop.wait(min(1.0, idle_s / 4)):
+                now = time.time()
+                if now - _LAST_PROGRESS[0] > idle_s:
+                    return on_fire("no progress for %.0f s" % (now - _LAST_PROGRESS[0]))
+                if now - t0 > total_s:
+                    return on_fire("section exceeded %.0f s" % total_s)
+        self.t = threading.Thread(target=loop, daemon=True)
+        self.t.start()
+
+    def cancel(self):
+        self.stop.set()
 
 
 def main():
@@ -1021,9 +1045,9 @@ def main():
             res["fused_default"] = fused
             return res
 
-        def fire():
+        def fire(reason):
             if rank == 0:
-                out["xgmi_allreduce"] = dict(partial, error="watchdog: section exceeded %g s" % args.watchdog_seconds)
+                out["xgmi_allreduce"] = dict(partial, error="watchdog: " + reason)
                 out["per_gpu_efficiency"] = efficiency(partial)
                 out["value_note"] = "the N>1 section timed out: the job exits 3 after this line"
                 print(json.dumps(out), flush=True)
@@ -1031,7 +1055,7 @@ def main():
             os._exit(3)
 
         progress("N>1 sections")
-        wd = arm_watchdog(args.watchdog_seconds, fire)
+        wd = Watchdog(args.watchdog_seconds, args.watchdog_total_seconds, fire)
         xr = xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial)
         wd.cancel()
         if rank == 0:

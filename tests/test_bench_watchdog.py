@@ -1,0 +1,47 @@
+"""CPU: bench.py's N>1 watchdog fires on a hang (no progress line for the
+idle limit) or past the section's total limit, and not while progress lines
+keep coming (a hung section must end the job non-zero, a slow
+one must not)."""
+import os
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def _run(idle, total, beat_for, beat_every=0.05):
+    fired = []
+    done = threading.Event()
+
+    def fire(reason):
+        fired.append((time.time(), reason))
+        done.set()
+    t0 = time.time()
+    wd = bench.Watchdog(idle, total, fire)
+    while time.time() - t0 < beat_for:
+        bench.progress("beat")
+        time.sleep(beat_every)
+    done.wait(5)
+    wd.cancel()
+    return t0, fired
+
+
+def test_fires_when_progress_stops():
+    t0, fired = _run(0.4, 60, beat_for=1.0)
+    assert fired and "no progress" in fired[0][1]
+    assert fired[0][0] - t0 >= 1.0  # not while the beats came
+
+
+def test_fires_past_total_limit_despite_progress():
+    t0, fired = _run(5, 0.8, beat_for=1.5)
+    assert fired and "exceeded" in fired[0][1]
+
+
+def test_cancel_stops_it():
+    fired = []
+    wd = bench.Watchdog(0.2, 60, lambda r: fired.append(r))
+    wd.cancel()
+    time.sleep(0.5)
+    assert not fired
