@@ -1205,6 +1205,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       copyBlocks_ = (unsigned)std::max(1, std::atoi(cb));
       copyBlocksLocal_ = copyBlocks_;
     }
+    if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS_LOCAL")) copyBlocksLocal_ = (unsigned)std::max(1, std::atoi(cb));
     const size_t tickets = std::max<size_t>(256, (size_t)P * GLOO_HIP_NUM_SLOTS * sizeof(unsigned));
     GLOO_AMD_HIP_ALLOC(hipMalloc(&ticket_, tickets));
     // zeroed on the executor's stream and complete before any copy kernel
