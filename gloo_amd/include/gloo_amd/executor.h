@@ -266,11 +266,14 @@ class PlanExecutor {
   bool kernelCopy_ = false;    // SEND = copy_signal_kernel instead of hipMemcpyAsync + signal
   bool autoCopy_ = false;      // GLOO_AMD_COPY=auto: the engine picked per SEND by size and peer placement
   unsigned copyBlocks_ = 64;        // per copy to a peer on another GPU (xGMI)
-  // per copy to a peer on this GPU: also 64 — ranks sharing a GPU run their
+  // per copy to a peer on this GPU: 128 — ranks sharing a GPU run their
   // copies concurrently, and whole-chip copy grids convoy behind each other
-  // (measured: 64 MiB HD over 4 ranks on one GPU, 462 us at 64 vs 1357 us
-  // at 512 workgroups per copy)
-  unsigned copyBlocksLocal_ = 64;
+  // (64 MiB HD over 4 ranks on one GPU: 462 us at 64 vs 1357 us at 512
+  // workgroups per copy); 128 against 64 (round 4, profiles/round4/
+  // r4j_latency_copy_blocks_local_ab.jsonl): HD 16 MiB per rank 45.4-47.1
+  // vs 47.2-48.2 us at 2 ranks, 64 MiB 226-230 vs 240-247 us at 4 ranks,
+  // even elsewhere.  GLOO_AMD_COPY_BLOCKS_LOCAL overrides.
+  unsigned copyBlocksLocal_ = 128;
   unsigned copyBlocksFor(int peer) const {
     return peers_[peer].device == ctx_->device() ? copyBlocksLocal_ : copyBlocks_;
   }
