@@ -128,6 +128,9 @@ CASES = [("ring_chunked/sum/f32/P2/k1/n1000", None), ("halving_doubling/sum/f32/
          # the reference ring's bytes from the mesh plan (two all-to-all hops)
          ("ring_chunked/sum/f32/P3/k2/n1000", "ring_chunked_mesh"),
          ("ring_chunked/max/f32/P5/k1/n999", "ring_chunked_mesh"),
+         # the pipelined ring route: three inboxes, fused reduce + send rounds
+         ("ring_chunked/sum/f32/P2/k1/n1000", "ring_chunked_pipe"),
+         ("ring_chunked/sum/f32/P3/k2/n1000", "ring_chunked_pipe"),
          # new-style gloo::allreduce BCUBE and gloo::reduce (tests/golden/newstyle_golden.npz)
          ("bcube/sum/f32/P2/i0/o1/n1000/s0", None), ("bcube/sum/f32/P6/i3/o2/n999/s0", None),
          ("reduce/sum/f32/P3/i0/n1000/r2/s128", None), ("reduce/sum/f32/P5/i1/n4099/r2/s0", None)]
