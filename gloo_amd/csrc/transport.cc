@@ -250,6 +250,12 @@ class RecvBuffer : public Buffer {
     // baseline before the record is published, i.e. before the peer's
     // first send can land (the sender resolves the record first)
     baseline_ = channel_->count.load(std::memory_order_acquire);
+    // payload records an earlier buffer of this channel left unconsumed are
+    // released, so the peer's sends here never wait for them
+    for (int i = 0; i < kPayloadRing; i++) {
+      Device::PayloadRecord& rec = dev_->payloadRecord(peer_, ctx.rank, idx_, (uint64_t)i);
+      rec.ack.store(rec.seq.load(std::memory_order_acquire), std::memory_order_release);
+    }
     RecvRecord r;
     std::memset(&r, 0, sizeof(r));
     r.pid = ctx.pid();
