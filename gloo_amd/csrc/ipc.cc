@@ -62,7 +62,8 @@ struct Pool {
 };
 
 // GLOO_AMD_IPC_POOL_MAX: bytes of exported slabs per process (suffix K, M
-// or G); an acquire that would pass it trims first.  Default 16 GiB.
+// or G); an executor whose slabs would take a rank's pool past it trims
+// collectively first (executor.cc).  Default 16 GiB.
 size_t poolMax() {
   static const size_t v = [] {
     const char* e = std::getenv("GLOO_AMD_IPC_POOL_MAX");
@@ -97,8 +98,9 @@ void closeUnusedLocked(Pool& p) {
 // this process is exported there, and a byte-identical handle keeps meaning
 // the same pages.  Freeing a slab a peer still maps is not safe on ROCm 7:
 // the next export of memory allocated over it can fail ("invalid argument",
-// profiles/round4/r4d_*), so callers free only after every peer has closed
-// its unused mappings (trimCollective, executor.cc).
+// profiles/round4/r4e_*), so callers free only after every peer has closed
+// its unused mappings (the collective trims of executor.cc and
+// gloo_hip_ipc_trim).
 void freeUnusedLocked(Pool& p) {
   for (Slab* s : p.free) {
     for (size_t i = 0; i < p.slabs.size(); i++)
