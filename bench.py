@@ -819,6 +819,17 @@ class HipEvent:
         if rc != 0:
             raise RuntimeError(f"hipEventRecord failed: {rc}")
 
+    def spin(self):
+        """Busy-poll until the stream has passed this event (hipEventQuery;
+        hipErrorNotReady = 600), so the host sees the end of the timed work
+        without a blocking wait's wake-up latency."""
+        while True:
+            rc = HipEvent._rt.hipEventQuery(self.h)
+            if rc != 600:
+                if rc != 0:
+                    raise RuntimeError(f"hipEventQuery failed: {rc}")
+                return
+
     def elapsed_ms(self, other):
         ms = ctypes.c_float()
         rc = HipEvent._rt.hipEventElapsedTime(ctypes.byref(ms), self.h, other.h)
@@ -924,10 +935,13 @@ def main():
     for i in range(skip, args.steps):
         step(i)
     e_end.record()
-    torch.cuda.synchronize(dev)
+    e_end.spin()                 # the end of the K launches, seen without a blocking wait's wake-up
+    torch.cuda.synchronize(dev)  # (returns at once: nothing else is queued)
+    # each rank's own K steps; the slowest rank's time is taken below (MAX
+    # over ranks), so the closing barrier's own latency stays outside
+    wall = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    wall = time.perf_counter() - t0
     region_ms = e_start.elapsed_ms(e_end)
     kern_ms = region_ms / (args.steps - skip)
     e_start.destroy()
