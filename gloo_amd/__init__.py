@@ -16,7 +16,9 @@ import enum
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgloo_amd.so")
+# GLOO_AMD_LIB: another build of the same library (A/B measurements of
+# compile-time kernel variants, tools/build_fold_variants.sh)
+LIB_PATH = os.environ.get("GLOO_AMD_LIB") or os.path.join(_HERE, "libgloo_amd.so")
 
 
 class ReductionType(enum.IntEnum):

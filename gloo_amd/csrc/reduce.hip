@@ -498,6 +498,11 @@ __device__ __forceinline__ typename Tr::Storage fold_elem(const SrcList& srcs, i
 
 // One vector tile of a k-source fold: `bytes` (<= BLOCK * UNROLL * 16) of
 // the body starting `base` bytes past element `head`, into acc.
+// FOLD_PRELOAD: the chain folds (MODE 0 / 1) issue every source's loads
+// before the first op, as the tree does; 0 loads source by source.
+#ifndef FOLD_PRELOAD
+#define FOLD_PRELOAD 1
+#endif
 template <class Tr, int OP, int UNROLL, int BLOCK, int MODE>
 __device__ __forceinline__ void fold_tile(const SrcList& srcs, int k, size_t head, size_t base, uint32_t bytes,
                                           u32x4 (&acc)[UNROLL]) {
@@ -524,6 +529,28 @@ __device__ __forceinline__ void fold_tile(const SrcList& srcs, int k, size_t hea
       }
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) acc[u] = v[0][u];
+  } else if (FOLD_PRELOAD) {
+    // every source's loads in flight before the first op (k <= 8, uniform),
+    // then the chain in order: a k-source fold keeps k tiles in flight per
+    // wave instead of two
+    u32x4 v[GLOO_HIP_MAX_SRCS][UNROLL];
+#pragma unroll
+    for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++)
+      if (j < k) {
+        const Src sj = src_of(static_cast<const S*>(srcs.p[j]) + head);
+        const auto rj = make_rsrc(sj.base + base, bytes + sj.mis);
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++) v[j][u] = bload<kAuxNT>(rj, lane_off + u * BLOCK * 16, sj.mis);
+      }
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) acc[u] = v[0][u];
+#pragma unroll
+    for (int j = 1; j < GLOO_HIP_MAX_SRCS; j++)
+      if (j < k) {
+#pragma unroll
+        for (int u = 0; u < UNROLL; u++)
+          acc[u] = MODE == 1 ? apply_packet<Tr, OP>(v[j][u], acc[u]) : apply_packet<Tr, OP>(acc[u], v[j][u]);
+      }
   } else {
     {
       const Src s0 = src_of(static_cast<const S*>(srcs.p[0]) + head);
