@@ -498,10 +498,14 @@ __device__ __forceinline__ typename Tr::Storage fold_elem(const SrcList& srcs, i
 
 // One vector tile of a k-source fold: `bytes` (<= BLOCK * UNROLL * 16) of
 // the body starting `base` bytes past element `head`, into acc.
-// FOLD_PRELOAD: the chain folds (MODE 0 / 1) issue every source's loads
-// before the first op, as the tree does; 0 loads source by source.
+// FOLD_PRELOAD=1: the chain folds (MODE 0 / 1) issue every source's loads
+// before the first op, as the tree does.  Measured slower (round 4, 64 MiB
+// fp32 per source, profiles/round4/r4t_multi_*: k = 4..8 at 54.3-98.7 us
+// against 53.1-97.8 us loading source by source): the extra VGPRs cost
+// more waves than the extra loads in flight gain.  So the default (0) keeps
+// two tiles per source step and relies on occupancy.
 #ifndef FOLD_PRELOAD
-#define FOLD_PRELOAD 1
+#define FOLD_PRELOAD 0
 #endif
 template <class Tr, int OP, int UNROLL, int BLOCK, int MODE>
 __device__ __forceinline__ void fold_tile(const SrcList& srcs, int k, size_t head, size_t base, uint32_t bytes,

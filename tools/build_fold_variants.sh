@@ -1,8 +1,8 @@
 #!/bin/bash
-# Measurement only: libgloo_amd.so with the k-source fold loading source by
-# source (FOLD_PRELOAD=0, the round-3 kernel) under
-# tools/fold_variants/<name>/, for A/B against the default (every source's
-# loads in flight first).  Load one with GLOO_AMD_LIB=<that .so>.  Built here.
+# Measurement only: libgloo_amd.so with the k-source chain folds issuing
+# every source's loads first (FOLD_PRELOAD=1) under
+# tools/fold_variants/<name>/, for A/B against the default (source by
+# source).  Load one with GLOO_AMD_LIB=<that .so>.  Built here.
 set -e
 cd "$(dirname "$0")/.."
 make -C gloo_amd -j8 >/dev/null
@@ -15,5 +15,5 @@ build() {  # name defines...
   hipcc --offload-arch=gfx950 -shared $OBJS tools/fold_variants/$name/reduce.o -o tools/fold_variants/$name/libgloo_amd.so
   rm tools/fold_variants/$name/reduce.o
 }
-build serial -DFOLD_PRELOAD=0
+build preload -DFOLD_PRELOAD=1
 ls -la tools/fold_variants/*/
