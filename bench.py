@@ -512,6 +512,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                      "frac_of_mesh_link_bound": round(2 * n * 4 / world / B / t, 4)}
         return {"plan": "mesh" if mesh == "1" and world <= 8 else "ring", "copy_engine": engine,
                 "workspace": workspace, "graph": all(g["graph"] for g in gathered),
+                **({"env": extra_env} if extra_env else {}),
                 "ms_p50": round(t * 1e3, 3), "algbw_gib_s": round(n * 4 / t / GIB, 2),
                 "busbw_gib_s": round(busbw / GIB, 2), **links,
                 "schedule": ("%s%s" % ("mesh" if mesh == "1" and world <= 8 else "ring",
@@ -553,6 +554,10 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     # SURVEY 8(e)'s efficiency on the unfused mesh (a pure fold kernel between
     # the sends), beside the default fused schedule above
     variants["mesh_unfused"] = ring_once("auto", extra_env={"GLOO_AMD_FOLD_SEND": "0"})
+    # the single-release completion protocol against a release in every
+    # workgroup, over the links (both bit-checked)
+    if not args.quick:
+        variants["mesh_release_each"] = ring_once("auto", extra_env={"GLOO_AMD_FWD_RELEASE": "each"})
     specs = {"ring_memcpy": ("memcpy", "device", "0"), "ring_kernel": ("kernel", "device", "0"),
              "mesh_memcpy_forked": ("memcpy", "device", "1"), "mesh_host_workspace": ("auto", "host", "1")}
     chosen = (args.config3_variants.split(",") if args.config3_variants

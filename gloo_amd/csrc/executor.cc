@@ -1199,6 +1199,8 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     // Fold + forward (enqueue, FOLD): "0" keeps the fold and its SENDs apart.
     const char* fs = std::getenv("GLOO_AMD_FOLD_SEND");
     foldSend_ = !(fs && std::string(fs) == "0");
+    // Completion protocol of the signalling kernels (GLOO_AMD_FWD_RELEASE)
+    refreshFwdLean();
     // Workgroups per copy (executor.h): a few dozen saturate an xGMI link.
     // GLOO_AMD_COPY_BLOCKS overrides both the remote and the same-GPU size.
     if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS")) {

@@ -31,6 +31,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 #include <string>
@@ -264,13 +265,20 @@ constexpr int kAuxWT = 1 | 2 | 16;      // `sc0 nt sc1`: streamed once, written 
 // publishes the flag with a relaxed store.  The interpreter's sends work the
 // same way, and its credits (NOTIFY) publish no data, so neither releases.
 // "each" = every workgroup releases at system scope before its ticket or
-// flag (rounds 1-2).
-int fwdLean() {
-  static const int v = [] {
-    const char* e = std::getenv("GLOO_AMD_FWD_RELEASE");
-    return e && std::string(e) == "each" ? 0 : 1;
-  }();
+// flag (rounds 1-2).  Read when an executor is built (refreshFwdLean), so one
+// process can measure both; a graph keeps the protocol it was captured with.
+std::atomic<int> g_fwdLean{-1};
+
+int readFwdLean() {
+  const char* e = std::getenv("GLOO_AMD_FWD_RELEASE");
+  const int v = e && std::string(e) == "each" ? 0 : 1;
+  g_fwdLean.store(v, std::memory_order_relaxed);
   return v;
+}
+
+int fwdLean() {
+  const int v = g_fwdLean.load(std::memory_order_relaxed);
+  return v < 0 ? readFwdLean() : v;
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
@@ -1287,6 +1295,8 @@ int dispatch_multi(int op, int dtype, void* d, const void* const* srcs, int k, s
 }
 
 }  // namespace
+
+int refreshFwdLean() { return readFwdLean(); }
 
 unsigned copySignalGrid(size_t bytes, unsigned maxBlocks) {
   const size_t tiles = (bytes + (size_t)kCopyBlock * kCopyUnroll * 16 - 1) / ((size_t)kCopyBlock * kCopyUnroll * 16);

@@ -59,6 +59,8 @@ def test_config3_variants_in_bench_order_verified(gpu):
     assert eff["fused_default"]["value"] and "fused" in eff["fused_default"]["data_path"], eff
     assert "fold + forward fused" in out["xgmi_allreduce"]["schedule"], out["xgmi_allreduce"]
     assert "unfused" in out["xgmi_allreduce"]["variants"]["mesh_unfused"]["schedule"]
+    # the per-workgroup release protocol, built in the same process
+    assert "mesh_release_each" in out["xgmi_allreduce"]["variants"]
 
 
 @pytest.mark.timeout(200)
