@@ -1208,6 +1208,8 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       copyBlocksLocal_ = copyBlocks_;
     }
     if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS_LOCAL")) copyBlocksLocal_ = (unsigned)std::max(1, std::atoi(cb));
+    if (const char* cb = std::getenv("GLOO_AMD_COPY_OUT_BYTES")) copyOutKernelBytes_ = std::strtoull(cb, nullptr, 10);
+    if (const char* cb = std::getenv("GLOO_AMD_COPY_OUT_BLOCKS")) copyOutBlocks_ = (unsigned)std::max(1, std::atoi(cb));
     const size_t tickets = std::max<size_t>(256, (size_t)P * GLOO_HIP_NUM_SLOTS * sizeof(unsigned));
     GLOO_AMD_HIP_ALLOC(hipMalloc(&ticket_, tickets));
     // zeroed on the executor's stream and complete before any copy kernel
@@ -1855,7 +1857,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         int nd = 0;
         for (size_t k = 0; k < ops.size(); k++)
           if (lens[k]) d[nd++] = CopyDesc{ops[k].first, ops[k].second, lens[k], nullptr, Seq{}, nullptr,
-                                          copySignalGrid(lens[k], 256)};
+                                          copySignalGrid(lens[k], copyOutBlocks_)};
         if (nd) checkRc(launchCopySignalMulti(d, nd, epoch, stream_), "copy kernel (local batch)");
         i = j - 1;
         continue;
@@ -1988,7 +1990,13 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
       case GLOO_HIP_STEP_COPY: {
         char* dst = userOrArena(s.flags & GLOO_HIP_DST_ARENA, s.dst_off, s.length);
         const char* src = userOrArena(s.flags & GLOO_HIP_SRC_ARENA, s.src_off, s.length);
-        deviceMove(dst, src, s.length * es_, stream_);
+        const size_t bytes = s.length * es_;
+        if (deviceSignal_ && bytes >= copyOutKernelBytes_ && bytes > 0 && (dst + bytes <= src || src + bytes <= dst)) {
+          const CopyDesc d{dst, src, bytes, nullptr, Seq{}, nullptr, copySignalGrid(bytes, copyOutBlocks_)};
+          checkRc(launchCopySignalMulti(&d, 1, epoch, stream_), "copy kernel (local)");
+          break;
+        }
+        deviceMove(dst, src, bytes, stream_);
         break;
       }
       case GLOO_HIP_STEP_NOTIFY:

@@ -278,6 +278,12 @@ class PlanExecutor {
     return peers_[peer].device == ctx_->device() ? copyBlocksLocal_ : copyBlocks_;
   }
   bool batchKernelCopy_ = true;  // a batch of SENDs = one multi-destination copy kernel
+  // A lone local COPY (a mesh result out of its inbox) of at least this many
+  // bytes runs on the copy kernel instead of hipMemcpyAsync
+  // (GLOO_AMD_COPY_OUT_BYTES); copyOutBlocks_ caps the workgroups per local
+  // copy there and in a batch of local COPYs (GLOO_AMD_COPY_OUT_BLOCKS)
+  size_t copyOutKernelBytes_ = SIZE_MAX;
+  unsigned copyOutBlocks_ = 256;
   bool foldSend_ = true;         // a FOLD's result SENDs ride in the fold's pass (launchFoldSend)
   bool foldSendUsed_ = false;    // ... and some enqueue did so
   unsigned* ticket_ = nullptr;   // copy_signal_kernel tickets, one counter per (peer, slot)

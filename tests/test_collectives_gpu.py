@@ -560,6 +560,11 @@ def test_processes_graph_replay(torch, golden_sched, case, env, graph):
     ("ring_chunked/product/f32/P3/k1/n777", {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_FUSE_BYTES": "0"}, True),
     ("ring_chunked/max/f32/P5/k1/n999", {"GLOO_AMD_GRAPH": "1"}, True),           # ragged: misaligned forwards
     ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_FWD_RELEASE": "each"}, True),
+    # a lone result COPY out of the inbox on the copy kernel (GLOO_AMD_COPY_OUT_BYTES)
+    ("halving_doubling/sum/f32/P2/k1/n1000", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_FUSE_BYTES": "0",
+                                             "GLOO_AMD_COPY_OUT_BYTES": "0"}, True),
+    ("ring_chunked/sum/f32/P2/k1/n1000", {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_FUSE_BYTES": "0",
+                                         "GLOO_AMD_COPY_OUT_BYTES": "0", "GLOO_AMD_COPY_OUT_BLOCKS": "1"}, True),
     ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_FOLD_SEND": "0"}, False),
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_MESH": "0"}, False),  # no FOLD
     # reduce-scatter owners: a fold and its credits (NOTIFY) in one launch
