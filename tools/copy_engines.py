@@ -2,7 +2,7 @@
 """Copy engines of a SEND step on one MI355X:
 the blit engine (hipMemcpyAsync, what GLOO_AMD_COPY=memcpy uses) against the
 kernel copy engine (copy_signal_kernel via gloo_hip_copy_kernel) at 4, 16 and
-64 MiB, with the workgroup counts the executor uses (64 per peer) and more.
+64 MiB (COPY_MIB), with the workgroup counts the executor uses (64 per peer) and more (COPY_BLOCKS).
 Same-GPU (HBM -> HBM) copies only: that is all one GPU can show; run under
 `rocprofv3 --kernel-trace --stats` for the kernel's own durations.  Buffers
 rotate over a 1 GiB footprint (> 256 MiB Infinity Cache).  One JSON line per
@@ -35,11 +35,13 @@ def main():
     s = torch.cuda.current_stream()
     src = torch.empty(FOOT // 4, device=dev).uniform_(-1, 1)
     dst = torch.empty(FOOT // 4, device=dev)
-    for mib in (4, 16, 64):
+    sizes = [int(v) for v in os.environ.get("COPY_MIB", "4,16,64").split(",")]
+    grids = [int(v) for v in os.environ.get("COPY_BLOCKS", "64,256,1024").split(",")]
+    for mib in sizes:
         nbytes = mib << 20
         slots = FOOT // nbytes
         k = max(40, 2560 // mib)
-        engines = [("memcpy", None)] + [("kernel", b) for b in (64, 256, 1024)]
+        engines = [("memcpy", None)] + [("kernel", b) for b in grids]
         for name, blocks in engines:
             def once(i):
                 d = dst.data_ptr() + (i % slots) * nbytes
