@@ -368,6 +368,16 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     `partial` collects each finished subsection, so a watchdog firing late
     still reports everything measured before it."""
     import tempfile
+    # wall seconds per section on rank 0's clock (where an 8-GPU run spends its time)
+    sections = {}
+    partial["section_s"] = sections
+    t_mark = [time.perf_counter()]
+
+    def mark(name):
+        now = time.perf_counter()
+        sections[name] = round(now - t_mark[0], 1)
+        t_mark[0] = now
+
     obj = [tempfile.mkdtemp(prefix="gloo_amd_bench_")] if rank == 0 else [None]
     dist.broadcast_object_list(obj, src=0)
     n = args.allreduce_mib * (1 << 20) // 4
@@ -566,6 +576,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         engine, workspace, mesh = specs[name]
         variants[name if name not in variants else "%s#%d" % (name, k + 1)] = ring_once(engine, workspace, mesh)
     partial["ipc_pool"] = hip.ipc_stats()
+    mark("config3")
     if args.config3_only:
         return dict(partial)
 
@@ -664,6 +675,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
             continue
         big = k in ("mesh", "reference_route") and not args.quick
         hd_summary[k] = hd_sweep(k, v, full_sizes if big else short_sizes)
+    mark("config4_halving_doubling")
 
     # Config 5: reduce-scatter (HD), fp16 / bf16 buckets, every op, 16 Mi
     # elements per rank, recvElems = an even split.
@@ -710,6 +722,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     rs_summary = [rs_once(dt, op, {}) for dt in ("f16", "bf16") for op in ("sum", "product", "min", "max")]
     if args.quick:
         partial["reduce_scatter"] = rs_summary
+        mark("config5_reduce_scatter")
         return dict(partial)
     rs_summary += [rs_once(dt, "sum", {"GLOO_AMD_MESH": "0"}) for dt in ("f16", "bf16")]
     partial["reduce_scatter"] = rs_summary
@@ -761,10 +774,12 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     ns_sizes = (64 << 10, 1 << 20, 16 << 20, 256 << 20)
     ns = {}
     partial["new_style"] = ns
+    mark("config5_reduce_scatter")
     ref_route = {"GLOO_AMD_MESH": "0"}
     for kind, label in (("ring", "ring_allreduce"), ("bcube", "bcube_allreduce"), ("reduce", "reduce_to_root0")):
         ns[label] = [newstyle(kind, b) for b in ns_sizes]
         ns[label + "_reference_route"] = [newstyle(kind, b, ref_route) for b in ns_sizes[2:]]
+    mark("new_style")
     dist.barrier()
     if rank == 0:
         import shutil
