@@ -338,6 +338,52 @@ print("INTERP", a.mode()["interp"])
 '''
 
 
+ZERO_COUNT_WORKER = r'''
+import os, sys
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+import torch, gloo_amd
+rank, size, store, algo = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+torch.cuda.set_device(0)
+buf = torch.full((4,), float(rank + 1), device="cuda:0")
+ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=30000)
+recv = [0] * size if algo == "reduce_scatter" else None
+a = gloo_amd.Algorithm(ctx, algo, "sum", "f32", [buf.data_ptr()], 0, recv_elems=recv)
+for _ in range(4):  # eager, then enqueued / captured / replayed where graphs apply
+    a.run()
+torch.cuda.synchronize()
+assert (buf == rank + 1).all(), buf
+a.close()
+# and a non-empty collective on the same context afterwards
+b = torch.full((1000,), float(rank + 1), device="cuda:0")
+recv = [1000 // size + (1 if r < 1000 % size else 0) for r in range(size)] if algo == "reduce_scatter" else None
+a = gloo_amd.Algorithm(ctx, algo, "sum", "f32", [b.data_ptr()], 1000, recv_elems=recv)
+a.run()
+torch.cuda.synchronize()
+want = size * (size + 1) / 2
+got = b[:recv[rank]] if recv else b
+assert (got == want).all(), got
+a.close(); ctx.close()
+print("OK", flush=True)
+'''
+
+
+@pytest.mark.parametrize("algo", ["ring_chunked", "halving_doubling", "ring", "reduce_scatter"])
+@pytest.mark.parametrize("P,env", [(2, {}), (3, {"GLOO_AMD_MESH": "0"}), (4, {"GLOO_AMD_GRAPH": "1"})])
+def test_processes_zero_count(torch, algo, P, env):
+    """count = 0 (the reference's algorithms accept it: every chunk empty):
+    runs complete without a launch fault or a hang, the buffer is untouched,
+    and the context still runs a real collective afterwards."""
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(ZERO_COUNT_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
+        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), algo],
+                                  env=e, stdout=subprocess.PIPE, text=True) for r in range(P)]
+        outs = [p.communicate(timeout=120)[0] for p in procs]
+        assert [p.returncode for p in procs] == [0] * P, outs
+    assert all("OK" in o for o in outs), outs
+
+
 @pytest.mark.parametrize("mode,interp", [("device", "1"), ("device", "0"), ("host", "1")])
 def test_dead_peer_times_out(torch, mode, interp):
     """Failure detection (SURVEY §5: context timeout -> IoException): a peer
