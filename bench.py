@@ -568,6 +568,10 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     # workgroup, over the links (both bit-checked)
     if not args.quick:
         variants["mesh_release_each"] = ring_once("auto", extra_env={"GLOO_AMD_FWD_RELEASE": "each"})
+        # workgroups per peer copy (64 by default, sized for one link without
+        # measurement over real links): half and double, for the next tuning
+        for blocks in ("32", "128"):
+            variants["mesh_copy_blocks_" + blocks] = ring_once("auto", extra_env={"GLOO_AMD_COPY_BLOCKS": blocks})
     specs = {"ring_memcpy": ("memcpy", "device", "0"), "ring_kernel": ("kernel", "device", "0"),
              "mesh_memcpy_forked": ("memcpy", "device", "1"), "mesh_host_workspace": ("auto", "host", "1")}
     chosen = (args.config3_variants.split(",") if args.config3_variants
@@ -665,6 +669,8 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                    "mesh_eager": {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_INTERP": "0"},
                    "mesh_no_interp": {"GLOO_AMD_INTERP": "0"},
                    "mesh_host_block_flags": {"GLOO_AMD_MAILBOX": "0"},
+                   "mesh_copy_blocks_32": {"GLOO_AMD_COPY_BLOCKS": "32"},
+                   "mesh_copy_blocks_128": {"GLOO_AMD_COPY_BLOCKS": "128"},
                    "reference_route": {"GLOO_AMD_MESH": "0"},
                    "reference_route_kernel_copy": {"GLOO_AMD_MESH": "0", "GLOO_AMD_COPY": "kernel"},
                    "reference_route_eager": {"GLOO_AMD_MESH": "0", "GLOO_AMD_GRAPH": "0", "GLOO_AMD_INTERP": "0"}}
@@ -1080,13 +1086,32 @@ def main():
             return res
 
         def fire(reason):
-            if rank == 0:
-                out["xgmi_allreduce"] = dict(partial, error="watchdog: " + reason)
-                out["per_gpu_efficiency"] = efficiency(partial)
-                out["value_note"] = "the N>1 section timed out: the job exits 3 after this line"
-                print(json.dumps(out), flush=True)
-            # a hung section must show in the driver's record: non-zero exit
-            os._exit(3)
+            # runs on the watchdog thread while the main thread may still be
+            # filling `partial`: a snapshot can race ("dictionary changed size
+            # during iteration"), so retry it, and print the line without the
+            # partial results if it keeps failing — and exit 3 whatever happens
+            try:
+                if rank == 0:
+                    line = None
+                    for _ in range(5):
+                        try:
+                            snap = json.loads(json.dumps(partial))
+                            out["xgmi_allreduce"] = dict(snap, error="watchdog: " + reason)
+                            out["per_gpu_efficiency"] = efficiency(snap)
+                            out["value_note"] = "the N>1 section timed out: the job exits 3 after this line"
+                            line = json.dumps(out)
+                            break
+                        except Exception:  # noqa: BLE001
+                            time.sleep(0.05)
+                    if line is None:
+                        out["xgmi_allreduce"] = {"error": "watchdog: " + reason + " (partial results unreadable)"}
+                        out["value_note"] = "the N>1 section timed out: the job exits 3 after this line"
+                        out.pop("per_gpu_efficiency", None)
+                        line = json.dumps(out)
+                    print(line, flush=True)
+            finally:
+                # a hung section must show in the driver's record: non-zero exit
+                os._exit(3)
 
         progress("N>1 sections")
         wd = Watchdog(args.watchdog_seconds, args.watchdog_total_seconds, fire)

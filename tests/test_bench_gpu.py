@@ -61,6 +61,7 @@ def test_config3_variants_in_bench_order_verified(gpu):
     assert "unfused" in out["xgmi_allreduce"]["variants"]["mesh_unfused"]["schedule"]
     # the per-workgroup release protocol, built in the same process
     assert "mesh_release_each" in out["xgmi_allreduce"]["variants"]
+    assert "mesh_copy_blocks_128" in out["xgmi_allreduce"]["variants"]
     assert out["xgmi_allreduce"]["section_s"]["config3"] > 0
 
 
