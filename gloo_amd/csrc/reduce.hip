@@ -266,7 +266,9 @@ constexpr int kAuxWT = 1 | 2 | 16;      // `sc0 nt sc1`: streamed once, written 
 // same way, and its credits (NOTIFY) publish no data, so neither releases.
 // "each" = every workgroup releases at system scope before its ticket or
 // flag (rounds 1-2).  Read when an executor is built (refreshFwdLean), so one
-// process can measure both; a graph keeps the protocol it was captured with.
+// process can measure both; the value is process-wide (the latest build's
+// applies to every later launch: both protocols are correct, they differ in
+// speed), and a graph keeps the protocol it was captured with.
 std::atomic<int> g_fwdLean{-1};
 
 int readFwdLean() {
