@@ -668,6 +668,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                    "mesh_memcpy_forked": {"GLOO_AMD_COPY": "memcpy"},
                    "mesh_eager": {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_INTERP": "0"},
                    "mesh_no_interp": {"GLOO_AMD_INTERP": "0"},
+                   "mesh_interp_unbatched": {"GLOO_AMD_INTERP_BATCH": "0"},
                    "mesh_host_block_flags": {"GLOO_AMD_MAILBOX": "0"},
                    "mesh_copy_blocks_32": {"GLOO_AMD_COPY_BLOCKS": "32"},
                    "mesh_copy_blocks_128": {"GLOO_AMD_COPY_BLOCKS": "128"},

@@ -1707,6 +1707,44 @@ void PlanExecutor::buildInterp() {
     if (v.size() > (size_t)kInterpMaxSteps) return fail();
   }
   if (v.empty()) return;
+  // Batches (signal.h kInterpDefer): a run of waits polls every flag before
+  // its one acquire and barrier, and a run of mutually independent data steps
+  // (a mesh owner's sends to every peer, its copies out of the inboxes, the
+  // credits after them) drains once and publishes its flags together — one
+  // memory round trip per run instead of per step.  GLOO_AMD_INTERP_BATCH=0
+  // keeps every step on its own.
+  const char* ib = std::getenv("GLOO_AMD_INTERP_BATCH");
+  if (!(ib && ib[0] == '0')) {
+    using Range = std::pair<const char*, const char*>;
+    auto touch = [&](const InterpStep& t, std::vector<Range>* rd, std::vector<Range>* wr) {
+      const size_t bytes = t.n * es_;
+      if (t.kind == kInterpCopy || t.kind == kInterpSend) {
+        rd->push_back({t.src[0], t.src[0] + bytes});
+        wr->push_back({t.dst, t.dst + bytes});
+      } else if (t.kind == kInterpFold) {
+        for (int j = 0; j < t.nsrc; j++) rd->push_back({t.src[j], t.src[j] + bytes});
+        wr->push_back({t.dst, t.dst + bytes});
+      }
+    };
+    auto meet = [](const std::vector<Range>& x, const std::vector<Range>& y) {
+      for (const Range& a : x)
+        for (const Range& b : y)
+          if (a.first < b.second && b.first < a.second) return true;
+      return false;
+    };
+    for (size_t i = 0; i + 1 < v.size(); i++) {
+      const InterpStep &a = v[i], &b = v[i + 1];
+      const bool aw = a.kind == kInterpWait, bw = b.kind == kInterpWait;
+      bool batch = aw && bw;
+      if (!aw && !bw) {
+        std::vector<Range> ra, wa, rb, wb;
+        touch(a, &ra, &wa);
+        touch(b, &rb, &wb);
+        batch = !meet(wa, rb) && !meet(wa, wb) && !meet(ra, wb);
+      }
+      if (batch) v[i].flags |= kInterpDefer;
+    }
+  }
   // the bound the ranks agreed on (slicedInterpSteps) must cover what was
   // emitted; an under-count would have let an unrunnable plan be proposed
   GLOO_AMD_ENFORCE(slices_ == 1 || v.size() <= slicedInterpSteps(plan_, (int)inputs_.size(), (int)ptrs_.size()),

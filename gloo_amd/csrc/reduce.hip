@@ -842,27 +842,34 @@ __global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpS
   constexpr uint64_t kV = 16 / sizeof(S);
   __shared__ int ok;
   const uint64_t g = blockIdx.x, G = gridDim.x;
+  int good = 1;   // lane 0: no wait of this launch has timed out
+  int batch = 0;  // first step of the current batch (kInterpDefer)
   for (int k = 0; k < nsteps; k++) {
     const InterpStep& st = steps[k];
     const int kind = st.kind;
-    const uint64_t value = st.base + run * st.perRun;
+    const bool defer = st.flags & kInterpDefer;
     if (kind == kInterpWait) {
       if (threadIdx.x == 0) {
+        const uint64_t value = st.base + run * st.perRun;
         const uint64_t* flag = st.flag + g;
-        int good = 1;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         // signed difference: a target below the counter is already met
-        while ((int64_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - value) < 0) {
+        while (good && (int64_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - value) < 0) {
           __builtin_amdgcn_s_sleep(2);
           if (__builtin_amdgcn_s_memrealtime() - t0 > timeoutTicks) {
             __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             good = 0;
-            break;
           }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        ok = good;
+        // a batch of waits: every flag polled first, then ONE acquire (it
+        // orders every relaxed load above before the inbox reads below)
+        if (!defer) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+          ok = good;
+        }
       }
+      batch = k + 1;
+      if (defer) continue;
       __syncthreads();
       if (!ok) return;  // timed out: no further work, no further signal
       continue;
@@ -879,19 +886,30 @@ __global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpS
     } else if (kind == kInterpFold) {
       interp_fold<Tr, OP>(st, lo, hi);
     }
-    // every wave's reads and writes of this step are performed before the barrier
+    // the next step neither reads nor writes what this one touches: keep
+    // this step's memory operations in flight, publish its flag with the batch's
+    if (defer) continue;
+    // every wave's reads and writes of the batch are performed before the barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if ((kind == kInterpSend || kind == kInterpSignal) && threadIdx.x == 0) {
+    if (threadIdx.x == 0) {
       // lean (fwdLean): a SEND's bytes went out write-through and a SIGNAL is
       // a credit that publishes no data (its reads are complete), so neither
-      // needs the L2 write-back of a release
-      if (!lean) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // needs the L2 write-back of a release; otherwise one release covers
+      // the whole batch
+      bool released = lean;
+      for (int j = batch; j <= k; j++) {
+        const InterpStep& sj = steps[j];
+        if (sj.kind != kInterpSend && sj.kind != kInterpSignal) continue;
+        if (!released) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          released = true;
+        }
+        __hip_atomic_store(sj.flag + g, sj.base + run * sj.perRun, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
-      __hip_atomic_store(st.flag + g, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    batch = k + 1;
   }
 }
 

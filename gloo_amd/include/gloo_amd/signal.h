@@ -105,7 +105,7 @@ struct InterpStep {
   int32_t kind;       // kInterp*
   int32_t mode;       // FOLD: 0 left fold, 1 reverse (acc = s op acc), 2 balanced tree
   int32_t nsrc;       // FOLD: sources
-  int32_t pad;
+  int32_t flags;      // kInterpDefer: the next step is independent of this one (executor.cc buildInterp)
   uint64_t* flag;     // SEND / SIGNAL: the flag written; WAIT: the flag polled (slice 0's)
   uint64_t base, perRun;
   char* dst;
@@ -113,6 +113,14 @@ struct InterpStep {
   uint64_t n;         // elements
 };
 constexpr int kInterpMaxSteps = 512;
+// InterpStep.flags: this step and the next form one batch.  A WAIT then only
+// polls (the batch's last wait takes the one acquire and the barrier); a data
+// step's memory operations are not drained before the next step, and the
+// flags of the batch's SENDs / SIGNALs are published together after the
+// batch's last step drains.  Set only where the next step of the same kind
+// (wait after wait; data or signal after data or signal) touches no byte this
+// one writes and writes no byte it reads.
+constexpr int kInterpDefer = 1;
 // Flag words per (sender, slot) in a device mailbox: one per slice.
 constexpr int kMaxSlices = 256;
 int launchPlanInterp(int op, int dtype, const InterpStep* steps, int nsteps, uint64_t run, uint64_t timeoutTicks,
