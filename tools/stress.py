@@ -3,7 +3,8 @@
 each build the same set of algorithms — ring-chunked, halving-doubling, ring,
 reduce-scatter; sum / max / min over f32 / bf16 / i32; sizes from 1 element to
 8 MiB, so every launch mode (fused steps, interpreter one- and many-workgroup,
-graph replay, eager) appears — and then run them in one shared seeded random
+graph replay, eager) appears; plus new-style gloo::allreduce RING / BCUBE and
+gloo::reduce calls with separate input and output — and then run them in one shared seeded random
 order for `seconds`, refilling inputs and checking every result exactly
 against its closed form (rank r contributes r + 1 at every position, or
 (r + 1) * (i % 7 + 1) for sum).  A wrong byte, a timeout or a fault ends the
@@ -63,6 +64,31 @@ for algo, op, dt, n in cases:
         want = want[off:off + recv[rank]]
     lim = recv[rank] if recv is not None else n
     built.append((a, buf, mine, want, lim, (algo, op, dt, n)))
+# new-style calls (gloo::allreduce RING / BCUBE, gloo::reduce to a rotating
+# root) with separate input and output: out = sum over ranks of in
+class NewStyle:
+    def __init__(self, kind, n, root=0):
+        self.kind, self.n, self.root = kind, n, root
+        self.inp = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.out = torch.zeros(n, dtype=torch.float32, device=dev)
+    def run(self):
+        if self.kind == "reduce":
+            gloo_amd.reduce_to_root(ctx, self.out.data_ptr(), self.n, "f32", self.root, "sum", input=self.inp.data_ptr())
+        else:
+            gloo_amd.allreduce(ctx, [self.out.data_ptr()], self.n, "f32", "sum", inputs=[self.inp.data_ptr()],
+                               algorithm=self.kind)
+    def mode(self):
+        return {"interp": False, "graph": False}
+for kind in ("ring", "bcube", "reduce"):
+    for j, n in enumerate((1000, 65539, (1 << 20) + 5)):
+        ns = NewStyle(kind, n, root=j % P)
+        idx = torch.arange(n, device=dev)
+        mine = ((rank + 1) * (idx % 7 + 1)).to(torch.float32)
+        want = (P * (P + 1) // 2 * (idx % 7 + 1)).to(torch.float32)
+        # the reduce's non-root outputs are unspecified: check the root only
+        lim = n if (kind != "reduce" or rank == ns.root) else 0
+        built.append((ns, ns.out, mine, want[:lim], lim, ("new_" + kind, "sum", "f32", n)))
+        ns.inp.copy_(mine)
 flag = torch.zeros(1, dtype=torch.int32, device=dev)
 stopper = gloo_amd.Algorithm(ctx, "ring_chunked", "max", "i32", [flag.data_ptr()], 1)
 order = np.random.default_rng(seed + 1)
@@ -73,7 +99,10 @@ while True:
     # every rank draws the same case; a run ends only on a round boundary all agree on
     k = int(order.integers(len(built)))
     a, buf, mine, want, lim, key = built[k]
-    buf.copy_(mine)
+    if key[0].startswith("new_"):
+        buf.zero_()  # the output; the input keeps this rank's contribution
+    else:
+        buf.copy_(mine)
     torch.cuda.synchronize()
     a.run()
     torch.cuda.synchronize()
@@ -94,7 +123,8 @@ while True:
         if int(flag.item()):
             break
 for a, *_ in built:
-    a.close()
+    if not isinstance(a, NewStyle):
+        a.close()
 stopper.close()
 ctx.close()
 print(json.dumps({"rank": rank, "runs": runs, "seconds": round(time.time() - t0, 1), "cases": len(built),
