@@ -112,8 +112,9 @@ while True:
         sys.exit(2)
     runs += 1
     m = a.mode()
-    modes[key[0] + "/" + ("interp" if m["interp"] else "graph" if m["graph"] else "eager")] = \
-        modes.get(key[0] + "/" + ("interp" if m["interp"] else "graph" if m["graph"] else "eager"), 0) + 1
+    label = key[0] + "/" + ("call" if isinstance(a, NewStyle) else
+                            "interp" if m["interp"] else "graph" if m["graph"] else "eager")
+    modes[label] = modes.get(label, 0) + 1
     if runs % 200 == 0:
         # agree on stopping: rank 0's clock decides, through a one-element max allreduce
         flag.fill_(1 if (rank == 0 and time.time() - t0 > seconds) else 0)
