@@ -671,6 +671,9 @@ def test_processes_fold_send(torch, golden_sched, case, env, fused):
     ("reduce_scatter/max/bf16/P8/n4096", {}, True),
     ("reduce_scatter/sum/f32/P8/n10007", {}, True),                 # previous-run credits
     ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_INTERP_BYTES": "1000000000"}, True),
+    # every step on its own (no batches: signal.h kInterpDefer)
+    ("halving_doubling/sum/f32/P8/k1/n1000", {"GLOO_AMD_INTERP_BATCH": "0"}, True),
+    ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_INTERP_BATCH": "0"}, True),
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_INTERP": "0"}, False),
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_INTERP_BYTES": "1024"}, False),
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, False),
