@@ -871,6 +871,25 @@ class HipEvent:
             self.h = ctypes.c_void_p()
 
 
+def watchdog_line(out, partial, reason, efficiency, tries=5):
+    """The JSON line a firing watchdog prints.  It runs on the watchdog thread
+    while the main thread may still be filling `partial`, so a snapshot can
+    race ("dictionary changed size during iteration"): retry it, and fall back
+    to the line without the partial results if it keeps failing."""
+    note = "the N>1 section timed out: the job exits 3 after this line"
+    for _ in range(tries):
+        try:
+            snap = json.loads(json.dumps(partial))
+            line = dict(out, xgmi_allreduce=dict(snap, error="watchdog: " + reason),
+                        per_gpu_efficiency=efficiency(snap), value_note=note)
+            return json.dumps(line)
+        except Exception:  # noqa: BLE001
+            time.sleep(0.05)
+    line = {k: v for k, v in dict(out).items() if k != "per_gpu_efficiency"}
+    line.update(xgmi_allreduce={"error": "watchdog: " + reason + " (partial results unreadable)"}, value_note=note)
+    return json.dumps(line)
+
+
 class Watchdog:
     """Fires on_fire(reason) once the section has gone `idle_s` without a
     progress() line (every rank's sections end in a gather, so one hung rank
@@ -1087,29 +1106,9 @@ def main():
             return res
 
         def fire(reason):
-            # runs on the watchdog thread while the main thread may still be
-            # filling `partial`: a snapshot can race ("dictionary changed size
-            # during iteration"), so retry it, and print the line without the
-            # partial results if it keeps failing — and exit 3 whatever happens
             try:
                 if rank == 0:
-                    line = None
-                    for _ in range(5):
-                        try:
-                            snap = json.loads(json.dumps(partial))
-                            out["xgmi_allreduce"] = dict(snap, error="watchdog: " + reason)
-                            out["per_gpu_efficiency"] = efficiency(snap)
-                            out["value_note"] = "the N>1 section timed out: the job exits 3 after this line"
-                            line = json.dumps(out)
-                            break
-                        except Exception:  # noqa: BLE001
-                            time.sleep(0.05)
-                    if line is None:
-                        out["xgmi_allreduce"] = {"error": "watchdog: " + reason + " (partial results unreadable)"}
-                        out["value_note"] = "the N>1 section timed out: the job exits 3 after this line"
-                        out.pop("per_gpu_efficiency", None)
-                        line = json.dumps(out)
-                    print(line, flush=True)
+                    print(watchdog_line(out, partial, reason, efficiency), flush=True)
             finally:
                 # a hung section must show in the driver's record: non-zero exit
                 os._exit(3)

@@ -45,3 +45,39 @@ def test_cancel_stops_it():
     wd.cancel()
     time.sleep(0.5)
     assert not fired
+
+
+def test_watchdog_line_survives_concurrent_updates():
+    """The line is built on the watchdog thread while the main thread keeps
+    adding results: every attempt yields parseable JSON with the error set
+    (the race a bare dict(partial) lost once)."""
+    import json
+    partial = {"variants": {}}
+    stop = threading.Event()
+
+    def writer():
+        i = 0
+        while not stop.is_set():
+            partial["variants"]["v%d" % (i % 500)] = {"ms_p50": i, "samples": list(range(i % 50))}
+            partial["k%d" % (i % 300)] = i
+            i += 1
+    t = threading.Thread(target=writer)
+    t.start()
+    try:
+        for _ in range(200):
+            line = json.loads(bench.watchdog_line({"metric": "m", "value": 1.0}, partial, "no progress",
+                                                  lambda x: {"value": None}))
+            assert line["value"] == 1.0 and "watchdog" in line["xgmi_allreduce"]["error"]
+    finally:
+        stop.set()
+        t.join()
+
+
+def test_watchdog_line_falls_back_when_unreadable():
+    import json
+
+    # a snapshot that can never be serialised (a set is not JSON)
+    line = json.loads(bench.watchdog_line({"metric": "m", "value": 2.0, "per_gpu_efficiency": {}},
+                                          {"a": {1, 2}}, "stuck", lambda x: {}, tries=2))
+    assert line["value"] == 2.0 and "unreadable" in line["xgmi_allreduce"]["error"]
+    assert "per_gpu_efficiency" not in line
