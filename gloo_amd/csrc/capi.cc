@@ -1,5 +1,6 @@
 // capi.cc — C-ABI over Context / PlanExecutor; no exception crosses it.
 #include <chrono>
+#include <cstring>
 #include <list>
 #include <memory>
 #include <string>
@@ -11,6 +12,7 @@
 #include "gloo_amd/errors.h"
 #include "gloo_amd/executor.h"
 #include "gloo_amd/ipc.h"
+#include "gloo_amd/signal.h"
 #include "gloo_amd/transport.h"
 
 struct gloo_hip_context {
@@ -183,6 +185,29 @@ int gloo_hip_algorithm_create(gloo_hip_context_t ctx, int algo, int op, int dtyp
                               gloo_hip_algorithm_t* out) {
   return gloo_hip_algorithm_create_ws(ctx, algo, op, dtype, ptrs, nptrs, count, recv_elems, stream,
                                       GLOO_HIP_WORKSPACE_DEVICE, out);
+}
+
+int gloo_hip_interp_batches(const gloo_hip_interp_desc_t* steps, int n, int* defer_out) {
+  if (n < 0 || (n > 0 && (!steps || !defer_out)))
+    return gloo_amd::setError(GLOO_HIP_EINVAL_ARG, "gloo_hip_interp_batches: bad arguments");
+  return guarded([&] {
+    std::vector<gloo_amd::InterpStep> v((size_t)n);
+    for (int i = 0; i < n; i++) {
+      const gloo_hip_interp_desc_t& d = steps[i];
+      GLOO_AMD_ENFORCE(d.kind >= gloo_amd::kInterpCopy && d.kind <= gloo_amd::kInterpFold && d.nsrc >= 0 &&
+                           d.nsrc <= GLOO_HIP_MAX_SRCS,
+                       "gloo_hip_interp_batches: bad step ", i);
+      gloo_amd::InterpStep& t = v[(size_t)i];
+      std::memset(&t, 0, sizeof t);
+      t.kind = d.kind;
+      t.nsrc = d.kind == gloo_amd::kInterpFold ? d.nsrc : 1;
+      t.dst = reinterpret_cast<char*>(d.dst);
+      for (int j = 0; j < GLOO_HIP_MAX_SRCS; j++) t.src[j] = reinterpret_cast<const char*>(d.src[j]);
+      t.n = d.bytes;
+    }
+    gloo_amd::markInterpBatches(v.data(), v.size(), 1);
+    for (int i = 0; i < n; i++) defer_out[i] = v[(size_t)i].flags & gloo_amd::kInterpDefer ? 1 : 0;
+  });
 }
 
 int gloo_hip_ipc_stats(uint64_t* out) {

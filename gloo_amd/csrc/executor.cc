@@ -433,6 +433,47 @@ int maxSlices() {
 
 }  // namespace
 
+void markInterpBatches(InterpStep* v, size_t n, size_t es) {
+  using Range = std::pair<const char*, const char*>;
+  auto touch = [&](const InterpStep& t, std::vector<Range>* rd, std::vector<Range>* wr) {
+    const size_t bytes = t.n * es;
+    if (t.kind == kInterpCopy || t.kind == kInterpSend) {
+      rd->push_back({t.src[0], t.src[0] + bytes});
+      wr->push_back({t.dst, t.dst + bytes});
+    } else if (t.kind == kInterpFold) {
+      for (int j = 0; j < t.nsrc; j++) rd->push_back({t.src[j], t.src[j] + bytes});
+      wr->push_back({t.dst, t.dst + bytes});
+    }
+  };
+  auto meet = [](const std::vector<Range>& x, const std::vector<Range>& y) {
+    for (const Range& a : x)
+      for (const Range& b : y)
+        if (a.first < b.second && b.first < a.second) return true;
+    return false;
+  };
+  // The kernel drains only at a batch's last step, so step i+1 may join the
+  // open batch only if it is independent of EVERY step already in it, not
+  // just of step i: a SIGNAL touches no bytes, and a pairwise check would let
+  // REDUCE, NOTIFY, SEND-from-inside-the-reduced-range (the halving-doubling
+  // reduce-scatter, plan.cc) run without a drain between the fold's stores
+  // and the send's loads.
+  std::vector<Range> brd, bwr;  // reads and writes of the open batch
+  for (size_t i = 0; i < n; i++) v[i].flags &= ~kInterpDefer;
+  for (size_t i = 0; i + 1 < n; i++) {
+    const InterpStep &a = v[i], &b = v[i + 1];
+    if (i == 0 || !(v[i - 1].flags & kInterpDefer)) brd.clear(), bwr.clear();
+    touch(a, &brd, &bwr);
+    const bool aw = a.kind == kInterpWait, bw = b.kind == kInterpWait;
+    bool batch = aw && bw;
+    if (!aw && !bw) {
+      std::vector<Range> rb, wb;
+      touch(b, &rb, &wb);
+      batch = !meet(bwr, rb) && !meet(bwr, wb) && !meet(brd, wb);
+    }
+    if (batch) v[i].flags |= kInterpDefer;
+  }
+}
+
 // A pinned host-memory segment every rank of the node can map (HOST workspace).
 struct PlanExecutor::HostShm {
   std::string name;
@@ -1714,37 +1755,7 @@ void PlanExecutor::buildInterp() {
   // memory round trip per run instead of per step.  GLOO_AMD_INTERP_BATCH=0
   // keeps every step on its own.
   const char* ib = std::getenv("GLOO_AMD_INTERP_BATCH");
-  if (!(ib && ib[0] == '0')) {
-    using Range = std::pair<const char*, const char*>;
-    auto touch = [&](const InterpStep& t, std::vector<Range>* rd, std::vector<Range>* wr) {
-      const size_t bytes = t.n * es_;
-      if (t.kind == kInterpCopy || t.kind == kInterpSend) {
-        rd->push_back({t.src[0], t.src[0] + bytes});
-        wr->push_back({t.dst, t.dst + bytes});
-      } else if (t.kind == kInterpFold) {
-        for (int j = 0; j < t.nsrc; j++) rd->push_back({t.src[j], t.src[j] + bytes});
-        wr->push_back({t.dst, t.dst + bytes});
-      }
-    };
-    auto meet = [](const std::vector<Range>& x, const std::vector<Range>& y) {
-      for (const Range& a : x)
-        for (const Range& b : y)
-          if (a.first < b.second && b.first < a.second) return true;
-      return false;
-    };
-    for (size_t i = 0; i + 1 < v.size(); i++) {
-      const InterpStep &a = v[i], &b = v[i + 1];
-      const bool aw = a.kind == kInterpWait, bw = b.kind == kInterpWait;
-      bool batch = aw && bw;
-      if (!aw && !bw) {
-        std::vector<Range> ra, wa, rb, wb;
-        touch(a, &ra, &wa);
-        touch(b, &rb, &wb);
-        batch = !meet(wa, rb) && !meet(wa, wb) && !meet(ra, wb);
-      }
-      if (batch) v[i].flags |= kInterpDefer;
-    }
-  }
+  if (!(ib && ib[0] == '0')) markInterpBatches(v.data(), v.size(), es_);
   // the bound the ranks agreed on (slicedInterpSteps) must cover what was
   // emitted; an under-count would have let an unrunnable plan be proposed
   GLOO_AMD_ENFORCE(slices_ == 1 || v.size() <= slicedInterpSteps(plan_, (int)inputs_.size(), (int)ptrs_.size()),

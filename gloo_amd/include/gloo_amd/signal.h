@@ -121,6 +121,11 @@ constexpr int kInterpMaxSteps = 512;
 // (wait after wait; data or signal after data or signal) touches no byte this
 // one writes and writes no byte it reads.
 constexpr int kInterpDefer = 1;
+// Sets kInterpDefer on v[0..n) (executor.cc): step i is deferred when step
+// i+1 is of the same class (wait / non-wait) and touches nothing that any
+// step of the open batch (every step since the last non-deferred one) writes,
+// and writes nothing any of them reads.  `es` = bytes per element of `n`.
+void markInterpBatches(InterpStep* v, size_t n, size_t es);
 // Flag words per (sender, slot) in a device mailbox: one per slice.
 constexpr int kMaxSlices = 256;
 int launchPlanInterp(int op, int dtype, const InterpStep* steps, int nsteps, uint64_t run, uint64_t timeoutTicks,

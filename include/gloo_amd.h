@@ -283,6 +283,21 @@ int gloo_hip_arena_slabs(int algo, int rank, int size, size_t count, int ninputs
                          size_t elem_size, size_t max_segment_bytes, const int* recv_elems,
                          uint64_t* ranges, size_t capacity, size_t* nslabs);
 
+/* (new, tests and tooling) The batching rule of the one-launch plan
+ * interpreter: which steps of a step list are not drained before the next
+ * (signal.h kInterpDefer).  Each step is a kind (0 copy, 1 send, 2 signal,
+ * 3 wait, 4 fold), its destination and nsrc source addresses and its length
+ * in bytes; addresses are only compared, never dereferenced.  defer_out[i]
+ * receives 1 where step i and step i+1 share one drain. */
+typedef struct {
+  int32_t kind;
+  int32_t nsrc;
+  uint64_t dst;
+  uint64_t src[GLOO_HIP_MAX_SRCS];
+  uint64_t bytes;
+} gloo_hip_interp_desc_t;
+int gloo_hip_interp_batches(const gloo_hip_interp_desc_t* steps, int n, int* defer_out);
+
 /* ------------------------------------------------------------------------
  * Contexts and algorithms (the GPU allreduce / reduce-scatter drop-ins).
  *
