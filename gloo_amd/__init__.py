@@ -481,7 +481,8 @@ class AllreduceOptions(ctypes.Structure):
 
 
 lib.gloo_hip_allreduce.argtypes = [ctypes.c_void_p, ctypes.POINTER(AllreduceOptions)]
-EXPORTED = EXPORTED + ("gloo_hip_allreduce", "gloo_hip_plan_ex", "gloo_hip_arena_slabs")
+EXPORTED = EXPORTED + ("gloo_hip_allreduce", "gloo_hip_plan_ex", "gloo_hip_arena_slabs",
+                       "gloo_hip_interp_batches")
 
 
 ALLREDUCE_ALGORITHMS = {"ring": 1, "bcube": 2}  # AllreduceOptions::Algorithm (gloo/allreduce.h:38-42)
