@@ -584,7 +584,9 @@ std::vector<std::pair<size_t, size_t>> arenaSegments(const Plan& p, size_t es) {
   }
   std::vector<std::pair<size_t, size_t>> segs;
   for (const auto& a : atoms) {
-    GLOO_AMD_ENFORCE(a.second - a.first <= kSegMax, "one inbox region of ", a.second - a.first,
+    // the slab requested for an atom alone is its length plus its residue
+    // mod kSegAlign (the slab keeps that residue), and must stay <= kSegMax
+    GLOO_AMD_ENFORCE(a.second - a.first + a.first % kSegAlign <= kSegMax, "one inbox region of ", a.second - a.first,
                      " B would be shared between processes; HIP IPC imports of 2 GiB and more hang on this "
                      "platform, so a message may span at most ", kSegMax,
                      " B: split the call, or run the ranks as threads of one process");

@@ -106,3 +106,21 @@ def test_two_gib_mesh_arena_is_two_one_gib_slabs():
     assert len(slabs("mesh_halving_doubling", 0, 2, 510_000_000)) == 2
     # at or below 1.75 GiB: one block, as before
     assert slabs("mesh_halving_doubling", 0, 2, 7 << 26) == []
+
+
+def test_unaligned_atom_at_the_limit_is_refused():
+    """an atom's slab is its length plus its start's residue mod
+    256 B.  A region of 1.75 GiB - 4 B starting 252 B past a 256 B boundary
+    would need 1.75 GiB + 248 B, the 2 GiB size class (the hanging import):
+    refused.  The same region 256-aligned (rank 0's first one) fits."""
+    L = SEG_MAX // 4 - 1
+    recv = [L, L, L]
+    steps, _ = ps.get_plan("mesh_reduce_scatter", 0, 3, 3 * L, recv=recv)
+    atoms = sorted(set(arena_ranges(steps)))
+    assert atoms[1][0] % 256 == 252 and atoms[1][1] - atoms[1][0] <= SEG_MAX
+    assert atoms[1][1] - atoms[1][0] + atoms[1][0] % 256 > SEG_MAX
+    assert slabs("mesh_reduce_scatter", 0, 3, 3 * L, recv) is None
+    # one element shorter per rank still leaves an unaligned start, but its slab fits
+    L2 = SEG_MAX // 4 - 64
+    segs = slabs("mesh_reduce_scatter", 0, 3, 3 * L2, [L2] * 3)
+    assert segs and all(e - s + s % 256 <= SEG_MAX for s, e in segs)
