@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <memory>
@@ -16,6 +17,8 @@
 
 #include "gloo_amd.h"
 #include "gloo_amd/common.h"
+#include "gloo_amd/errors.h"
+#include "gloo_amd/signal.h"
 
 namespace gloo_amd {
 namespace transport {
@@ -29,11 +32,13 @@ struct RecvRecord {
   uint64_t size;    // bytes the peer may write
   uint64_t offset;  // from the start of its allocation (IPC maps whole allocations)
   int32_t ipc;      // handle valid (device memory)
-  int32_t host;     // host memory: written directly within one process, as payload words across processes
+  int32_t host;     // host memory: written directly within one process, through `landing` across processes
   int32_t channel;  // this buffer's channel of the transport block
   int32_t pad;
   uint64_t alloc;   // bytes of the device allocation an import would map
+  uint64_t baseline;  // the channel's arrival count when the buffer was created
   hipIpcMemHandle_t handle;
+  char landing[48];   // host memory: the landing segment a peer process writes messages into
 };
 
 // An IPC import maps the exporter's whole allocation, and importing a block
@@ -41,6 +46,12 @@ struct RecvRecord {
 // (profiles/round3/r3t_*, r3u_*): a receive buffer inside such an allocation
 // is refused to a peer process before any import is attempted.
 constexpr uint64_t kMaxImportBytes = uint64_t(1) << 31;
+
+// Most workgroups one device-to-device message's copy kernel takes: a few
+// dozen saturate an xGMI link (a link, not HBM, bounds a peer copy), a copy
+// within one GPU's HBM takes more (the executor's defaults, executor.h).
+constexpr unsigned kSendBlocks = 64;
+constexpr unsigned kSendBlocksLocal = 256;
 
 std::string recordKey(uint64_t inst, int sender, int receiver, uint64_t slot) {
   return strcat_("gloo_amd/xgmi/", inst, "/", sender, "->", receiver, "/", slot);
@@ -53,48 +64,6 @@ bool isDevice(const void* p) {
   const bool dev = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeDevice;
   (void)hipGetLastError();
   return dev;
-}
-
-void bump(void* p) { static_cast<std::atomic<uint64_t>*>(p)->fetch_add(1, std::memory_order_acq_rel); }
-
-// A message for a host receive buffer in another process: its bytes go into
-// the payload record of its arrival number, then the arrival is published.
-// Runs as a stream host function; a record still holding an unconsumed
-// message (kPayloadRing sends ahead of the receiver's waits) is waited for,
-// up to the context timeout, after which the message is dropped and
-// `failed` is set for the sending thread to raise.
-struct PayloadSend {
-  Device* dev;
-  int src, dst, idx;
-  const char* bytes;  // read when the stream reaches this point
-  uint32_t off, len;
-  std::chrono::milliseconds timeout;
-  std::atomic<int>* failed;
-};
-void payloadSend(void* p) {
-  std::unique_ptr<PayloadSend> s(static_cast<PayloadSend*>(p));
-  Device::Channel& ch = s->dev->channel(s->src, s->dst, s->idx);
-  const uint64_t k = ch.count.load(std::memory_order_acquire) + 1;
-  Device::PayloadRecord& rec = s->dev->payloadRecord(s->src, s->dst, s->idx, k);
-  const auto deadline = std::chrono::steady_clock::now() + s->timeout;
-  for (uint64_t i = 0;; i++) {
-    const uint64_t seq = rec.seq.load(std::memory_order_acquire);
-    if (seq == 0 || rec.ack.load(std::memory_order_acquire) == seq) break;
-    if (std::chrono::steady_clock::now() > deadline) {
-      s->failed->store(1, std::memory_order_release);
-      return;
-    }
-    if (i < 4096) {
-      __builtin_ia32_pause();
-    } else {
-      std::this_thread::sleep_for(std::chrono::microseconds(20));
-    }
-  }
-  if (s->len) std::memcpy(rec.payload, s->bytes, s->len);
-  rec.off = s->off;
-  rec.len = s->len;
-  rec.seq.store(k, std::memory_order_release);
-  ch.count.fetch_add(1, std::memory_order_acq_rel);
 }
 
 // Polls `done` with back-off until it holds, `abort` is set (returns false)
@@ -118,18 +87,55 @@ bool pollUntil(F done, const std::atomic<bool>* abort, std::chrono::milliseconds
 }
 
 std::atomic<uint64_t> g_staged{0};
+std::atomic<uint64_t> g_landing{0};
+
+// A named node shared-memory segment of `bytes` (zero-filled, pages on first
+// touch), mapped read-write.
+void* createSegment(const std::string& name, size_t bytes) {
+  const int fd = ::shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+  GLOO_AMD_ENFORCE(fd >= 0, "shm_open(create) failed for ", name);
+  void* m = ::ftruncate(fd, (off_t)bytes) == 0 ? ::mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0)
+                                               : MAP_FAILED;
+  ::close(fd);
+  if (m == MAP_FAILED) {
+    ::shm_unlink(name.c_str());
+    GLOO_AMD_ENFORCE(false, "landing segment of ", bytes, " B: ftruncate/mmap failed");
+  }
+  return m;
+}
+
+// GLOO_AMD_TRANSPORT_HOSTFN=1: publish device-side arrivals from a stream
+// host function instead of the device (the rounds 1-4 mechanism, kept only
+// as the A/B baseline of tools/transport_bench).
+bool hostPublish() {
+  static const bool v = [] {
+    const char* e = std::getenv("GLOO_AMD_TRANSPORT_HOSTFN");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+struct HostPublish {
+  std::atomic<uint64_t>* count;
+  uint64_t value;
+};
+void publishFromHost(void* p) {
+  std::unique_ptr<HostPublish> h(static_cast<HostPublish*>(p));
+  h->count->store(h->value, std::memory_order_release);
+}
 
 class SendBuffer : public Buffer {
  public:
   SendBuffer(Device* dev, int peer, uint64_t slot, void* ptr, size_t size)
-      : Buffer(slot, ptr, size), dev_(dev), peer_(peer) {
+      : Buffer(slot, ptr, size), dev_(dev), peer_(peer), srcDevice_(isDevice(ptr)) {
     dev_->claim(true, peer_, slot_);
     GLOO_AMD_HIP_CHECK(hipEventCreateWithFlags(&sent_, hipEventDisableTiming));
   }
   ~SendBuffer() override {
     (void)hipEventSynchronize(sent_);
     (void)hipEventDestroy(sent_);
-    if (staging_) (void)hipHostFree(staging_);
+    if (ticket_) GLOO_AMD_HIP_RELEASE(hipFree(ticket_));
+    if (landingRegistered_) GLOO_AMD_HIP_RELEASE(hipHostUnregister(landing_));
+    if (landing_) ::munmap(landing_, peerSize_);
     if (opened_) GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(opened_));
     dev_->release(true, peer_, slot_);
   }
@@ -137,44 +143,63 @@ class SendBuffer : public Buffer {
   void send(size_t offset, size_t length, size_t roffset) override {
     Context& ctx = *dev_->context();
     GLOO_AMD_HIP_CHECK(hipSetDevice(ctx.device()));
-    raiseIfFailed();
     resolve();
     GLOO_AMD_ENFORCE(offset + length <= size_, "send of [", offset, ", +", length, ") beyond a ", size_,
                      "-byte send buffer");
     GLOO_AMD_ENFORCE(roffset + length <= peerSize_, "send of ", length, " bytes at ", roffset, " beyond rank ", peer_,
                      "'s ", peerSize_, "-byte receive buffer (slot ", slot_, ")");
+    const uint64_t k = baseline_ + ++sends_;  // this message's arrival number on the channel
     hipStream_t s = dev_->stream();
-    if (payload_) {
-      GLOO_AMD_ENFORCE(length <= kPayloadBytes, "rank ", peer_, "'s receive buffer (slot ", slot_,
-                       ") is host memory of another process: a message carries at most ", kPayloadBytes,
-                       " bytes there, not ", length);
-      const char* src = ptr_ + offset;
-      if (length && isDevice(ptr_)) {  // stage device bytes in pinned memory first, stream-ordered
-        if (!staging_) GLOO_AMD_HIP_ALLOC(hipHostMalloc(reinterpret_cast<void**>(&staging_), kPayloadBytes, 0));
-        GLOO_AMD_HIP_CHECK(hipMemcpyAsync(staging_, src, length, hipMemcpyDeviceToHost, s));
-        src = staging_;
-      }
-      GLOO_AMD_HIP_CHECK(hipLaunchHostFunc(s, payloadSend,
-                                           new PayloadSend{dev_, ctx.rank, peer_, channelIdx_, src, (uint32_t)roffset,
-                                                           (uint32_t)length, ctx.timeout(), &failed_}));
+    const char* src = ptr_ + offset;
+    char* dst = nullptr;
+    if (landing_) {
+      // a host buffer of another process: the message lands in its segment,
+      // described by the record of its arrival number, which must be free
+      Device::MsgRecord& rec = dev_->msgRecord(ctx.rank, peer_, channelIdx_, k);
+      pollUntil(
+          [&] {
+            const uint64_t q = rec.seq.load(std::memory_order_acquire);
+            return q == 0 || rec.ack.load(std::memory_order_acquire) == q;
+          },
+          nullptr, ctx.timeout(),
+          strcat_("waiting for rank ", peer_, " to consume ", kMsgRing, " earlier messages (slot ", slot_, ")"));
+      rec.off = roffset;
+      rec.len = length;
+      rec.seq.store(k, std::memory_order_release);  // read only once the arrival count reaches k
+      dst = landing_ + roffset;
+    } else if (remote_) {
+      dst = remote_ + roffset;
+    }
+    if (!srcDevice_ && !dstDevice_) {
+      // host to host (or a notification from host memory): the sending
+      // thread writes and publishes; nothing of this buffer is on the stream
+      if (length) std::memcpy(dst, src, length);
+      channel_->count.store(k, std::memory_order_release);
+      return;
+    }
+    if (hostPublish()) {
+      // measurement baseline (GLOO_AMD_TRANSPORT_HOSTFN=1): the arrival
+      // published by a stream host function, as rounds 1-4 did
+      if (length) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(dst, src, length, hipMemcpyDefault, s));
+      GLOO_AMD_HIP_CHECK(hipLaunchHostFunc(s, publishFromHost, new HostPublish{&channel_->count, k}));
+    } else if (srcDevice_ && dstDevice_ && length) {
+      // device to device: one copy kernel, the arrival published by its last workgroup
+      checkRc(launchCopySignal(dst, src, length, channelDev_, Seq{k, 0}, ticket_, nullptr,
+                               copySignalGrid(length, sameGpu_ ? kSendBlocksLocal : kSendBlocks), s),
+              "transport copy_signal_kernel");
     } else {
-      if (length) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(remote_ + roffset, ptr_ + offset, length, hipMemcpyDefault, s));
-      // stream-ordered: the arrival is published only once the bytes landed
-      GLOO_AMD_HIP_CHECK(hipLaunchHostFunc(s, bump, &channel_->count));
+      if (length) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(dst, src, length, hipMemcpyDefault, s));
+      // stream-ordered: the arrival is published once the bytes landed
+      GLOO_AMD_HIP_CHECK(launchSignal(channelDev_, Seq{k, 0}, nullptr, s));
     }
     GLOO_AMD_HIP_CHECK(hipEventRecord(sent_, s));
   }
   void waitRecv() override { throw EnforceNotMet("waitRecv on a send buffer"); }
-  void waitSend() override {
-    GLOO_AMD_HIP_CHECK(hipEventSynchronize(sent_));
-    raiseIfFailed();
-  }
+  void waitSend() override { GLOO_AMD_HIP_CHECK(hipEventSynchronize(sent_)); }
 
  private:
-  void raiseIfFailed() {
-    if (failed_.exchange(0, std::memory_order_acq_rel))
-      throw IoException(strcat_("Timed out waiting for rank ", peer_, " to consume ", kPayloadRing,
-                                " earlier messages (slot ", slot_, "); a message was dropped"));
+  static void checkRc(int rc, const char* what) {
+    GLOO_AMD_ENFORCE(rc == GLOO_HIP_OK, what, ": ", gloo_hip_last_error());
   }
 
   // The peer's receive buffer of this slot (published when it was created).
@@ -187,18 +212,33 @@ class SendBuffer : public Buffer {
     std::memcpy(&r, v.data(), sizeof(r));
     peerSize_ = r.size;
     channelIdx_ = r.channel;
+    baseline_ = r.baseline;
     channel_ = &dev_->channel(ctx.rank, peer_, r.channel);
+    sameGpu_ = r.device == ctx.device();
     if (r.size == 0) {
       remote_ = nullptr;  // a notification buffer: arrivals only
     } else if (r.pid == ctx.pid()) {
       remote_ = reinterpret_cast<char*>(r.ptr);
+      dstDevice_ = !r.host;
       if (!r.host && r.device != ctx.device()) {
         hipError_t e = hipDeviceEnablePeerAccess(r.device, 0);
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
         (void)hipGetLastError();
       }
     } else if (r.host) {
-      payload_ = true;  // host memory of another process: payload words
+      // host memory of another process: its landing segment, registered for
+      // the device's copies when this buffer's bytes are device memory
+      r.landing[sizeof(r.landing) - 1] = 0;
+      const int fd = ::shm_open(r.landing, O_RDWR, 0600);
+      GLOO_AMD_ENFORCE(fd >= 0, "shm_open failed for rank ", peer_, "'s landing segment ", r.landing);
+      void* m = ::mmap(nullptr, r.size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+      ::close(fd);
+      GLOO_AMD_ENFORCE(m != MAP_FAILED, "mmap of rank ", peer_, "'s landing segment failed");
+      landing_ = static_cast<char*>(m);
+      if (srcDevice_) {
+        GLOO_AMD_HIP_ALLOC(hipHostRegister(landing_, r.size, hipHostRegisterPortable));
+        landingRegistered_ = true;
+      }
     } else {
       GLOO_AMD_ENFORCE(r.alloc < kMaxImportBytes, "rank ", peer_, "'s receive buffer (slot ", slot_,
                        ") lies in a device allocation of ", r.alloc, " B; HIP IPC imports of 2 GiB and more hang "
@@ -212,6 +252,7 @@ class SendBuffer : public Buffer {
       GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&base, r.handle, hipIpcMemLazyEnablePeerAccess));
       opened_ = base;
       remote_ = static_cast<char*>(base) + r.offset;
+      dstDevice_ = true;
       void* rb = nullptr;
       size_t rs = 0;
       if (hipMemGetAddressRange(&rb, &rs, base) == hipSuccess && rb) {
@@ -222,21 +263,33 @@ class SendBuffer : public Buffer {
         (void)hipGetLastError();
       }
     }
+    if (srcDevice_ || dstDevice_) {
+      channelDev_ = dev_->channelDevicePtr(ctx.rank, peer_, r.channel);
+      if (srcDevice_ && dstDevice_) {
+        GLOO_AMD_HIP_ALLOC(hipMalloc(reinterpret_cast<void**>(&ticket_), sizeof(unsigned)));
+        GLOO_AMD_HIP_CHECK(hipMemset(ticket_, 0, sizeof(unsigned)));
+      }
+    }
     resolved_ = true;
   }
 
   Device* dev_;
   int peer_;
+  const bool srcDevice_;   // this buffer is device memory
+  bool dstDevice_ = false; // the peer's buffer is device memory (its bytes move on the device)
+  bool sameGpu_ = false;   // ... on this rank's own GPU
   bool resolved_ = false;
-  bool payload_ = false;
   char* remote_ = nullptr;
+  char* landing_ = nullptr;
+  bool landingRegistered_ = false;
   void* opened_ = nullptr;
-  char* staging_ = nullptr;
   size_t peerSize_ = 0;
   int channelIdx_ = -1;
+  uint64_t baseline_ = 0, sends_ = 0;
   Device::Channel* channel_ = nullptr;
+  uint64_t* channelDev_ = nullptr;
+  unsigned* ticket_ = nullptr;
   hipEvent_t sent_ = nullptr;
-  std::atomic<int> failed_{0};
 };
 
 class RecvBuffer : public Buffer {
@@ -250,10 +303,10 @@ class RecvBuffer : public Buffer {
     // baseline before the record is published, i.e. before the peer's
     // first send can land (the sender resolves the record first)
     baseline_ = channel_->count.load(std::memory_order_acquire);
-    // payload records an earlier buffer of this channel left unconsumed are
+    // message records an earlier buffer of this channel left unconsumed are
     // released, so the peer's sends here never wait for them
-    for (int i = 0; i < kPayloadRing; i++) {
-      Device::PayloadRecord& rec = dev_->payloadRecord(peer_, ctx.rank, idx_, (uint64_t)i);
+    for (int i = 0; i < kMsgRing; i++) {
+      Device::MsgRecord& rec = dev_->msgRecord(peer_, ctx.rank, idx_, (uint64_t)i);
       rec.ack.store(rec.seq.load(std::memory_order_acquire), std::memory_order_release);
     }
     RecvRecord r;
@@ -263,6 +316,7 @@ class RecvBuffer : public Buffer {
     r.ptr = reinterpret_cast<uint64_t>(ptr_);
     r.size = ptr_ ? size_ : 0;
     r.channel = idx_;
+    r.baseline = baseline_;
     if (ptr_ && size_) {
       if (isDevice(ptr_)) {
         void* base = nullptr;
@@ -276,6 +330,10 @@ class RecvBuffer : public Buffer {
       } else {
         r.host = 1;
         host_ = true;
+        // where a sender in another process writes (pages only once touched)
+        landingName_ = strcat_("/glr_", ctx.pid(), "_", ++g_landing);
+        landing_ = static_cast<char*>(createSegment(landingName_, size_));
+        std::snprintf(r.landing, sizeof(r.landing), "%s", landingName_.c_str());
       }
       (void)hipGetLastError();
     }
@@ -284,6 +342,10 @@ class RecvBuffer : public Buffer {
     ctx.store().set(recordKey(dev_->instance(), peer_, ctx.rank, slot_), blob);
   }
   ~RecvBuffer() override {
+    if (landing_) {
+      ::munmap(landing_, size_);
+      ::shm_unlink(landingName_.c_str());
+    }
     dev_->freeChannel(peer_, idx_);
     dev_->release(false, peer_, slot_);
   }
@@ -296,14 +358,16 @@ class RecvBuffer : public Buffer {
     pollUntil([&] { return (int64_t)(channel_->count.load(std::memory_order_acquire) - target) >= 0; }, nullptr,
               ctx.timeout(), strcat_("waiting for rank ", peer_, " (slot ", slot_, ") on rank ", ctx.rank));
     if (!host_) return;  // device memory: always written in place
-    // A host buffer's sender in another process carries the bytes in the
-    // payload record tagged with this arrival; one in this process wrote
-    // them in place (no record carries this arrival number then).
-    Device::PayloadRecord& rec = dev_->payloadRecord(peer_, ctx.rank, idx_, target);
+    // A host buffer's sender in another process wrote the bytes into the
+    // landing segment and described them in the record of this arrival; one
+    // in this process wrote them in place (no record carries this arrival
+    // number then).
+    Device::MsgRecord& rec = dev_->msgRecord(peer_, ctx.rank, idx_, target);
     if (rec.seq.load(std::memory_order_acquire) != target) return;
-    GLOO_AMD_ENFORCE((size_t)rec.off + rec.len <= size_, "payload of ", rec.len, " B at ", rec.off,
-                     " beyond the ", size_, "-byte receive buffer");
-    if (rec.len) std::memcpy(ptr_ + rec.off, rec.payload, rec.len);
+    const uint64_t off = rec.off, len = rec.len;
+    GLOO_AMD_ENFORCE(off + len <= size_, "message of ", len, " B at ", off, " beyond the ", size_,
+                     "-byte receive buffer");
+    if (len) std::memcpy(ptr_ + off, landing_ + off, len);
     rec.ack.store(target, std::memory_order_release);
   }
 
@@ -314,6 +378,8 @@ class RecvBuffer : public Buffer {
   int idx_ = -1;
   Device::Channel* channel_ = nullptr;
   uint64_t baseline_ = 0, received_ = 0;
+  std::string landingName_;
+  char* landing_ = nullptr;
 };
 
 }  // namespace
@@ -331,7 +397,7 @@ Device::Device(std::shared_ptr<Context> ctx, hipStream_t stream) : ctx_(std::mov
   }
   const size_t P = (size_t)ctx_->size;
   blockBytes_ = 4096 + P * P * kChannels * sizeof(Channel) + P * P * kAnnouncements * sizeof(Announcement) + P * 64 +
-                P * P * kChannels * kPayloadRing * sizeof(PayloadRecord);
+                P * P * kChannels * kMsgRing * sizeof(MsgRecord);
   blockBytes_ = (blockBytes_ + 4095) / 4096 * 4096;
   std::string name;
   if (ctx_->rank == 0) {
@@ -372,6 +438,7 @@ Device::~Device() {
         uint32_t ready = 2;
         if (a.state.compare_exchange_strong(ready, 3) && a.name[0]) ::shm_unlink(a.name);
       }
+    if (blockDev_) GLOO_AMD_HIP_RELEASE(hipHostUnregister(block_));
     ::munmap(block_, blockBytes_);
   }
   ctx_->releaseInstance(inst_);
@@ -416,12 +483,26 @@ std::atomic<uint64_t>& Device::orderCounter(int dst) {
   return *reinterpret_cast<std::atomic<uint64_t>*>(p);
 }
 
-Device::PayloadRecord& Device::payloadRecord(int src, int dst, int idx, uint64_t k) {
+Device::MsgRecord& Device::msgRecord(int src, int dst, int idx, uint64_t k) {
   const size_t P = (size_t)ctx_->size;
   GLOO_AMD_ENFORCE(idx >= 0 && idx < kChannels, "bad channel ", idx);
-  auto* base = reinterpret_cast<PayloadRecord*>(static_cast<char*>(block_) + 4096 + P * P * kChannels * sizeof(Channel) +
-                                                P * P * kAnnouncements * sizeof(Announcement) + P * 64);
-  return base[(((size_t)src * P + (size_t)dst) * kChannels + (size_t)idx) * kPayloadRing + (size_t)(k % kPayloadRing)];
+  auto* base = reinterpret_cast<MsgRecord*>(static_cast<char*>(block_) + 4096 + P * P * kChannels * sizeof(Channel) +
+                                            P * P * kAnnouncements * sizeof(Announcement) + P * 64);
+  return base[(((size_t)src * P + (size_t)dst) * kChannels + (size_t)idx) * kMsgRing + (size_t)(k % kMsgRing)];
+}
+
+uint64_t* Device::channelDevicePtr(int src, int dst, int idx) {
+  {
+    std::lock_guard<std::mutex> lk(m_);
+    if (!blockDev_) {
+      GLOO_AMD_HIP_ALLOC(hipHostRegister(block_, blockBytes_, hipHostRegisterMapped | hipHostRegisterPortable));
+      void* d = nullptr;
+      GLOO_AMD_HIP_CHECK(hipHostGetDevicePointer(&d, block_, 0));
+      blockDev_ = d;
+    }
+  }
+  const size_t off = reinterpret_cast<char*>(&channel(src, dst, idx).count) - static_cast<char*>(block_);
+  return reinterpret_cast<uint64_t*>(static_cast<char*>(blockDev_) + off);
 }
 
 int Device::allocChannel(int src) {

@@ -8,33 +8,42 @@
 //   Pair::createRecvBuffer(slot, ptr, size)   registers memory the peer writes
 //        into: DEVICE memory is exported (HIP IPC across processes, the raw
 //        pointer within one); HOST memory is written directly within one
-//        process, and across processes carried in payload records (at most
-//        kPayloadBytes per message: the reference's notification buffers,
-//        &dummy_ / sizeof(dummy_), gloo/cuda_allreduce_ring_chunked.cc:119-123);
+//        process, and across processes through a LANDING segment of the same
+//        size in node shared memory that the receiver creates with the buffer:
+//        the sender writes a message at its offset there, and the receiver's
+//        waitRecv copies exactly that message's range into the buffer — any
+//        length, as the reference's TCP pair writes any length into a
+//        registered buffer (gloo/transport/tcp/pair.cc:413-426);
 //   Pair::createSendBuffer(slot, ptr, size)   a local buffer; on its first send
 //        it resolves the peer's receive buffer of the same slot;
-//   Buffer::send(offset, length, roffset)     one-sided write: a device copy
-//        (over the direct xGMI link when the peer is another GPU) into the
-//        peer's buffer at roffset, then — stream-ordered, after the bytes
-//        landed — the channel's arrival counter is bumped;
+//   Buffer::send(offset, length, roffset)     one-sided write into the peer's
+//        buffer at roffset, then the channel's arrival counter := the
+//        message's arrival number.  Device bytes move stream-ordered and the
+//        arrival is published FROM THE DEVICE: a device-to-device message is
+//        one copy kernel with the signal fused in (signal.h launchCopySignal;
+//        over the direct xGMI link when the peer is another GPU), any other
+//        device-side copy is followed by the signal kernel — no host callback
+//        and no host round trip per message.  Host-to-host messages are
+//        written and published by the sending thread itself;
 //   Buffer::waitRecv()                        blocks until the next message of
 //        this receive buffer has arrived (bounded by the context timeout ->
 //        IoException, as gloo/transport/tcp/buffer.cc:67-73);
 //   Buffer::waitSend()                        blocks until the last send's copy
 //        out of this buffer has completed.
 // Every receive buffer owns one channel (an arrival counter, plus a ring of
-// kPayloadRing payload records) of the transport block, allocated by the
-// receiver per (sender, slot) and
-// published with its record, so any number of slots may be live — as many
-// as kChannels per (sender, receiver) at once — and Gloo's ever-increasing
-// context->nextSlot() values never collide.  A payload message k (the k-th
-// arrival of its channel) lands in record k % kPayloadRing, tagged with k;
-// the receiver copies it out in the waitRecv that expects arrival k and
-// acknowledges it, and the sender reuses a record only once its last message
-// was acknowledged (waiting, bounded by the context timeout, when
-// kPayloadRing messages are unconsumed).  So a second send before the
-// receiver's wait keeps both messages, as the reference's direct writes do,
-// and a device receive buffer reusing the channel never reads a payload.
+// kMsgRing message records) of the transport block, allocated by the
+// receiver per (sender, slot) and published with its record (with the
+// counter's value at creation, so the sender numbers its messages), so any
+// number of slots may be live — as many as kChannels per (sender, receiver)
+// at once — and Gloo's ever-increasing context->nextSlot() values never
+// collide.  A landed message k (the k-th arrival of its channel) is described
+// by record k % kMsgRing, tagged with k; the receiver copies it out in the
+// waitRecv that expects arrival k and acknowledges it, and the sender reuses a
+// record only once its last message was acknowledged (waiting on the sending
+// thread, bounded by the context timeout, when kMsgRing messages are
+// unconsumed).  So a second send before the receiver's wait keeps both
+// messages, as the reference's direct writes do, and a device receive buffer
+// reusing the channel never reads a record.
 //
 // Unbound buffers (the new-style collectives, gloo/allreduce.cc,
 // gloo/allgather.cc, gloo/reduce.cc): two-sided send / recv matched per
@@ -78,8 +87,7 @@ class Pair;
 
 constexpr int kChannels = 128;       // live receive buffers per (sender, receiver)
 constexpr int kAnnouncements = 128;  // unbound messages in flight per (sender, receiver)
-constexpr size_t kPayloadBytes = 40;
-constexpr int kPayloadRing = 4;       // payload messages in flight per channel
+constexpr int kMsgRing = 16;          // landed messages in flight per channel (host receive buffers)
 
 // One per rank: the transport device over a connected gloo_amd::Context.
 // Construction is collective (every rank, in the same order as its
@@ -106,16 +114,19 @@ class Device {
     uint64_t pad[7];
   };
   static_assert(sizeof(Channel) == 64, "one line per channel");
-  struct PayloadRecord {
-    std::atomic<uint64_t> seq;  // the arrival number of the message it holds (0: never used)
+  struct MsgRecord {
+    std::atomic<uint64_t> seq;  // the arrival number of the message it describes (0: never used)
     std::atomic<uint64_t> ack;  // the arrival number the receiver consumed from it
-    uint32_t off, len;          // the message's place in the receive buffer
-    char payload[kPayloadBytes];
+    uint64_t off, len;          // the message's place in the receive buffer (and its landing segment)
+    uint64_t pad[4];
   };
-  static_assert(sizeof(PayloadRecord) == 64, "one line per record");
+  static_assert(sizeof(MsgRecord) == 64, "one line per record");
   Channel& channel(int src, int dst, int idx);
+  // The channel's arrival counter as a device kernel addresses it (the
+  // transport block registered with HIP on first use).
+  uint64_t* channelDevicePtr(int src, int dst, int idx);
   // The record arrival `k` of channel (src -> dst, idx) uses.
-  PayloadRecord& payloadRecord(int src, int dst, int idx, uint64_t k);
+  MsgRecord& msgRecord(int src, int dst, int idx, uint64_t k);
   int allocChannel(int src);  // receiver side: a free channel of (src -> me)
   void freeChannel(int src, int idx);
 
@@ -148,6 +159,7 @@ class Device {
   std::vector<std::vector<bool>> channelUsed_;  // [src][idx], this rank as receiver
   void* block_ = nullptr;
   size_t blockBytes_ = 0;
+  void* blockDev_ = nullptr;  // block_ as registered with HIP (channelDevicePtr)
 };
 
 class Buffer {

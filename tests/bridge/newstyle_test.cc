@@ -178,27 +178,16 @@ std::string run(const Meta& m, const std::string& dir, bool hipHost) {
 
 }  // namespace
 
-int main(int argc, char** argv) {
-  if (argc < 2) {
-    std::fprintf(stderr, "usage: newstyle_test DIR\n");
-    return 2;
-  }
-  const std::string dir = argv[1];
-  const std::string mode = argc > 2 ? argv[2] : "device";
-  if (mode != "device" && mode != "hip-transport-host") {
-    std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
-    return 2;
-  }
-  const bool hh = mode == "hip-transport-host";
+// One case directory (meta.txt, init.bin, in.bin) -> its out_*.bin files;
+// returns the error ("" on success).
+std::string runDir(const std::string& dir, bool hh, Meta* mo) {
   Meta m;
   {
     std::istringstream s(std::string(readFile(dir + "/meta.txt").data(), readFile(dir + "/meta.txt").size()));
     s >> m.kind >> m.op >> m.dtype >> m.P >> m.nin >> m.nout >> m.n >> m.root >> m.seg;
-    if (!s) {
-      std::fprintf(stderr, "bad meta.txt\n");
-      return 2;
-    }
+    if (!s) return "bad meta.txt";
   }
+  *mo = m;
   std::string err;
   try {
     if (m.dtype == "f32") err = run<float>(m, dir, hh);
@@ -214,7 +203,49 @@ int main(int argc, char** argv) {
   } catch (const std::exception& e) {
     err = e.what();
   }
-  std::printf("%s %s/%s/%s/P%d\n%s\n", err.empty() ? "ok  " : "FAIL", m.kind.c_str(), m.op.c_str(), m.dtype.c_str(),
-              m.P, err.c_str());
-  return err.empty() ? 0 : 1;
+  return err;
+}
+
+// newstyle_test DIR [MODE]            one case
+// newstyle_test --batch LIST [MODE]   every case directory named in LIST (one
+//                                     per line) in this one process; each gets
+//                                     a result.txt ("ok" or "FAIL <why>")
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: newstyle_test DIR [MODE] | --batch LIST [MODE]\n");
+    return 2;
+  }
+  const bool batch = std::string(argv[1]) == "--batch";
+  if (batch && argc < 3) return 2;
+  const std::string mode = argc > (batch ? 3 : 2) ? argv[batch ? 3 : 2] : "device";
+  if (mode != "device" && mode != "hip-transport-host") {
+    std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
+    return 2;
+  }
+  const bool hh = mode == "hip-transport-host";
+  std::vector<std::string> dirs;
+  if (batch) {
+    std::istringstream list(std::string(readFile(argv[2]).data(), readFile(argv[2]).size()));
+    for (std::string line; std::getline(list, line);)
+      if (!line.empty()) dirs.push_back(line);
+  } else {
+    dirs.push_back(argv[1]);
+  }
+  int failed = 0;
+  for (const std::string& dir : dirs) {
+    Meta m;
+    const std::string err = runDir(dir, hh, &m);
+    std::printf("%s %s/%s/%s/P%d\n%s\n", err.empty() ? "ok  " : "FAIL", m.kind.c_str(), m.op.c_str(), m.dtype.c_str(),
+                m.P, err.c_str());
+    std::fflush(stdout);
+    if (batch) {
+      std::FILE* f = std::fopen((dir + "/result.txt").c_str(), "w");
+      if (f) {
+        std::fprintf(f, "%s%s%s\n", err.empty() ? "ok" : "FAIL ", err.c_str(), "");
+        std::fclose(f);
+      }
+    }
+    failed += !err.empty();
+  }
+  return failed ? 1 : 0;
 }

@@ -312,6 +312,21 @@ std::string refHostCase(int P, int count) {
   });
 }
 
+// One rank of a reference host-memory allreduce template, two runs, against
+// the closed form.
+template <typename A>
+void refHostRank(std::shared_ptr<gloo::Context> ctx, int count, int P, const char* name) {
+  std::vector<float> h(count);
+  std::vector<float*> ptrs{h.data()};
+  A a(ctx, ptrs, count);
+  for (int r = 0; r < 2; r++) {
+    fill(h, P, ctx->rank);
+    a.run();
+    const std::string e = checkClosedForm(h, P, r);
+    if (!e.empty()) throw std::runtime_error(std::string(name) + " over processes: " + e);
+  }
+}
+
 std::string connectCase(int P) {
   return spawn(P, 30000, [&](std::shared_ptr<gloo::Context> ctx) {
     for (int i = 0; i < P; i++) {
@@ -538,6 +553,12 @@ int procMain(int rank, int P, const std::string& dir, int count) {
     auto ctx = connectHip(rank, P, 60000, store);
     deviceRank(ctx, count, 2, deviceRingChunked());
     deviceRank(ctx, count, 1, bridgeRingChunked());
+    // the reference's own host-memory templates between processes: their
+    // inboxes are malloc'ed host buffers of chunkBytes_ registered as receive
+    // buffers (gloo/allreduce_ring_chunked.h:44-46,60-61), so every data
+    // message crosses through the receiver's landing segment
+    refHostRank<gloo::AllreduceRingChunked<float>>(ctx, count, P, "AllreduceRingChunked<float>");
+    refHostRank<gloo::AllreduceHalvingDoubling<float>>(ctx, count, P, "AllreduceHalvingDoubling<float>");
     // the reference's own gloo::allreduce on host buffers between processes
     // (unbound buffers staged in node shared memory)
     {

@@ -21,6 +21,8 @@ import uuid
 import numpy as np
 import pytest
 
+import sched_pool
+
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -150,19 +152,19 @@ def test_threads_large_ring_chunked(torch):
 WORKER = r'''
 import os, sys, numpy as np
 sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
-import torch, gloo_amd
+sys.path.insert(0, os.path.join(os.environ["GLOO_AMD_ROOT"], "tests"))
+import gloo_amd, hip_rt
 rank, size = int(sys.argv[1]), int(sys.argv[2])
 store, algo, inp, out = sys.argv[3], sys.argv[4], sys.argv[5], sys.argv[6]
-dev = rank % torch.cuda.device_count()
-torch.cuda.set_device(dev)
+hip_rt.set_device(0)
 x = np.load(inp)[rank]
-buf = torch.from_numpy(x.view(np.uint8).copy()).to(f"cuda:{dev}")
-torch.cuda.synchronize()
-ctx = gloo_amd.Context(rank, size, store, device=dev, timeout_ms=120000)
-a = gloo_amd.Algorithm(ctx, algo, "sum", "f32", [buf.data_ptr()], x.size)
+buf = hip_rt.malloc(x.nbytes)
+hip_rt.h2d(buf, x)
+ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=120000)
+a = gloo_amd.Algorithm(ctx, algo, "sum", "f32", [buf], x.size)
 a.run(); a.run()
 a.close(); ctx.close()
-np.save(out, buf.cpu().numpy().view(np.float32))
+np.save(out, hip_rt.d2h(buf, x))
 '''
 
 
@@ -339,49 +341,64 @@ print("INTERP", a.mode()["interp"])
 
 
 ZERO_COUNT_WORKER = r'''
-import os, sys
+import os, sys, numpy as np
 sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
-import torch, gloo_amd
-rank, size, store, algo = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
-torch.cuda.set_device(0)
-buf = torch.full((4,), float(rank + 1), device="cuda:0")
-ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=30000)
-recv = [0] * size if algo == "reduce_scatter" else None
-a = gloo_amd.Algorithm(ctx, algo, "sum", "f32", [buf.data_ptr()], 0, recv_elems=recv)
-for _ in range(4):  # eager, then enqueued / captured / replayed where graphs apply
+sys.path.insert(0, os.path.join(os.environ["GLOO_AMD_ROOT"], "tests"))
+import gloo_amd, hip_rt
+rank, size, store = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+hip_rt.set_device(0)
+for i, algo in enumerate(sys.argv[4].split(",")):
+    x = np.full(4, float(rank + 1), np.float32)
+    buf = hip_rt.malloc(x.nbytes)
+    hip_rt.h2d(buf, x)
+    ctx = gloo_amd.Context(rank, size, store + f"_{i}", device=0, timeout_ms=30000)
+    recv = [0] * size if algo == "reduce_scatter" else None
+    a = gloo_amd.Algorithm(ctx, algo, "sum", "f32", [buf], 0, recv_elems=recv)
+    for _ in range(4):  # eager, then enqueued / captured / replayed where graphs apply
+        a.run()
+    hip_rt.synchronize()
+    assert (hip_rt.d2h(buf, x) == rank + 1).all()
+    a.close()
+    # and a non-empty collective on the same context afterwards
+    y = np.full(1000, float(rank + 1), np.float32)
+    b = hip_rt.malloc(y.nbytes)
+    hip_rt.h2d(b, y)
+    recv = [1000 // size + (1 if r < 1000 % size else 0) for r in range(size)] if algo == "reduce_scatter" else None
+    a = gloo_amd.Algorithm(ctx, algo, "sum", "f32", [b], 1000, recv_elems=recv)
     a.run()
-torch.cuda.synchronize()
-assert (buf == rank + 1).all(), buf
-a.close()
-# and a non-empty collective on the same context afterwards
-b = torch.full((1000,), float(rank + 1), device="cuda:0")
-recv = [1000 // size + (1 if r < 1000 % size else 0) for r in range(size)] if algo == "reduce_scatter" else None
-a = gloo_amd.Algorithm(ctx, algo, "sum", "f32", [b.data_ptr()], 1000, recv_elems=recv)
-a.run()
-torch.cuda.synchronize()
-want = size * (size + 1) / 2
-got = b[:recv[rank]] if recv else b
-assert (got == want).all(), got
-a.close(); ctx.close()
-print("OK", flush=True)
+    want = size * (size + 1) / 2
+    got = hip_rt.d2h(b, y)
+    got = got[:recv[rank]] if recv else got
+    assert (got == want).all(), got
+    a.close(); ctx.close()
+    hip_rt.free(buf); hip_rt.free(b)
+    print("OK", algo, flush=True)
 '''
 
+ZERO_ALGOS = ["ring_chunked", "halving_doubling", "ring", "reduce_scatter"]
+_zero_runs = {}
 
-@pytest.mark.parametrize("algo", ["ring_chunked", "halving_doubling", "ring", "reduce_scatter"])
+
+@pytest.mark.parametrize("algo", ZERO_ALGOS)
 @pytest.mark.parametrize("P,env", [(2, {}), (3, {"GLOO_AMD_MESH": "0"}), (4, {"GLOO_AMD_GRAPH": "1"})])
 def test_processes_zero_count(torch, algo, P, env):
     """count = 0 (the reference's algorithms accept it: every chunk empty):
     runs complete without a launch fault or a hang, the buffer is untouched,
-    and the context still runs a real collective afterwards."""
-    with tempfile.TemporaryDirectory() as d:
-        w = os.path.join(d, "w.py")
-        open(w, "w").write(ZERO_COUNT_WORKER)
-        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
-        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), algo],
-                                  env=e, stdout=subprocess.PIPE, text=True) for r in range(P)]
-        outs = [p.communicate(timeout=120)[0] for p in procs]
-        assert [p.returncode for p in procs] == [0] * P, outs
-    assert all("OK" in o for o in outs), outs
+    and the context still runs a real collective afterwards.  One set of rank
+    processes per (P, environment) runs every algorithm in turn."""
+    key = (P, tuple(sorted(env.items())))
+    if key not in _zero_runs:
+        with tempfile.TemporaryDirectory() as d:
+            w = os.path.join(d, "w.py")
+            open(w, "w").write(ZERO_COUNT_WORKER)
+            e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
+            procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"),
+                                       ",".join(ZERO_ALGOS)], env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True) for r in range(P)]
+            outs = [p.communicate(timeout=240)[0] for p in procs]
+        _zero_runs[key] = outs
+    outs = _zero_runs[key]
+    assert all(f"OK {algo}\n" in o for o in outs), outs
 
 
 @pytest.mark.parametrize("mode,interp", [("device", "1"), ("device", "0"), ("host", "1")])
@@ -402,28 +419,7 @@ def test_dead_peer_times_out(torch, mode, interp):
     assert ("INTERP True" in outs[0]) == (mode == "device" and interp == "1"), outs[0]
 
 
-GOLDEN_PROC_WORKER = r'''
-import os, sys, numpy as np
-sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
-import torch, gloo_amd
-rank, size, store, case, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
-g = np.load(os.path.join(os.environ["GLOO_AMD_ROOT"], "tests", "golden", "sched_golden.npz"))
-algo, op, dtype = case.split("/")[:3]
-x = g[case + "/in"]
-recv = g[case + "/recv"] if algo == "reduce_scatter" else None
-xr = x[rank] if algo == "reduce_scatter" else x[rank, 0]
-torch.cuda.set_device(0)
-buf = torch.from_numpy(xr.view(np.uint8).copy()).to("cuda:0")
-torch.cuda.synchronize()
-ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=60000)
-a = gloo_amd.Algorithm(ctx, algo, op, dtype, [buf.data_ptr()], xr.size, recv_elems=recv)
-a.run()
-a.close(); ctx.close()
-np.save(out, buf.cpu().numpy().view(xr.dtype))
-'''
-
-
-@pytest.mark.parametrize("case,env", [
+DEVICE_SIGNALLING_CASES = [
     ("halving_doubling/sum/f32/P5/k1/n10007", {}),
     ("halving_doubling/sum/f32/P8/k1/n1000", {}),
     ("ring_chunked/sum/f32/P8/k1/n10007", {}),
@@ -445,28 +441,32 @@ np.save(out, buf.cpu().numpy().view(xr.dtype))
     ("halving_doubling/min/f32/P5/k1/n1000", {"GLOO_AMD_COPY": "memcpy"}),
     ("reduce_scatter/product/f16/P8/n4096", {"GLOO_AMD_COPY": "memcpy"}),
     ("reduce_scatter/sum/f16/P4/n1024", {}),
-])
+]
+for _c, _e in DEVICE_SIGNALLING_CASES:
+    sched_pool.register(_c, _e, 1)
+
+
+def check_pool_golden(golden_sched, case, res, runs):
+    """Every run of every rank equals the reference's output byte for byte."""
+    assert res.err is None, res.err
+    algo = case.split("/")[0]
+    P = len(res.outs)
+    want = golden_sched[case + "/out"]
+    for it in range(runs):
+        if algo == "reduce_scatter":
+            recv = golden_sched[case + "/recv"]
+            assert same_bytes(np.concatenate([res.outs[r][it][:recv[r]] for r in range(P)]), want), it
+        else:
+            for r in range(P):
+                assert same_bytes(res.outs[r][it], want), (r, it)
+
+
+@pytest.mark.parametrize("case,env", DEVICE_SIGNALLING_CASES)
 def test_processes_golden_device_signalling(torch, golden_sched, case, env):
     """Ranks as processes on the box's GPU(s): device-side signalling with the
-    small-step fusion (default) and without it; bytes vs the reference."""
-    algo = case.split("/")[0]
-    P = int(case.split("/")[3][1:])
-    with tempfile.TemporaryDirectory() as d:
-        w = os.path.join(d, "w.py")
-        open(w, "w").write(GOLDEN_PROC_WORKER)
-        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
-        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), case,
-                                   os.path.join(d, f"o{r}.npy")], env=e) for r in range(P)]
-        assert [p.wait(timeout=300) for p in procs] == [0] * P
-        outs = [np.load(os.path.join(d, f"o{r}.npy")) for r in range(P)]
-    want = golden_sched[case + "/out"]
-    if algo == "reduce_scatter":
-        recv = golden_sched[case + "/recv"]
-        got = np.concatenate([outs[r][:recv[r]] for r in range(P)])
-        assert same_bytes(got, want)
-    else:
-        for r in range(P):
-            assert same_bytes(outs[r], want), r
+    small-step fusion (default) and without it; bytes vs the reference.
+    (Rank processes are batched per (P, environment): tests/sched_pool.py.)"""
+    check_pool_golden(golden_sched, case, sched_pool.result(case, env, 1), 1)
 
 
 @pytest.mark.parametrize("case", ["ring_chunked/sum/f32/P3/k2/n1000", "halving_doubling/sum/f32/P3/k3/n500",
@@ -504,35 +504,7 @@ def test_multi_pointer_across_gpus(torch, golden_sched):
         assert same_bytes(b.cpu().numpy(), want)
 
 
-GRAPH_WORKER = r'''
-import os, sys, json, numpy as np
-sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
-import torch, gloo_amd
-rank, size, store, case, out, runs = (int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5],
-                                      int(sys.argv[6]))
-g = np.load(os.path.join(os.environ["GLOO_AMD_ROOT"], "tests", "golden", "sched_golden.npz"))
-algo, op, dtype = case.split("/")[:3]
-x = g[case + "/in"]
-recv = g[case + "/recv"] if algo == "reduce_scatter" else None
-xr = x[rank] if algo == "reduce_scatter" else x[rank, 0]
-torch.cuda.set_device(0)
-src = torch.from_numpy(xr.view(np.uint8).copy()).to("cuda:0")
-buf = torch.empty_like(src)
-ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=60000)
-a = gloo_amd.Algorithm(ctx, algo, op, dtype, [buf.data_ptr()], xr.size, recv_elems=recv)
-modes = []
-for it in range(runs):
-    buf.copy_(src)
-    torch.cuda.synchronize()
-    a.run()
-    modes.append(a.mode())
-    np.save(out + f".{it}.npy", buf.cpu().numpy().view(xr.dtype))
-a.close(); ctx.close()
-print("MODES", json.dumps(modes))
-'''
-
-
-@pytest.mark.parametrize("case,env,graph", [
+GRAPH_REPLAY_CASES = [
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, True),  # fused small steps in the graph
     ("halving_doubling/sum/f32/P8/k1/n1000", {"GLOO_AMD_GRAPH": "1"}, True),
     ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_FUSE_BYTES": "0"}, True),   # auto: unfused steps
@@ -563,41 +535,27 @@ print("MODES", json.dumps(modes))
     ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_GRAPH": "1"}, True),
     ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_COPY": "memcpy"}, True),
     ("reduce_scatter/sum/f32/P5/n100", {"GLOO_AMD_SIGNAL": "host"}, False),
-])
+]
+for _c, _e, _g in GRAPH_REPLAY_CASES:
+    sched_pool.register(_c, _e, 5)
+
+
+@pytest.mark.parametrize("case,env,graph", GRAPH_REPLAY_CASES)
 def test_processes_graph_replay(torch, golden_sched, case, env, graph):
     """hipGraph replay: run 1 is enqueued eagerly, run 2 captures the plan and
     runs 3.. replay it; sequence numbers come from the device run epoch.  The
     buffer is reset to the input before every run, so every run must equal
     the reference's output byte for byte."""
-    algo = case.split("/")[0]
-    P = int(case.split("/")[3][1:])
     runs = 5
-    with tempfile.TemporaryDirectory() as d:
-        w = os.path.join(d, "w.py")
-        open(w, "w").write(GRAPH_WORKER)
-        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
-        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), case,
-                                   os.path.join(d, f"o{r}"), str(runs)], env=e, stdout=subprocess.PIPE, text=True)
-                 for r in range(P)]
-        outs = [p.communicate(timeout=300)[0] for p in procs]
-        assert [p.returncode for p in procs] == [0] * P
-        ys = [[np.load(os.path.join(d, f"o{r}.{it}.npy")) for it in range(runs)] for r in range(P)]
-    want = golden_sched[case + "/out"]
-    for it in range(runs):
-        if algo == "reduce_scatter":
-            recv = golden_sched[case + "/recv"]
-            assert same_bytes(np.concatenate([ys[r][it][:recv[r]] for r in range(P)]), want), it
-        else:
-            for r in range(P):
-                assert same_bytes(ys[r][it], want), (r, it)
-    for r in range(P):
-        modes = json.loads(outs[r].split("MODES", 1)[1])
+    res = sched_pool.result(case, env, runs)
+    check_pool_golden(golden_sched, case, res, runs)
+    for modes in res.modes:
         assert not modes[0]["graph"]
         assert [m["graph"] for m in modes[1:]] == [graph] * (runs - 1), modes
         assert modes[-1]["graph_error"] == "", modes[-1]
 
 
-@pytest.mark.parametrize("case,env,fused", [
+FOLD_SEND_CASES = [(c, dict(e, GLOO_AMD_INTERP="0"), f) for c, e, f in [
     ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, True),      # tree fold, 7 forwards
     ("halving_doubling/sum/f32/P2/k1/n1000", {"GLOO_AMD_GRAPH": "1"}, True),
     ("halving_doubling/min/f32/P5/k1/n1000", {"GLOO_AMD_GRAPH": "1"}, True),       # pairwise temporaries
@@ -616,7 +574,12 @@ def test_processes_graph_replay(torch, golden_sched, case, env, graph):
     # reduce-scatter owners: a fold and its credits (NOTIFY) in one launch
     ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_GRAPH": "1"}, True),
     ("reduce_scatter/max/bf16/P8/n4096", {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_FUSE_BYTES": "0"}, True),
-])
+]]
+for _c, _e, _f in FOLD_SEND_CASES:
+    sched_pool.register(_c, _e, 5)
+
+
+@pytest.mark.parametrize("case,env,fused", FOLD_SEND_CASES)
 def test_processes_fold_send(torch, golden_sched, case, env, fused):
     """Fold + forward: a mesh owner's fold stores its finished range into
     every peer's inbox in the same pass and signals them from its last
@@ -624,30 +587,11 @@ def test_processes_fold_send(torch, golden_sched, case, env, fused):
     (eager, or enqueued / captured / replayed) must each equal the reference's
     output byte for byte; `fused` says whether the mode query must report the
     fused launch (None: not asserted)."""
-    algo = case.split("/")[0]
-    P = int(case.split("/")[3][1:])
     runs = 5
-    with tempfile.TemporaryDirectory() as d:
-        w = os.path.join(d, "w.py")
-        open(w, "w").write(GRAPH_WORKER)
-        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_INTERP="0", **env)
-        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), case,
-                                   os.path.join(d, f"o{r}"), str(runs)], env=e, stdout=subprocess.PIPE, text=True)
-                 for r in range(P)]
-        outs = [p.communicate(timeout=300)[0] for p in procs]
-        assert [p.returncode for p in procs] == [0] * P
-        ys = [[np.load(os.path.join(d, f"o{r}.{it}.npy")) for it in range(runs)] for r in range(P)]
-    want = golden_sched[case + "/out"]
-    for it in range(runs):
-        if algo == "reduce_scatter":
-            recv = golden_sched[case + "/recv"]
-            assert same_bytes(np.concatenate([ys[r][it][:recv[r]] for r in range(P)]), want), it
-        else:
-            for r in range(P):
-                assert same_bytes(ys[r][it], want), (r, it)
+    res = sched_pool.result(case, env, runs)
+    check_pool_golden(golden_sched, case, res, runs)
     last = []
-    for r in range(P):
-        modes = json.loads(outs[r].split("MODES", 1)[1])
+    for modes in res.modes:
         assert not any(m["interp"] for m in modes), modes
         if env.get("GLOO_AMD_GRAPH") == "1":
             assert modes[-1]["graph"], modes[-1]
@@ -658,7 +602,7 @@ def test_processes_fold_send(torch, golden_sched, case, env, fused):
         assert any(last) == fused, last
 
 
-@pytest.mark.parametrize("case,env,interp", [
+INTERP_CASES = [
     ("halving_doubling/sum/f32/P5/k1/n10007", {}, True),
     ("halving_doubling/sum/f32/P8/k1/n1000", {}, True),             # tree fold
     ("halving_doubling/sum/f64/P7/k1/n3001", {}, True),             # pairwise temporaries
@@ -678,36 +622,22 @@ def test_processes_fold_send(torch, golden_sched, case, env, fused):
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_INTERP_BYTES": "1024"}, False),
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, False),
     ("reduce_scatter/sum/f32/P5/n100", {"GLOO_AMD_SIGNAL": "host"}, False),
-])
+]
+for _c, _e, _i in INTERP_CASES:
+    sched_pool.register(_c, _e, 5)
+
+
+@pytest.mark.parametrize("case,env,interp", INTERP_CASES)
 def test_processes_interp(torch, golden_sched, case, env, interp):
     """One-launch plan interpreter: every run() of a small plan is ONE
     one-workgroup kernel walking the resolved step list (waits, sends,
     signals, folds, copies).  Five runs with the buffer reset to the input
     each time, every one byte for byte the reference's output; interp=False
     cases check the knobs and shapes that keep the enqueued path."""
-    algo = case.split("/")[0]
-    P = int(case.split("/")[3][1:])
     runs = 5
-    with tempfile.TemporaryDirectory() as d:
-        w = os.path.join(d, "w.py")
-        open(w, "w").write(GRAPH_WORKER)
-        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
-        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), case,
-                                   os.path.join(d, f"o{r}"), str(runs)], env=e, stdout=subprocess.PIPE, text=True)
-                 for r in range(P)]
-        outs = [p.communicate(timeout=300)[0] for p in procs]
-        assert [p.returncode for p in procs] == [0] * P
-        ys = [[np.load(os.path.join(d, f"o{r}.{it}.npy")) for it in range(runs)] for r in range(P)]
-    want = golden_sched[case + "/out"]
-    for it in range(runs):
-        if algo == "reduce_scatter":
-            recv = golden_sched[case + "/recv"]
-            assert same_bytes(np.concatenate([ys[r][it][:recv[r]] for r in range(P)]), want), it
-        else:
-            for r in range(P):
-                assert same_bytes(ys[r][it], want), (r, it)
-    for r in range(P):
-        modes = json.loads(outs[r].split("MODES", 1)[1])
+    res = sched_pool.result(case, env, runs)
+    check_pool_golden(golden_sched, case, res, runs)
+    for modes in res.modes:
         assert [m["interp"] for m in modes] == [interp] * runs, modes
 
 
@@ -744,7 +674,7 @@ def _expected_slices(case, env):
     return g if g > 1 else 1
 
 
-@pytest.mark.parametrize("case,env", [
+SLICED_CASES = [
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "4096"}),
     ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024"}),
     ("halving_doubling/sum/f64/P7/k1/n3001", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024"}),
@@ -757,36 +687,22 @@ def _expected_slices(case, env):
     ("ring_chunked/product/f32/P3/k1/n777", {"GLOO_AMD_INTERP_SLICE_BYTES": "100"}),   # ragged slices
     ("reduce_scatter/max/bf16/P8/n4096", {"GLOO_AMD_INTERP_SLICE_BYTES": "256"}),
     ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024"}),    # refused: uneven pieces
-])
+]
+for _c, _e in SLICED_CASES:
+    sched_pool.register(_c, _e, 5)
+
+
+@pytest.mark.parametrize("case,env", SLICED_CASES)
 def test_processes_sliced_interp(torch, golden_sched, case, env):
     """Sliced interpreter: every rank runs its plan in several workgroups,
     workgroup g on slice g of every step with its own flag words.  The ranks
     must agree on the slice count the rule predicts (1 where a plan is
     refused), and five back-to-back runs must give the reference's bytes."""
-    algo = case.split("/")[0]
-    P = int(case.split("/")[3][1:])
     want_slices = _expected_slices(case, env)
     runs = 5
-    with tempfile.TemporaryDirectory() as d:
-        w = os.path.join(d, "w.py")
-        open(w, "w").write(GRAPH_WORKER)
-        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
-        procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), case,
-                                   os.path.join(d, f"o{r}"), str(runs)], env=e, stdout=subprocess.PIPE, text=True)
-                 for r in range(P)]
-        outs = [p.communicate(timeout=300)[0] for p in procs]
-        assert [p.returncode for p in procs] == [0] * P
-        ys = [[np.load(os.path.join(d, f"o{r}.{it}.npy")) for it in range(runs)] for r in range(P)]
-    want = golden_sched[case + "/out"]
-    for it in range(runs):
-        if algo == "reduce_scatter":
-            recv = golden_sched[case + "/recv"]
-            assert same_bytes(np.concatenate([ys[r][it][:recv[r]] for r in range(P)]), want), it
-        else:
-            for r in range(P):
-                assert same_bytes(ys[r][it], want), (r, it)
-    for r in range(P):
-        modes = json.loads(outs[r].split("MODES", 1)[1])
+    res = sched_pool.result(case, env, runs)
+    check_pool_golden(golden_sched, case, res, runs)
+    for modes in res.modes:
         assert all(m["interp"] for m in modes), modes
         assert [m["interp_slices"] for m in modes] == [want_slices] * runs, (want_slices, modes)
 

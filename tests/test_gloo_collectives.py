@@ -46,8 +46,56 @@ def test_header_is_gloo_side_only():
         assert "gloo_collectives.h" not in open(os.path.join(ROOT, "gloo_amd", "csrc", f)).read(), f
 
 
+def _meta(src, case):
+    z = np.load(SCHED if src == "sched" else NEWSTYLE)
+    parts = case.split("/")
+    kind = {"allreduce_new": "ring", "bcube": "bcube", "reduce": "reduce"}[parts[0]]
+    op, dtype, P = parts[1], parts[2], int(parts[3][1:])
+    if kind == "reduce":
+        nin, n, root, seg = int(parts[4][1:]), int(parts[5][1:]), int(parts[6][1:]), int(parts[7][1:])
+        nout = 1
+    else:
+        nin, nout, n, seg = int(parts[4][1:]), int(parts[5][1:]), int(parts[6][1:]), int(parts[7][1:])
+        root = 0
+    return z, kind, op, dtype, P, nin, nout, n, root, seg
+
+
+_batches = {}  # mode -> (tempdir, {(src, case): case dir})
+
+
+def _batch(mode):
+    """Every case of `mode` in ONE run of the program (newstyle_test --batch):
+    a process per case cost more than the cases themselves."""
+    if mode not in _batches:
+        root = tempfile.mkdtemp(prefix="gloo_opts_")
+        dirs = {}
+        for i, (src, case) in enumerate(_cases()):
+            z, kind, op, dtype, P, nin, nout, n, rt, seg = _meta(src, case)
+            d = os.path.join(root, f"c{i}")
+            os.makedirs(d)
+            open(os.path.join(d, "meta.txt"), "w").write(f"{kind} {op} {dtype} {P} {nin} {nout} {n} {rt} {seg}\n")
+            z[case + "/init"].tofile(os.path.join(d, "init.bin"))
+            if nin:
+                z[case + "/in"].tofile(os.path.join(d, "in.bin"))
+            dirs[(src, case)] = d
+        lst = os.path.join(root, "list.txt")
+        open(lst, "w").write("\n".join(dirs.values()) + "\n")
+        r = subprocess.run([PROGRAM, "--batch", lst, mode], capture_output=True, text=True, timeout=600)
+        _batches[mode] = (root, dirs, r.stdout[-3000:] + r.stderr[-3000:])
+    return _batches[mode]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _cleanup_batches():
+    yield
+    import shutil
+    for root, _, _ in _batches.values():
+        shutil.rmtree(root, ignore_errors=True)
+    _batches.clear()
+
+
 @pytest.mark.gpu
-@pytest.mark.timeout(120)
+@pytest.mark.timeout(600)
 @pytest.mark.parametrize("mode", ["device", "hip-transport-host"])
 @pytest.mark.parametrize("src,case", _cases())
 def test_gloo_options_golden(src, case, mode):
@@ -60,30 +108,20 @@ def test_gloo_options_golden(src, case, mode):
         pytest.skip("no GPU")
     if not os.path.exists(PROGRAM):
         pytest.skip("oracle/_ref/newstyle_test not built (needs /root/reference at build time)")
-    z = np.load(SCHED if src == "sched" else NEWSTYLE)
-    parts = case.split("/")
-    kind = {"allreduce_new": "ring", "bcube": "bcube", "reduce": "reduce"}[parts[0]]
-    op, dtype, P = parts[1], parts[2], int(parts[3][1:])
+    z, kind, op, dtype, P, nin, nout, n, root, seg = _meta(src, case)
     init = z[case + "/init"]
     want = z[case + "/out"]
-    if kind == "reduce":
-        nin, n, root, seg = int(parts[4][1:]), int(parts[5][1:]), int(parts[6][1:]), int(parts[7][1:])
-        nout = 1
-    else:
-        nin, nout, n, seg = int(parts[4][1:]), int(parts[5][1:]), int(parts[6][1:]), int(parts[7][1:])
-        root = 0
-    with tempfile.TemporaryDirectory() as d:
-        open(os.path.join(d, "meta.txt"), "w").write(f"{kind} {op} {dtype} {P} {nin} {nout} {n} {root} {seg}\n")
-        init.tofile(os.path.join(d, "init.bin"))
-        if nin:
-            z[case + "/in"].tofile(os.path.join(d, "in.bin"))
-        r = subprocess.run([PROGRAM, d, mode], capture_output=True, text=True, timeout=110)
-        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-        for rank in range(P):
-            if kind == "reduce" and rank != root and mode == "device":
-                continue  # the mesh route leaves other scratch there (the reference's algorithm: partials)
-            for call in range(2):
-                got = np.fromfile(os.path.join(d, f"out_{rank}_{call}.bin"), dtype=init.dtype).reshape(nout, n)
-                expect = want[rank] if kind == "reduce" else want
-                for j in range(nout):
-                    assert got[j].view(np.uint8).tobytes() == expect.view(np.uint8).tobytes(), (rank, call, j)
+    _, dirs, log = _batch(mode)
+    d = dirs[(src, case)]
+    res = os.path.join(d, "result.txt")
+    assert os.path.exists(res), "the batch ended before this case: " + log
+    text = open(res).read()
+    assert text.startswith("ok"), text
+    for rank in range(P):
+        if kind == "reduce" and rank != root and mode == "device":
+            continue  # the mesh route leaves other scratch there (the reference's algorithm: partials)
+        for call in range(2):
+            got = np.fromfile(os.path.join(d, f"out_{rank}_{call}.bin"), dtype=init.dtype).reshape(nout, n)
+            expect = want[rank] if kind == "reduce" else want
+            for j in range(nout):
+                assert got[j].view(np.uint8).tobytes() == expect.view(np.uint8).tobytes(), (rank, call, j)

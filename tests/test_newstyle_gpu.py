@@ -140,27 +140,28 @@ def test_reduce_threads_golden(torch, golden_new, case, mesh, monkeypatch):
 WORKER = r'''
 import os, sys, json, numpy as np
 sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
-import torch, gloo_amd
+sys.path.insert(0, os.path.join(os.environ["GLOO_AMD_ROOT"], "tests"))
+import gloo_amd, hip_rt
 rank, size, store, kind, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
 n = int(os.environ.get("GLOO_AMD_TEST_N", "300000"))
-dev = rank % torch.cuda.device_count()
-torch.cuda.set_device(dev)
-ctx = gloo_amd.Context(rank, size, store, device=dev, timeout_ms=60000)
-sets = [(torch.empty(n, device=dev), torch.empty(n, device=dev)) for _ in range(2)]
+hip_rt.set_device(0)
+ctx = gloo_amd.Context(rank, size, store, device=0, timeout_ms=60000)
+sets = [(hip_rt.malloc(4 * n), hip_rt.malloc(4 * n)) for _ in range(2)]
+like = np.empty(n, np.float32)
 res = []
 modes = []
 for it, s in enumerate([0, 0, 0, 1, 1, 0]):
     inp, outp = sets[s]
-    inp.fill_((rank + 1) * (it + 1))
-    outp.fill_(-1)
-    torch.cuda.synchronize()
+    hip_rt.h2d(inp, np.full(n, (rank + 1) * (it + 1), np.float32))
+    hip_rt.h2d(outp, np.full(n, -1, np.float32))
     if kind in ("bcube", "ring"):
-        gloo_amd.allreduce(ctx, [outp.data_ptr()], n, "f32", "sum", inputs=[inp.data_ptr()], algorithm=kind,
+        gloo_amd.allreduce(ctx, [outp], n, "f32", "sum", inputs=[inp], algorithm=kind,
                            max_segment_bytes=128 << 10)
     else:
-        gloo_amd.reduce_to_root(ctx, outp.data_ptr(), n, "f32", it % size, "sum", input=inp.data_ptr(),
+        gloo_amd.reduce_to_root(ctx, outp, n, "f32", it % size, "sum", input=inp,
                                 max_segment_bytes=256 << 10)
-    res.append(outp.cpu().numpy())
+    hip_rt.synchronize()
+    res.append(hip_rt.d2h(outp, like))
     modes.append(ctx.last_mode()["interp_slices"])
 ctx.close()
 np.save(out, np.array(res))

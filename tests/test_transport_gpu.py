@@ -60,7 +60,7 @@ def hp(a):
     return a.ctypes.data
 if case == "reuse":
     # ADVICE r3: a receive buffer on a channel an earlier HOST buffer of a
-    # peer process used must not act on that buffer's payload record
+    # peer process used must not act on that buffer's message record
     if rank == 1:
         h = np.zeros(4, np.uint32)
         rb = t.buffer(0, 1, hp(h), h.nbytes, False)
@@ -96,7 +96,7 @@ if case == "reuse":
         nb.close()
 elif case == "burst":
     # ADVICE r3: sends to a host buffer of another process before the
-    # receiver waits keep every message (more than the payload ring's depth)
+    # receiver waits keep every message
     k = 7
     if rank == 1:
         h = np.zeros(k, np.uint32)
@@ -108,6 +108,62 @@ elif case == "burst":
         rb.close()
     else:
         src = np.arange(100, 100 + k, dtype=np.uint32)
+        sb = t.buffer(1, 1, hp(src), src.nbytes, True)
+        for i in range(k):
+            sb.send(4 * i, 4, 4 * i)
+        sb.wait_send()
+        sb.close()
+elif case == "large_host":
+    # VERDICT r4 #1: a HOST receive buffer of another process takes messages
+    # of any length (the reference's TCP pair writes any length into it,
+    # gloo/transport/tcp/pair.cc:413-426), from host memory (slot 1) and from
+    # device memory (slot 2), at any offset, sent before the receiver waits
+    n1, n2 = (1 << 20) + 17, (2 << 20) + 5
+    w1 = np.zeros(n1, np.uint8)
+    w1[:1 << 20] = np.arange(1 << 20) % 251
+    w1[n1 - 17:] = 200 + np.arange(17)
+    w2 = np.zeros(n2, np.uint8)
+    w2[5:] = (np.arange(2 << 20) * 7) % 253
+    if rank == 1:
+        h1, h2 = np.zeros(n1, np.uint8), np.zeros(n2, np.uint8)
+        r1 = t.buffer(0, 1, hp(h1), n1, False)
+        r2 = t.buffer(0, 2, hp(h2), n2, False)
+        time.sleep(0.5)                                 # the sender runs ahead
+        r1.wait_recv()
+        r1.wait_recv()
+        r2.wait_recv()
+        out["bad"] = [int((h1 != w1).sum()), int((h2 != w2).sum())]
+        r1.close()
+        r2.close()
+    else:
+        hs = np.zeros(n1, np.uint8)
+        hs[:1 << 20] = w1[:1 << 20]
+        hs[n1 - 17:] = w1[n1 - 17:]
+        ds = torch.from_numpy(w2[5:].copy()).to("cuda:0")
+        torch.cuda.synchronize()
+        s1 = t.buffer(1, 1, hp(hs), n1, True)
+        s2 = t.buffer(1, 2, ds.data_ptr(), 2 << 20, True)
+        s1.send(0, 1 << 20, 0)
+        s1.send(n1 - 17, 17, n1 - 17)
+        s2.send(0, 2 << 20, 5)
+        s1.wait_send()
+        s2.wait_send()
+        s1.close()
+        s2.close()
+elif case == "ring_depth":
+    # more sends ahead of the receiver than the channel's record ring holds
+    # (transport.h kMsgRing): the sender waits on its own thread, nothing is lost
+    k = 40
+    if rank == 1:
+        h = np.zeros(k, np.uint32)
+        rb = t.buffer(0, 1, hp(h), h.nbytes, False)
+        time.sleep(1.0)
+        for _ in range(k):
+            rb.wait_recv()
+        out["host"] = h.tolist()
+        rb.close()
+    else:
+        src = np.arange(1000, 1000 + k, dtype=np.uint32)
         sb = t.buffer(1, 1, hp(src), src.nbytes, True)
         for i in range(k):
             sb.send(4 * i, 4, 4 * i)
@@ -172,6 +228,18 @@ def test_transport_channel_reuse_after_host_buffer(tmp_path):
 def test_transport_host_sends_before_wait_all_kept(tmp_path):
     res = run_transport_case(tmp_path, "burst")
     assert res[1]["host"] == list(range(100, 107)), res
+
+
+@pytest.mark.timeout(150)
+def test_transport_host_buffer_any_length_across_processes(tmp_path):
+    res = run_transport_case(tmp_path, "large_host")
+    assert res[1]["bad"] == [0, 0], res
+
+
+@pytest.mark.timeout(150)
+def test_transport_sender_waits_beyond_record_ring(tmp_path):
+    res = run_transport_case(tmp_path, "ring_depth")
+    assert res[1]["host"] == list(range(1000, 1040)), res
 
 
 @pytest.mark.timeout(150)
