@@ -423,6 +423,84 @@ size_t slicedInterpSteps(const Plan& plan, int nin, int nout) {
 // Most workgroups of a sliced launch (<= kMaxSlices).  Ranks that share a
 // GPU each bring this many, and a slice spins until its peer slice runs, so
 // the default keeps 8 ranks on one GPU co-resident.
+// The environment knobs that choose which plan a collective executes
+// (INTEGRATION.md §4).  They are read here and nowhere else; every rank must
+// read them alike, and the "where" exchange carries them with a fingerprint
+// of the plan they produce, so a rank-inconsistent choice is refused on
+// every rank instead of running mismatched step lists.
+struct RouteKnobs {
+  bool mesh = true;      // GLOO_AMD_MESH: derived mesh plans (mesh.cc) where P allows
+  bool ringMesh = true;  // GLOO_AMD_RING_MESH: ring-chunked as its mesh plan
+  bool ringPipe = true;  // GLOO_AMD_RING_PIPE: ring-chunked's ring route pipelined
+  int32_t bits() const { return (mesh ? 1 : 0) | (ringMesh ? 2 : 0) | (ringPipe ? 4 : 0); }
+};
+RouteKnobs routeKnobs() {
+  auto on = [](const char* name) {
+    const char* e = std::getenv(name);
+    return !(e && e[0] == '0');
+  };
+  RouteKnobs k;
+  k.mesh = on("GLOO_AMD_MESH");
+  k.ringMesh = on("GLOO_AMD_RING_MESH");
+  k.ringPipe = on("GLOO_AMD_RING_PIPE");
+  return k;
+}
+std::string knobText(int32_t bits) {
+  return strcat_("GLOO_AMD_MESH=", bits & 1 ? 1 : 0, " GLOO_AMD_RING_MESH=", bits & 2 ? 1 : 0,
+                 " GLOO_AMD_RING_PIPE=", bits & 4 ? 1 : 0);
+}
+
+// The plan `algo` executes as, given the knobs.  A custom op is called as the
+// reference calls its function: two operands at a time on the reference's own
+// routes (the mesh plans fold with reverse / tree association), and its ring
+// keeps the reference's literal two-inbox order.
+int selectPlanAlgo(int algo, int P, bool custom, const RouteKnobs& k) {
+  int planAlgo = algo;
+  const bool mesh = k.mesh && P >= 2 && P <= GLOO_HIP_MAX_SRCS && !custom;
+  // AllreduceRingChunked's result with mesh data movement (plan.cc
+  // planRingChunkedMesh): same bytes, two all-to-all hops over every xGMI
+  // link instead of 2(P-1) hops around the ring.  Halving-doubling,
+  // reduce-scatter and the new-style collectives likewise run as their
+  // derived mesh plans (mesh.cc).
+  if (mesh && algo == GLOO_HIP_ALGO_RING_CHUNKED && k.ringMesh) planAlgo = GLOO_HIP_ALGO_RING_CHUNKED_MESH;
+  if (mesh && (algo == GLOO_HIP_ALGO_HALVING_DOUBLING || algo == GLOO_HIP_ALGO_REDUCE_SCATTER || isNewStyle(algo)))
+    planAlgo = algo | GLOO_HIP_ALGO_MESH;
+  // Ring-chunked on its ring route (the mesh off, or P > 8): three inboxes
+  // per channel, so each round reduces and forwards in one pass (plan.cc
+  // planRingChunkedPipe; the reference's bytes).
+  if (planAlgo == GLOO_HIP_ALGO_RING_CHUNKED && !custom && k.ringPipe) planAlgo = GLOO_HIP_ALGO_RING_CHUNKED_PIPE;
+  return planAlgo;
+}
+
+uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+  const unsigned char* b = static_cast<const unsigned char*>(p);
+  for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 0x100000001b3ull;
+  return h;
+}
+template <typename T>
+uint64_t fnvOf(uint64_t h, const T& v) {
+  return fnv1a(h, &v, sizeof(v));
+}
+// What a rank's peers depend on in its plan: every step that talks to a peer
+// (its kind, peer, slot, length, and the region offset of a SEND or a
+// DECL_RECV), in order.  Local steps may differ between ranks (their pointer
+// counts may), so they are left out.
+uint64_t exchangeHash(const Plan& p) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (const Step& s : p.steps) {
+    const bool talks = s.kind == GLOO_HIP_STEP_SEND || s.kind == GLOO_HIP_STEP_DECL_RECV ||
+                       s.kind == GLOO_HIP_STEP_WAIT_RECV || s.kind == GLOO_HIP_STEP_NOTIFY ||
+                       s.kind == GLOO_HIP_STEP_WAIT_NOTIFY || s.kind == GLOO_HIP_STEP_WAIT_SEND;
+    if (!talks) continue;
+    h = fnvOf(h, s.kind);
+    h = fnvOf(h, s.peer);
+    h = fnvOf(h, s.slot);
+    h = fnvOf(h, s.length);
+    if (s.kind == GLOO_HIP_STEP_SEND || s.kind == GLOO_HIP_STEP_DECL_RECV) h = fnvOf(h, s.dst_off);
+  }
+  return h;
+}
+
 int maxSlices() {
   static const int v = [] {
     const char* e = std::getenv("GLOO_AMD_INTERP_MAX_SLICES");
@@ -747,35 +825,11 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   GLOO_AMD_ENFORCE(!ptrs_.empty(), "need at least one pointer");
   for (void* p : ptrs_) GLOO_AMD_ENFORCE(p != nullptr || count_ == 0, "null device pointer");
   const int me = ctx_->rank, P = ctx_->size;
-  // AllreduceRingChunked's result with mesh data movement (plan.cc
-  // planRingChunkedMesh): same bytes, two all-to-all hops over every xGMI
-  // link instead of 2(P-1) hops around the ring.  Every rank must choose
-  // alike, so the choice depends only on the environment and P.
-  // Halving-doubling and reduce-scatter likewise run as their derived mesh
-  // plans (mesh.cc).  GLOO_AMD_MESH=0 keeps the reference routes;
-  // GLOO_AMD_RING_MESH=0 only ring-chunked's.
-  planAlgo_ = algo_;
-  const char* m = std::getenv("GLOO_AMD_MESH");
-  // a custom op is called as the reference calls its function: two operands
-  // at a time on the reference's own routes (the mesh plans fold with
-  // reverse / tree association)
-  const bool mesh = !(m && m[0] == '0') && P >= 2 && P <= GLOO_HIP_MAX_SRCS && !custom_;
-  if (mesh && algo_ == GLOO_HIP_ALGO_RING_CHUNKED) {
-    const char* rm = std::getenv("GLOO_AMD_RING_MESH");
-    if (!(rm && rm[0] == '0')) planAlgo_ = GLOO_HIP_ALGO_RING_CHUNKED_MESH;
-  }
-  if (mesh && (algo_ == GLOO_HIP_ALGO_HALVING_DOUBLING || algo_ == GLOO_HIP_ALGO_REDUCE_SCATTER ||
-               isNewStyle(algo_)))
-    planAlgo_ = algo_ | GLOO_HIP_ALGO_MESH;
-  // Ring-chunked on its ring route (the mesh off, or P > 8): three inboxes
-  // per channel, so each round reduces and forwards in one pass (plan.cc
-  // planRingChunkedPipe; the reference's bytes).  GLOO_AMD_RING_PIPE=0 keeps
-  // the reference's literal two-inbox order.  A custom op keeps it too: it
-  // is called as the reference calls it, on the reference's steps.
-  if (planAlgo_ == GLOO_HIP_ALGO_RING_CHUNKED && !custom_) {
-    const char* rp = std::getenv("GLOO_AMD_RING_PIPE");
-    if (!(rp && rp[0] == '0')) planAlgo_ = GLOO_HIP_ALGO_RING_CHUNKED_PIPE;
-  }
+  // The executed plan: the algorithm's, or its mesh / pipelined form
+  // (selectPlanAlgo).  Every rank must choose alike; the choice depends only
+  // on the route knobs and P, and the "where" exchange below checks it.
+  const RouteKnobs knobs = routeKnobs();
+  planAlgo_ = selectPlanAlgo(algo_, P, custom_, knobs);
   plan_ = planFor(planAlgo_, me, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_, maxSegmentBytes_,
                   recvElems_);
   GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
@@ -844,27 +898,71 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     return (std::max<size_t>(256, p.arena * es_) + kArenaGranule - 1) / kArenaGranule * kArenaGranule;
   };
   // (pid, device, whether this rank's IPC pool would pass its ceiling with
-  // this executor's slabs)
-  std::vector<std::vector<char>> where;
+  // this executor's slabs, and the plan fingerprint: the route knobs, the
+  // executed plan, the call's shape and the hash of the plan's exchange)
+  struct Where {
+    int32_t pid, device, overCeiling, knobs;
+    int32_t planAlgo, pad;
+    uint64_t call, exchange;
+  };
+  const uint64_t callHash = [&] {
+    uint64_t h = 0xcbf29ce484222325ull;
+    h = fnvOf(h, algo_);
+    h = fnvOf(h, op_);
+    h = fnvOf(h, dtype_);
+    h = fnvOf(h, (uint64_t)count_);
+    h = fnvOf(h, (uint64_t)maxSegmentBytes_);
+    for (int v : recvElems_) h = fnvOf(h, v);
+    return h;
+  }();
+  std::vector<Where> where(P);
   {
-    int32_t hello[3] = {ctx_->pid(), ctx_->device(), ipc::overCeiling(arenaBytesOf(plan_) + (2u << 20)) ? 1 : 0};
-    std::vector<char> blob(sizeof(hello));
-    std::memcpy(blob.data(), hello, sizeof(hello));
-    where = ctx_->allgather(strcat_("inst", inst_, "/where"), blob);
+    Where w{ctx_->pid(), ctx_->device(), ipc::overCeiling(arenaBytesOf(plan_) + (2u << 20)) ? 1 : 0, knobs.bits(),
+            planAlgo_, 0, callHash, exchangeHash(plan_)};
+    std::vector<char> blob(sizeof(w));
+    std::memcpy(blob.data(), &w, sizeof(w));
+    const auto all = ctx_->allgather(strcat_("inst", inst_, "/where"), blob);
+    for (int r = 0; r < P; r++) {
+      GLOO_AMD_ENFORCE(all.at(r).size() == sizeof(Where), "bad record from rank ", r);
+      std::memcpy(&where[r], all[r].data(), sizeof(Where));
+    }
   }
   GLOO_AMD_TRACE_PHASE("where exchanged");
+  // Rank-consistent plans: every rank sees the same
+  // records and reaches the same verdict, so an inconsistent choice raises
+  // on every rank (after the collective release) instead of running step
+  // lists that do not match — a hang at best, writes into regions a peer
+  // never declared at worst.
+  {
+    std::string why;
+    for (int r = 0; r < P && why.empty(); r++) {
+      const Where& w = where[r];
+      if (w.planAlgo != where[0].planAlgo)
+        why = strcat_("rank ", r, " executes plan ", w.planAlgo, " (", knobText(w.knobs), ") but rank 0 executes plan ",
+                      where[0].planAlgo, " (", knobText(where[0].knobs), ")");
+      else if (w.call != where[0].call)
+        why = strcat_("rank ", r, " was called with another algorithm, op, dtype, count, segment size or receive "
+                      "counts than rank 0");
+    }
+    for (int r = 0; r < P && why.empty(); r++) {
+      const Plan pr = r == me ? plan_
+                              : planFor(where[r].planAlgo, r, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
+      if (exchangeHash(pr) != where[r].exchange)
+        why = strcat_("rank ", r, "'s exchange steps differ from the plan every rank derives for it");
+    }
+    if (!why.empty()) {
+      release();
+      GLOO_AMD_ENFORCE(false, "rank-inconsistent collective: ", why, ". The plan-selecting knobs (GLOO_AMD_MESH, "
+                       "GLOO_AMD_RING_MESH, GLOO_AMD_RING_PIPE) and the call's arguments must be equal on every rank");
+    }
+  }
   // The IPC pool's ceiling (ipc.h): when any rank would pass it, every rank
   // closes the mappings no executor holds, and once all have (a peer's
   // slab freed while still mapped breaks the next export over its memory)
   // frees its unused slabs, before any slab of this executor is acquired.
   {
     bool trim = false;
-    for (int r = 0; r < P; r++) {
-      int32_t w[3];
-      GLOO_AMD_ENFORCE(where.at(r).size() == sizeof(w), "bad record from rank ", r);
-      std::memcpy(w, where[r].data(), sizeof(w));
-      trim = trim || w[2] != 0;
-    }
+    for (int r = 0; r < P; r++) trim = trim || where[r].overCeiling != 0;
     if (trim) {
       GLOO_AMD_TRACE_PHASE("trimming the IPC pool");
       ipc::closeUnusedImports();
@@ -880,11 +978,8 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   // ranks together rather than some waiting at the next exchange.
   {
     bool anyCross = false;
-    for (int r = 0; r < P; r++) {
-      int32_t w[3];
-      std::memcpy(w, where.at(r).data(), sizeof(w));
-      if (w[0] != ctx_->pid()) anyCross = true;
-    }
+    for (int r = 0; r < P; r++)
+      if (where[r].pid != ctx_->pid()) anyCross = true;
     const char* hm = std::getenv("GLOO_AMD_ARENA");
     const bool host = workspace == GLOO_HIP_WORKSPACE_HOST || (hm && std::string(hm) == "host");
     if (anyCross && !host)
@@ -898,14 +993,12 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   peers_.resize(P);
   bool sharesDeviceInProcess = false, crossSender = false;
   for (int peer : planPeers) {
-    const std::vector<char>& v = where.at(peer);
-    int32_t w[3];
-    std::memcpy(w, v.data(), sizeof(w));
-    peers_[peer].pid = w[0];
-    peers_[peer].device = w[1];
-    if (w[0] == ctx_->pid() && w[1] == ctx_->device()) sharesDeviceInProcess = true;
-    if (recvPeers.count(peer) && (w[1] != ctx_->device() || w[0] != ctx_->pid())) crossSender = true;
-    if (w[0] != ctx_->pid()) crossProcess_ = true;
+    const Where& w = where.at(peer);
+    peers_[peer].pid = w.pid;
+    peers_[peer].device = w.device;
+    if (w.pid == ctx_->pid() && w.device == ctx_->device()) sharesDeviceInProcess = true;
+    if (recvPeers.count(peer) && (w.device != ctx_->device() || w.pid != ctx_->pid())) crossSender = true;
+    if (w.pid != ctx_->pid()) crossProcess_ = true;
   }
   const char* sig = std::getenv("GLOO_AMD_SIGNAL");
   const std::string sigMode = sig ? sig : "auto";
