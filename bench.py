@@ -511,15 +511,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         per_gpu = [g["reduce_b"] / g["reduce_s"] / GIB for g in gathered if g["reduce_s"] > 0]
         fused = all(g["stamp_fused"] for g in gathered)
         busbw = 2 * (world - 1) / world * n * 4 / t
-        links = {}
-        if link.get("bytes_per_s"):
-            B = link["bytes_per_s"]
-            # ring: every byte crosses one link per hop, 2(P-1) hops of S/P;
-            # mesh: each link carries S/P per phase, two phases, links at once
-            links = {"busbw_frac_of_link": round(busbw / B, 4),
-                     "ring_link_bound_ms": round(2 * (world - 1) / world * n * 4 / B * 1e3, 3),
-                     "mesh_link_bound_ms": round(2 * n * 4 / world / B * 1e3, 3),
-                     "frac_of_mesh_link_bound": round(2 * n * 4 / world / B / t, 4)}
+        links = link_bounds(world, n * 4, t, link["figures"])
         return {"plan": "mesh" if mesh == "1" and world <= 8 else "ring", "copy_engine": engine,
                 "workspace": workspace, "graph": all(g["graph"] for g in gathered),
                 **({"env": extra_env} if extra_env else {}),
@@ -546,12 +538,10 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                           "bit-exact; after the last run every rank's 256 MiB digest equal"}
 
     ngpu = torch.cuda.device_count()
-    # B_link for the link-bound fractions: one peer copy GPU 0 -> GPU 1 over
-    # its direct xGMI link, measured by rank 0 while the others wait
-    link = one_link_bandwidth(torch, dist, rank, n * 4) if ngpu >= 2 and ngpu >= world else \
-        {"bytes_per_s": None, "why": f"{world} ranks on {ngpu} GPU(s): no link to measure"}
-    partial["link"] = {k: (round(v / 1e9, 2) if k == "bytes_per_s" and v else v) for k, v in link.items()}
-    partial["link"]["unit"] = "GB/s (bytes_per_s / 1e9)"
+    # the link figures the ring / mesh bounds use (link_figures): measured by
+    # rank 0 over its direct xGMI links, null with the reason on one GPU
+    link = link_figures(torch, dist, rank, world, n * 4)
+    partial["link"] = link
     # default: the mesh plan (batched sends = one multi-destination copy kernel)
     ring = ring_once("auto")
     partial["config"] = "allreduce_ring_chunked fp32 sum, %d ranks, %d MiB/rank" % (world, args.allreduce_mib)
@@ -794,34 +784,167 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     return dict(partial)
 
 
-def one_link_bandwidth(torch, dist, rank, nbytes):
-    """One-peer copy GPU 0 -> GPU 1 (hipMemcpyPeerAsync over the direct xGMI
-    link), best of 5 timed with events on GPU 0, by rank 0 alone; every rank
-    joins the barriers.  Returns {"bytes_per_s", "how"}."""
+# The link figures the xGMI bounds are set from: the
+# product's own copy kernel (64 and 256 workgroups per copy) and the runtime's
+# peer copy, one peer one direction, one peer both directions at once, and
+# all P-1 peers at once from one GPU (the mesh send pattern, one
+# multi-destination launch) — SURVEY 8(e); gloo/benchmark/runner.cc:497-506.
+LINK_FIGURES = ("kernel64_one_peer_one_dir", "kernel256_one_peer_one_dir", "memcpy_one_peer_one_dir",
+                "kernel64_one_peer_both_dirs", "memcpy_one_peer_both_dirs",
+                "kernel64_all_peers_one_gpu", "memcpy_all_peers_one_gpu")
+# which figure bounds which route: a ring hop is one link in one direction
+# (the copy kernel: the product's eager SEND engine); a mesh phase sends to
+# every peer at once (one multi-destination copy kernel launch)
+RING_BOUND_FIGURE = "kernel64_one_peer_one_dir"
+MESH_BOUND_FIGURE = "kernel64_all_peers_one_gpu"
+
+
+def link_bounds(world, nbytes, t, figures):
+    """The link-bound fields of a config-3 line: ring and mesh lower bounds
+    on the allreduce time of `nbytes` per rank over `world` ranks, from the
+    named figures (GB/s per link), and the measured time `t` (s) against
+    them.  A missing figure gives null bounds with the reason.
+      ring: 2(P-1) hops of S/P, each over one link: 2(P-1)/P * S / B_ring
+      mesh: two phases, each moving S/P over every link at once: 2 S/P / B_mesh
+      busbw = 2(P-1)/P * S / t (the nccl-tests bus bandwidth)"""
+    busbw = 2 * (world - 1) / world * nbytes / t
+    out = {}
+    for route, name, traffic in (("ring", RING_BOUND_FIGURE, 2 * (world - 1) / world * nbytes),
+                                 ("mesh", MESH_BOUND_FIGURE, 2 * nbytes / world)):
+        f = figures.get(name) or {}
+        B = f.get("GBps_per_link") or f.get("GBps")
+        out[route + "_bound_figure"] = name
+        if B:
+            out[route + "_link_bound_ms"] = round(traffic / (B * 1e9) * 1e3, 3)
+            out["frac_of_%s_link_bound" % route] = round(traffic / (B * 1e9) / t, 4)
+        else:
+            out[route + "_link_bound_ms"] = None
+            out["frac_of_%s_link_bound" % route] = None
+            out[route + "_bound_why"] = f.get("why", "figure not measured")
+    ring = figures.get(RING_BOUND_FIGURE) or {}
+    out["busbw_frac_of_link"] = round(busbw / (ring["GBps"] * 1e9), 4) if ring.get("GBps") else None
+    return out
+
+
+def link_figures(torch, dist, rank, world, nbytes):
+    """LINK_FIGURES measured by rank 0 alone on the GPUs it sees (every rank
+    joins the barriers), best of 5 timed with HIP events; each figure is
+    {"GBps"...} or {"GBps": None, "why": ...}."""
+    ngpu = torch.cuda.device_count()
     res = [None]
     dist.barrier()
     if rank == 0:
-        try:
-            src = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
-            dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda:1")
-            best = None
-            for _ in range(6):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                dst.copy_(src, non_blocking=True)
-                e1.record()
-                torch.cuda.synchronize("cuda:0")
-                torch.cuda.synchronize("cuda:1")
-                ms = e0.elapsed_time(e1)
-                best = ms if best is None else min(best, ms)
-            res[0] = {"bytes_per_s": nbytes / (best / 1e3), "bytes": nbytes,
-                      "how": "torch copy cuda:0 -> cuda:1 (one xGMI link), best of 6, events on GPU 0"}
-            del src, dst
-            torch.cuda.empty_cache()
-        except Exception as e:  # noqa: BLE001
-            res[0] = {"bytes_per_s": None, "why": repr(e)}
+        figs = {}
+        if ngpu < 2:
+            why = f"{world} ranks on {ngpu} GPU(s): no xGMI link to measure"
+            figs = {k: {"GBps": None, "why": why} for k in LINK_FIGURES}
+        else:
+            try:
+                figs = _measure_links(torch, min(ngpu, max(2, world)), nbytes)
+            except Exception as e:  # noqa: BLE001
+                figs = {k: {"GBps": None, "why": repr(e)} for k in LINK_FIGURES}
+        res[0] = {"unit": "GB/s (1e9 B/s)", "bytes": nbytes, "figures": figs,
+                  "ring_bound_figure": RING_BOUND_FIGURE, "mesh_bound_figure": MESH_BOUND_FIGURE}
     dist.broadcast_object_list(res, src=0)
     return res[0]
+
+
+def _measure_links(torch, P, nbytes):
+    import gloo_amd as hip
+    rt = ctypes.CDLL("libamdhip64.so.7")
+    for a in range(P):  # peer access both ways between GPU 0 and every peer
+        for b in ((range(1, P)) if a == 0 else (0,)):
+            rt.hipSetDevice(a)
+            rt.hipDeviceEnablePeerAccess(b, 0)
+    rt.hipGetLastError()
+    rt.hipSetDevice(0)
+    dev = [torch.device("cuda", g) for g in range(P)]
+    src0 = torch.empty(nbytes, dtype=torch.uint8, device=dev[0])
+    dst = [None] + [torch.empty(nbytes, dtype=torch.uint8, device=dev[g]) for g in range(1, P)]
+    src1 = torch.empty(nbytes, dtype=torch.uint8, device=dev[1])
+    dst0 = torch.empty(nbytes, dtype=torch.uint8, device=dev[0])
+    s0 = torch.cuda.Stream(dev[0])
+    s1 = torch.cuda.Stream(dev[1])
+    peers = [torch.cuda.Stream(dev[0]) for _ in range(1, P)]
+
+    def timed(stream, fn, reps=6):
+        best = None
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        return best / 1e3
+
+    figs = {}
+    for blocks in (64, 256):
+        t = timed(s0, lambda: hip.copy_kernel(dst[1].data_ptr(), src0.data_ptr(), nbytes, blocks, s0.cuda_stream))
+        figs[f"kernel{blocks}_one_peer_one_dir"] = {"GBps": round(nbytes / t / 1e9, 2)}
+
+    def memcpy_one():
+        with torch.cuda.stream(s0):
+            dst[1].copy_(src0, non_blocking=True)
+    figs["memcpy_one_peer_one_dir"] = {"GBps": round(nbytes / timed(s0, memcpy_one) / 1e9, 2)}
+
+    def both(kernel):
+        # GPU 0 -> 1 on GPU 0's stream, GPU 1 -> 0 on GPU 1's, started together
+        best = None
+        for _ in range(6):
+            torch.cuda.synchronize(dev[0])
+            torch.cuda.synchronize(dev[1])
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(2)]
+            evs[0][0].record(s0)
+            evs[1][0].record(s1)
+            if kernel:
+                hip.copy_kernel(dst[1].data_ptr(), src0.data_ptr(), nbytes, 64, s0.cuda_stream)
+                hip.copy_kernel(dst0.data_ptr(), src1.data_ptr(), nbytes, 64, s1.cuda_stream)
+            else:
+                with torch.cuda.stream(s0):
+                    dst[1].copy_(src0, non_blocking=True)
+                with torch.cuda.stream(s1):
+                    dst0.copy_(src1, non_blocking=True)
+            evs[0][1].record(s0)
+            evs[1][1].record(s1)
+            evs[0][1].synchronize()
+            evs[1][1].synchronize()
+            ms = max(evs[0][0].elapsed_time(evs[0][1]), evs[1][0].elapsed_time(evs[1][1]))
+            best = ms if best is None else min(best, ms)
+        t = best / 1e3
+        return {"GBps": round(nbytes / t / 1e9, 2), "GBps_total": round(2 * nbytes / t / 1e9, 2),
+                "how": "per direction, both directions at once (the slower one's time)"}
+    figs["kernel64_one_peer_both_dirs"] = both(True)
+    figs["memcpy_one_peer_both_dirs"] = both(False)
+
+    k = P - 1
+    t = timed(s0, lambda: hip.copy_kernel_multi([d.data_ptr() for d in dst[1:]], [src0.data_ptr()] * k, nbytes, 64,
+                                                s0.cuda_stream))
+    figs["kernel64_all_peers_one_gpu"] = {"peers": k, "GBps_per_link": round(nbytes / t / 1e9, 2),
+                                          "GBps_total": round(k * nbytes / t / 1e9, 2),
+                                          "how": "one multi-destination copy launch, 64 workgroups per peer"}
+
+    def memcpy_all():
+        fork = torch.cuda.Event()
+        fork.record(s0)
+        joins = []
+        for j, st in enumerate(peers):
+            st.wait_event(fork)
+            with torch.cuda.stream(st):
+                dst[j + 1].copy_(src0, non_blocking=True)
+            e = torch.cuda.Event()
+            e.record(st)
+            joins.append(e)
+        for e in joins:
+            s0.wait_event(e)
+    t = timed(s0, memcpy_all)
+    figs["memcpy_all_peers_one_gpu"] = {"peers": k, "GBps_per_link": round(nbytes / t / 1e9, 2),
+                                        "GBps_total": round(k * nbytes / t / 1e9, 2),
+                                        "how": "one peer copy per stream, forked and joined on GPU 0"}
+    del src0, dst, src1, dst0
+    torch.cuda.empty_cache()
+    return figs
 
 
 class HipEvent:

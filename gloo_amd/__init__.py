@@ -51,7 +51,7 @@ OP_NAMES = {"sum": ReductionType.SUM, "product": ReductionType.PRODUCT,
 EXPORTED = ("gloo_hip_reduce", "gloo_hip_reduce3", "gloo_hip_reduce_multi",
             "gloo_hip_dtype_size", "gloo_hip_last_error", "gloo_hip_version",
             "gloo_hip_set_variant", "gloo_hip_plan", "gloo_hip_reduce_staged", "gloo_hip_register_op",
-            "gloo_hip_copy_kernel")
+            "gloo_hip_copy_kernel", "gloo_hip_copy_kernel_multi")
 
 
 class GlooHipError(RuntimeError):
@@ -82,6 +82,8 @@ def _load():
     L.gloo_hip_reduce_staged.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, sz, vp, vp, sz, vp]
     L.gloo_hip_register_op.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int)]
     L.gloo_hip_copy_kernel.argtypes = [vp, vp, sz, ctypes.c_uint, vp]
+    L.gloo_hip_copy_kernel_multi.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz), ctypes.c_int,
+                                             ctypes.c_uint, vp]
     return L
 
 
@@ -147,6 +149,16 @@ def register_op(fn_ptr, user=None):
 def copy_kernel(dst, src, nbytes, blocks=0, stream=0):
     """gloo_hip_copy_kernel: the SEND steps' kernel copy engine."""
     _check(lib.gloo_hip_copy_kernel(dst, src, nbytes, blocks, stream or None))
+
+
+def copy_kernel_multi(dsts, srcs, nbytes, blocks=0, stream=0):
+    """gloo_hip_copy_kernel_multi: several copies in one launch (a mesh
+    schedule's sends to every peer); nbytes is one size or one per copy."""
+    n = len(dsts)
+    sizes = list(nbytes) if hasattr(nbytes, "__len__") else [nbytes] * n
+    vp = ctypes.c_void_p
+    _check(lib.gloo_hip_copy_kernel_multi((vp * n)(*dsts), (vp * n)(*srcs), (ctypes.c_size_t * n)(*sizes), n,
+                                          blocks, stream or None))
 
 
 def set_variant(v):

@@ -1555,6 +1555,21 @@ int gloo_hip_copy_kernel(void* dst, const void* src, size_t bytes, unsigned bloc
   return launchCopySignalMulti(&d, 1, nullptr, static_cast<hipStream_t>(stream));
 }
 
+int gloo_hip_copy_kernel_multi(void* const* dsts, const void* const* srcs, const size_t* bytes, int n, unsigned blocks,
+                               gloo_hip_stream_t stream) {
+  if (n < 1 || n > kMaxCopies) return set_error(GLOO_HIP_EINVAL_ARG, "copy list size out of range");
+  if (!dsts || !srcs || !bytes) return set_error(GLOO_HIP_EINVAL_PTR, "null argument");
+  CopyDesc d[kMaxCopies];
+  int m = 0;
+  for (int j = 0; j < n; j++) {
+    if (bytes[j] == 0) continue;
+    if (!dsts[j] || !srcs[j]) return set_error(GLOO_HIP_EINVAL_PTR, "null buffer pointer");
+    d[m++] = CopyDesc{dsts[j], srcs[j], bytes[j], nullptr, Seq{}, nullptr, copySignalGrid(bytes[j], blocks ? blocks : 64u)};
+  }
+  if (m == 0) return GLOO_HIP_OK;
+  return launchCopySignalMulti(d, m, nullptr, static_cast<hipStream_t>(stream));
+}
+
 int gloo_hip_register_op(gloo_hip_custom_fn fn, void* user, int* op_out) {
   if (!fn || !op_out) return set_error(GLOO_HIP_EINVAL_ARG, "null argument");
   std::lock_guard<std::mutex> lk(customMutex());

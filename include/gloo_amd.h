@@ -142,6 +142,12 @@ int gloo_hip_register_op(gloo_hip_custom_fn fn, void* user, int* op_out);
  * DESIGN.md §4) and callers that want a copy with no DMA-engine dependence. */
 int gloo_hip_copy_kernel(void* dst, const void* src, size_t bytes, unsigned blocks, gloo_hip_stream_t stream);
 
+/* (new, measurement) Up to 8 such copies in ONE launch, all in flight together
+ * — the mesh schedules' sends to every peer (one xGMI link each): copy j gets
+ * at most `blocks` workgroups (0: 64, the executor's per-peer default). */
+int gloo_hip_copy_kernel_multi(void* const* dsts, const void* const* srcs, const size_t* bytes, int n,
+                               unsigned blocks, gloo_hip_stream_t stream);
+
 /* Size in bytes of one element of `dtype`, or 0 when dtype is unknown. */
 size_t gloo_hip_dtype_size(int dtype);
 
