@@ -267,7 +267,11 @@ class SendBuffer : public Buffer {
       channelDev_ = dev_->channelDevicePtr(ctx.rank, peer_, r.channel);
       if (srcDevice_ && dstDevice_) {
         GLOO_AMD_HIP_ALLOC(hipMalloc(reinterpret_cast<void**>(&ticket_), sizeof(unsigned)));
-        GLOO_AMD_HIP_CHECK(hipMemset(ticket_, 0, sizeof(unsigned)));
+        // zeroed on the transport's stream, ahead of the first copy kernel: a
+        // plain hipMemset goes to the null stream, which a non-blocking
+        // stream does not wait for (a late zero lost a ticket and the
+        // arrival with it: transport_test device_ring_chunked/P5, r5b)
+        GLOO_AMD_HIP_CHECK(hipMemsetAsync(ticket_, 0, sizeof(unsigned), dev_->stream()));
       }
     }
     resolved_ = true;

@@ -61,3 +61,10 @@ def d2h(src, like):
 
 def synchronize():
     check(lib().hipDeviceSynchronize(), "hipDeviceSynchronize")
+
+
+def mem_info():
+    """(free, total) bytes of the current device."""
+    f, t = ctypes.c_size_t(), ctypes.c_size_t()
+    check(lib().hipMemGetInfo(ctypes.byref(f), ctypes.byref(t)), "hipMemGetInfo")
+    return f.value, t.value

@@ -1008,7 +1008,10 @@ try:
     print("NO-ERROR", flush=True)
 except gloo_amd.GlooHipError as e:
     print("RAISED", round(time.time() - t0, 2), str(e)[:400], flush=True)
-# the context still runs a consistent collective afterwards
+# the context still runs a consistent collective afterwards (the knobs
+# made equal: the library reads them at construction, putenv reaches it)
+for k in ("GLOO_AMD_MESH", "GLOO_AMD_RING_MESH", "GLOO_AMD_RING_PIPE"):
+    os.environ.pop(k, None)
 x = np.full(1000, rank + 1, np.float32)
 hip_rt.h2d(buf, x)
 a = gloo_amd.Algorithm(ctx, "ring_chunked", "sum", "f32", [buf], 1000)

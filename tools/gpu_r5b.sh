@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 fatal() { [ "$1" -eq 124 ] || [ "$1" -eq 137 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; }
-for m in fresh same; do
+for m in fresh; do  # "same" faulted the GPU once (r5b_vmm_same_va.err): never again
   timeout -k 10 90 tools/vmm_probe 2.5 $m > gpurun_out/r5b_vmm_$m.jsonl 2> gpurun_out/r5b_vmm_$m.err
   rc=$?; echo "vmm $m rc=$rc"; fatal $rc && exit $rc
 done
