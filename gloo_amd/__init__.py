@@ -343,16 +343,16 @@ class TransportBuffer:
 
 
 def ipc_stats():
-    """This process's IPC slab pool (gloo_amd/include/gloo_amd/ipc.h): slabs
-    exported and their bytes, slabs free for reuse, peer slabs mapped,
-    hipIpcOpenMemHandle calls made; trims, bytes they freed, mappings they
-    closed, retired addresses, allocations parked at one, and the ceiling
+    """This process's pool of cross-process slabs (gloo_amd/include/gloo_amd/ipc.h):
+    slabs exported and their bytes, slabs free for reuse, peer slabs mapped,
+    imports made; trims, bytes they released, mappings they closed, virtual
+    ranges retired (never mapped again) and their bytes, and the ceiling
     (GLOO_AMD_IPC_POOL_MAX)."""
     out = (ctypes.c_uint64 * 11)()
     _check(lib.gloo_hip_ipc_stats_ex(out, 11))
     return {"slabs": out[0], "slab_bytes": out[1], "free": out[2], "peer_slabs_mapped": out[3],
             "ipc_opens": out[4], "trims": out[5], "trimmed_bytes": out[6], "mappings_closed": out[7],
-            "retired_addresses": out[8], "parked_allocations": out[9], "pool_max_bytes": out[10]}
+            "retired_ranges": out[8], "retired_bytes": out[9], "pool_max_bytes": out[10]}
 
 
 def ipc_trim(ctx=None):
@@ -493,8 +493,7 @@ class AllreduceOptions(ctypes.Structure):
 
 
 lib.gloo_hip_allreduce.argtypes = [ctypes.c_void_p, ctypes.POINTER(AllreduceOptions)]
-EXPORTED = EXPORTED + ("gloo_hip_allreduce", "gloo_hip_plan_ex", "gloo_hip_arena_slabs",
-                       "gloo_hip_interp_batches")
+EXPORTED = EXPORTED + ("gloo_hip_allreduce", "gloo_hip_plan_ex", "gloo_hip_interp_batches")
 
 
 ALLREDUCE_ALGORITHMS = {"ring": 1, "bcube": 2}  # AllreduceOptions::Algorithm (gloo/allreduce.h:38-42)

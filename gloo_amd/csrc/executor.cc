@@ -30,30 +30,18 @@ namespace gloo_amd {
 
 namespace {
 
-// A cross-process inbox arena larger than kSegMax is split into slabs.
-// Importing a block of 2^31 bytes or more hangs in hipIpcOpenMemHandle on
-// ROCm 7 / MI355X (profiles/round3/r3t_*, r3u_*), and the pool's size classes
-// above 1 GiB are multiples of 256 MiB (ipc.cc), so 1.75 GiB is the largest
-// class an import may map.  Every range a step or a peer's message touches
-// lies inside one slab (arenaSegments), so pointers into the arena are
-// resolved per range and no kernel ever sees a slab boundary.
-constexpr int kMaxArenaSegs = 16;
-constexpr size_t kSegMax = size_t(7) << 28;     // 1.75 GiB
-constexpr size_t kSegTarget = size_t(1) << 30;  // accesses are packed into slabs of about 1 GiB
-constexpr size_t kSegAlign = 256;               // a logical offset keeps its residue mod 256 B in its slab
-
 struct ArenaRecord {
   int32_t pid;
   int32_t device;
   uint64_t ptr;
   uint64_t bytes;
-  hipIpcMemHandle_t handle;  // DEVICE workspace
+  uint64_t slabId;           // DEVICE workspace shared with other processes: the pool slab (ipc.h)
   int32_t host;              // HOST workspace: the arena is the shm segment `shm`
   char shm[60];
   int32_t deviceSignal;      // this rank signals with stream-ordered kernels
   int32_t hasMailbox;        // ... into device-resident mailboxes
   uint64_t mailboxPtr;
-  hipIpcMemHandle_t mailboxHandle;
+  uint64_t mailboxSlabId;
   int32_t interpSlices;      // slices this rank could run its plan in (0: no sliced interpreter)
   uint64_t nonce;            // written at the start of a DEVICE arena: the importer checks its mapping
   uint64_t mailboxNonce;     // written behind the mailbox's counters: likewise
@@ -61,28 +49,11 @@ struct ArenaRecord {
   uint64_t mailboxBytes;
   uint64_t slabBytes;        // size class of the arena's pool slab (ipc.h): what an import maps
   uint64_t mailboxSlabBytes; // likewise for the mailbox's slab
-  // > 0: the arena is nseg pool slabs, none of 2 GiB or more (arenaSegments),
-  // described by the nseg ArenaSeg records that follow this one in the blob;
-  // `ptr`, `handle`, `nonce` and `slabBytes` above are then unused
-  int32_t nseg;
-  int32_t pad;
 };
-struct ArenaSegRecord {
-  uint64_t start, end;  // the logical arena bytes [start, end) it holds
-  uint64_t ptr;         // the slab; logical `start` sits at ptr + (start % kSegAlign)
-  uint64_t slabBytes;
-  uint64_t nonce;       // written at the slab's first word, checked by every importer
-  hipIpcMemHandle_t handle;
-};
-// A peer's arena record and its slab records, checked for shape.
-void parseArena(const std::vector<char>& v, int peer, ArenaRecord* r, std::vector<ArenaSegRecord>* segs) {
-  GLOO_AMD_ENFORCE(v.size() >= sizeof(ArenaRecord), "bad arena record from rank ", peer);
+// A peer's arena record, checked for shape.
+void parseArena(const std::vector<char>& v, int peer, ArenaRecord* r) {
+  GLOO_AMD_ENFORCE(v.size() == sizeof(ArenaRecord), "bad arena record from rank ", peer);
   std::memcpy(r, v.data(), sizeof(*r));
-  GLOO_AMD_ENFORCE(r->nseg >= 0 && r->nseg <= kMaxArenaSegs &&
-                       v.size() == sizeof(ArenaRecord) + (size_t)r->nseg * sizeof(ArenaSegRecord),
-                   "bad arena record from rank ", peer);
-  segs->resize((size_t)r->nseg);
-  if (r->nseg) std::memcpy(segs->data(), v.data() + sizeof(ArenaRecord), segs->size() * sizeof(ArenaSegRecord));
 }
 
 // A value no earlier arena of this process or its peers is likely to hold.
@@ -115,17 +86,6 @@ bool traceOn() {
     if (traceOn()) std::fprintf(stderr, "[trace r%d inst%llu] %s\n", ctx_->rank, (unsigned long long)inst_, \
                                 strcat_(__VA_ARGS__).c_str());                                          \
   } while (0)
-
-std::string handleHex(const hipIpcMemHandle_t& h) {
-  const unsigned char* hb = reinterpret_cast<const unsigned char*>(&h);
-  std::string hex;
-  char t[3];
-  for (size_t i = 0; i < sizeof(h); i++) {
-    std::snprintf(t, sizeof(t), "%02x", hb[i]);
-    hex += t;
-  }
-  return hex;
-}
 
 struct DiagLog {
   std::mutex m;
@@ -628,96 +588,7 @@ Plan planFor(int algo, int rank, int size, size_t count, int nin, int nout, size
 
 // The text of a failed import check (tests and tools look for it).
 constexpr const char* kStaleImport = "does not show its contents";
-
-// The slabs of a segmented arena (kSegMax): the byte ranges of the arena
-// every step of `p` reads or writes — its inbox regions (DECL_RECV, which
-// bound every peer's message), the REDUCE inboxes and the arena operands of
-// copies, sends and folds — merged where they overlap into atoms, and the
-// atoms packed in order into slabs of at most kSegTarget bytes (an atom
-// larger than that gets a slab of its own, up to kSegMax).  An atom above
-// kSegMax, or more than kMaxArenaSegs slabs, is refused.
-std::vector<std::pair<size_t, size_t>> arenaSegments(const Plan& p, size_t es) {
-  std::vector<std::pair<size_t, size_t>> iv;
-  auto add = [&](uint64_t off, uint64_t len) {
-    if (len) iv.push_back({(size_t)off * es, (size_t)(off + len) * es});
-  };
-  for (const Step& s : p.steps) {
-    if (s.kind == GLOO_HIP_STEP_DECL_RECV) {
-      add(s.dst_off, s.length);
-    } else if (s.kind == GLOO_HIP_STEP_REDUCE) {
-      add(s.src_off, s.length);
-    } else {
-      if (s.flags & GLOO_HIP_SRC_ARENA) add(s.src_off, s.length);
-      if (s.flags & GLOO_HIP_DST_ARENA) add(s.dst_off, s.length);
-    }
-  }
-  std::sort(iv.begin(), iv.end());
-  std::vector<std::pair<size_t, size_t>> atoms;
-  for (const auto& x : iv) {
-    if (!atoms.empty() && x.first < atoms.back().second) {
-      atoms.back().second = std::max(atoms.back().second, x.second);
-    } else {
-      atoms.push_back(x);
-    }
-  }
-  std::vector<std::pair<size_t, size_t>> segs;
-  for (const auto& a : atoms) {
-    // the slab requested for an atom alone is its length plus its residue
-    // mod kSegAlign (the slab keeps that residue), and must stay <= kSegMax
-    GLOO_AMD_ENFORCE(a.second - a.first + a.first % kSegAlign <= kSegMax, "one inbox region of ", a.second - a.first,
-                     " B would be shared between processes; HIP IPC imports of 2 GiB and more hang on this "
-                     "platform, so a message may span at most ", kSegMax,
-                     " B: split the call, or run the ranks as threads of one process");
-    if (!segs.empty() && a.second - segs.back().first <= kSegTarget) {
-      segs.back().second = a.second;
-    } else {
-      segs.push_back(a);
-    }
-  }
-  GLOO_AMD_ENFORCE(segs.size() <= (size_t)kMaxArenaSegs, "an inbox arena of ", segs.size(),
-                   " slabs (at most ", kMaxArenaSegs, "): split the call");
-  return segs;
-}
 }  // namespace
-
-}  // namespace gloo_amd
-
-// Test and tooling hook (include/gloo_amd.h): the slabs a rank's inbox arena
-// is split into when other processes map it (executor.cc kSegMax); 0 slabs
-// when it stays one block.
-extern "C" int gloo_hip_arena_slabs(int algo, int rank, int size, size_t count, int ninputs, int noutputs,
-                                    size_t elem_size, size_t max_segment_bytes, const int* recv_elems,
-                                    uint64_t* ranges, size_t capacity, size_t* nslabs) {
-  using namespace gloo_amd;
-  try {
-    GLOO_AMD_ENFORCE(nslabs && size >= 1 && rank >= 0 && rank < size && elem_size > 0, "bad arguments");
-    std::vector<int> re;
-    if (recv_elems) re.assign(recv_elems, recv_elems + size);
-    const Plan p = planFor(algo, rank, size, count, ninputs, noutputs, elem_size, max_segment_bytes, re);
-    constexpr size_t kArenaGranule = 2u << 20;
-    const size_t bytes = (std::max<size_t>(256, p.arena * elem_size) + kArenaGranule - 1) / kArenaGranule * kArenaGranule;
-    std::vector<std::pair<size_t, size_t>> segs;
-    if (bytes > kSegMax) segs = arenaSegments(p, elem_size);
-    *nslabs = segs.size();
-    for (size_t k = 0; ranges && k < segs.size() && k < capacity; k++) {
-      ranges[2 * k] = segs[k].first;
-      ranges[2 * k + 1] = segs[k].second;
-    }
-    return GLOO_HIP_OK;
-  } catch (const std::exception& e) {
-    return gloo_amd::setError(GLOO_HIP_EINVAL_ARG, e.what());
-  }
-}
-
-namespace gloo_amd {
-
-char* PlanExecutor::segAt(const std::vector<ArenaSeg>& segs, char* base, size_t off, size_t bytes) {
-  if (segs.empty()) return base + off;
-  for (const ArenaSeg& g : segs)
-    if (g.start <= off && off + bytes <= g.end) return g.ptr + (off - g.start);
-  GLOO_AMD_ENFORCE(bytes == 0, "arena range [", off, ", +", bytes, ") crosses a slab boundary");
-  return segs.front().ptr;  // an empty message: never dereferenced
-}
 
 void PlanExecutor::setBuffers(const std::vector<void*>& inputs, const std::vector<void*>& outputs) {
   GLOO_AMD_ENFORCE(inputs.size() == inputs_.size() && outputs.size() == ptrs_.size(),
@@ -970,26 +841,6 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       ipc::freeUnusedSlabs();
     }
   }
-  // Inbox arenas other processes map: no imported block may reach 2 GiB
-  // (importing one hangs in hipIpcOpenMemHandle on ROCm 7 / MI355X,
-  // profiles/round3/r3t_*, r3u_*), so an arena above kSegMax becomes several
-  // slabs (arenaSegments).  Every rank checks every rank's plan (the same
-  // data everywhere), so a layout that cannot be split is refused by all
-  // ranks together rather than some waiting at the next exchange.
-  {
-    bool anyCross = false;
-    for (int r = 0; r < P; r++)
-      if (where[r].pid != ctx_->pid()) anyCross = true;
-    const char* hm = std::getenv("GLOO_AMD_ARENA");
-    const bool host = workspace == GLOO_HIP_WORKSPACE_HOST || (hm && std::string(hm) == "host");
-    if (anyCross && !host)
-      for (int r = 0; r < P; r++) {
-        const Plan pr = r == me ? plan_
-                                : planFor(planAlgo_, r, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_,
-                                          maxSegmentBytes_, recvElems_);
-        if (arenaBytesOf(pr) > kSegMax) (void)arenaSegments(pr, es_);
-      }
-  }
   peers_.resize(P);
   bool sharesDeviceInProcess = false, crossSender = false;
   for (int peer : planPeers) {
@@ -1019,28 +870,16 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   fineArena_ = !hostArena_ && (arMode == "fine" || (arMode == "auto" && crossSender));
 
   // Phase 2: the inbox arena.  Whole 2 MiB granules.  When a peer in
-  // another process maps it, it is a slab of the process-wide IPC pool
-  // (ipc.h): exported once, never freed while the process lives, so an
-  // address a peer has imported always maps these pages (a freed and
-  // re-exported block of the same size at the same address was imported as
-  // the OLD block's pages: DESIGN.md §4, profiles/round3/r3b_*).
+  // another process maps it, it is a slab of the process-wide pool (ipc.h):
+  // a VMM block at a virtual range never mapped before, exported once as a
+  // dma-buf and reused by later executors of its size class, so a mapping a
+  // peer holds always shows these pages.  Any size: there is no 2 GiB import
+  // limit on this route (profiles/round5/r5b_vmm_fresh_va.jsonl).
   const size_t arenaBytes = arenaBytesOf(plan_);
   arenaBytes_ = arenaBytes;
   if (hostArena_) {
     arenaShm_ = HostShm::create(arenaBytes);
     arena_ = static_cast<char*>(arenaShm_->dev);
-  } else if (crossProcess_ && arenaBytes > kSegMax) {
-    // several slabs, each below 2 GiB; the ranges of the plan never straddle two
-    for (const auto& g : arenaSegments(plan_, es_)) {
-      ArenaSeg a;
-      a.start = g.first;
-      a.end = g.second;
-      GLOO_AMD_TRACE_PHASE("acquiring a slab for arena bytes [", a.start, ", ", a.end, ") fine=", fineArena_);
-      a.slab = ipc::acquire(ctx_->device(), a.end - a.start + a.start % kSegAlign, fineArena_);
-      arenaSegs_.push_back(a);  // released with the executor even if a later acquire fails
-      arenaSegs_.back().ptr = a.slab->ptr + a.start % kSegAlign;
-    }
-    arena_ = arenaSegs_.front().ptr;  // non-null; every access goes through arenaAt
   } else if (crossProcess_) {
     GLOO_AMD_TRACE_PHASE("acquiring a slab of ", arenaBytes, " B fine=", fineArena_);
     arenaSlab_ = ipc::acquire(ctx_->device(), arenaBytes, fineArena_);
@@ -1122,23 +961,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   rec.ptr = reinterpret_cast<uint64_t>(arena_);
   rec.bytes = arenaBytes;
   rec.deviceSignal = deviceSignal_ ? 1 : 0;
-  std::vector<ArenaSegRecord> segRecs(arenaSegs_.size());
-  if (!arenaSegs_.empty()) {
-    rec.nseg = (int32_t)arenaSegs_.size();
-    for (size_t k = 0; k < arenaSegs_.size(); k++) {
-      const ArenaSeg& a = arenaSegs_[k];
-      ArenaSegRecord& g = segRecs[k];
-      std::memset(&g, 0, sizeof(g));
-      g.start = a.start;
-      g.end = a.end;
-      g.ptr = reinterpret_cast<uint64_t>(a.slab->ptr);
-      g.slabBytes = a.slab->bytes;
-      g.handle = a.slab->handle;
-      g.nonce = arenaNonce();
-      GLOO_AMD_HIP_CHECK(hipMemcpyAsync(a.slab->ptr, &g.nonce, sizeof(g.nonce), hipMemcpyHostToDevice, stream_));
-    }
-    GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
-  } else if (!hostArena_) {
+  if (!hostArena_) {
     // the first 8 bytes of the arena carry a nonce until the first message
     // lands; a peer that maps the arena over IPC reads it back (below)
     rec.nonce = arenaNonce();
@@ -1164,7 +987,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     rec.mailboxBytes = mbBytes;
     rec.mailboxNonce = mbNonce;
     if (mailboxSlab_) {
-      rec.mailboxHandle = mailboxSlab_->handle;
+      rec.mailboxSlabId = mailboxSlab_->id;
       rec.mailboxSlabBytes = mailboxSlab_->bytes;
     }
   }
@@ -1173,11 +996,10 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     GLOO_AMD_ENFORCE(arenaShm_->name.size() < sizeof(rec.shm), "shm name too long");
     std::memcpy(rec.shm, arenaShm_->name.c_str(), arenaShm_->name.size() + 1);
   } else if (arenaSlab_) {
-    rec.handle = arenaSlab_->handle;  // exported once, when the pool allocated the slab
+    rec.slabId = arenaSlab_->id;  // exported once, when the pool allocated the slab
   }
-  std::vector<char> blob(sizeof(rec) + segRecs.size() * sizeof(ArenaSegRecord));
+  std::vector<char> blob(sizeof(rec));
   std::memcpy(blob.data(), &rec, sizeof(rec));
-  if (!segRecs.empty()) std::memcpy(blob.data() + sizeof(rec), segRecs.data(), segRecs.size() * sizeof(ArenaSegRecord));
   GLOO_AMD_TRACE_PHASE("exchanging arena records");
   const std::vector<std::vector<char>> arenas = ctx_->allgather(strcat_("inst", inst_, "/arena"), blob);
   GLOO_AMD_TRACE_PHASE("arena records exchanged");
@@ -1198,8 +1020,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   peerMailboxIpc_.assign(P, false);
   for (int peer : planPeers) {
     ArenaRecord pr;
-    std::vector<ArenaSegRecord> prSegs;
-    parseArena(arenas.at(peer), peer, &pr, &prSegs);
+    parseArena(arenas.at(peer), peer, &pr);
     if (mailbox_ && pr.deviceSignal && pr.hasMailbox) {
       if (pr.pid == ctx_->pid()) {
         peerMailbox_[peer] = reinterpret_cast<uint64_t*>(pr.mailboxPtr);
@@ -1209,8 +1030,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
           (void)hipGetLastError();
         }
       } else {
-        void* p = ipc::import(pr.pid, pr.incarnation, pr.mailboxPtr,
-                              std::max<uint64_t>(pr.mailboxBytes + 4096, pr.mailboxSlabBytes), pr.mailboxHandle);
+        void* p = ipc::import(pr.pid, pr.incarnation, pr.mailboxSlabId, pr.mailboxBytes + 4096, ctx_->device());
         uint64_t seen = 0;
         GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, static_cast<char*>(p) + pr.mailboxBytes, sizeof(seen),
                                           hipMemcpyDeviceToHost, stream_));
@@ -1223,37 +1043,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       }
     }
     if (!sendPeers.count(peer)) continue;
-    if (pr.nseg > 0) {
-      // a segmented arena: every slab mapped (or, in this process, used) on
-      // its own and checked by its nonce
-      for (int k = 0; k < pr.nseg; k++) {
-        const ArenaSegRecord& g = prSegs[(size_t)k];
-        char* base = reinterpret_cast<char*>(g.ptr);
-        const size_t need = g.end - g.start + g.start % kSegAlign;
-        if (pr.pid != ctx_->pid()) {
-          GLOO_AMD_TRACE_PHASE("importing rank ", peer, "'s arena slab ", k, " ", (void*)g.ptr, " (", g.slabBytes, " B)");
-          base = static_cast<char*>(ipc::import(pr.pid, pr.incarnation, g.ptr, std::max<uint64_t>(need, g.slabBytes),
-                                                g.handle));
-          peers_[peer].ipc = true;
-        } else if (pr.device != ctx_->device()) {
-          hipError_t e = hipDeviceEnablePeerAccess(pr.device, 0);
-          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
-          (void)hipGetLastError();
-        }
-        uint64_t seen = 0;
-        GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, base, sizeof(seen), hipMemcpyDeviceToHost, stream_));
-        GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
-        GLOO_AMD_ENFORCE(seen == g.nonce, "rank ", me, ": the mapping of rank ", peer, "'s arena slab ", k, " (",
-                         (void*)g.ptr, ", ", g.slabBytes, " B, in pid ", pr.pid, ", mapped at ", (void*)base, ") ",
-                         kStaleImport, ": read ", seen, ", expected ", g.nonce);
-        ArenaSeg a;
-        a.start = g.start;
-        a.end = g.end;
-        a.ptr = base + g.start % kSegAlign;
-        peers_[peer].segs.push_back(a);
-      }
-      peers_[peer].base = peers_[peer].segs.front().ptr;
-    } else if (pr.host && pr.pid != ctx_->pid()) {
+    if (pr.host && pr.pid != ctx_->pid()) {
       // another process's host workspace: map the same pages here
       peerShm_.push_back(HostShm::open(std::string(pr.shm), pr.bytes));
       peers_[peer].base = static_cast<char*>(peerShm_.back()->dev);
@@ -1270,8 +1060,8 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       // must show the nonce the owner just wrote at the slab's start, and
       // the runtime's record of it must span the arena; anything else is a
       // hard error, never a silent misdelivery.
-      GLOO_AMD_TRACE_PHASE("importing rank ", peer, "'s arena ", (void*)pr.ptr, " (", pr.bytes, " B)");
-      void* p = ipc::import(pr.pid, pr.incarnation, pr.ptr, std::max<uint64_t>(pr.bytes, pr.slabBytes), pr.handle);
+      GLOO_AMD_TRACE_PHASE("importing rank ", peer, "'s arena slab ", pr.slabId, " (", pr.bytes, " B)");
+      void* p = ipc::import(pr.pid, pr.incarnation, pr.slabId, pr.bytes, ctx_->device());
       GLOO_AMD_TRACE_PHASE("imported at ", p);
       uint64_t seen = 0;
       GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, p, sizeof(seen), hipMemcpyDeviceToHost, stream_));
@@ -1296,7 +1086,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       GLOO_AMD_ENFORCE(seen == pr.nonce && mapped >= pr.bytes, "rank ", me, ": the IPC mapping of rank ", peer,
                        "'s inbox arena (", (void*)pr.ptr, ", ", pr.bytes, " B, in pid ", pr.pid, ", mapped at ", p,
                        ") ", kStaleImport, ": read ", seen, ", expected ", pr.nonce, "; the runtime maps ", mapped,
-                       " B there; handle ", handleHex(pr.handle));
+                       " B there; slab ", pr.slabId);
     }
     const Plan theirs = planFor(planAlgo_, peer, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
     for (const Step& d : theirs.steps)
@@ -1314,8 +1104,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   for (int r = 0; r < P && agreed > 1; r++) {
     if (r == me) continue;
     ArenaRecord pr;
-    std::vector<ArenaSegRecord> prSegs;
-    parseArena(arenas.at(r), r, &pr, &prSegs);
+    parseArena(arenas.at(r), r, &pr);
     agreed = std::min(agreed, pr.interpSlices);
   }
   slices_ = agreed > 1 ? agreed : 1;
@@ -1424,8 +1213,7 @@ void PlanExecutor::release() {
       // nobody reuses or frees an arena a peer may still write
       for (auto& p : peers_) {
         if (!p.ipc) continue;
-        if (p.segs.empty()) ipc::unimport(p.base);
-        for (const ArenaSeg& a : p.segs) ipc::unimport(a.ptr - a.start % kSegAlign);
+        ipc::unimport(p.base);
       }
       for (size_t q = 0; q < peerMailbox_.size(); q++)
         if (peerMailboxIpc_[q]) ipc::unimport(peerMailbox_[q]);
@@ -1435,14 +1223,11 @@ void PlanExecutor::release() {
       peerShm_.clear();
       if (arenaShm_) {
         arenaShm_.reset();
-      } else if (!arenaSegs_.empty()) {
-        for (ArenaSeg& a : arenaSegs_) ipc::release(a.slab);  // back to the pool, never freed
       } else if (arenaSlab_) {
         ipc::release(arenaSlab_);  // back to the pool, never freed
       } else if (arena_) {
         GLOO_AMD_HIP_RELEASE(hipFree(arena_));  // never exported
       }
-      arenaSegs_.clear();
       arenaSlab_ = nullptr;
       arena_ = nullptr;
       if (mailboxSlab_) {

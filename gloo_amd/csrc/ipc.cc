@@ -1,15 +1,23 @@
 // ipc.cc — see gloo_amd/ipc.h.
 #include "gloo_amd/ipc.h"
 
+#include <errno.h>
+#include <sys/socket.h>
+#include <sys/time.h>
+#include <sys/un.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstddef>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <random>
-#include <set>
+#include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -27,9 +35,8 @@ size_t sizeClass(size_t bytes) {
     return e && e[0] == '1';
   }();
   if (exact) return (bytes + kGranule - 1) / kGranule * kGranule;
-  // powers of two up to 1 GiB, then multiples of 256 MiB: a 1.5 GiB arena
-  // stays below 2^31 bytes (importing blocks of 2 GiB and more concurrently
-  // hangs: executor.cc)
+  // powers of two up to 1 GiB, then multiples of 256 MiB (no upper bound:
+  // VMM imports of any size map, ipc.h)
   constexpr size_t kBig = size_t(1) << 30, kStep = size_t(256) << 20;
   if (bytes > kBig) return (bytes + kStep - 1) / kStep * kStep;
   size_t c = kGranule;
@@ -37,24 +44,55 @@ size_t sizeClass(size_t bytes) {
   return c;
 }
 
+hipMemAllocationProp propFor(int device, bool fine) {
+  hipMemAllocationProp p;
+  std::memset(&p, 0, sizeof(p));
+  // uncached: what a peer GPU or process writes is never behind a stale
+  // line of this GPU's caches (the executor's cross-written inboxes and
+  // mailboxes, as hipDeviceMallocFinegrained memory was before)
+  p.type = fine ? hipMemAllocationTypeUncached : hipMemAllocationTypePinned;
+  p.requestedHandleType = hipMemHandleTypePosixFileDescriptor;
+  p.location.type = hipMemLocationTypeDevice;
+  p.location.id = device;
+  return p;
+}
+
+// A virtual range of `bytes` never mapped before (ranges are never freed:
+// a range mapped twice kept the first mapping's translations, ipc.h).
+void* freshRange(size_t bytes) {
+  void* va = nullptr;
+  GLOO_AMD_HIP_ALLOC(hipMemAddressReserve(&va, bytes, kGranule, nullptr, 0));
+  return va;
+}
+
+void mapAt(void* va, size_t bytes, hipMemGenericAllocationHandle_t h, int device) {
+  GLOO_AMD_HIP_CHECK(hipMemMap(va, bytes, 0, h, 0));
+  hipMemAccessDesc d;
+  std::memset(&d, 0, sizeof(d));
+  d.location.type = hipMemLocationTypeDevice;
+  d.location.id = device;
+  d.flags = hipMemAccessFlagsProtReadWrite;
+  const hipError_t e = hipMemSetAccess(va, bytes, &d, 1);
+  if (e != hipSuccess) {
+    (void)hipMemUnmap(va, bytes);
+    GLOO_AMD_HIP_CHECK(e);
+  }
+}
+
 struct Pool {
   std::mutex m;
-  std::vector<std::unique_ptr<Slab>> slabs;  // every live exported slab (freed only by a trim)
+  std::vector<std::unique_ptr<Slab>> slabs;  // every live exported slab (released only by a trim)
   std::vector<Slab*> free;
-  // device -> [start, end) of every slab a trim freed: no later slab may
-  // overlap one (the runtime caches freed blocks and hands out pieces of
-  // them again; an export over such memory failed, and a peer's import of
-  // it showed stale pages, profiles/round4/r4d_*, r4e_*)
-  std::map<int, std::map<uintptr_t, uintptr_t>> retired;
-  size_t retiredCount = 0;
+  uint64_t nextId = 1;
   struct Mapping {
     uint64_t incarnation;
     void* ptr;
     size_t bytes;
     size_t users;  // executors holding it (import / unimport)
+    hipMemGenericAllocationHandle_t handle;
   };
-  std::map<std::pair<int, uint64_t>, Mapping> imports;  // (pid, exporter address)
-  size_t opens = 0, trims = 0, trimmedBytes = 0, closes = 0, parked = 0;
+  std::map<std::pair<int, uint64_t>, Mapping> imports;  // (exporter pid, slab id)
+  size_t opens = 0, trims = 0, trimmedBytes = 0, closes = 0, retired = 0, retiredBytes = 0;
   static Pool& get() {
     static Pool* p = new Pool();  // never destroyed: process exit releases device memory
     return *p;
@@ -79,12 +117,152 @@ size_t poolMax() {
   return v;
 }
 
+// ---- the fd server ---------------------------------------------------------
+//
+// Requests are one uint64 slab id per connection; the answer is a Reply,
+// with the slab's dma-buf fd attached (SCM_RIGHTS) when ok.  Only processes
+// of this user are answered (SO_PEERCRED).
+
+struct Reply {
+  int32_t ok;
+  int32_t pad;
+  uint64_t bytes;
+};
+
+void socketName(int pid, uint64_t inc, sockaddr_un* a, socklen_t* len) {
+  std::memset(a, 0, sizeof(*a));
+  a->sun_family = AF_UNIX;
+  // abstract namespace: sun_path[0] == 0, nothing on the filesystem
+  const int n = std::snprintf(a->sun_path + 1, sizeof(a->sun_path) - 1, "gloo_amd_vmm/%d/%016llx", pid,
+                              (unsigned long long)inc);
+  *len = (socklen_t)(offsetof(sockaddr_un, sun_path) + 1 + (size_t)n);
+}
+
+void serveConnection(int c) {
+  timeval tv{5, 0};
+  (void)setsockopt(c, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  ucred cred;
+  socklen_t cl = sizeof(cred);
+  if (getsockopt(c, SOL_SOCKET, SO_PEERCRED, &cred, &cl) != 0 || cred.uid != ::getuid()) return;
+  uint64_t id = 0;
+  if (::recv(c, &id, sizeof(id), MSG_WAITALL) != (ssize_t)sizeof(id)) return;
+  Reply r{0, 0, 0};
+  int fd = -1;
+  {
+    Pool& p = Pool::get();
+    std::lock_guard<std::mutex> lk(p.m);
+    for (const auto& s : p.slabs)
+      if (s->id == id) {
+        fd = s->fd;
+        r.ok = 1;
+        r.bytes = s->bytes;
+      }
+  }
+  iovec iov{&r, sizeof(r)};
+  msghdr h;
+  std::memset(&h, 0, sizeof(h));
+  h.msg_iov = &iov;
+  h.msg_iovlen = 1;
+  alignas(cmsghdr) char ctl[CMSG_SPACE(sizeof(int))];
+  if (fd >= 0) {
+    h.msg_control = ctl;
+    h.msg_controllen = sizeof(ctl);
+    cmsghdr* cm = CMSG_FIRSTHDR(&h);
+    cm->cmsg_level = SOL_SOCKET;
+    cm->cmsg_type = SCM_RIGHTS;
+    cm->cmsg_len = CMSG_LEN(sizeof(int));
+    std::memcpy(CMSG_DATA(cm), &fd, sizeof(fd));
+  }
+  (void)::sendmsg(c, &h, MSG_NOSIGNAL);
+}
+
+std::mutex& serverMutex() {
+  static std::mutex m;
+  return m;
+}
+int g_serverPid = 0;
+
+// Starts this process's fd server (again after a fork).
+void ensureServer() {
+  std::lock_guard<std::mutex> lk(serverMutex());
+  if (g_serverPid == ::getpid()) return;
+  const int s = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  GLOO_AMD_ENFORCE(s >= 0, "fd server: socket() failed: ", std::strerror(errno));
+  sockaddr_un a;
+  socklen_t len;
+  socketName(::getpid(), incarnation(), &a, &len);
+  if (::bind(s, reinterpret_cast<sockaddr*>(&a), len) != 0 || ::listen(s, 128) != 0) {
+    const int e = errno;
+    ::close(s);
+    GLOO_AMD_ENFORCE(false, "fd server: bind/listen failed: ", std::strerror(e));
+  }
+  std::thread([s] {
+    for (;;) {
+      const int c = ::accept4(s, nullptr, nullptr, SOCK_CLOEXEC);
+      if (c < 0) {
+        if (errno == EINTR || errno == ECONNABORTED) continue;
+        return;
+      }
+      serveConnection(c);
+      ::close(c);
+    }
+  }).detach();
+  g_serverPid = ::getpid();
+}
+
+// The dma-buf fd of slab `id` of process (pid, inc); its size class in *bytes.
+int fetchFd(int pid, uint64_t inc, uint64_t id, size_t* bytes) {
+  sockaddr_un a;
+  socklen_t len;
+  socketName(pid, inc, &a, &len);
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(30);
+  int c = -1;
+  for (;;) {
+    c = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    GLOO_AMD_ENFORCE(c >= 0, "fd client: socket() failed: ", std::strerror(errno));
+    if (::connect(c, reinterpret_cast<sockaddr*>(&a), len) == 0) break;
+    const int e = errno;
+    ::close(c);
+    GLOO_AMD_ENFORCE(std::chrono::steady_clock::now() < deadline, "no fd server of pid ", pid, ": ",
+                     std::strerror(e));
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  }
+  timeval tv{30, 0};
+  (void)setsockopt(c, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  const bool sent = ::send(c, &id, sizeof(id), MSG_NOSIGNAL) == (ssize_t)sizeof(id);
+  Reply r{0, 0, 0};
+  iovec iov{&r, sizeof(r)};
+  msghdr h;
+  std::memset(&h, 0, sizeof(h));
+  h.msg_iov = &iov;
+  h.msg_iovlen = 1;
+  alignas(cmsghdr) char ctl[CMSG_SPACE(sizeof(int))];
+  h.msg_control = ctl;
+  h.msg_controllen = sizeof(ctl);
+  const ssize_t got = sent ? ::recvmsg(c, &h, MSG_WAITALL | MSG_CMSG_CLOEXEC) : -1;
+  int fd = -1;
+  if (got == (ssize_t)sizeof(r))
+    for (cmsghdr* cm = CMSG_FIRSTHDR(&h); cm; cm = CMSG_NXTHDR(&h, cm))
+      if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_RIGHTS) std::memcpy(&fd, CMSG_DATA(cm), sizeof(int));
+  ::close(c);
+  if (got != (ssize_t)sizeof(r) || !r.ok || fd < 0) {
+    if (fd >= 0) ::close(fd);
+    GLOO_AMD_ENFORCE(false, "pid ", pid, " did not hand over its slab ", id, " (", got != (ssize_t)sizeof(r) ? "no reply" : "unknown slab", ")");
+  }
+  *bytes = r.bytes;
+  return fd;
+}
+
 // Closes every mapping of a peer slab that no executor holds; p.m held.
 void closeUnusedLocked(Pool& p) {
   for (auto it = p.imports.begin(); it != p.imports.end();) {
-    if (it->second.users == 0) {
-      GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(it->second.ptr));
+    Pool::Mapping& mp = it->second;
+    if (mp.users == 0) {
+      GLOO_AMD_HIP_RELEASE(hipMemUnmap(mp.ptr, mp.bytes));
+      GLOO_AMD_HIP_RELEASE(hipMemRelease(mp.handle));
       p.closes++;
+      p.retired++;  // the range stays reserved, never mapped again
+      p.retiredBytes += mp.bytes;
       it = p.imports.erase(it);
     } else {
       ++it;
@@ -92,26 +270,19 @@ void closeUnusedLocked(Pool& p) {
   }
 }
 
-// Frees every free-listed slab and retires its address; p.m held.  A slab is
-// free-listed only after its executor's collective tear-down barrier (no
-// peer writes it any more); the address is retired so that no later slab of
-// this process is exported there, and a byte-identical handle keeps meaning
-// the same pages.  Freeing a slab a peer still maps is not safe on ROCm 7:
-// the next export of memory allocated over it can fail ("invalid argument",
-// profiles/round4/r4e_*), so callers free only after every peer has closed
-// its unused mappings (the collective trims of executor.cc and
-// gloo_hip_ipc_trim).
+// Releases every free-listed slab; p.m held.  A slab is free-listed only
+// after its executor's collective tear-down barrier (no peer writes it any
+// more), and the trims that call this are collective: every peer has closed
+// the mappings no executor holds first.
 void freeUnusedLocked(Pool& p) {
   for (Slab* s : p.free) {
     for (size_t i = 0; i < p.slabs.size(); i++)
       if (p.slabs[i].get() == s) {
-        int prev = -1;
-        (void)hipGetDevice(&prev);
-        (void)hipSetDevice(s->device);
-        GLOO_AMD_HIP_RELEASE(hipFree(s->ptr));
-        if (prev >= 0) (void)hipSetDevice(prev);
-        p.retired[s->device][reinterpret_cast<uintptr_t>(s->ptr)] = reinterpret_cast<uintptr_t>(s->ptr) + s->bytes;
-        p.retiredCount++;
+        GLOO_AMD_HIP_RELEASE(hipMemUnmap(s->ptr, s->bytes));
+        GLOO_AMD_HIP_RELEASE(hipMemRelease(s->handle));
+        if (s->fd >= 0) ::close(s->fd);
+        p.retired++;
+        p.retiredBytes += s->bytes;
         p.trimmedBytes += s->bytes;
         p.slabs.erase(p.slabs.begin() + (long)i);
         break;
@@ -121,46 +292,23 @@ void freeUnusedLocked(Pool& p) {
   p.trims++;
 }
 
-bool overlapsRetired(const Pool& p, int device, const void* ptr, size_t bytes) {
-  auto d = p.retired.find(device);
-  if (d == p.retired.end()) return false;
-  const uintptr_t a = reinterpret_cast<uintptr_t>(ptr), b = a + bytes;
-  auto it = d->second.upper_bound(a);  // first range starting after a
-  if (it != d->second.end() && it->first < b) return true;
-  if (it != d->second.begin()) {
-    --it;
-    if (it->second > a) return true;
-  }
-  return false;
-}
-
 size_t slabBytesLocked(const Pool& p) {
   size_t b = 0;
   for (const auto& x : p.slabs) b += x->bytes;
   return b;
 }
 
-// Bytes the runtime maps from `m` to the end of its allocation (the
-// exporter's whole slab), or 0 when it keeps no record.
-size_t mappedSpan(void* m) {
-  void* rb = nullptr;
-  size_t rs = 0;
-  size_t span = 0;
-  if (hipMemGetAddressRange(&rb, &rs, m) == hipSuccess && rb && static_cast<char*>(rb) + rs > static_cast<char*>(m))
-    span = (size_t)(static_cast<char*>(rb) + rs - static_cast<char*>(m));
-  (void)hipGetLastError();
-  return span;
-}
+// The device the caller runs on, restored on scope exit.
+struct DeviceScope {
+  explicit DeviceScope(int device) {
+    GLOO_AMD_HIP_CHECK(hipGetDevice(&prev));
+    if (device != prev) GLOO_AMD_HIP_CHECK(hipSetDevice(device));
+  }
+  ~DeviceScope() { (void)hipSetDevice(prev); }
+  int prev = 0;
+};
 
 }  // namespace
-
-bool poolEnabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("GLOO_AMD_IPC_POOL");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
 
 uint64_t incarnation() {
   static const uint64_t v = [] {
@@ -172,53 +320,34 @@ uint64_t incarnation() {
 
 Slab* acquire(int device, size_t bytes, bool fine) {
   const size_t want = sizeClass(bytes);
+  ensureServer();
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
-  for (size_t i = 0; poolEnabled() && i < p.free.size(); i++) {
+  for (size_t i = 0; i < p.free.size(); i++) {
     Slab* s = p.free[i];
     if (s->device == device && s->fine == fine && s->bytes == want) {
       p.free.erase(p.free.begin() + (long)i);
       return s;
     }
   }
+  DeviceScope ds(device);
   auto s = std::make_unique<Slab>();
   s->bytes = want;
   s->device = device;
   s->fine = fine;
-  int prev = -1;
-  GLOO_AMD_HIP_CHECK(hipGetDevice(&prev));
-  GLOO_AMD_HIP_CHECK(hipSetDevice(device));
-  // Never export memory overlapping a retired slab, and never keep a block
-  // the runtime refuses to export: park it (allocated, not exported) and
-  // allocate again while it is held, then free the parked blocks.
-  std::vector<void*> parked;
-  void* ptr = nullptr;
-  hipError_t eh = hipSuccess;
-  for (;;) {
-    ptr = nullptr;
-    hipError_t e = fine ? hipExtMallocWithFlags(&ptr, want, hipDeviceMallocFinegrained) : hipMalloc(&ptr, want);
-    if (e != hipSuccess) {
-      for (void* q : parked) (void)hipFree(q);
-      (void)hipSetDevice(prev);
-      GLOO_AMD_HIP_ALLOC(e);
-    }
-    if (!overlapsRetired(p, device, ptr, want)) {
-      eh = hipIpcGetMemHandle(&s->handle, ptr);
-      if (eh == hipSuccess) break;
-      (void)hipGetLastError();
-    }
-    parked.push_back(ptr);
-    p.parked++;
-    if (parked.size() > 64) {
-      for (void* q : parked) (void)hipFree(q);
-      (void)hipSetDevice(prev);
-      GLOO_AMD_ENFORCE(false, "IPC pool: no exportable block of ", want, " B after 64 tries (",
-                       eh == hipSuccess ? "retired ranges" : hipGetErrorString(eh), ")");
-    }
+  const hipMemAllocationProp prop = propFor(device, fine);
+  GLOO_AMD_HIP_ALLOC(hipMemCreate(&s->handle, want, &prop, 0));
+  try {
+    void* va = freshRange(want);
+    mapAt(va, want, s->handle, device);
+    s->ptr = static_cast<char*>(va);
+    GLOO_AMD_HIP_CHECK(hipMemExportToShareableHandle(&s->fd, s->handle, hipMemHandleTypePosixFileDescriptor, 0));
+  } catch (...) {
+    if (s->ptr) (void)hipMemUnmap(s->ptr, want);
+    (void)hipMemRelease(s->handle);
+    throw;
   }
-  for (void* q : parked) GLOO_AMD_HIP_RELEASE(hipFree(q));
-  s->ptr = static_cast<char*>(ptr);
-  (void)hipSetDevice(prev);
+  s->id = p.nextId++;
   p.slabs.push_back(std::move(s));
   return p.slabs.back().get();
 }
@@ -227,30 +356,17 @@ void release(Slab* s) {
   if (!s) return;
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
-  if (poolEnabled()) {
-    p.free.push_back(s);
-    return;
-  }
-  // diagnosis (GLOO_AMD_IPC_POOL=0): free at once, as before the pool
-  for (size_t i = 0; i < p.slabs.size(); i++)
-    if (p.slabs[i].get() == s) {
-      GLOO_AMD_HIP_RELEASE(hipFree(s->ptr));
-      p.slabs.erase(p.slabs.begin() + (long)i);
-      return;
-    }
+  p.free.push_back(s);
 }
 
 void unimport(void* mapped) {
   if (!mapped) return;
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
-  for (auto it = p.imports.begin(); it != p.imports.end(); ++it)
-    if (it->second.ptr == mapped) {
-      if (it->second.users) it->second.users--;
-      if (poolEnabled()) return;  // mappings of pool slabs are kept until a trim
-      GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(mapped));
-      p.imports.erase(it);
-      return;
+  for (auto& kv : p.imports)
+    if (kv.second.ptr == mapped) {
+      if (kv.second.users) kv.second.users--;
+      return;  // kept until a trim
     }
 }
 
@@ -269,34 +385,49 @@ void freeUnusedSlabs() {
 bool overCeiling(size_t more) {
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
-  return poolEnabled() && !p.free.empty() && slabBytesLocked(p) + more > poolMax();
+  return !p.free.empty() && slabBytesLocked(p) + more > poolMax();
 }
 
-void* import(int pid, uint64_t inc, uint64_t ptr, size_t bytes, const hipIpcMemHandle_t& handle) {
+void* import(int pid, uint64_t inc, uint64_t id, size_t bytes, int device) {
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
-  const auto key = std::make_pair(pid, ptr);
+  const auto key = std::make_pair(pid, id);
   auto it = p.imports.find(key);
   if (it != p.imports.end()) {
-    if (it->second.incarnation == inc && poolEnabled()) {
-      if (it->second.bytes < bytes) it->second.bytes = std::max(it->second.bytes, mappedSpan(it->second.ptr));
-      GLOO_AMD_ENFORCE(it->second.bytes >= bytes, "slab of pid ", pid, " at ", (void*)ptr, " imported at ",
-                       it->second.bytes, " B, now published at ", bytes, " B");
+    if (it->second.incarnation == inc) {
+      GLOO_AMD_ENFORCE(it->second.bytes >= bytes, "slab ", id, " of pid ", pid, " mapped at ", it->second.bytes,
+                       " B, now published at ", bytes, " B");
       it->second.users++;
       return it->second.ptr;
     }
     // a new process reusing a dead one's pid: its mapping is of no use
-    GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(it->second.ptr));
+    GLOO_AMD_HIP_RELEASE(hipMemUnmap(it->second.ptr, it->second.bytes));
+    GLOO_AMD_HIP_RELEASE(hipMemRelease(it->second.handle));
+    p.retired++;
+    p.retiredBytes += it->second.bytes;
     p.imports.erase(it);
   }
-  void* m = nullptr;
-  GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&m, handle, hipIpcMemLazyEnablePeerAccess));
+  size_t slabBytes = 0;
+  const int fd = fetchFd(pid, inc, id, &slabBytes);
+  GLOO_AMD_ENFORCE(slabBytes >= bytes, "slab ", id, " of pid ", pid, " holds ", slabBytes, " B, ", bytes,
+                   " B expected");
+  DeviceScope ds(device);
+  hipMemGenericAllocationHandle_t h = nullptr;
+  const hipError_t e = hipMemImportFromShareableHandle(&h, reinterpret_cast<void*>(static_cast<intptr_t>(fd)),
+                                                       hipMemHandleTypePosixFileDescriptor);
+  ::close(fd);
+  GLOO_AMD_HIP_ALLOC(e);
+  void* va = nullptr;
+  try {
+    va = freshRange(slabBytes);
+    mapAt(va, slabBytes, h, device);
+  } catch (...) {
+    (void)hipMemRelease(h);
+    throw;
+  }
   p.opens++;
-  // The mapping spans the exporter's whole slab (its size class), not just
-  // the bytes this first importer asked for: a later use of the same slab
-  // (a mailbox slab reused as an arena) may publish more of it.
-  p.imports[key] = {inc, m, std::max(bytes, mappedSpan(m)), 1};
-  return m;
+  p.imports[key] = {inc, va, slabBytes, 1, h};
+  return va;
 }
 
 Stats stats() {
@@ -311,8 +442,8 @@ Stats stats() {
   s.trims = p.trims;
   s.trimmedBytes = p.trimmedBytes;
   s.closes = p.closes;
-  s.retired = p.retiredCount;
-  s.parked = p.parked;
+  s.retired = p.retired;
+  s.retiredBytes = p.retiredBytes;
   s.max = poolMax();
   return s;
 }

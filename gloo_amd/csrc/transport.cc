@@ -18,6 +18,7 @@
 #include "gloo_amd.h"
 #include "gloo_amd/common.h"
 #include "gloo_amd/errors.h"
+#include "gloo_amd/ipc.h"
 #include "gloo_amd/signal.h"
 
 namespace gloo_amd {
@@ -39,12 +40,19 @@ struct RecvRecord {
   uint64_t baseline;  // the channel's arrival count when the buffer was created
   hipIpcMemHandle_t handle;
   char landing[48];   // host memory: the landing segment a peer process writes messages into
+  int32_t deviceLanding;  // device memory in an allocation of 2 GiB or more: a landing slab (ipc.h) instead
+  int32_t pad2;
+  uint64_t landingSlab, landingIncarnation;
 };
 
-// An IPC import maps the exporter's whole allocation, and importing a block
-// of 2^31 bytes or more hangs in hipIpcOpenMemHandle on ROCm 7 / MI355X
-// (profiles/round3/r3t_*, r3u_*): a receive buffer inside such an allocation
-// is refused to a peer process before any import is attempted.
+// A hipIpc import maps the exporter's whole allocation, and importing a
+// block of 2^31 bytes or more hangs in hipIpcOpenMemHandle on ROCm 7 /
+// MI355X (profiles/round3/r3t_*, r3u_*).  A device receive buffer inside
+// such an allocation therefore gets a LANDING slab of its own size from the
+// cross-process pool (VMM, any size: ipc.h): peer processes write their
+// messages there and waitRecv copies each message's range into the buffer.
+// (A caller's hipMalloc memory cannot be exported through VMM:
+// hipMemGetHandleForAddressRange refuses it, profiles/round5/r5b_vmm_*.)
 constexpr uint64_t kMaxImportBytes = uint64_t(1) << 31;
 
 // Most workgroups one device-to-device message's copy kernel takes: a few
@@ -137,6 +145,7 @@ class SendBuffer : public Buffer {
     if (landingRegistered_) GLOO_AMD_HIP_RELEASE(hipHostUnregister(landing_));
     if (landing_) ::munmap(landing_, peerSize_);
     if (opened_) GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(opened_));
+    if (landingImport_) ipc::unimport(landingImport_);
     dev_->release(true, peer_, slot_);
   }
 
@@ -152,9 +161,10 @@ class SendBuffer : public Buffer {
     hipStream_t s = dev_->stream();
     const char* src = ptr_ + offset;
     char* dst = nullptr;
-    if (landing_) {
-      // a host buffer of another process: the message lands in its segment,
-      // described by the record of its arrival number, which must be free
+    if (viaLanding_) {
+      // a buffer of another process reached through its landing segment or
+      // slab: the message lands there, described by the record of its
+      // arrival number, which must be free
       Device::MsgRecord& rec = dev_->msgRecord(ctx.rank, peer_, channelIdx_, k);
       pollUntil(
           [&] {
@@ -166,7 +176,7 @@ class SendBuffer : public Buffer {
       rec.off = roffset;
       rec.len = length;
       rec.seq.store(k, std::memory_order_release);  // read only once the arrival count reaches k
-      dst = landing_ + roffset;
+      dst = (landing_ ? landing_ : remote_) + roffset;
     } else if (remote_) {
       dst = remote_ + roffset;
     }
@@ -235,15 +245,19 @@ class SendBuffer : public Buffer {
       ::close(fd);
       GLOO_AMD_ENFORCE(m != MAP_FAILED, "mmap of rank ", peer_, "'s landing segment failed");
       landing_ = static_cast<char*>(m);
+      viaLanding_ = true;
       if (srcDevice_) {
         GLOO_AMD_HIP_ALLOC(hipHostRegister(landing_, r.size, hipHostRegisterPortable));
         landingRegistered_ = true;
       }
+    } else if (r.deviceLanding) {
+      // device memory of another process in a 2 GiB+ allocation: its landing slab
+      landingImport_ = static_cast<char*>(
+          ipc::import(r.pid, r.landingIncarnation, r.landingSlab, r.size, ctx.device()));
+      remote_ = landingImport_;
+      viaLanding_ = true;
+      dstDevice_ = true;
     } else {
-      GLOO_AMD_ENFORCE(r.alloc < kMaxImportBytes, "rank ", peer_, "'s receive buffer (slot ", slot_,
-                       ") lies in a device allocation of ", r.alloc, " B; HIP IPC imports of 2 GiB and more hang "
-                       "on this platform, so a peer process cannot write into it: allocate receive buffers below ",
-                       kMaxImportBytes, " B, or run the ranks as threads of one process");
       GLOO_AMD_ENFORCE(r.ipc, "rank ", peer_, "'s receive buffer is not IPC-exportable");
       // The caller's memory cannot come from the IPC slab pool (ipc.h);
       // this import is used by eager copies only, never captured into a
@@ -284,8 +298,10 @@ class SendBuffer : public Buffer {
   bool sameGpu_ = false;   // ... on this rank's own GPU
   bool resolved_ = false;
   char* remote_ = nullptr;
-  char* landing_ = nullptr;
+  char* landing_ = nullptr;         // a host buffer's landing segment (mapped here)
   bool landingRegistered_ = false;
+  char* landingImport_ = nullptr;   // a device buffer's landing slab (imported)
+  bool viaLanding_ = false;         // messages go through a landing area, with records
   void* opened_ = nullptr;
   size_t peerSize_ = 0;
   int channelIdx_ = -1;
@@ -325,8 +341,15 @@ class RecvBuffer : public Buffer {
       if (isDevice(ptr_)) {
         void* base = nullptr;
         size_t allocSize = 0;
-        if (hipMemGetAddressRange(&base, &allocSize, ptr_) == hipSuccess && base &&
-            hipIpcGetMemHandle(&r.handle, base) == hipSuccess) {
+        const bool ranged = hipMemGetAddressRange(&base, &allocSize, ptr_) == hipSuccess && base;
+        (void)hipGetLastError();
+        if (ranged && allocSize >= kMaxImportBytes) {
+          deviceLanding_ = ipc::acquire(ctx.device(), size_, true);
+          r.deviceLanding = 1;
+          r.landingSlab = deviceLanding_->id;
+          r.landingIncarnation = ipc::incarnation();
+          r.alloc = allocSize;
+        } else if (ranged && hipIpcGetMemHandle(&r.handle, base) == hipSuccess) {
           r.ipc = 1;
           r.offset = (uint64_t)(ptr_ - static_cast<char*>(base));
           r.alloc = allocSize;
@@ -346,6 +369,7 @@ class RecvBuffer : public Buffer {
     ctx.store().set(recordKey(dev_->instance(), peer_, ctx.rank, slot_), blob);
   }
   ~RecvBuffer() override {
+    if (deviceLanding_) ipc::release(deviceLanding_);
     if (landing_) {
       ::munmap(landing_, size_);
       ::shm_unlink(landingName_.c_str());
@@ -361,6 +385,24 @@ class RecvBuffer : public Buffer {
     const uint64_t target = baseline_ + ++received_;
     pollUntil([&] { return (int64_t)(channel_->count.load(std::memory_order_acquire) - target) >= 0; }, nullptr,
               ctx.timeout(), strcat_("waiting for rank ", peer_, " (slot ", slot_, ") on rank ", ctx.rank));
+    if (deviceLanding_) {
+      // a sender in another process wrote into the landing slab and described
+      // the message in the record of this arrival (one in this process wrote
+      // in place: no record carries this arrival number then)
+      Device::MsgRecord& rec = dev_->msgRecord(peer_, ctx.rank, idx_, target);
+      if (rec.seq.load(std::memory_order_acquire) != target) return;
+      const uint64_t off = rec.off, len = rec.len;
+      GLOO_AMD_ENFORCE(off + len <= size_, "message of ", len, " B at ", off, " beyond the ", size_,
+                       "-byte receive buffer");
+      if (len) {
+        GLOO_AMD_HIP_CHECK(hipSetDevice(ctx.device()));
+        GLOO_AMD_HIP_CHECK(hipMemcpyAsync(ptr_ + off, deviceLanding_->ptr + off, len, hipMemcpyDeviceToDevice,
+                                          dev_->stream()));
+        GLOO_AMD_HIP_CHECK(hipStreamSynchronize(dev_->stream()));
+      }
+      rec.ack.store(target, std::memory_order_release);
+      return;
+    }
     if (!host_) return;  // device memory: always written in place
     // A host buffer's sender in another process wrote the bytes into the
     // landing segment and described them in the record of this arrival; one
@@ -384,6 +426,7 @@ class RecvBuffer : public Buffer {
   uint64_t baseline_ = 0, received_ = 0;
   std::string landingName_;
   char* landing_ = nullptr;
+  ipc::Slab* deviceLanding_ = nullptr;  // device memory in a 2 GiB+ allocation: where peer processes write
 };
 
 }  // namespace

@@ -150,23 +150,11 @@ class PlanExecutor {
   size_t lastReduceCount() const { return reduceCount_; }
 
  private:
-  // One slab of a segmented inbox arena: logical arena bytes [start, end),
-  // with logical `start` at ptr (executor.cc kSegMax).
-  struct ArenaSeg {
-    size_t start = 0, end = 0;
-    char* ptr = nullptr;
-    ipc::Slab* slab = nullptr;  // own arena only
-  };
-  // The address of logical arena byte `off` of a range of `bytes`: base + off
-  // for a one-block arena, else inside the slab that holds the whole range.
-  static char* segAt(const std::vector<ArenaSeg>& segs, char* base, size_t off, size_t bytes);
-  char* arenaAt(uint64_t elems, uint64_t len) const { return segAt(arenaSegs_, arena_, elems * es_, len * es_); }
-  char* peerAt(int peer, uint64_t elems, uint64_t len) const {
-    return segAt(peers_[peer].segs, peers_[peer].base, elems * es_, len * es_);
-  }
+  // Pointers into an arena, by element offset.
+  char* arenaAt(uint64_t elems, uint64_t) const { return arena_ + elems * es_; }
+  char* peerAt(int peer, uint64_t elems, uint64_t) const { return peers_[peer].base + elems * es_; }
   struct Peer {
     char* base = nullptr;
-    std::vector<ArenaSeg> segs;  // its arena's slabs (empty: one block at base)
     bool ipc = false;
     int pid = -1;
     int device = -1;
@@ -214,7 +202,6 @@ class PlanExecutor {
   char* arena_ = nullptr;       // device-visible address of this rank's inboxes
   bool crossProcess_ = false;   // a plan peer lives in another process: arena and mailbox are IPC pool slabs
   ipc::Slab* arenaSlab_ = nullptr;
-  std::vector<ArenaSeg> arenaSegs_;  // a segmented arena's slabs (empty: one block at arena_)
   ipc::Slab* mailboxSlab_ = nullptr;
   size_t arenaBytes_ = 0;       // its allocated size (whole 2 MiB granules)
   bool hostArena_ = false;      // inboxes in shared pinned host memory (HOST workspace)

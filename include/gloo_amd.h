@@ -278,17 +278,6 @@ int gloo_hip_plan_ex(int algo, int rank, int size, size_t count, int ninputs, in
                      gloo_hip_step_t* steps, size_t capacity, size_t* nsteps,
                      size_t* arena_elems);
 
-/* (new, tests and tooling) The IPC slabs a rank's inbox arena is split into
- * when processes share it: an arena above 1.75 GiB becomes slabs of at most
- * 1.75 GiB (HIP IPC imports of 2 GiB and more hang on ROCm 7 / MI355X), each
- * holding whole step and message ranges.  ranges[2k], ranges[2k+1] = the
- * arena bytes [start, end) of slab k; *nslabs = 0: one block.  Arguments as
- * gloo_hip_plan_ex (algo = the executed plan, e.g. GLOO_HIP_ALGO_MESH | HD).
- * Fails (GLOO_HIP_EINVAL_ARG) where the executor would refuse the layout. */
-int gloo_hip_arena_slabs(int algo, int rank, int size, size_t count, int ninputs, int noutputs,
-                         size_t elem_size, size_t max_segment_bytes, const int* recv_elems,
-                         uint64_t* ranges, size_t capacity, size_t* nslabs);
-
 /* (new, tests and tooling) The batching rule of the one-launch plan
  * interpreter: which steps of a step list are not drained before the next
  * (signal.h kInterpDefer).  Each step is a kind (0 copy, 1 send, 2 signal,
