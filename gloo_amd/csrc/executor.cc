@@ -1066,15 +1066,6 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       uint64_t seen = 0;
       GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, p, sizeof(seen), hipMemcpyDeviceToHost, stream_));
       GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
-      size_t mapped = pr.bytes;
-      {
-        void* rb = nullptr;
-        size_t rs = 0;
-        if (hipMemGetAddressRange(&rb, &rs, p) == hipSuccess && rb)
-          mapped = static_cast<char*>(rb) + rs > static_cast<char*>(p)
-                       ? (size_t)(static_cast<char*>(rb) + rs - static_cast<char*>(p)) : 0;
-        (void)hipGetLastError();
-      }
       if (ipcDiag())
         std::fprintf(stderr, "[ipc-diag %d r%d inst%llu] import rank %d arena %p %llu B (pid %d) -> %p: seen %llx "
                      "want %llx%s%s\n", ctx_->pid(), me, (unsigned long long)inst_, peer, (void*)pr.ptr,
@@ -1083,10 +1074,10 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
                      seen == pr.nonce ? "" : diagProbe(p, stream_).c_str());
       peers_[peer].base = static_cast<char*>(p);
       peers_[peer].ipc = true;
-      GLOO_AMD_ENFORCE(seen == pr.nonce && mapped >= pr.bytes, "rank ", me, ": the IPC mapping of rank ", peer,
-                       "'s inbox arena (", (void*)pr.ptr, ", ", pr.bytes, " B, in pid ", pr.pid, ", mapped at ", p,
-                       ") ", kStaleImport, ": read ", seen, ", expected ", pr.nonce, "; the runtime maps ", mapped,
-                       " B there; slab ", pr.slabId);
+      // (ipc::import maps the whole slab, at least pr.bytes, or raises)
+      GLOO_AMD_ENFORCE(seen == pr.nonce, "rank ", me, ": the mapping of rank ", peer, "'s inbox arena (",
+                       (void*)pr.ptr, ", ", pr.bytes, " B, slab ", pr.slabId, " of pid ", pr.pid, ", mapped at ", p,
+                       ") ", kStaleImport, ": read ", seen, ", expected ", pr.nonce);
     }
     const Plan theirs = planFor(planAlgo_, peer, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
     for (const Step& d : theirs.steps)

@@ -308,6 +308,32 @@ struct DeviceScope {
   int prev = 0;
 };
 
+// At process exit, before the HIP runtime tears down (atexit handlers run in
+// reverse order of registration, and this one is registered after the
+// runtime's first use): unmap and release every mapping and slab, so the
+// runtime never finds VMM mappings of its own allocations or imports alive.
+void releaseAllAtExit() {
+  Pool& p = Pool::get();
+  std::lock_guard<std::mutex> lk(p.m);
+  if (g_serverPid != ::getpid() && p.imports.empty()) return;  // a forked child owns nothing
+  for (auto& kv : p.imports) {
+    (void)hipMemUnmap(kv.second.ptr, kv.second.bytes);
+    (void)hipMemRelease(kv.second.handle);
+  }
+  p.imports.clear();
+  for (auto& s : p.slabs) {
+    (void)hipMemUnmap(s->ptr, s->bytes);
+    (void)hipMemRelease(s->handle);
+    if (s->fd >= 0) ::close(s->fd);
+  }
+  p.slabs.clear();
+  p.free.clear();
+}
+void registerAtExit() {
+  static std::once_flag once;
+  std::call_once(once, [] { std::atexit(releaseAllAtExit); });
+}
+
 }  // namespace
 
 uint64_t incarnation() {
@@ -321,6 +347,7 @@ uint64_t incarnation() {
 Slab* acquire(int device, size_t bytes, bool fine) {
   const size_t want = sizeClass(bytes);
   ensureServer();
+  registerAtExit();
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
   for (size_t i = 0; i < p.free.size(); i++) {
@@ -389,24 +416,30 @@ bool overCeiling(size_t more) {
 }
 
 void* import(int pid, uint64_t inc, uint64_t id, size_t bytes, int device) {
+  registerAtExit();
   Pool& p = Pool::get();
-  std::lock_guard<std::mutex> lk(p.m);
   const auto key = std::make_pair(pid, id);
-  auto it = p.imports.find(key);
-  if (it != p.imports.end()) {
-    if (it->second.incarnation == inc) {
-      GLOO_AMD_ENFORCE(it->second.bytes >= bytes, "slab ", id, " of pid ", pid, " mapped at ", it->second.bytes,
-                       " B, now published at ", bytes, " B");
-      it->second.users++;
-      return it->second.ptr;
+  {
+    std::lock_guard<std::mutex> lk(p.m);
+    auto it = p.imports.find(key);
+    if (it != p.imports.end()) {
+      if (it->second.incarnation == inc) {
+        GLOO_AMD_ENFORCE(it->second.bytes >= bytes, "slab ", id, " of pid ", pid, " mapped at ", it->second.bytes,
+                         " B, now published at ", bytes, " B");
+        it->second.users++;
+        return it->second.ptr;
+      }
+      // a new process reusing a dead one's pid: its mapping is of no use
+      GLOO_AMD_HIP_RELEASE(hipMemUnmap(it->second.ptr, it->second.bytes));
+      GLOO_AMD_HIP_RELEASE(hipMemRelease(it->second.handle));
+      p.retired++;
+      p.retiredBytes += it->second.bytes;
+      p.imports.erase(it);
     }
-    // a new process reusing a dead one's pid: its mapping is of no use
-    GLOO_AMD_HIP_RELEASE(hipMemUnmap(it->second.ptr, it->second.bytes));
-    GLOO_AMD_HIP_RELEASE(hipMemRelease(it->second.handle));
-    p.retired++;
-    p.retiredBytes += it->second.bytes;
-    p.imports.erase(it);
   }
+  // The pool's lock is NOT held across the request: the exporter may be
+  // importing from this process at the same moment, and its request is
+  // answered by this process's fd server, which takes the lock.
   size_t slabBytes = 0;
   const int fd = fetchFd(pid, inc, id, &slabBytes);
   GLOO_AMD_ENFORCE(slabBytes >= bytes, "slab ", id, " of pid ", pid, " holds ", slabBytes, " B, ", bytes,
@@ -424,6 +457,17 @@ void* import(int pid, uint64_t inc, uint64_t id, size_t bytes, int device) {
   } catch (...) {
     (void)hipMemRelease(h);
     throw;
+  }
+  std::lock_guard<std::mutex> lk(p.m);
+  auto it = p.imports.find(key);
+  if (it != p.imports.end() && it->second.incarnation == inc) {
+    // another thread of this process mapped it meanwhile: keep that one
+    GLOO_AMD_HIP_RELEASE(hipMemUnmap(va, slabBytes));
+    GLOO_AMD_HIP_RELEASE(hipMemRelease(h));
+    p.retired++;
+    p.retiredBytes += slabBytes;
+    it->second.users++;
+    return it->second.ptr;
   }
   p.opens++;
   p.imports[key] = {inc, va, slabBytes, 1, h};

@@ -216,7 +216,7 @@ def run_transport_case(tmp_path, case):
     import sys
     w = tmp_path / "w.py"
     w.write_text(TRANSPORT_WORKER)
-    env = dict(os.environ, GLOO_AMD_ROOT=ROOT)
+    env = dict(os.environ, GLOO_AMD_ROOT=ROOT, PYTHONFAULTHANDLER="1")
     procs = [subprocess.Popen([sys.executable, str(w), str(r), "file:" + str(tmp_path / "s"), case], env=env,
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
     res = []
