@@ -345,14 +345,15 @@ class TransportBuffer:
 def ipc_stats():
     """This process's pool of cross-process slabs (gloo_amd/include/gloo_amd/ipc.h):
     slabs exported and their bytes, slabs free for reuse, peer slabs mapped,
-    imports made; trims, bytes they released, mappings they closed, virtual
-    ranges retired (never mapped again) and their bytes, and the ceiling
-    (GLOO_AMD_IPC_POOL_MAX)."""
-    out = (ctypes.c_uint64 * 11)()
-    _check(lib.gloo_hip_ipc_stats_ex(out, 11))
+    imports made; trims, bytes they freed, mappings they closed, retired
+    ranges (VMM: virtual ranges never mapped again; hipIpc: freed addresses
+    never exported again), allocations parked (hipIpc), the ceiling
+    (GLOO_AMD_IPC_POOL_MAX) and the mechanism (1: VMM, 0: hipIpc)."""
+    out = (ctypes.c_uint64 * 12)()
+    _check(lib.gloo_hip_ipc_stats_ex(out, 12))
     return {"slabs": out[0], "slab_bytes": out[1], "free": out[2], "peer_slabs_mapped": out[3],
             "ipc_opens": out[4], "trims": out[5], "trimmed_bytes": out[6], "mappings_closed": out[7],
-            "retired_ranges": out[8], "retired_bytes": out[9], "pool_max_bytes": out[10]}
+            "retired_ranges": out[8], "parked_allocations": out[9], "pool_max_bytes": out[10], "vmm": out[11]}
 
 
 def ipc_trim(ctx=None):

@@ -219,7 +219,7 @@ int gloo_hip_ipc_stats_ex(uint64_t* out, size_t n) {
     GLOO_AMD_ENFORCE(out, "null argument");
     const gloo_amd::ipc::Stats st = gloo_amd::ipc::stats();
     const uint64_t v[] = {st.slabs, st.slabBytes, st.free,    st.imports, st.opens, st.trims,
-                          st.trimmedBytes, st.closes, st.retired, st.retiredBytes, st.max};
+                          st.trimmedBytes, st.closes, st.retired, st.parked, st.max, st.vmm};
     for (size_t i = 0; i < n && i < sizeof(v) / sizeof(v[0]); i++) out[i] = v[i];
   });
 }

@@ -81,7 +81,7 @@ void mapAt(void* va, size_t bytes, hipMemGenericAllocationHandle_t h, int device
 
 struct Pool {
   std::mutex m;
-  std::vector<std::unique_ptr<Slab>> slabs;  // every live exported slab (released only by a trim)
+  std::vector<std::unique_ptr<Slab>> slabs;  // every live exported slab (freed only by a trim)
   std::vector<Slab*> free;
   uint64_t nextId = 1;
   struct Mapping {
@@ -89,10 +89,16 @@ struct Pool {
     void* ptr;
     size_t bytes;
     size_t users;  // executors holding it (import / unimport)
-    hipMemGenericAllocationHandle_t handle;
+    hipMemGenericAllocationHandle_t handle;  // VMM (nullptr: a hipIpc mapping)
   };
-  std::map<std::pair<int, uint64_t>, Mapping> imports;  // (exporter pid, slab id)
-  size_t opens = 0, trims = 0, trimmedBytes = 0, closes = 0, retired = 0, retiredBytes = 0;
+  // (exporter pid, slab id (VMM) or exporter address (hipIpc))
+  std::map<std::pair<int, uint64_t>, Mapping> imports;
+  // hipIpc: device -> [start, end) of every slab a trim freed: no later slab
+  // may overlap one (the runtime hands out pieces of freed blocks again; an
+  // export over such memory failed, and a peer's import of it showed stale
+  // pages, profiles/round4/r4d_*, r4e_*)
+  std::map<int, std::map<uintptr_t, uintptr_t>> retiredRanges;
+  size_t opens = 0, trims = 0, trimmedBytes = 0, closes = 0, retired = 0, parked = 0;
   static Pool& get() {
     static Pool* p = new Pool();  // never destroyed: process exit releases device memory
     return *p;
@@ -117,7 +123,20 @@ size_t poolMax() {
   return v;
 }
 
-// ---- the fd server ---------------------------------------------------------
+bool overlapsRetired(const Pool& p, int device, const void* ptr, size_t bytes) {
+  auto d = p.retiredRanges.find(device);
+  if (d == p.retiredRanges.end()) return false;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(ptr), b = a + bytes;
+  auto it = d->second.upper_bound(a);  // first range starting after a
+  if (it != d->second.end() && it->first < b) return true;
+  if (it != d->second.begin()) {
+    --it;
+    if (it->second > a) return true;
+  }
+  return false;
+}
+
+// ---- the fd server (VMM) -----------------------------------------------------
 //
 // Requests are one uint64 slab id per connection; the answer is a Reply,
 // with the slab's dma-buf fd attached (SCM_RIGHTS) when ok.  Only processes
@@ -258,11 +277,14 @@ void closeUnusedLocked(Pool& p) {
   for (auto it = p.imports.begin(); it != p.imports.end();) {
     Pool::Mapping& mp = it->second;
     if (mp.users == 0) {
-      GLOO_AMD_HIP_RELEASE(hipMemUnmap(mp.ptr, mp.bytes));
-      GLOO_AMD_HIP_RELEASE(hipMemRelease(mp.handle));
+      if (mp.handle) {
+        GLOO_AMD_HIP_RELEASE(hipMemUnmap(mp.ptr, mp.bytes));
+        GLOO_AMD_HIP_RELEASE(hipMemRelease(mp.handle));
+        p.retired++;  // the range stays reserved, never mapped again
+      } else {
+        GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(mp.ptr));
+      }
       p.closes++;
-      p.retired++;  // the range stays reserved, never mapped again
-      p.retiredBytes += mp.bytes;
       it = p.imports.erase(it);
     } else {
       ++it;
@@ -270,19 +292,31 @@ void closeUnusedLocked(Pool& p) {
   }
 }
 
-// Releases every free-listed slab; p.m held.  A slab is free-listed only
-// after its executor's collective tear-down barrier (no peer writes it any
-// more), and the trims that call this are collective: every peer has closed
-// the mappings no executor holds first.
+// Frees every free-listed slab; p.m held.  A slab is free-listed only after
+// its executor's collective tear-down barrier (no peer writes it any more),
+// and the trims that call this are collective: every peer has closed the
+// mappings no executor holds first (ROCm 7 fails the next hipIpc export of
+// memory allocated over a slab freed while a peer still mapped it,
+// profiles/round4/r4e_*).  VMM: unmap and release, the range stays reserved;
+// hipIpc: hipFree, and the address range is retired.
 void freeUnusedLocked(Pool& p) {
   for (Slab* s : p.free) {
     for (size_t i = 0; i < p.slabs.size(); i++)
       if (p.slabs[i].get() == s) {
-        GLOO_AMD_HIP_RELEASE(hipMemUnmap(s->ptr, s->bytes));
-        GLOO_AMD_HIP_RELEASE(hipMemRelease(s->handle));
-        if (s->fd >= 0) ::close(s->fd);
+        if (s->handle) {
+          GLOO_AMD_HIP_RELEASE(hipMemUnmap(s->ptr, s->bytes));
+          GLOO_AMD_HIP_RELEASE(hipMemRelease(s->handle));
+          if (s->fd >= 0) ::close(s->fd);
+        } else {
+          int prev = -1;
+          (void)hipGetDevice(&prev);
+          (void)hipSetDevice(s->device);
+          GLOO_AMD_HIP_RELEASE(hipFree(s->ptr));
+          if (prev >= 0) (void)hipSetDevice(prev);
+          p.retiredRanges[s->device][reinterpret_cast<uintptr_t>(s->ptr)] =
+              reinterpret_cast<uintptr_t>(s->ptr) + s->bytes;
+        }
         p.retired++;
-        p.retiredBytes += s->bytes;
         p.trimmedBytes += s->bytes;
         p.slabs.erase(p.slabs.begin() + (long)i);
         break;
@@ -315,19 +349,17 @@ struct DeviceScope {
 void releaseAllAtExit() {
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
-  if (g_serverPid != ::getpid() && p.imports.empty()) return;  // a forked child owns nothing
-  for (auto& kv : p.imports) {
-    (void)hipMemUnmap(kv.second.ptr, kv.second.bytes);
-    (void)hipMemRelease(kv.second.handle);
-  }
-  p.imports.clear();
-  for (auto& s : p.slabs) {
-    (void)hipMemUnmap(s->ptr, s->bytes);
-    (void)hipMemRelease(s->handle);
-    if (s->fd >= 0) ::close(s->fd);
-  }
-  p.slabs.clear();
-  p.free.clear();
+  for (auto& kv : p.imports)
+    if (kv.second.handle) {
+      (void)hipMemUnmap(kv.second.ptr, kv.second.bytes);
+      (void)hipMemRelease(kv.second.handle);
+    }
+  for (auto& s : p.slabs)
+    if (s->handle) {
+      (void)hipMemUnmap(s->ptr, s->bytes);
+      (void)hipMemRelease(s->handle);
+      if (s->fd >= 0) ::close(s->fd);
+    }
 }
 void registerAtExit() {
   static std::once_flag once;
@@ -344,10 +376,48 @@ uint64_t incarnation() {
   return v;
 }
 
+bool vmm() {
+  static const bool v = [] {
+    const char* e = std::getenv("GLOO_AMD_IPC");
+    if (e && std::string(e) == "hipipc") return false;
+    if (e && std::string(e) == "vmm") return true;
+    // HIP 7.0.51831 (PyTorch's bundled runtime) crashes in
+    // hipMemImportFromShareableHandle: profiles/round5/r5h_*
+    int version = 0;
+    if (hipRuntimeGetVersion(&version) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return version >= 70200000;
+  }();
+  return v;
+}
+
+size_t maxSlabBytes() {
+  // hipIpc: imports of 2^31 bytes and more hang (profiles/round3/r3t_*); the
+  // size classes above 1 GiB are multiples of 256 MiB, so 1.75 GiB
+  return vmm() ? ~size_t(0) : size_t(7) << 28;
+}
+
+Remote describe(const Slab& s) {
+  Remote r;
+  r.pid = (int)::getpid();
+  r.incarnation = incarnation();
+  r.id = s.id;
+  r.ptr = reinterpret_cast<uint64_t>(s.ptr);
+  r.ipcHandle = s.ipcHandle;
+  return r;
+}
+
 Slab* acquire(int device, size_t bytes, bool fine) {
   const size_t want = sizeClass(bytes);
-  ensureServer();
-  registerAtExit();
+  GLOO_AMD_ENFORCE(want <= maxSlabBytes(), "a cross-process block of ", want, " B: HIP IPC imports of 2 GiB and more ",
+                   "hang on this HIP runtime, so at most ", maxSlabBytes(), " B can be shared (the VMM mechanism of HIP ",
+                   "7.2 and later has no such limit: ipc.h)");
+  if (vmm()) {
+    ensureServer();
+    registerAtExit();
+  }
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
   for (size_t i = 0; i < p.free.size(); i++) {
@@ -362,17 +432,48 @@ Slab* acquire(int device, size_t bytes, bool fine) {
   s->bytes = want;
   s->device = device;
   s->fine = fine;
-  const hipMemAllocationProp prop = propFor(device, fine);
-  GLOO_AMD_HIP_ALLOC(hipMemCreate(&s->handle, want, &prop, 0));
-  try {
-    void* va = freshRange(want);
-    mapAt(va, want, s->handle, device);
-    s->ptr = static_cast<char*>(va);
-    GLOO_AMD_HIP_CHECK(hipMemExportToShareableHandle(&s->fd, s->handle, hipMemHandleTypePosixFileDescriptor, 0));
-  } catch (...) {
-    if (s->ptr) (void)hipMemUnmap(s->ptr, want);
-    (void)hipMemRelease(s->handle);
-    throw;
+  if (vmm()) {
+    const hipMemAllocationProp prop = propFor(device, fine);
+    GLOO_AMD_HIP_ALLOC(hipMemCreate(&s->handle, want, &prop, 0));
+    try {
+      void* va = freshRange(want);
+      mapAt(va, want, s->handle, device);
+      s->ptr = static_cast<char*>(va);
+      GLOO_AMD_HIP_CHECK(hipMemExportToShareableHandle(&s->fd, s->handle, hipMemHandleTypePosixFileDescriptor, 0));
+    } catch (...) {
+      if (s->ptr) (void)hipMemUnmap(s->ptr, want);
+      (void)hipMemRelease(s->handle);
+      throw;
+    }
+  } else {
+    // Never export memory overlapping a retired slab, and never keep a block
+    // the runtime refuses to export: park it (allocated, not exported) and
+    // allocate again while it is held, then free the parked blocks.
+    std::vector<void*> parked;
+    void* ptr = nullptr;
+    hipError_t eh = hipSuccess;
+    for (;;) {
+      ptr = nullptr;
+      hipError_t e = fine ? hipExtMallocWithFlags(&ptr, want, hipDeviceMallocFinegrained) : hipMalloc(&ptr, want);
+      if (e != hipSuccess) {
+        for (void* q : parked) (void)hipFree(q);
+        GLOO_AMD_HIP_ALLOC(e);
+      }
+      if (!overlapsRetired(p, device, ptr, want)) {
+        eh = hipIpcGetMemHandle(&s->ipcHandle, ptr);
+        if (eh == hipSuccess) break;
+        (void)hipGetLastError();
+      }
+      parked.push_back(ptr);
+      p.parked++;
+      if (parked.size() > 64) {
+        for (void* q : parked) (void)hipFree(q);
+        GLOO_AMD_ENFORCE(false, "IPC pool: no exportable block of ", want, " B after 64 tries (",
+                         eh == hipSuccess ? "retired ranges" : hipGetErrorString(eh), ")");
+      }
+    }
+    for (void* q : parked) GLOO_AMD_HIP_RELEASE(hipFree(q));
+    s->ptr = static_cast<char*>(ptr);
   }
   s->id = p.nextId++;
   p.slabs.push_back(std::move(s));
@@ -415,34 +516,68 @@ bool overCeiling(size_t more) {
   return !p.free.empty() && slabBytesLocked(p) + more > poolMax();
 }
 
-void* import(int pid, uint64_t inc, uint64_t id, size_t bytes, int device) {
-  registerAtExit();
+namespace {
+// Drops a mapping of either kind; p.m held.
+void dropMapping(Pool& p, Pool::Mapping& mp) {
+  if (mp.handle) {
+    GLOO_AMD_HIP_RELEASE(hipMemUnmap(mp.ptr, mp.bytes));
+    GLOO_AMD_HIP_RELEASE(hipMemRelease(mp.handle));
+    p.retired++;
+  } else {
+    GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(mp.ptr));
+  }
+}
+
+// Bytes the runtime maps from `m` to the end of its allocation (a hipIpc
+// import spans the exporter's whole slab), or 0 when it keeps no record.
+size_t mappedSpan(void* m) {
+  void* rb = nullptr;
+  size_t rs = 0;
+  size_t span = 0;
+  if (hipMemGetAddressRange(&rb, &rs, m) == hipSuccess && rb && static_cast<char*>(rb) + rs > static_cast<char*>(m))
+    span = (size_t)(static_cast<char*>(rb) + rs - static_cast<char*>(m));
+  (void)hipGetLastError();
+  return span;
+}
+}  // namespace
+
+void* import(const Remote& r, size_t bytes, int device) {
   Pool& p = Pool::get();
-  const auto key = std::make_pair(pid, id);
+  const bool viaVmm = vmm();
+  if (viaVmm) registerAtExit();
+  const auto key = std::make_pair(r.pid, viaVmm ? r.id : r.ptr);
   {
     std::lock_guard<std::mutex> lk(p.m);
     auto it = p.imports.find(key);
     if (it != p.imports.end()) {
-      if (it->second.incarnation == inc) {
-        GLOO_AMD_ENFORCE(it->second.bytes >= bytes, "slab ", id, " of pid ", pid, " mapped at ", it->second.bytes,
+      if (it->second.incarnation == r.incarnation) {
+        if (!viaVmm && it->second.bytes < bytes) it->second.bytes = std::max(it->second.bytes, mappedSpan(it->second.ptr));
+        GLOO_AMD_ENFORCE(it->second.bytes >= bytes, "slab of pid ", r.pid, " mapped at ", it->second.bytes,
                          " B, now published at ", bytes, " B");
         it->second.users++;
         return it->second.ptr;
       }
       // a new process reusing a dead one's pid: its mapping is of no use
-      GLOO_AMD_HIP_RELEASE(hipMemUnmap(it->second.ptr, it->second.bytes));
-      GLOO_AMD_HIP_RELEASE(hipMemRelease(it->second.handle));
-      p.retired++;
-      p.retiredBytes += it->second.bytes;
+      dropMapping(p, it->second);
       p.imports.erase(it);
     }
+    if (!viaVmm) {
+      void* m = nullptr;
+      DeviceScope ds(device);
+      GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&m, r.ipcHandle, hipIpcMemLazyEnablePeerAccess));
+      p.opens++;
+      // the mapping spans the exporter's whole slab (its size class), not
+      // just what this first importer asked for
+      p.imports[key] = {r.incarnation, m, std::max(bytes, mappedSpan(m)), 1, nullptr};
+      return m;
+    }
   }
-  // The pool's lock is NOT held across the request: the exporter may be
+  // VMM.  The pool's lock is NOT held across the request: the exporter may be
   // importing from this process at the same moment, and its request is
   // answered by this process's fd server, which takes the lock.
   size_t slabBytes = 0;
-  const int fd = fetchFd(pid, inc, id, &slabBytes);
-  GLOO_AMD_ENFORCE(slabBytes >= bytes, "slab ", id, " of pid ", pid, " holds ", slabBytes, " B, ", bytes,
+  const int fd = fetchFd(r.pid, r.incarnation, r.id, &slabBytes);
+  GLOO_AMD_ENFORCE(slabBytes >= bytes, "slab ", r.id, " of pid ", r.pid, " holds ", slabBytes, " B, ", bytes,
                    " B expected");
   DeviceScope ds(device);
   hipMemGenericAllocationHandle_t h = nullptr;
@@ -460,17 +595,16 @@ void* import(int pid, uint64_t inc, uint64_t id, size_t bytes, int device) {
   }
   std::lock_guard<std::mutex> lk(p.m);
   auto it = p.imports.find(key);
-  if (it != p.imports.end() && it->second.incarnation == inc) {
+  if (it != p.imports.end() && it->second.incarnation == r.incarnation) {
     // another thread of this process mapped it meanwhile: keep that one
     GLOO_AMD_HIP_RELEASE(hipMemUnmap(va, slabBytes));
     GLOO_AMD_HIP_RELEASE(hipMemRelease(h));
     p.retired++;
-    p.retiredBytes += slabBytes;
     it->second.users++;
     return it->second.ptr;
   }
   p.opens++;
-  p.imports[key] = {inc, va, slabBytes, 1, h};
+  p.imports[key] = {r.incarnation, va, slabBytes, 1, h};
   return va;
 }
 
@@ -487,8 +621,9 @@ Stats stats() {
   s.trimmedBytes = p.trimmedBytes;
   s.closes = p.closes;
   s.retired = p.retired;
-  s.retiredBytes = p.retiredBytes;
+  s.parked = p.parked;
   s.max = poolMax();
+  s.vmm = vmm() ? 1 : 0;
   return s;
 }
 

@@ -252,12 +252,20 @@ class SendBuffer : public Buffer {
       }
     } else if (r.deviceLanding) {
       // device memory of another process in a 2 GiB+ allocation: its landing slab
-      landingImport_ = static_cast<char*>(
-          ipc::import(r.pid, r.landingIncarnation, r.landingSlab, r.size, ctx.device()));
+      ipc::Remote rm;
+      rm.pid = r.pid;
+      rm.incarnation = r.landingIncarnation;
+      rm.id = r.landingSlab;
+      landingImport_ = static_cast<char*>(ipc::import(rm, r.size, ctx.device()));
       remote_ = landingImport_;
       viaLanding_ = true;
       dstDevice_ = true;
     } else {
+      GLOO_AMD_ENFORCE(r.alloc < kMaxImportBytes, "rank ", peer_, "'s receive buffer (slot ", slot_,
+                       ") lies in a device allocation of ", r.alloc, " B; HIP IPC imports of 2 GiB and more hang, ",
+                       "and this HIP runtime lacks a working VMM import (ipc.h), so a peer process cannot write into ",
+                       "it: allocate receive buffers below ", kMaxImportBytes, " B, run the ranks as threads, or use ",
+                       "HIP 7.2 or later");
       GLOO_AMD_ENFORCE(r.ipc, "rank ", peer_, "'s receive buffer is not IPC-exportable");
       // The caller's memory cannot come from the IPC slab pool (ipc.h);
       // this import is used by eager copies only, never captured into a
@@ -343,7 +351,7 @@ class RecvBuffer : public Buffer {
         size_t allocSize = 0;
         const bool ranged = hipMemGetAddressRange(&base, &allocSize, ptr_) == hipSuccess && base;
         (void)hipGetLastError();
-        if (ranged && allocSize >= kMaxImportBytes) {
+        if (ranged && allocSize >= kMaxImportBytes && ipc::vmm()) {
           deviceLanding_ = ipc::acquire(ctx.device(), size_, true);
           r.deviceLanding = 1;
           r.landingSlab = deviceLanding_->id;

@@ -1,46 +1,51 @@
-// ipc.h — device memory shared between rank processes (inbox arenas and
-// mailboxes), through HIP's virtual memory management with dma-buf file
-// descriptors.
+// ipc.h — device memory shared between rank processes (inbox arenas,
+// mailboxes, transport landing slabs).
 //
-// Why this form ("Cross-process memory"):
-//   * hipIpcGetMemHandle / hipIpcOpenMemHandle, the route of rounds 1-4,
-//     hangs on imports of 2 GiB and more on ROCm 7 / MI355X, and an import of
-//     a byte-identical handle (a freed block re-exported at the same address)
-//     was handed the old pages (profiles/round3/r3b_*, r3t_*, r3u_*).
-//   * A VMM block (hipMemCreate, POSIX-fd handle type) exported with
-//     hipMemExportToShareableHandle and imported with
-//     hipMemImportFromShareableHandle maps at any size — 2.5 GiB end to end in
-//     22 ms (tools/vmm_probe, profiles/round5/r5b_vmm_fresh_va.jsonl).
-//   * But a virtual range must never be mapped twice: a new block mapped at a
-//     virtual address an earlier mapping used showed the earlier block's
-//     pages, and then faulted (r5a_vmm_same_va_*, r5b_vmm_same_va.err) —
-//     translations of the old mapping survive the unmap.  With every mapping
-//     at a range never used before, the same churn — free, re-allocate,
-//     re-import, graph copies into the mapping — is exact (r5b_vmm_fresh_va).
-// So:
-//   Exporter side: every block another process maps is a Slab of a
-//   process-wide pool: a VMM allocation mapped at a fresh virtual range,
-//   exported once as a dma-buf fd that the process keeps open.  Peers obtain
-//   that fd from this process's fd server — a thread on an abstract Unix
-//   socket named by (pid, incarnation) that answers "slab id" with the fd
-//   (SCM_RIGHTS), to processes of the same user only.  An executor that no
-//   longer needs a slab returns it to the pool; the next executor of that
-//   size class on that device reuses it (its peers' mappings too).  A trim
-//   (when the pool would pass GLOO_AMD_IPC_POOL_MAX, default 16 GiB) unmaps
-//   and releases the free slabs; their virtual ranges stay reserved and are
-//   never mapped again (retired).  Trims are collective (every rank first
-//   closes the mappings no executor holds, then frees), so no slab is
-//   released while a peer still maps it.
-//   Importer side: a mapping is opened once per (exporter pid, incarnation,
-//   slab id) at a fresh virtual range and kept, counted by the executors that
-//   hold it; a trim closes the ones no executor holds (unmap, release; the
-//   range is retired).  The incarnation (a random word per process) tells a
-//   new process that reuses a dead one's pid apart.
-//   Size classes are powers of two of 2 MiB up to 1 GiB, then multiples of
-//   256 MiB; there is no upper bound.
+// Two mechanisms, one per HIP runtime build ("Cross-process
+// memory"); every rank of a collective must use the same one, and the
+// executor refuses a mix on every rank:
 //
-// Callers still verify each import (executor.cc writes a nonce at the slab's
-// start and every importer reads it back): a mismatch is a hard error.
+// VMM (HIP runtime 7.2 and later: the system ROCm of this image).  A slab is
+//   a hipMemCreate block exported once as a dma-buf file descriptor.
+//   * Any size maps: 2.5 GiB end to end in 22 ms (tools/vmm_probe,
+//     profiles/round5/r5b_vmm_fresh_va.jsonl), where a hipIpc import of 2 GiB
+//     or more hangs (profiles/round3/r3t_*, r3u_*).
+//   * A virtual range is never mapped twice: a new block mapped where an
+//     earlier mapping lived showed the earlier block's pages, then faulted
+//     (r5a_vmm_same_va_*, r5b_vmm_same_va.err); with every mapping at a fresh
+//     range the same churn is exact.  Released slabs and closed imports leave
+//     their ranges reserved (retired).
+//   * Peers obtain a slab's fd from its owner's fd server: a thread on an
+//     abstract Unix socket named by (pid, incarnation) that answers a slab id
+//     with the fd (SCM_RIGHTS), to processes of the same user only.
+//   * hipMemImportFromShareableHandle of HIP 7.0.51831 — the runtime PyTorch
+//     2.10+rocm7.0 bundles and loads in place of the system one — crashes
+//     (fd by value) or refuses (fd by address): profiles/round5/r5h_*.
+//     Processes on such a runtime use hipIpc below.
+//
+// hipIpc (older runtimes; GLOO_AMD_IPC=hipipc forces it).  A slab is a
+//   hipMalloc / fine-grained block exported with hipIpcGetMemHandle, ONCE:
+//   a freed block re-exported at the same address was imported as the old
+//   pages (profiles/round3/r3b_*), so slabs are reused, not freed, and a
+//   trim's freed slabs retire their address ranges (a block the runtime
+//   hands out inside one is parked, never exported).  Imports of 2 GiB and
+//   more hang, so slabs stay below 2^31 bytes (size classes stop at
+//   multiples of 256 MiB; the executor refuses larger cross-process arenas
+//   on this mechanism).  Under heavy churn the runtime can keep handing out
+//   retired addresses until acquire gives up (64 tries): the round-5 churn
+//   test hit that (profiles/round5/r5c_pytest_churn_hipipc.log); it runs on
+//   the VMM mechanism.
+//
+// Both: every executor that no longer needs a slab returns it to the pool,
+// and the next executor of that size class on that device reuses it (its
+// peers' mappings too).  A trim (when the pool would pass
+// GLOO_AMD_IPC_POOL_MAX, default 16 GiB) is collective: every rank first
+// closes the mappings no executor holds, then frees its free slabs.  Imports
+// are kept per (exporter pid, incarnation, slab) and counted per executor;
+// the incarnation (a random word per process) tells a new process that
+// reuses a dead one's pid apart.  Callers verify each import (the executor
+// writes a nonce at the slab's start and every importer reads it back): a
+// mismatch is a hard error.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -51,33 +56,48 @@
 namespace gloo_amd {
 namespace ipc {
 
+// The mechanism of this process: true = VMM (see above).
+bool vmm();
+// Largest slab the mechanism can share (hipIpc: below 2 GiB; VMM: no limit).
+size_t maxSlabBytes();
+
 struct Slab {
   char* ptr = nullptr;   // this process's mapping
   size_t bytes = 0;      // the size class (>= what was asked for)
   int device = -1;
-  bool fine = false;     // uncached (cross-device coherent) memory
-  uint64_t id = 0;       // names the slab to peers (the fd server)
-  hipMemGenericAllocationHandle_t handle = nullptr;
-  int fd = -1;           // the exported dma-buf
+  bool fine = false;     // cross-device coherent memory (VMM: uncached; hipIpc: fine-grained)
+  uint64_t id = 0;       // names the slab to peers
+  hipMemGenericAllocationHandle_t handle = nullptr;  // VMM
+  int fd = -1;                                       // VMM: the exported dma-buf
+  hipIpcMemHandle_t ipcHandle;                       // hipIpc
 };
+
+// What a peer publishes about one of its slabs.
+struct Remote {
+  int pid = 0;
+  uint64_t incarnation = 0;
+  uint64_t id = 0;                 // VMM
+  uint64_t ptr = 0;                // hipIpc: the exporter's address
+  hipIpcMemHandle_t ipcHandle;     // hipIpc
+};
+Remote describe(const Slab& s);
 
 // A random word fixed for the life of this process.
 uint64_t incarnation();
 
-// A slab of at least `bytes` on `device` (uncached or not), exported; starts
-// this process's fd server on first use.
+// A slab of at least `bytes` on `device`, exported (VMM: starts this
+// process's fd server on first use).
 Slab* acquire(int device, size_t bytes, bool fine);
-// Back to the pool (not released).  The caller has made sure no peer still
-// writes into it (the executor's tear-down barrier).
+// Back to the pool.  The caller has made sure no peer still writes into it
+// (the executor's tear-down barrier).
 void release(Slab* s);
 
-// The mapping of a peer process's slab `id`, accessible from `device`
-// (opened once, kept).  `bytes`: what the caller will touch.
-void* import(int pid, uint64_t incarnation, uint64_t id, size_t bytes, int device);
+// The mapping of a peer process's slab, accessible from `device` (opened
+// once, kept).  `bytes`: what the caller will touch.
+void* import(const Remote& r, size_t bytes, int device);
 // Drops an executor's hold on a mapping (kept until a trim).
 void unimport(void* mapped);
-// The two halves of a trim (above): close this process's mappings no
-// executor holds; release its free-listed slabs.
+// The two halves of a trim (above).
 void closeUnusedImports();
 void freeUnusedSlabs();
 // Whether the pool holds free slabs and would pass its ceiling with `more`
@@ -91,7 +111,8 @@ inline void trim() {
 
 struct Stats {
   size_t slabs = 0, slabBytes = 0, free = 0, imports = 0, opens = 0;
-  size_t trims = 0, trimmedBytes = 0, closes = 0, retired = 0, retiredBytes = 0, max = 0;
+  size_t trims = 0, trimmedBytes = 0, closes = 0, retired = 0, parked = 0, max = 0;
+  size_t vmm = 0;  // 1: the VMM mechanism
 };
 Stats stats();
 

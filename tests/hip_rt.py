@@ -68,3 +68,8 @@ def mem_info():
     f, t = ctypes.c_size_t(), ctypes.c_size_t()
     check(lib().hipMemGetInfo(ctypes.byref(f), ctypes.byref(t)), "hipMemGetInfo")
     return f.value, t.value
+
+
+def memset(p, value, nbytes):
+    check(lib().hipMemset(ctypes.c_void_p(p), ctypes.c_int(value), ctypes.c_size_t(nbytes)), "hipMemset")
+    synchronize()

@@ -50,9 +50,10 @@ TRANSPORT_WORKER = r'''
 import ctypes, os, sys, time, json
 import numpy as np
 sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
-import torch, gloo_amd
+sys.path.insert(0, os.path.join(os.environ["GLOO_AMD_ROOT"], "tests"))
+import gloo_amd, hip_rt   # no torch: the system HIP runtime (ipc.h)
 rank, store, case = int(sys.argv[1]), sys.argv[2], sys.argv[3]
-torch.cuda.set_device(0)
+hip_rt.set_device(0)
 ctx = gloo_amd.Context(rank, 2, store, device=0, timeout_ms=20000)
 t = gloo_amd.Transport(ctx)
 out = {}
@@ -67,11 +68,11 @@ if case == "reuse":
         rb.wait_recv()
         out["host"] = h.tolist()
         rb.close()
-        d = torch.zeros(4, dtype=torch.int32, device="cuda:0")
-        rb = t.buffer(0, 2, d.data_ptr(), 16, False)   # the same channel, now device memory
+        d = hip_rt.malloc(16)
+        hip_rt.memset(d, 0, 16)
+        rb = t.buffer(0, 2, d, 16, False)               # the same channel, now device memory
         rb.wait_recv()
-        torch.cuda.synchronize()
-        out["device"] = d.cpu().tolist()
+        out["device"] = hip_rt.d2h(d, np.zeros(4, np.int32)).tolist()
         rb.close()
         nb = t.buffer(0, 3, 0, 0, False)               # a notification buffer on it
         nb.wait_recv()
@@ -83,9 +84,9 @@ if case == "reuse":
         sb.send(0, 16)
         sb.wait_send()
         sb.close()
-        dsrc = torch.tensor([5, 6, 7, 8], dtype=torch.int32, device="cuda:0")
-        torch.cuda.synchronize()
-        sb = t.buffer(1, 2, dsrc.data_ptr(), 16, True)
+        dsrc = hip_rt.malloc(16)
+        hip_rt.h2d(dsrc, np.array([5, 6, 7, 8], np.int32))
+        sb = t.buffer(1, 2, dsrc, 16, True)
         sb.send(0, 16)
         sb.wait_send()
         sb.close()
@@ -139,10 +140,10 @@ elif case == "large_host":
         hs = np.zeros(n1, np.uint8)
         hs[:1 << 20] = w1[:1 << 20]
         hs[n1 - 17:] = w1[n1 - 17:]
-        ds = torch.from_numpy(w2[5:].copy()).to("cuda:0")
-        torch.cuda.synchronize()
+        ds = hip_rt.malloc(2 << 20)
+        hip_rt.h2d(ds, w2[5:].copy())
         s1 = t.buffer(1, 1, hp(hs), n1, True)
-        s2 = t.buffer(1, 2, ds.data_ptr(), 2 << 20, True)
+        s2 = t.buffer(1, 2, ds, 2 << 20, True)
         s1.send(0, 1 << 20, 0)
         s1.send(n1 - 17, 17, n1 - 17)
         s2.send(0, 2 << 20, 5)
@@ -177,30 +178,29 @@ elif case == "big_alloc":
     n = 5 << 29                                         # 2.5 GiB
     far = n - (16 << 20) - 5                            # past 2 GiB, unaligned
     if rank == 1:
-        big = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
-        torch.cuda.synchronize()
-        rb = t.buffer(0, 1, big.data_ptr(), n, False)
+        big = hip_rt.malloc(n)
+        hip_rt.memset(big, 0, n)
+        rb = t.buffer(0, 1, big, n, False)
         rb.wait_recv()
         rb.wait_recv()
-        torch.cuda.synchronize()
-        a = big[:1 << 20].cpu().numpy()
-        b = big[far:far + (16 << 20)].cpu().numpy()
+        a = hip_rt.d2h(big, np.zeros(1 << 20, np.uint8))
+        b = hip_rt.d2h(big + far, np.zeros(16 << 20, np.uint8))
+        c = hip_rt.d2h(big + (1 << 20), np.zeros(4096, np.uint8))
         out["bad"] = [int((a != (np.arange(1 << 20) % 251)).sum()),
                       int((b != (np.arange(16 << 20) % 253)).sum()),
-                      int(big[(1 << 20):(1 << 20) + 4096].sum().item())]
+                      int(c.astype(np.int64).sum())]
         rb.close()
-        del big
+        hip_rt.free(big)
     else:
-        src = torch.from_numpy((np.arange(16 << 20) % 253).astype(np.uint8)).to("cuda:0")
-        src[:1 << 20] = torch.from_numpy((np.arange(1 << 20) % 251).astype(np.uint8)).to("cuda:0")
+        src = hip_rt.malloc(16 << 20)
+        hip_rt.h2d(src, (np.arange(16 << 20) % 253).astype(np.uint8))
+        hip_rt.h2d(src, (np.arange(1 << 20) % 251).astype(np.uint8))
         # the second message's bytes: a second buffer on the same slot is not
         # allowed, so send [0, 1 MiB) first, then restore and send the rest
-        torch.cuda.synchronize()
-        sb = t.buffer(1, 1, src.data_ptr(), 16 << 20, True)
+        sb = t.buffer(1, 1, src, 16 << 20, True)
         sb.send(0, 1 << 20, 0)
         sb.wait_send()
-        src[:1 << 20] = torch.from_numpy((np.arange(1 << 20) % 253).astype(np.uint8)).to("cuda:0")
-        torch.cuda.synchronize()
+        hip_rt.h2d(src, (np.arange(1 << 20) % 253).astype(np.uint8))
         sb.send(0, 16 << 20, far)
         sb.wait_send()
         sb.close()
@@ -211,7 +211,7 @@ print("RESULT" + json.dumps(out), flush=True)
 
 
 def run_transport_case(tmp_path, case):
-    pytest.importorskip("torch")
+    pytest.importorskip("torch")  # (the GPU check; the worker itself runs without torch)
     import json
     import sys
     w = tmp_path / "w.py"
