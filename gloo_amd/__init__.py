@@ -304,8 +304,10 @@ class Transport:
     """The xGMI transport's bound buffers (gloo::transport::Pair /
     Buffer, gloo/transport/pair.h:33-41, buffer.h:26-34) over a Context:
     construction is collective.  Receive buffers in device memory are written
-    in place by the peer (HIP IPC across processes); host memory across
-    processes travels in payload records of at most 40 bytes per message."""
+    in place by the peer (hipIpc across processes; an allocation of 2 GiB or
+    more through a VMM landing slab); host receive buffers across processes,
+    of any length, through a landing segment in node shared memory, copied
+    into the buffer at wait_recv."""
 
     def __init__(self, ctx, stream=0):
         h = ctypes.c_void_p()
@@ -346,9 +348,9 @@ def ipc_stats():
     """This process's pool of cross-process slabs (gloo_amd/include/gloo_amd/ipc.h):
     slabs exported and their bytes, slabs free for reuse, peer slabs mapped,
     imports made; trims, bytes they freed, mappings they closed, retired
-    ranges (VMM: virtual ranges never mapped again; hipIpc: freed addresses
-    never exported again), allocations parked (hipIpc), the ceiling
-    (GLOO_AMD_IPC_POOL_MAX) and the mechanism (1: VMM, 0: hipIpc)."""
+    addresses and allocations parked (hipIpc only: VMM never frees a slab),
+    the ceiling (GLOO_AMD_IPC_POOL_MAX, hipIpc) and the mechanism (1: VMM,
+    0: hipIpc)."""
     out = (ctypes.c_uint64 * 12)()
     _check(lib.gloo_hip_ipc_stats_ex(out, 12))
     return {"slabs": out[0], "slab_bytes": out[1], "free": out[2], "peer_slabs_mapped": out[3],
@@ -358,7 +360,8 @@ def ipc_stats():
 
 def ipc_trim(ctx=None):
     """Collective over ctx's ranks: close the peer mappings no executor
-    holds, barrier, free the pooled slabs no executor holds (ipc.h).
+    holds, barrier, free the pooled slabs no executor holds (ipc.h; hipIpc
+    only, VMM slabs stay for reuse).
     ctx=None: this process alone (its peers are gone)."""
     lib.gloo_hip_ipc_trim.argtypes = [ctypes.c_void_p]
     _check(lib.gloo_hip_ipc_trim(ctx._h if ctx is not None else None))

@@ -276,14 +276,10 @@ int fetchFd(int pid, uint64_t inc, uint64_t id, size_t* bytes) {
 void closeUnusedLocked(Pool& p) {
   for (auto it = p.imports.begin(); it != p.imports.end();) {
     Pool::Mapping& mp = it->second;
-    if (mp.users == 0) {
-      if (mp.handle) {
-        GLOO_AMD_HIP_RELEASE(hipMemUnmap(mp.ptr, mp.bytes));
-        GLOO_AMD_HIP_RELEASE(hipMemRelease(mp.handle));
-        p.retired++;  // the range stays reserved, never mapped again
-      } else {
-        GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(mp.ptr));
-      }
+    // VMM mappings stay: their memory would only come back with their virtual
+    // range, and a freed range handed out again showed stale pages (ipc.h)
+    if (mp.users == 0 && !mp.handle) {
+      GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(mp.ptr));
       p.closes++;
       it = p.imports.erase(it);
     } else {
@@ -292,37 +288,34 @@ void closeUnusedLocked(Pool& p) {
   }
 }
 
-// Frees every free-listed slab; p.m held.  A slab is free-listed only after
-// its executor's collective tear-down barrier (no peer writes it any more),
-// and the trims that call this are collective: every peer has closed the
-// mappings no executor holds first (ROCm 7 fails the next hipIpc export of
-// memory allocated over a slab freed while a peer still mapped it,
-// profiles/round4/r4e_*).  VMM: unmap and release, the range stays reserved;
-// hipIpc: hipFree, and the address range is retired.
+// Frees every free-listed hipIpc slab and retires its address range; p.m
+// held.  A slab is free-listed only after its executor's collective tear-down
+// barrier (no peer writes it any more), and the trims that call this are
+// collective: every peer has closed the mappings no executor holds first
+// (ROCm 7 fails the next hipIpc export of memory allocated over a slab freed
+// while a peer still mapped it, profiles/round4/r4e_*).  VMM slabs stay.
 void freeUnusedLocked(Pool& p) {
+  std::vector<Slab*> keep;
   for (Slab* s : p.free) {
+    if (s->handle) {  // VMM: kept for reuse (see closeUnusedLocked)
+      keep.push_back(s);
+      continue;
+    }
     for (size_t i = 0; i < p.slabs.size(); i++)
       if (p.slabs[i].get() == s) {
-        if (s->handle) {
-          GLOO_AMD_HIP_RELEASE(hipMemUnmap(s->ptr, s->bytes));
-          GLOO_AMD_HIP_RELEASE(hipMemRelease(s->handle));
-          if (s->fd >= 0) ::close(s->fd);
-        } else {
-          int prev = -1;
-          (void)hipGetDevice(&prev);
-          (void)hipSetDevice(s->device);
-          GLOO_AMD_HIP_RELEASE(hipFree(s->ptr));
-          if (prev >= 0) (void)hipSetDevice(prev);
-          p.retiredRanges[s->device][reinterpret_cast<uintptr_t>(s->ptr)] =
-              reinterpret_cast<uintptr_t>(s->ptr) + s->bytes;
-        }
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(s->device);
+        GLOO_AMD_HIP_RELEASE(hipFree(s->ptr));
+        if (prev >= 0) (void)hipSetDevice(prev);
+        p.retiredRanges[s->device][reinterpret_cast<uintptr_t>(s->ptr)] = reinterpret_cast<uintptr_t>(s->ptr) + s->bytes;
         p.retired++;
         p.trimmedBytes += s->bytes;
         p.slabs.erase(p.slabs.begin() + (long)i);
         break;
       }
   }
-  p.free.clear();
+  p.free = keep;
   p.trims++;
 }
 
@@ -376,19 +369,19 @@ uint64_t incarnation() {
   return v;
 }
 
+int runtimeVersion() {
+  static const int v = [] {
+    int version = 0;
+    if (hipRuntimeGetVersion(&version) != hipSuccess) (void)hipGetLastError();
+    return version;
+  }();
+  return v;
+}
+
 bool vmm() {
   static const bool v = [] {
     const char* e = std::getenv("GLOO_AMD_IPC");
-    if (e && std::string(e) == "hipipc") return false;
-    if (e && std::string(e) == "vmm") return true;
-    // HIP 7.0.51831 (PyTorch's bundled runtime) crashes in
-    // hipMemImportFromShareableHandle: profiles/round5/r5h_*
-    int version = 0;
-    if (hipRuntimeGetVersion(&version) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-    return version >= 70200000;
+    return !(e && std::string(e) == "hipipc");
   }();
   return v;
 }
@@ -513,7 +506,8 @@ void freeUnusedSlabs() {
 bool overCeiling(size_t more) {
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
-  return !p.free.empty() && slabBytesLocked(p) + more > poolMax();
+  // VMM slabs are never released (closeUnusedLocked): nothing to trim
+  return !vmm() && !p.free.empty() && slabBytesLocked(p) + more > poolMax();
 }
 
 namespace {
@@ -581,8 +575,13 @@ void* import(const Remote& r, size_t bytes, int device) {
                    " B expected");
   DeviceScope ds(device);
   hipMemGenericAllocationHandle_t h = nullptr;
-  const hipError_t e = hipMemImportFromShareableHandle(&h, reinterpret_cast<void*>(static_cast<intptr_t>(fd)),
-                                                       hipMemHandleTypePosixFileDescriptor);
+  // HIP 7.2 takes the fd by value (as CUDA does); HIP 7.0.51831, the runtime
+  // PyTorch 2.10+rocm7.0 bundles, takes its address and crashes on the value
+  // (tools/vmm_probe, profiles/round5/r5j_vmm_torch_*)
+  int fdv = fd;
+  void* osHandle = runtimeVersion() >= 70200000 ? reinterpret_cast<void*>(static_cast<intptr_t>(fd))
+                                                : static_cast<void*>(&fdv);
+  const hipError_t e = hipMemImportFromShareableHandle(&h, osHandle, hipMemHandleTypePosixFileDescriptor);
   ::close(fd);
   GLOO_AMD_HIP_ALLOC(e);
   void* va = nullptr;

@@ -1,51 +1,52 @@
 // ipc.h — device memory shared between rank processes (inbox arenas,
 // mailboxes, transport landing slabs).
 //
-// Two mechanisms, one per HIP runtime build ("Cross-process
-// memory"); every rank of a collective must use the same one, and the
-// executor refuses a mix on every rank:
+// The mechanism is HIP's virtual memory management with dma-buf file
+// descriptors (VMM); the rounds 3-4 hipIpc pool remains behind
+// GLOO_AMD_IPC=hipipc.  Every rank of a collective must use the same one,
+// and the executor refuses a mix on every rank.
 //
-// VMM (HIP runtime 7.2 and later: the system ROCm of this image).  A slab is
-//   a hipMemCreate block exported once as a dma-buf file descriptor.
-//   * Any size maps: 2.5 GiB end to end in 22 ms (tools/vmm_probe,
+// VMM.  A slab is a hipMemCreate block exported once as a dma-buf fd.
+//   * Any size maps: 2.5 GiB end to end in ~20 ms (tools/vmm_probe,
 //     profiles/round5/r5b_vmm_fresh_va.jsonl), where a hipIpc import of 2 GiB
 //     or more hangs (profiles/round3/r3t_*, r3u_*).
-//   * A virtual range is never mapped twice: a new block mapped where an
-//     earlier mapping lived showed the earlier block's pages, then faulted
-//     (r5a_vmm_same_va_*, r5b_vmm_same_va.err); with every mapping at a fresh
-//     range the same churn is exact.  Released slabs and closed imports leave
-//     their ranges reserved (retired).
+//   * A virtual range is never mapped twice, and never freed: a new block
+//     mapped where an earlier mapping lived showed the earlier block's pages,
+//     then faulted (r5a_vmm_same_va_*, r5b_vmm_same_va.err), and so did a
+//     range freed with hipMemAddressFree and handed out again by the next
+//     reserve (r5j_vmm_sys_freeva_uncached.jsonl).  Since HIP returns a
+//     block's memory only when its range is freed (tools/vmm_leak.py,
+//     r5i_*), slabs and imports are never released: they are reused by
+//     size class (powers of two of 2 MiB up to 1 GiB, then multiples of
+//     256 MiB), which bounds the pool by the classes a process uses.
 //   * Peers obtain a slab's fd from its owner's fd server: a thread on an
 //     abstract Unix socket named by (pid, incarnation) that answers a slab id
 //     with the fd (SCM_RIGHTS), to processes of the same user only.
-//   * hipMemImportFromShareableHandle of HIP 7.0.51831 — the runtime PyTorch
-//     2.10+rocm7.0 bundles and loads in place of the system one — crashes
-//     (fd by value) or refuses (fd by address): profiles/round5/r5h_*.
-//     Processes on such a runtime use hipIpc below.
+//   * hipMemImportFromShareableHandle takes the fd by value on HIP 7.2 (the
+//     system ROCm) and by address on HIP 7.0.51831 (the runtime PyTorch
+//     2.10+rocm7.0 bundles and loads in place of the system one), which
+//     crashes on the value (r5j_vmm_torch_*): chosen by runtime version.
 //
-// hipIpc (older runtimes; GLOO_AMD_IPC=hipipc forces it).  A slab is a
-//   hipMalloc / fine-grained block exported with hipIpcGetMemHandle, ONCE:
-//   a freed block re-exported at the same address was imported as the old
-//   pages (profiles/round3/r3b_*), so slabs are reused, not freed, and a
-//   trim's freed slabs retire their address ranges (a block the runtime
-//   hands out inside one is parked, never exported).  Imports of 2 GiB and
-//   more hang, so slabs stay below 2^31 bytes (size classes stop at
-//   multiples of 256 MiB; the executor refuses larger cross-process arenas
-//   on this mechanism).  Under heavy churn the runtime can keep handing out
-//   retired addresses until acquire gives up (64 tries): the round-5 churn
-//   test hit that (profiles/round5/r5c_pytest_churn_hipipc.log); it runs on
-//   the VMM mechanism.
+// hipIpc (GLOO_AMD_IPC=hipipc).  A slab is a hipMalloc / fine-grained block
+//   exported with hipIpcGetMemHandle, ONCE: a freed block re-exported at the
+//   same address was imported as the old pages (profiles/round3/r3b_*), so
+//   slabs are reused, and a trim's freed slabs retire their address ranges (a
+//   block the runtime hands out inside one is parked, never exported).
+//   Imports of 2 GiB and more hang, so slabs stay below 2^31 bytes and the
+//   executor refuses larger cross-process arenas.  Under heavy churn the
+//   runtime can keep handing out retired addresses until acquire gives up
+//   after 64 tries (profiles/round5/r5c_pytest_churn_hipipc.log).
+//   Trims (when the pool would pass GLOO_AMD_IPC_POOL_MAX, default 16 GiB)
+//   are collective: every rank first closes the mappings no executor holds,
+//   then frees its free slabs.
 //
-// Both: every executor that no longer needs a slab returns it to the pool,
-// and the next executor of that size class on that device reuses it (its
-// peers' mappings too).  A trim (when the pool would pass
-// GLOO_AMD_IPC_POOL_MAX, default 16 GiB) is collective: every rank first
-// closes the mappings no executor holds, then frees its free slabs.  Imports
-// are kept per (exporter pid, incarnation, slab) and counted per executor;
-// the incarnation (a random word per process) tells a new process that
-// reuses a dead one's pid apart.  Callers verify each import (the executor
-// writes a nonce at the slab's start and every importer reads it back): a
-// mismatch is a hard error.
+// Both: an executor that no longer needs a slab returns it to the pool, and
+// the next executor of that size class on that device reuses it (its peers'
+// mappings too).  Imports are kept per (exporter pid, incarnation, slab) and
+// counted per executor; the incarnation (a random word per process) tells a
+// new process that reuses a dead one's pid apart.  Callers verify each
+// import (the executor writes a nonce at the slab's start and every importer
+// reads it back): a mismatch is a hard error.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -58,6 +59,8 @@ namespace ipc {
 
 // The mechanism of this process: true = VMM (see above).
 bool vmm();
+// hipRuntimeGetVersion() of the loaded HIP runtime (e.g. 70226015 for 7.2).
+int runtimeVersion();
 // Largest slab the mechanism can share (hipIpc: below 2 GiB; VMM: no limit).
 size_t maxSlabBytes();
 

@@ -382,15 +382,18 @@ int gloo_hip_algorithm_run(gloo_hip_algorithm_t algo);
  * [3] = peer slabs mapped, [4] = hipIpcOpenMemHandle calls made (a peer
  * slab is opened once and kept until a trim finds no executor holding it). */
 int gloo_hip_ipc_stats(uint64_t* out5);
-/* The same, up to 11 words: + trims, bytes trimmed, imports closed, retired
+/* The same, up to 12 words: + trims, bytes trimmed, imports closed, retired
  * addresses, allocations parked at a retired address, the pool's ceiling
- * (GLOO_AMD_IPC_POOL_MAX, default 16 GiB; an acquire that would pass it
- * first frees the slabs no executor holds). */
+ * (GLOO_AMD_IPC_POOL_MAX, default 16 GiB; hipIpc: an acquire that would pass
+ * it first frees the slabs no executor holds), the mechanism (1: VMM, whose
+ * slabs and mappings are never freed while the process lives, only reused;
+ * 0: hipIpc, GLOO_AMD_IPC=hipipc). */
 int gloo_hip_ipc_stats_ex(uint64_t* out, size_t n);
 /* Collective over ctx (every rank calls it, in the same order as its other
  * collective calls): each rank closes the peer mappings no executor holds,
  * then, after a barrier, frees the pooled slabs no executor holds (retiring
- * their addresses, so no later slab is exported there).  ctx = NULL: this
+ * their addresses, so no later slab is exported there; VMM: a no-op beyond
+ * the barrier, its slabs stay for reuse).  ctx = NULL: this
  * process alone, for when its peers are gone.  Executor construction runs
  * the same trim by itself when a rank's pool would pass its ceiling. */
 int gloo_hip_ipc_trim(gloo_hip_context_t ctx);
