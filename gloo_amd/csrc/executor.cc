@@ -1165,6 +1165,8 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS_LOCAL")) copyBlocksLocal_ = (unsigned)std::max(1, std::atoi(cb));
     if (const char* cb = std::getenv("GLOO_AMD_COPY_OUT_BYTES")) copyOutKernelBytes_ = std::strtoull(cb, nullptr, 10);
     if (const char* cb = std::getenv("GLOO_AMD_COPY_OUT_BLOCKS")) copyOutBlocks_ = (unsigned)std::max(1, std::atoi(cb));
+    if (const char* cs = std::getenv("GLOO_AMD_LOCAL_COPY_STORE"))
+      localStore_ = std::string(cs) == "nt" ? kCopyStoreNT : std::string(cs) == "wt" ? kCopyStoreWT : kCopyStorePlain;
     const size_t tickets = std::max<size_t>(256, (size_t)P * GLOO_HIP_NUM_SLOTS * sizeof(unsigned));
     GLOO_AMD_HIP_ALLOC(hipMalloc(&ticket_, tickets));
     // zeroed on the executor's stream and complete before any copy kernel
@@ -1817,7 +1819,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         for (size_t k = 0; k < ops.size(); k++)
           if (lens[k]) d[nd++] = CopyDesc{ops[k].first, ops[k].second, lens[k], nullptr, Seq{}, nullptr,
                                           copySignalGrid(lens[k], copyOutBlocks_)};
-        if (nd) checkRc(launchCopySignalMulti(d, nd, epoch, stream_), "copy kernel (local batch)");
+        if (nd) checkRc(launchCopySignalMulti(d, nd, epoch, stream_, localStore_), "copy kernel (local batch)");
         i = j - 1;
         continue;
       }
@@ -1952,7 +1954,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         const size_t bytes = s.length * es_;
         if (deviceSignal_ && bytes >= copyOutKernelBytes_ && bytes > 0 && (dst + bytes <= src || src + bytes <= dst)) {
           const CopyDesc d{dst, src, bytes, nullptr, Seq{}, nullptr, copySignalGrid(bytes, copyOutBlocks_)};
-          checkRc(launchCopySignalMulti(&d, 1, epoch, stream_), "copy kernel (local)");
+          checkRc(launchCopySignalMulti(&d, 1, epoch, stream_, localStore_), "copy kernel (local)");
           break;
         }
         deviceMove(dst, src, bytes, stream_);

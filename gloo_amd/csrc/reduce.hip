@@ -955,6 +955,7 @@ struct CopyList {
   Seq seq[kMaxCopies];
   unsigned* ticket[kMaxCopies];
   int lean;  // completion protocol (fwdLean): write-through stores, one release by the ticket holder
+  int plainStore;  // stores of a flag-less copy (CopyStore, signal.h)
 };
 
 __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(CopyList L, const uint64_t* epoch) {
@@ -984,9 +985,12 @@ __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(CopyList L, con
     u32x4 v[kCopyUnroll];
 #pragma unroll
     for (int u = 0; u < kCopyUnroll; u++) v[u] = bload<kAuxNT>(rs, lane_off + u * kCopyBlock * 16, ss.mis);
-    if (L.lean && L.flag[j]) {
+    if ((L.lean && L.flag[j]) || (!L.flag[j] && L.plainStore == kCopyStoreWT)) {
 #pragma unroll
       for (int u = 0; u < kCopyUnroll; u++) bstore<kAuxWT>(rd, lane_off + u * kCopyBlock * 16, v[u]);
+    } else if (!L.flag[j] && L.plainStore == kCopyStorePlain) {
+#pragma unroll
+      for (int u = 0; u < kCopyUnroll; u++) bstore<0>(rd, lane_off + u * kCopyBlock * 16, v[u]);
     } else {
 #pragma unroll
       for (int u = 0; u < kCopyUnroll; u++) bstore<kAuxNT>(rd, lane_off + u * kCopyBlock * 16, v[u]);
@@ -1061,6 +1065,7 @@ struct FwdList {
   Seq seq[kMaxCopyEntries];
   unsigned* ticket;                 // zero between launches; nullptr: no signals
   int lean;                         // completion protocol (launchFoldSend)
+  int plainLocal;                   // dst stores plain instead of `nt` (GLOO_AMD_FOLD_STORE)
 };
 
 template <class Tr, int OP>
@@ -1098,8 +1103,13 @@ __global__ __launch_bounds__(kVecBlock) void fold_send_kernel(typename Tr::Stora
     else if (mode == 1) fold_tile<Tr, OP, UNROLL, BLOCK, 1>(srcs, k, head, base, bytes, acc);
     else fold_tile<Tr, OP, UNROLL, BLOCK, 0>(srcs, k, head, base, bytes, acc);
     const auto rd = make_rsrc(reinterpret_cast<const char*>(dst + head) + base, bytes);
+    if (F.plainLocal) {
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rd, lane_off + u * BLOCK * 16, acc[u]);
+      for (int u = 0; u < UNROLL; u++) bstore<0>(rd, lane_off + u * BLOCK * 16, acc[u]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rd, lane_off + u * BLOCK * 16, acc[u]);
+    }
     for (int r = 0; r < F.n; r++) {
       if (!F.dst[r]) continue;  // a credit: no data
       // a forward destination may sit at another residue mod 16 B than dst
@@ -1324,7 +1334,7 @@ unsigned copySignalGrid(size_t bytes, unsigned maxBlocks) {
   return (unsigned)(g == 0 ? 1 : g);
 }
 
-int launchCopySignalMulti(const CopyDesc* d, int n, const uint64_t* epoch, hipStream_t s) {
+int launchCopySignalMulti(const CopyDesc* d, int n, const uint64_t* epoch, hipStream_t s, CopyStore localStore) {
   if (n < 1 || n > kMaxCopies) return set_error(GLOO_HIP_EINVAL_ARG, "copy list size out of range");
   CopyList L;
   memset(&L, 0, sizeof(L));
@@ -1343,6 +1353,7 @@ int launchCopySignalMulti(const CopyDesc* d, int n, const uint64_t* epoch, hipSt
   }
   L.first[n] = total;
   L.lean = fwdLean();
+  L.plainStore = localStore;
   copy_signal_kernel<<<total, kCopyBlock, 0, s>>>(L, epoch);
   return check_launch("copy_signal_kernel");
 }
@@ -1441,6 +1452,11 @@ int launchFoldSend(int op, int dtype, void* dst, const void* const* srcs, int k,
   F.n = nf;
   F.ticket = ticket;
   F.lean = fwdLean();
+  static const int plainLocal = [] {
+    const char* e = std::getenv("GLOO_AMD_FOLD_STORE");
+    return e && std::string(e) == "plain" ? 1 : 0;
+  }();
+  F.plainLocal = plainLocal;
   for (int r = 0; r < nf; r++) {
     if (!fwd[r].dst && !fwd[r].flag) return set_error(GLOO_HIP_EINVAL_ARG, "forward entry with neither data nor flag");
     if ((uintptr_t)fwd[r].dst % es)

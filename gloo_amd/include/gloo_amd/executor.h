@@ -267,10 +267,13 @@ class PlanExecutor {
   bool batchKernelCopy_ = true;  // a batch of SENDs = one multi-destination copy kernel
   // A lone local COPY (a mesh result out of its inbox) of at least this many
   // bytes runs on the copy kernel instead of hipMemcpyAsync
-  // (GLOO_AMD_COPY_OUT_BYTES); copyOutBlocks_ caps the workgroups per local
-  // copy there and in a batch of local COPYs (GLOO_AMD_COPY_OUT_BLOCKS)
-  size_t copyOutKernelBytes_ = SIZE_MAX;
+  // (GLOO_AMD_COPY_OUT_BYTES; default every size, with device signalling);
+  // copyOutBlocks_ caps the workgroups per local copy there and in a batch
+  // of local COPYs (GLOO_AMD_COPY_OUT_BLOCKS); localStore_ is their store
+  // flavour (signal.h CopyStore; GLOO_AMD_LOCAL_COPY_STORE = plain | nt | wt)
+  size_t copyOutKernelBytes_ = 0;
   unsigned copyOutBlocks_ = 256;
+  CopyStore localStore_ = kCopyStorePlain;
   bool foldSend_ = true;         // a FOLD's result SENDs ride in the fold's pass (launchFoldSend)
   bool foldSendUsed_ = false;    // ... and some enqueue did so
   unsigned* ticket_ = nullptr;   // copy_signal_kernel tickets, one counter per (peer, slot)

@@ -75,7 +75,15 @@ struct CopyDesc {
   unsigned* ticket;  // this entry's ticket counter (zero at launch)
   unsigned blocks;   // copySignalGrid(bytes, ...)
 };
-int launchCopySignalMulti(const CopyDesc* d, int n, const uint64_t* epoch, hipStream_t stream);
+// The stores of a flag-less (local) entry.  `nt` streams the bytes past the
+// die's Infinity Cache; plain stores leave them there for the next reader.
+// A collective's copy-out is re-read by the caller's next use of its buffer
+// (and by the next call's fold), and plain stores made the HD call 3-11 %
+// faster (profiles/round5/r5n_*, r5o_*).  Signalled entries
+// (sends) keep `nt` / write-through.
+enum CopyStore { kCopyStoreNT = 0, kCopyStoreWT = 1, kCopyStorePlain = 2 };
+int launchCopySignalMulti(const CopyDesc* d, int n, const uint64_t* epoch, hipStream_t stream,
+                          CopyStore localStore = kCopyStoreNT);
 
 // Wait for several flags in one launch (one lane per flag), then ONE
 // system-scope acquire.  n <= kMaxWaitEntries.

@@ -63,8 +63,17 @@ def _guard(body, r, errors):
         errors.append((r, repr(e)))
 
 
-@pytest.mark.parametrize("mesh", ["1", "0"])
-@pytest.mark.parametrize("case", _keys("bcube/"))
+def _bcube_cases():
+    """Every bcube golden: both routes up to P = 8 (the mesh plan's range),
+    the reference's route alone above (P = 12: 3 x 4 groups)."""
+    out = []
+    for k in _keys("bcube/", max_p=64):
+        for mesh in (["1", "0"] if int(k.split("/")[3][1:]) <= 8 else ["0"]):
+            out.append((k, mesh))
+    return out
+
+
+@pytest.mark.parametrize("case,mesh", _bcube_cases())
 def test_bcube_threads_golden(torch, golden_new, case, mesh, monkeypatch):
     """BCUBE allreduce, ranks as threads on the visible GPU(s); called twice
     (the second call reuses the cached schedule with rebound buffers).  Both

@@ -112,6 +112,18 @@ def test_golden_nan_payloads(hip, golden_math, key, dtype, op):
     assert_same(dtype, op, run3(hip, op, dtype, a, b, offs=(2, 6, 10)), want)
 
 
+def test_f16_scalar_defect_golden_not_reproduced(hip, golden_math):
+    """The "f16_scalar_defect" golden: the reference's
+    scalar float16 body returns a for a = 0x5359, b = 0x7532.  The kernel
+    returns the round-to-nearest-even sum 0x7536, as the reference's F16C
+    vector body and its CUDA twin do (test_oracle.py pins the golden)."""
+    a, b = golden_math["f16_scalar_defect/a"], golden_math["f16_scalar_defect/b"]
+    assert golden_math["f16_scalar_defect/sum"][0] == 0x5359
+    for inplace in (False, True):
+        got = run3(hip, "sum", "f16", a, b, inplace=inplace)
+        assert got.view(np.uint16)[0] == 0x7536
+
+
 def rand_inputs(dtype, n, rng):
     code, npt = oracle.DTYPES[dtype]
     if dtype in ("f32", "f64"):
