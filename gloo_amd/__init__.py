@@ -273,7 +273,7 @@ EXPORTED = EXPORTED + ("gloo_hip_context_create", "gloo_hip_context_create_ex", 
                        "gloo_hip_algorithm_set_profiling", "gloo_hip_algorithm_stats",
                        "gloo_hip_algorithm_mode", "gloo_hip_algorithm_create_ws", "gloo_hip_context_mode",
                        "gloo_hip_algorithm_create_streams", "gloo_hip_algorithm_set_streams", "gloo_hip_ipc_stats",
-                       "gloo_hip_ipc_stats_ex", "gloo_hip_ipc_trim")
+                       "gloo_hip_ipc_stats_ex")
 # the xGMI transport's bound buffers (gloo_amd/include/gloo_amd/gloo_transport.h)
 EXPORTED = EXPORTED + ("gloo_hip_context_create_kv", "gloo_hip_transport_create", "gloo_hip_transport_destroy",
                        "gloo_hip_buffer_create", "gloo_hip_buffer_destroy", "gloo_hip_buffer_send",
@@ -345,26 +345,14 @@ class TransportBuffer:
 
 
 def ipc_stats():
-    """This process's pool of cross-process slabs (gloo_amd/include/gloo_amd/ipc.h):
-    slabs exported and their bytes, slabs free for reuse, peer slabs mapped,
-    imports made; trims, bytes they freed, mappings they closed, retired
-    addresses and allocations parked (hipIpc only: VMM never frees a slab),
-    the ceiling (GLOO_AMD_IPC_POOL_MAX, hipIpc) and the mechanism (1: VMM,
-    0: hipIpc)."""
-    out = (ctypes.c_uint64 * 12)()
-    _check(lib.gloo_hip_ipc_stats_ex(out, 12))
+    """This process's pool of cross-process slabs (gloo_amd/include/gloo_amd/ipc.h:
+    HIP VMM blocks, never freed while the process lives, reused by size
+    class): slabs exported and their bytes, slabs free for reuse, peer slabs
+    mapped, imports made, mappings of exited peers dropped."""
+    out = (ctypes.c_uint64 * 6)()
+    _check(lib.gloo_hip_ipc_stats_ex(out, 6))
     return {"slabs": out[0], "slab_bytes": out[1], "free": out[2], "peer_slabs_mapped": out[3],
-            "ipc_opens": out[4], "trims": out[5], "trimmed_bytes": out[6], "mappings_closed": out[7],
-            "retired_ranges": out[8], "parked_allocations": out[9], "pool_max_bytes": out[10], "vmm": out[11]}
-
-
-def ipc_trim(ctx=None):
-    """Collective over ctx's ranks: close the peer mappings no executor
-    holds, barrier, free the pooled slabs no executor holds (ipc.h; hipIpc
-    only, VMM slabs stay for reuse).
-    ctx=None: this process alone (its peers are gone)."""
-    lib.gloo_hip_ipc_trim.argtypes = [ctypes.c_void_p]
-    _check(lib.gloo_hip_ipc_trim(ctx._h if ctx is not None else None))
+            "imports": out[4], "dropped": out[5]}
 
 
 def _mode_dict(out):

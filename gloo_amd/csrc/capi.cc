@@ -115,10 +115,6 @@ int gloo_hip_context_destroy(gloo_hip_context_t ctx) {
   return guarded([&] {
     if (ctx) ctx->cache.clear();  // executors tear down before the context
     delete ctx;
-    // over the IPC pool's ceiling: drop this process's unused mappings of
-    // peer slabs (local and safe; the slabs themselves are freed by the next
-    // collective trim, ipc.h)
-    if (gloo_amd::ipc::overCeiling(0)) gloo_amd::ipc::closeUnusedImports();
   });
 }
 
@@ -218,21 +214,8 @@ int gloo_hip_ipc_stats_ex(uint64_t* out, size_t n) {
   return guarded([&] {
     GLOO_AMD_ENFORCE(out, "null argument");
     const gloo_amd::ipc::Stats st = gloo_amd::ipc::stats();
-    const uint64_t v[] = {st.slabs, st.slabBytes, st.free,    st.imports, st.opens, st.trims,
-                          st.trimmedBytes, st.closes, st.retired, st.parked, st.max, st.vmm};
+    const uint64_t v[] = {st.slabs, st.slabBytes, st.free, st.imports, st.opens, st.dropped};
     for (size_t i = 0; i < n && i < sizeof(v) / sizeof(v[0]); i++) out[i] = v[i];
-  });
-}
-
-int gloo_hip_ipc_trim(gloo_hip_context_t ctx) {
-  return guarded([&] {
-    if (!ctx || ctx->ctx->size == 1) {
-      gloo_amd::ipc::trim();  // no peers to wait for
-      return;
-    }
-    gloo_amd::ipc::closeUnusedImports();
-    ctx->ctx->barrier("ipc-trim");
-    gloo_amd::ipc::freeUnusedSlabs();
   });
 }
 

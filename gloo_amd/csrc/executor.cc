@@ -35,15 +35,13 @@ struct ArenaRecord {
   int32_t device;
   uint64_t ptr;
   uint64_t bytes;
-  uint64_t slabId;           // DEVICE workspace shared with other processes: the pool slab (ipc.h) ...
-  hipIpcMemHandle_t handle;  // ... and its hipIpc handle (the hipIpc mechanism)
+  uint64_t slabId;           // DEVICE workspace shared with other processes: the pool slab (ipc.h)
   int32_t host;              // HOST workspace: the arena is the shm segment `shm`
   char shm[60];
   int32_t deviceSignal;      // this rank signals with stream-ordered kernels
   int32_t hasMailbox;        // ... into device-resident mailboxes
   uint64_t mailboxPtr;
   uint64_t mailboxSlabId;
-  hipIpcMemHandle_t mailboxHandle;
   int32_t interpSlices;      // slices this rank could run its plan in (0: no sliced interpreter)
   uint64_t nonce;            // written at the start of a DEVICE arena: the importer checks its mapping
   uint64_t mailboxNonce;     // written behind the mailbox's counters: likewise
@@ -770,12 +768,10 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   auto arenaBytesOf = [&](const Plan& p) {
     return (std::max<size_t>(256, p.arena * es_) + kArenaGranule - 1) / kArenaGranule * kArenaGranule;
   };
-  // (pid, device, whether this rank's IPC pool would pass its ceiling with
-  // this executor's slabs, and the plan fingerprint: the route knobs, the
-  // executed plan, the call's shape and the hash of the plan's exchange)
+  // (pid, device, and the plan fingerprint: the route knobs, the executed
+  // plan, the call's shape and the hash of the plan's exchange)
   struct Where {
-    int32_t pid, device, overCeiling, knobs;
-    int32_t planAlgo, vmm;  // vmm: this process shares memory through VMM (ipc.h), else hipIpc
+    int32_t pid, device, knobs, planAlgo;
     uint64_t call, exchange;
   };
   const uint64_t callHash = [&] {
@@ -790,8 +786,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   }();
   std::vector<Where> where(P);
   {
-    Where w{ctx_->pid(), ctx_->device(), ipc::overCeiling(arenaBytesOf(plan_) + (2u << 20)) ? 1 : 0, knobs.bits(),
-            planAlgo_, ipc::vmm() ? 1 : 0, callHash, exchangeHash(plan_)};
+    Where w{ctx_->pid(), ctx_->device(), knobs.bits(), planAlgo_, callHash, exchangeHash(plan_)};
     std::vector<char> blob(sizeof(w));
     std::memcpy(blob.data(), &w, sizeof(w));
     const auto all = ctx_->allgather(strcat_("inst", inst_, "/where"), blob);
@@ -813,9 +808,6 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       if (w.planAlgo != where[0].planAlgo)
         why = strcat_("rank ", r, " executes plan ", w.planAlgo, " (", knobText(w.knobs), ") but rank 0 executes plan ",
                       where[0].planAlgo, " (", knobText(where[0].knobs), ")");
-      else if (w.vmm != where[0].vmm && w.pid != where[0].pid)
-        why = strcat_("rank ", r, " shares device memory through ", w.vmm ? "VMM" : "hipIpc", " and rank 0 through ",
-                      where[0].vmm ? "VMM" : "hipIpc", " (their HIP runtimes differ: ipc.h; GLOO_AMD_IPC selects one)");
       else if (w.call != where[0].call)
         why = strcat_("rank ", r, " was called with another algorithm, op, dtype, count, segment size or receive "
                       "counts than rank 0");
@@ -831,40 +823,6 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
       GLOO_AMD_ENFORCE(false, "rank-inconsistent collective: ", why, ". The plan-selecting knobs (GLOO_AMD_MESH, "
                        "GLOO_AMD_RING_MESH, GLOO_AMD_RING_PIPE) and the call's arguments must be equal on every rank");
     }
-  }
-  // The IPC pool's ceiling (ipc.h): when any rank would pass it, every rank
-  // closes the mappings no executor holds, and once all have (a peer's
-  // slab freed while still mapped breaks the next export over its memory)
-  // frees its unused slabs, before any slab of this executor is acquired.
-  {
-    bool trim = false;
-    for (int r = 0; r < P; r++) trim = trim || where[r].overCeiling != 0;
-    if (trim) {
-      GLOO_AMD_TRACE_PHASE("trimming the IPC pool");
-      ipc::closeUnusedImports();
-      ctx_->barrier(strcat_("inst", inst_, "/ipc-trim"));
-      ipc::freeUnusedSlabs();
-    }
-  }
-  // The hipIpc mechanism (older HIP runtimes, ipc.h) cannot share a block of
-  // 2 GiB or more: every rank checks every rank's arena (the same data
-  // everywhere), so such a collective is refused by all ranks together.
-  {
-    bool anyCross = false;
-    for (int r = 0; r < P; r++)
-      if (where[r].pid != ctx_->pid()) anyCross = true;
-    const char* hm = std::getenv("GLOO_AMD_ARENA");
-    const bool host = workspace == GLOO_HIP_WORKSPACE_HOST || (hm && std::string(hm) == "host");
-    if (anyCross && !host && !ipc::vmm())
-      for (int r = 0; r < P; r++) {
-        const Plan pr = r == me ? plan_
-                                : planFor(planAlgo_, r, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_,
-                                          maxSegmentBytes_, recvElems_);
-        GLOO_AMD_ENFORCE(arenaBytesOf(pr) <= ipc::maxSlabBytes(), "rank ", r, "'s inbox arena of ", arenaBytesOf(pr),
-                         " B would be shared between processes through HIP IPC, whose imports of 2 GiB and more ",
-                         "hang; this HIP runtime lacks a working VMM import (ipc.h): split the call, run the ranks ",
-                         "as threads, or use HIP 7.2 or later");
-      }
   }
   peers_.resize(P);
   bool sharesDeviceInProcess = false, crossSender = false;
@@ -1013,7 +971,6 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     rec.mailboxNonce = mbNonce;
     if (mailboxSlab_) {
       rec.mailboxSlabId = mailboxSlab_->id;
-      rec.mailboxHandle = mailboxSlab_->ipcHandle;
       rec.mailboxSlabBytes = mailboxSlab_->bytes;
     }
   }
@@ -1023,7 +980,6 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     std::memcpy(rec.shm, arenaShm_->name.c_str(), arenaShm_->name.size() + 1);
   } else if (arenaSlab_) {
     rec.slabId = arenaSlab_->id;  // exported once, when the pool allocated the slab
-    rec.handle = arenaSlab_->ipcHandle;
   }
   std::vector<char> blob(sizeof(rec));
   std::memcpy(blob.data(), &rec, sizeof(rec));
@@ -1061,8 +1017,6 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
         rm.pid = pr.pid;
         rm.incarnation = pr.incarnation;
         rm.id = pr.mailboxSlabId;
-        rm.ptr = pr.mailboxPtr;
-        rm.ipcHandle = pr.mailboxHandle;
         void* p = ipc::import(rm, pr.mailboxBytes + 4096, ctx_->device());
         uint64_t seen = 0;
         GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, static_cast<char*>(p) + pr.mailboxBytes, sizeof(seen),
@@ -1091,15 +1045,13 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     } else {
       // Another process's pool slab (ipc.h): mapped once, kept.  The mapping
       // must show the nonce the owner just wrote at the slab's start, and
-      // the runtime's record of it must span the arena; anything else is a
-      // hard error, never a silent misdelivery.
+      // span the arena; anything else is a hard error, never a silent
+      // misdelivery.
       GLOO_AMD_TRACE_PHASE("importing rank ", peer, "'s arena slab ", pr.slabId, " (", pr.bytes, " B)");
       ipc::Remote rm;
       rm.pid = pr.pid;
       rm.incarnation = pr.incarnation;
       rm.id = pr.slabId;
-      rm.ptr = pr.ptr;
-      rm.ipcHandle = pr.handle;
       void* p = ipc::import(rm, pr.bytes, ctx_->device());
       GLOO_AMD_TRACE_PHASE("imported at ", p);
       uint64_t seen = 0;

@@ -81,7 +81,7 @@ void mapAt(void* va, size_t bytes, hipMemGenericAllocationHandle_t h, int device
 
 struct Pool {
   std::mutex m;
-  std::vector<std::unique_ptr<Slab>> slabs;  // every live exported slab (freed only by a trim)
+  std::vector<std::unique_ptr<Slab>> slabs;  // every exported slab (never freed: ipc.h)
   std::vector<Slab*> free;
   uint64_t nextId = 1;
   struct Mapping {
@@ -89,54 +89,17 @@ struct Pool {
     void* ptr;
     size_t bytes;
     size_t users;  // executors holding it (import / unimport)
-    hipMemGenericAllocationHandle_t handle;  // VMM (nullptr: a hipIpc mapping)
+    hipMemGenericAllocationHandle_t handle;
   };
-  // (exporter pid, slab id (VMM) or exporter address (hipIpc))
-  std::map<std::pair<int, uint64_t>, Mapping> imports;
-  // hipIpc: device -> [start, end) of every slab a trim freed: no later slab
-  // may overlap one (the runtime hands out pieces of freed blocks again; an
-  // export over such memory failed, and a peer's import of it showed stale
-  // pages, profiles/round4/r4d_*, r4e_*)
-  std::map<int, std::map<uintptr_t, uintptr_t>> retiredRanges;
-  size_t opens = 0, trims = 0, trimmedBytes = 0, closes = 0, retired = 0, parked = 0;
+  std::map<std::pair<int, uint64_t>, Mapping> imports;  // (exporter pid, slab id)
+  size_t opens = 0, dropped = 0;
   static Pool& get() {
-    static Pool* p = new Pool();  // never destroyed: process exit releases device memory
+    static Pool* p = new Pool();  // never destroyed: releaseAllAtExit unmaps
     return *p;
   }
 };
 
-// GLOO_AMD_IPC_POOL_MAX: bytes of exported slabs per process (suffix K, M
-// or G); an executor whose slabs would take a rank's pool past it trims
-// collectively first (executor.cc).  Default 16 GiB.
-size_t poolMax() {
-  static const size_t v = [] {
-    const char* e = std::getenv("GLOO_AMD_IPC_POOL_MAX");
-    if (!e || !*e) return size_t(16) << 30;
-    char* end = nullptr;
-    const double x = std::strtod(e, &end);
-    size_t mul = 1;
-    if (end && (*end == 'K' || *end == 'k')) mul = size_t(1) << 10;
-    if (end && (*end == 'M' || *end == 'm')) mul = size_t(1) << 20;
-    if (end && (*end == 'G' || *end == 'g')) mul = size_t(1) << 30;
-    return (size_t)(x * (double)mul);
-  }();
-  return v;
-}
-
-bool overlapsRetired(const Pool& p, int device, const void* ptr, size_t bytes) {
-  auto d = p.retiredRanges.find(device);
-  if (d == p.retiredRanges.end()) return false;
-  const uintptr_t a = reinterpret_cast<uintptr_t>(ptr), b = a + bytes;
-  auto it = d->second.upper_bound(a);  // first range starting after a
-  if (it != d->second.end() && it->first < b) return true;
-  if (it != d->second.begin()) {
-    --it;
-    if (it->second > a) return true;
-  }
-  return false;
-}
-
-// ---- the fd server (VMM) -----------------------------------------------------
+// ---- the fd server -----------------------------------------------------------
 //
 // Requests are one uint64 slab id per connection; the answer is a Reply,
 // with the slab's dma-buf fd attached (SCM_RIGHTS) when ok.  Only processes
@@ -272,59 +235,6 @@ int fetchFd(int pid, uint64_t inc, uint64_t id, size_t* bytes) {
   return fd;
 }
 
-// Closes every mapping of a peer slab that no executor holds; p.m held.
-void closeUnusedLocked(Pool& p) {
-  for (auto it = p.imports.begin(); it != p.imports.end();) {
-    Pool::Mapping& mp = it->second;
-    // VMM mappings stay: their memory would only come back with their virtual
-    // range, and a freed range handed out again showed stale pages (ipc.h)
-    if (mp.users == 0 && !mp.handle) {
-      GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(mp.ptr));
-      p.closes++;
-      it = p.imports.erase(it);
-    } else {
-      ++it;
-    }
-  }
-}
-
-// Frees every free-listed hipIpc slab and retires its address range; p.m
-// held.  A slab is free-listed only after its executor's collective tear-down
-// barrier (no peer writes it any more), and the trims that call this are
-// collective: every peer has closed the mappings no executor holds first
-// (ROCm 7 fails the next hipIpc export of memory allocated over a slab freed
-// while a peer still mapped it, profiles/round4/r4e_*).  VMM slabs stay.
-void freeUnusedLocked(Pool& p) {
-  std::vector<Slab*> keep;
-  for (Slab* s : p.free) {
-    if (s->handle) {  // VMM: kept for reuse (see closeUnusedLocked)
-      keep.push_back(s);
-      continue;
-    }
-    for (size_t i = 0; i < p.slabs.size(); i++)
-      if (p.slabs[i].get() == s) {
-        int prev = -1;
-        (void)hipGetDevice(&prev);
-        (void)hipSetDevice(s->device);
-        GLOO_AMD_HIP_RELEASE(hipFree(s->ptr));
-        if (prev >= 0) (void)hipSetDevice(prev);
-        p.retiredRanges[s->device][reinterpret_cast<uintptr_t>(s->ptr)] = reinterpret_cast<uintptr_t>(s->ptr) + s->bytes;
-        p.retired++;
-        p.trimmedBytes += s->bytes;
-        p.slabs.erase(p.slabs.begin() + (long)i);
-        break;
-      }
-  }
-  p.free = keep;
-  p.trims++;
-}
-
-size_t slabBytesLocked(const Pool& p) {
-  size_t b = 0;
-  for (const auto& x : p.slabs) b += x->bytes;
-  return b;
-}
-
 // The device the caller runs on, restored on scope exit.
 struct DeviceScope {
   explicit DeviceScope(int device) {
@@ -342,17 +252,15 @@ struct DeviceScope {
 void releaseAllAtExit() {
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
-  for (auto& kv : p.imports)
-    if (kv.second.handle) {
-      (void)hipMemUnmap(kv.second.ptr, kv.second.bytes);
-      (void)hipMemRelease(kv.second.handle);
-    }
-  for (auto& s : p.slabs)
-    if (s->handle) {
-      (void)hipMemUnmap(s->ptr, s->bytes);
-      (void)hipMemRelease(s->handle);
-      if (s->fd >= 0) ::close(s->fd);
-    }
+  for (auto& kv : p.imports) {
+    (void)hipMemUnmap(kv.second.ptr, kv.second.bytes);
+    (void)hipMemRelease(kv.second.handle);
+  }
+  for (auto& s : p.slabs) {
+    (void)hipMemUnmap(s->ptr, s->bytes);
+    (void)hipMemRelease(s->handle);
+    if (s->fd >= 0) ::close(s->fd);
+  }
 }
 void registerAtExit() {
   static std::once_flag once;
@@ -378,39 +286,18 @@ int runtimeVersion() {
   return v;
 }
 
-bool vmm() {
-  static const bool v = [] {
-    const char* e = std::getenv("GLOO_AMD_IPC");
-    return !(e && std::string(e) == "hipipc");
-  }();
-  return v;
-}
-
-size_t maxSlabBytes() {
-  // hipIpc: imports of 2^31 bytes and more hang (profiles/round3/r3t_*); the
-  // size classes above 1 GiB are multiples of 256 MiB, so 1.75 GiB
-  return vmm() ? ~size_t(0) : size_t(7) << 28;
-}
-
 Remote describe(const Slab& s) {
   Remote r;
   r.pid = (int)::getpid();
   r.incarnation = incarnation();
   r.id = s.id;
-  r.ptr = reinterpret_cast<uint64_t>(s.ptr);
-  r.ipcHandle = s.ipcHandle;
   return r;
 }
 
 Slab* acquire(int device, size_t bytes, bool fine) {
   const size_t want = sizeClass(bytes);
-  GLOO_AMD_ENFORCE(want <= maxSlabBytes(), "a cross-process block of ", want, " B: HIP IPC imports of 2 GiB and more ",
-                   "hang on this HIP runtime, so at most ", maxSlabBytes(), " B can be shared (the VMM mechanism of HIP ",
-                   "7.2 and later has no such limit: ipc.h)");
-  if (vmm()) {
-    ensureServer();
-    registerAtExit();
-  }
+  ensureServer();
+  registerAtExit();
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
   for (size_t i = 0; i < p.free.size(); i++) {
@@ -425,48 +312,17 @@ Slab* acquire(int device, size_t bytes, bool fine) {
   s->bytes = want;
   s->device = device;
   s->fine = fine;
-  if (vmm()) {
-    const hipMemAllocationProp prop = propFor(device, fine);
-    GLOO_AMD_HIP_ALLOC(hipMemCreate(&s->handle, want, &prop, 0));
-    try {
-      void* va = freshRange(want);
-      mapAt(va, want, s->handle, device);
-      s->ptr = static_cast<char*>(va);
-      GLOO_AMD_HIP_CHECK(hipMemExportToShareableHandle(&s->fd, s->handle, hipMemHandleTypePosixFileDescriptor, 0));
-    } catch (...) {
-      if (s->ptr) (void)hipMemUnmap(s->ptr, want);
-      (void)hipMemRelease(s->handle);
-      throw;
-    }
-  } else {
-    // Never export memory overlapping a retired slab, and never keep a block
-    // the runtime refuses to export: park it (allocated, not exported) and
-    // allocate again while it is held, then free the parked blocks.
-    std::vector<void*> parked;
-    void* ptr = nullptr;
-    hipError_t eh = hipSuccess;
-    for (;;) {
-      ptr = nullptr;
-      hipError_t e = fine ? hipExtMallocWithFlags(&ptr, want, hipDeviceMallocFinegrained) : hipMalloc(&ptr, want);
-      if (e != hipSuccess) {
-        for (void* q : parked) (void)hipFree(q);
-        GLOO_AMD_HIP_ALLOC(e);
-      }
-      if (!overlapsRetired(p, device, ptr, want)) {
-        eh = hipIpcGetMemHandle(&s->ipcHandle, ptr);
-        if (eh == hipSuccess) break;
-        (void)hipGetLastError();
-      }
-      parked.push_back(ptr);
-      p.parked++;
-      if (parked.size() > 64) {
-        for (void* q : parked) (void)hipFree(q);
-        GLOO_AMD_ENFORCE(false, "IPC pool: no exportable block of ", want, " B after 64 tries (",
-                         eh == hipSuccess ? "retired ranges" : hipGetErrorString(eh), ")");
-      }
-    }
-    for (void* q : parked) GLOO_AMD_HIP_RELEASE(hipFree(q));
-    s->ptr = static_cast<char*>(ptr);
+  const hipMemAllocationProp prop = propFor(device, fine);
+  GLOO_AMD_HIP_ALLOC(hipMemCreate(&s->handle, want, &prop, 0));
+  try {
+    void* va = freshRange(want);
+    mapAt(va, want, s->handle, device);
+    s->ptr = static_cast<char*>(va);
+    GLOO_AMD_HIP_CHECK(hipMemExportToShareableHandle(&s->fd, s->handle, hipMemHandleTypePosixFileDescriptor, 0));
+  } catch (...) {
+    if (s->ptr) (void)hipMemUnmap(s->ptr, want);
+    (void)hipMemRelease(s->handle);
+    throw;
   }
   s->id = p.nextId++;
   p.slabs.push_back(std::move(s));
@@ -487,86 +343,33 @@ void unimport(void* mapped) {
   for (auto& kv : p.imports)
     if (kv.second.ptr == mapped) {
       if (kv.second.users) kv.second.users--;
-      return;  // kept until a trim
+      return;  // kept for reuse (ipc.h)
     }
 }
 
-void closeUnusedImports() {
-  Pool& p = Pool::get();
-  std::lock_guard<std::mutex> lk(p.m);
-  closeUnusedLocked(p);
-}
-
-void freeUnusedSlabs() {
-  Pool& p = Pool::get();
-  std::lock_guard<std::mutex> lk(p.m);
-  freeUnusedLocked(p);
-}
-
-bool overCeiling(size_t more) {
-  Pool& p = Pool::get();
-  std::lock_guard<std::mutex> lk(p.m);
-  // VMM slabs are never released (closeUnusedLocked): nothing to trim
-  return !vmm() && !p.free.empty() && slabBytesLocked(p) + more > poolMax();
-}
-
-namespace {
-// Drops a mapping of either kind; p.m held.
-void dropMapping(Pool& p, Pool::Mapping& mp) {
-  if (mp.handle) {
-    GLOO_AMD_HIP_RELEASE(hipMemUnmap(mp.ptr, mp.bytes));
-    GLOO_AMD_HIP_RELEASE(hipMemRelease(mp.handle));
-    p.retired++;
-  } else {
-    GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(mp.ptr));
-  }
-}
-
-// Bytes the runtime maps from `m` to the end of its allocation (a hipIpc
-// import spans the exporter's whole slab), or 0 when it keeps no record.
-size_t mappedSpan(void* m) {
-  void* rb = nullptr;
-  size_t rs = 0;
-  size_t span = 0;
-  if (hipMemGetAddressRange(&rb, &rs, m) == hipSuccess && rb && static_cast<char*>(rb) + rs > static_cast<char*>(m))
-    span = (size_t)(static_cast<char*>(rb) + rs - static_cast<char*>(m));
-  (void)hipGetLastError();
-  return span;
-}
-}  // namespace
-
 void* import(const Remote& r, size_t bytes, int device) {
   Pool& p = Pool::get();
-  const bool viaVmm = vmm();
-  if (viaVmm) registerAtExit();
-  const auto key = std::make_pair(r.pid, viaVmm ? r.id : r.ptr);
+  registerAtExit();
+  const auto key = std::make_pair(r.pid, r.id);
   {
     std::lock_guard<std::mutex> lk(p.m);
     auto it = p.imports.find(key);
     if (it != p.imports.end()) {
       if (it->second.incarnation == r.incarnation) {
-        if (!viaVmm && it->second.bytes < bytes) it->second.bytes = std::max(it->second.bytes, mappedSpan(it->second.ptr));
         GLOO_AMD_ENFORCE(it->second.bytes >= bytes, "slab of pid ", r.pid, " mapped at ", it->second.bytes,
                          " B, now published at ", bytes, " B");
         it->second.users++;
         return it->second.ptr;
       }
-      // a new process reusing a dead one's pid: its mapping is of no use
-      dropMapping(p, it->second);
+      // a new process reusing a dead one's pid: its mapping is of no use (the
+      // range stays reserved, never mapped again)
+      GLOO_AMD_HIP_RELEASE(hipMemUnmap(it->second.ptr, it->second.bytes));
+      GLOO_AMD_HIP_RELEASE(hipMemRelease(it->second.handle));
+      p.dropped++;
       p.imports.erase(it);
     }
-    if (!viaVmm) {
-      void* m = nullptr;
-      DeviceScope ds(device);
-      GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&m, r.ipcHandle, hipIpcMemLazyEnablePeerAccess));
-      p.opens++;
-      // the mapping spans the exporter's whole slab (its size class), not
-      // just what this first importer asked for
-      p.imports[key] = {r.incarnation, m, std::max(bytes, mappedSpan(m)), 1, nullptr};
-      return m;
-    }
   }
-  // VMM.  The pool's lock is NOT held across the request: the exporter may be
+  // The pool's lock is NOT held across the request: the exporter may be
   // importing from this process at the same moment, and its request is
   // answered by this process's fd server, which takes the lock.
   size_t slabBytes = 0;
@@ -598,7 +401,6 @@ void* import(const Remote& r, size_t bytes, int device) {
     // another thread of this process mapped it meanwhile: keep that one
     GLOO_AMD_HIP_RELEASE(hipMemUnmap(va, slabBytes));
     GLOO_AMD_HIP_RELEASE(hipMemRelease(h));
-    p.retired++;
     it->second.users++;
     return it->second.ptr;
   }
@@ -616,13 +418,7 @@ Stats stats() {
   s.free = p.free.size();
   s.imports = p.imports.size();
   s.opens = p.opens;
-  s.trims = p.trims;
-  s.trimmedBytes = p.trimmedBytes;
-  s.closes = p.closes;
-  s.retired = p.retired;
-  s.parked = p.parked;
-  s.max = poolMax();
-  s.vmm = vmm() ? 1 : 0;
+  s.dropped = p.dropped;
   return s;
 }
 

@@ -261,11 +261,9 @@ class SendBuffer : public Buffer {
       viaLanding_ = true;
       dstDevice_ = true;
     } else {
+      // (an allocation of 2 GiB or more always publishes a landing slab)
       GLOO_AMD_ENFORCE(r.alloc < kMaxImportBytes, "rank ", peer_, "'s receive buffer (slot ", slot_,
-                       ") lies in a device allocation of ", r.alloc, " B; HIP IPC imports of 2 GiB and more hang, ",
-                       "and this HIP runtime lacks a working VMM import (ipc.h), so a peer process cannot write into ",
-                       "it: allocate receive buffers below ", kMaxImportBytes, " B, run the ranks as threads, or use ",
-                       "HIP 7.2 or later");
+                       ") lies in a device allocation of ", r.alloc, " B but came without a landing slab");
       GLOO_AMD_ENFORCE(r.ipc, "rank ", peer_, "'s receive buffer is not IPC-exportable");
       // The caller's memory cannot come from the IPC slab pool (ipc.h);
       // this import is used by eager copies only, never captured into a
@@ -351,7 +349,7 @@ class RecvBuffer : public Buffer {
         size_t allocSize = 0;
         const bool ranged = hipMemGetAddressRange(&base, &allocSize, ptr_) == hipSuccess && base;
         (void)hipGetLastError();
-        if (ranged && allocSize >= kMaxImportBytes && ipc::vmm()) {
+        if (ranged && allocSize >= kMaxImportBytes) {
           deviceLanding_ = ipc::acquire(ctx.device(), size_, true);
           r.deviceLanding = 1;
           r.landingSlab = deviceLanding_->id;

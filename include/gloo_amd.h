@@ -376,27 +376,16 @@ int gloo_hip_algorithm_set_streams(gloo_hip_algorithm_t algo, const gloo_hip_str
 
 int gloo_hip_algorithm_run(gloo_hip_algorithm_t algo);
 
-/* This process's IPC slab pool (gloo_amd/include/gloo_amd/ipc.h; no
- * reference counterpart, for tests and tools): out5[0] = slabs exported
- * (freed only by a trim), [1] = their bytes, [2] = slabs free for reuse,
- * [3] = peer slabs mapped, [4] = hipIpcOpenMemHandle calls made (a peer
- * slab is opened once and kept until a trim finds no executor holding it). */
+/* This process's pool of cross-process slabs (gloo_amd/include/gloo_amd/ipc.h:
+ * HIP VMM blocks shared as dma-buf fds, never freed while the process lives,
+ * reused by size class; no reference counterpart, for tests and tools):
+ * out5[0] = slabs exported, [1] = their bytes, [2] = slabs free for reuse,
+ * [3] = peer slabs mapped, [4] = imports made (a peer slab is mapped once and
+ * kept). */
 int gloo_hip_ipc_stats(uint64_t* out5);
-/* The same, up to 12 words: + trims, bytes trimmed, imports closed, retired
- * addresses, allocations parked at a retired address, the pool's ceiling
- * (GLOO_AMD_IPC_POOL_MAX, default 16 GiB; hipIpc: an acquire that would pass
- * it first frees the slabs no executor holds), the mechanism (1: VMM, whose
- * slabs and mappings are never freed while the process lives, only reused;
- * 0: hipIpc, GLOO_AMD_IPC=hipipc). */
+/* The same, up to 6 words: + mappings of exited peers (their pid reused)
+ * dropped. */
 int gloo_hip_ipc_stats_ex(uint64_t* out, size_t n);
-/* Collective over ctx (every rank calls it, in the same order as its other
- * collective calls): each rank closes the peer mappings no executor holds,
- * then, after a barrier, frees the pooled slabs no executor holds (retiring
- * their addresses, so no later slab is exported there; VMM: a no-op beyond
- * the barrier, its slabs stay for reuse).  ctx = NULL: this
- * process alone, for when its peers are gone.  Executor construction runs
- * the same trim by itself when a rank's pool would pass its ceiling. */
-int gloo_hip_ipc_trim(gloo_hip_context_t ctx);
 int gloo_hip_algorithm_destroy(gloo_hip_algorithm_t algo);
 /* Host seconds the last run() spent blocked waiting for peers. */
 double gloo_hip_algorithm_wait_seconds(gloo_hip_algorithm_t algo);

@@ -241,7 +241,7 @@ mode = a.mode()
 a.close()
 ctx.close()
 print("RESULT" + json.dumps({"bad": res, "mode": mode, "slabs_before": before["slabs"],
-                             "slabs_after": after["slabs"], "vmm": after["vmm"]}), flush=True)
+                             "slabs_after": after["slabs"]}), flush=True)
 """
 
 
@@ -286,7 +286,7 @@ def test_ipc_arena_of_2gib_and_more(torch, algo, n, env):
     for o in outs:
         assert o["bad"] == [0, 0], o
         # one slab for the arena (and one for the mailbox), never a split
-        assert o["vmm"] == 1 and o["slabs_after"] - o["slabs_before"] <= 2, o
+        assert o["slabs_after"] - o["slabs_before"] <= 2, o
 
 
 def large_p_keys():

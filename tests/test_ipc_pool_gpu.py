@@ -1,15 +1,14 @@
 """GPU: the cross-process slab pool stays bounded (ipc.h).
 
-test_ipc_pool_bounded_with_trims covers the hipIpc mechanism
-(GLOO_AMD_IPC=hipipc), the one with trims: two rank processes build
-halving-doubling executors (mesh route: their inbox arenas are exported
-slabs) of ten size classes in sequence, then walk back down through classes
-that a trim freed.  With GLOO_AMD_IPC_POOL_MAX = 256 MiB the pool never holds
-more than the ceiling beyond the slabs of the live executor (an executor's
-construction trims collectively first), trims happen, their virtual ranges
-are retired (never mapped again), every run is exact (the closed form of rank r contributing (7 i + r) mod
-4096 at element i), and an explicit collective gloo_hip_ipc_trim leaves no
-slab and no mapping."""
+The pool's slabs are HIP VMM blocks that are never freed while the process
+lives (a freed virtual range handed out again shows stale pages) and are
+reused by size class instead.  test_ipc_pool_reuses_size_classes: two rank
+processes build halving-doubling executors (mesh route: their inbox arenas
+are exported slabs) of ten size classes in sequence, then walk back down
+through classes already used: the walk back creates no slab and maps no new
+peer slab, every slab is back in the free list after its executor closes,
+and every run is exact (the closed form of rank r contributing (7 i + r)
+mod 4096 at element i)."""
 import json
 import os
 import subprocess
@@ -37,7 +36,6 @@ for n in sizes:
     want = ((i7 % 4096) + ((i7 + 1) % 4096)).float()
     del i7
     a = gloo_amd.Algorithm(ctx, "halving_doubling", "sum", "f32", [buf.data_ptr()], n)
-    st = gloo_amd.ipc_stats()
     ok = []
     for it in range(2):
         if it:
@@ -47,51 +45,50 @@ for n in sizes:
         torch.cuda.synchronize()
         ok.append(bool((buf == want).all()))
     a.close()
-    out.append({"n": n, "ok": ok, "stats": st})
+    out.append({"n": n, "ok": ok, "stats": gloo_amd.ipc_stats()})
     del buf, want
-final = gloo_amd.ipc_stats()
-gloo_amd.ipc_trim(ctx)   # collective: every unused slab and mapping goes
-trimmed = gloo_amd.ipc_stats()
 ctx.close()
-print("RESULT" + json.dumps({"steps": out, "final": final, "trimmed": trimmed}), flush=True)
+print("RESULT" + json.dumps({"steps": out}), flush=True)
 '''
 
 
-@pytest.mark.timeout(300)
-def test_ipc_pool_bounded_with_trims():
-    pytest.importorskip("torch")
-    cap = 256 << 20
+def run_pair(worker, args, env, timeout):
     with tempfile.TemporaryDirectory() as d:
         w = os.path.join(d, "w.py")
-        open(w, "w").write(WORKER)
-        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_IPC_POOL_MAX=str(cap), GLOO_AMD_TRACE="1",
-                 GLOO_AMD_IPC="hipipc")
-        procs = [subprocess.Popen([sys.executable, w, str(r), "file:" + os.path.join(d, "s")], env=e,
+        open(w, "w").write(worker)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, **env)
+        procs = [subprocess.Popen([sys.executable, w, str(r), "file:" + os.path.join(d, "s")] + args, env=e,
                                   stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
         outs = []
         try:
             for p in procs:
-                outs.append(p.communicate(timeout=280))
+                outs.append(p.communicate(timeout=timeout))
         finally:
             for p in procs:
                 if p.poll() is None:
                     p.kill()
         assert [p.returncode for p in procs] == [0, 0], "\n".join(f"rank {r}: {e[-2500:]}"
                                                               for r, (o, e) in enumerate(outs))
-        res = [json.loads(o.split("RESULT", 1)[1]) for o, e in outs]
+        return [json.loads(o.split("RESULT", 1)[1]) for o, e in outs]
+
+
+@pytest.mark.timeout(300)
+def test_ipc_pool_reuses_size_classes():
+    pytest.importorskip("torch")
+    res = run_pair(WORKER, [], {}, 280)
     for r in res:
-        for s in r["steps"]:
+        steps = r["steps"]
+        for s in steps:
             assert s["ok"] == [True, True], s
-            live = 4 * s["n"] + (8 << 20)  # this executor's arena (about n fp32) and mailbox, rounded up
-            assert s["stats"]["slab_bytes"] <= cap + 2 * live, s
-            assert s["stats"]["pool_max_bytes"] == cap
-        f = r["final"]
-        assert f["vmm"] == 0, f
-        assert f["trims"] >= 1 and f["retired_ranges"] >= 1, f
-        assert f["slab_bytes"] <= cap + 4 * r["steps"][-1]["n"] + (8 << 20), f
-        t = r["trimmed"]
-        assert t["slabs"] == 0 and t["slab_bytes"] == 0 and t["free"] == 0, t
-        assert t["peer_slabs_mapped"] == 0, t
+            st = s["stats"]
+            assert st["free"] == st["slabs"], s   # every slab back in the pool
+        up, down = steps[9]["stats"], steps[-1]["stats"]
+        # the walk back down reuses: no new slab, no new peer mapping
+        assert down["slabs"] == up["slabs"] and down["slab_bytes"] == up["slab_bytes"], (up, down)
+        assert down["peer_slabs_mapped"] == up["peer_slabs_mapped"] and down["imports"] == up["imports"], (up, down)
+        # ten arena classes (2 MiB .. 1 GiB, an arena of n fp32 rounds up to
+        # at most 2 x 4 n B) and the mailboxes' class: below 2 x the sum
+        assert up["slab_bytes"] <= 2 * sum(4 * s["n"] for s in steps[:10]) + (64 << 20), up
 
 
 CHURN_WORKER = r'''
@@ -132,7 +129,6 @@ for it in range(count):
     hip_rt.free(buf)
     peak_used = max(peak_used, free0 - hip_rt.mem_info()[0])
 st = gloo_amd.ipc_stats()
-gloo_amd.ipc_trim(ctx)
 ctx.close()
 print("RESULT" + json.dumps({"bad": bad, "stats": st, "peak_used": peak_used,
                              "end_used": free0 - hip_rt.mem_info()[0]}), flush=True)
@@ -143,37 +139,19 @@ print("RESULT" + json.dumps({"bad": bad, "stats": st, "peak_used": peak_used,
 def test_ipc_pool_churn_bounded():
     """VERDICT r4 "next round" 2: pool churn.  200 executor constructions of
     random size classes (arenas of 16 KiB to 32 MiB) and algorithms stay
-    exact and bounded.  The hipIpc pool under a 64 MiB ceiling failed exactly
-    this (a collective trim before almost every construction; "no exportable
-    block ... after 64 tries (retired ranges)",
+    exact and bounded.  The rounds 3-4 hipIpc pool under a 64 MiB ceiling
+    failed exactly this (a collective trim before almost every construction;
+    "no exportable block ... after 64 tries (retired ranges)",
     profiles/round5/r5c_pytest_churn_hipipc.log).  The VMM pool never frees
-    a slab (ipc.h: a freed range handed out again shows stale pages) and
-    reuses them by size class instead, so it holds at most one slab per
-    class and kind per live executor: here below 256 MiB per rank, with no
-    trims."""
+    a slab and reuses them by size class instead, so it holds at most one
+    slab per class and kind per live executor: here below 256 MiB per
+    rank."""
     pytest.importorskip("torch")
-    cap = 64 << 20
-    with tempfile.TemporaryDirectory() as d:
-        w = os.path.join(d, "w.py")
-        open(w, "w").write(CHURN_WORKER)
-        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_IPC_POOL_MAX=str(cap))
-        procs = [subprocess.Popen([sys.executable, w, str(r), "file:" + os.path.join(d, "s"), "200"], env=e,
-                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
-        outs = []
-        try:
-            for p in procs:
-                outs.append(p.communicate(timeout=380))
-        finally:
-            for p in procs:
-                if p.poll() is None:
-                    p.kill()
-        assert [p.returncode for p in procs] == [0, 0], "\n".join(f"rank {r}: {e[-2500:]}"
-                                                              for r, (o, e) in enumerate(outs))
-        res = [json.loads(o.split("RESULT", 1)[1]) for o, e in outs]
+    res = run_pair(CHURN_WORKER, ["200"], {}, 380)
     for r in res:
         assert r["bad"] == [], r["bad"]
         st = r["stats"]
-        assert st["vmm"] == 1 and st["trims"] == 0, st
+        assert st["free"] == st["slabs"], st
         # classes 2 MiB .. 64 MiB (2 x the largest arena, rounded up), arena and
         # mailbox kinds: 2 x 126 MiB at most
         assert st["slab_bytes"] <= 256 << 20, st

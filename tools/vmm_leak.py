@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
-"""Does device memory come back when the cross-process pool trims?  Two rank
-processes (no torch: the system runtime, VMM unless GLOO_AMD_IPC says
-otherwise) build an HD executor of a new size every iteration, run it,
-close it and trim collectively (gloo_hip_ipc_trim); rank 0 prints the
-device's used bytes (hipMemGetInfo: both ranks share the GPU) per iteration.
+"""Device memory of the cross-process pool as executors come and go.  Two
+rank processes (no torch) build an HD executor of a new size every
+iteration, run it and close it; rank 0 prints the device's used bytes
+(hipMemGetInfo: both ranks share the GPU) and the pool's stats per
+iteration.  The round-5 runs (profiles/round5/r5i_*) also trimmed the pool
+collectively after each close, through the gloo_hip_ipc_trim of that
+round's two-mechanism pool (since removed): VMM memory came back only when
+its virtual range was freed, which is why the pool now never frees a slab.
 usage: vmm_leak.py ITERS [ENV=VAL ...]"""
 import json
 import os
@@ -31,12 +34,10 @@ for it in range(iters):
     a.run()
     ok = bool((hip_rt.d2h(buf, x) == 3).all())
     a.close()
-    gloo_amd.ipc_trim(ctx)
     st = gloo_amd.ipc_stats()
     if rank == 0:
         print(json.dumps({"it": it, "elems": m, "ok": ok, "used_mb": round((free0 - hip_rt.mem_info()[0]) / 2**20, 1),
-                          "slabs": st["slabs"], "slab_bytes": st["slab_bytes"], "mapped": st["peer_slabs_mapped"],
-                          "vmm": st["vmm"]}), flush=True)
+                          "slabs": st["slabs"], "slab_bytes": st["slab_bytes"], "mapped": st["peer_slabs_mapped"]}), flush=True)
 ctx.close()
 '''
 
