@@ -10,6 +10,7 @@ form one row each — a sweep tool's phases, in the order it ran them.
 
 usage: rocpd_summary.py RESULTS_DB [OUT_CSV] [--by-name | --segments]"""
 import csv
+import os
 import sqlite3
 import sys
 
@@ -20,6 +21,8 @@ def short(name):
 
 
 def main():
+    if len(sys.argv) < 2 or sys.argv[1].startswith("-") or not os.path.isfile(sys.argv[1]):
+        sys.exit(__doc__)  # never let sqlite3.connect create a file named after a flag
     db = sys.argv[1]
     out = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else None
     by_name = "--by-name" in sys.argv
