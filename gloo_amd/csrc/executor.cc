@@ -1117,6 +1117,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS_LOCAL")) copyBlocksLocal_ = (unsigned)std::max(1, std::atoi(cb));
     if (const char* cb = std::getenv("GLOO_AMD_COPY_OUT_BYTES")) copyOutKernelBytes_ = std::strtoull(cb, nullptr, 10);
     if (const char* cb = std::getenv("GLOO_AMD_COPY_OUT_BLOCKS")) copyOutBlocks_ = (unsigned)std::max(1, std::atoi(cb));
+    if (const char* cs = std::getenv("GLOO_AMD_REDUCE_STORE")) reducePlain_ = std::string(cs) != "nt";
     if (const char* cs = std::getenv("GLOO_AMD_LOCAL_COPY_STORE"))
       localStore_ = std::string(cs) == "nt" ? kCopyStoreNT : std::string(cs) == "wt" ? kCopyStoreWT : kCopyStorePlain;
     const size_t tickets = std::max<size_t>(256, (size_t)P * GLOO_HIP_NUM_SLOTS * sizeof(unsigned));
@@ -1685,6 +1686,12 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
     ~StampScope() { setLaunchStamp(prev); }
     uint64_t* prev;
   };
+  // the store flavour of this plan's REDUCE launches (signal.h)
+  struct ReduceStoreScope {
+    explicit ReduceStoreScope(bool plain) : prev(setReducePlainStores(plain)) {}
+    ~ReduceStoreScope() { setReducePlainStores(prev); }
+    bool prev;
+  } reduceStores(reducePlain_);
   auto slotOf = [&](size_t step) -> uint64_t* {
     if (!stamping_) return nullptr;
     auto it = stampSlotOf_.find(step);

@@ -359,6 +359,7 @@ __global__ void stamp_init_kernel(uint64_t* stamps, size_t words) {
 }
 
 thread_local uint64_t* t_stamp = nullptr;  // stamp slot of the next reduce launch on this thread
+thread_local bool t_plainStores = false;   // setReducePlainStores
 
 // Vector body.  `head` elements bring the destination c to a 16-B boundary;
 // a and b may sit at any element offset relative to it (Src).  One workgroup = one tile of BLOCK lanes x UNROLL
@@ -1239,6 +1240,7 @@ int launch3(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
       default: break;
     }
   }
+  if (t_plainStores) return launch_vec<Tr, OP, kUnroll, kVecBlock, kAuxNT, 0>(c, a, b, n, head, s);
   return launch_vec<Tr, OP, kUnroll, kVecBlock, kAuxNT, kAuxNT>(c, a, b, n, head, s);
 }
 
@@ -1483,6 +1485,12 @@ int launchFoldSend(int op, int dtype, void* dst, const void* const* srcs, int k,
     case GLOO_HIP_F64: return by_op_fold_send<TrF64>(op, dst, list, k, mode, n, F, epoch, s);
     default: return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
   }
+}
+
+bool setReducePlainStores(bool plain) {
+  const bool prev = t_plainStores;
+  t_plainStores = plain;
+  return prev;
 }
 
 uint64_t* setLaunchStamp(uint64_t* stamp) {

@@ -274,6 +274,11 @@ class PlanExecutor {
   size_t copyOutKernelBytes_ = 0;
   unsigned copyOutBlocks_ = 256;
   CopyStore localStore_ = kCopyStorePlain;
+  // REDUCE steps (the reference routes' reduce into the user buffer) store
+  // plain instead of `nt` (GLOO_AMD_REDUCE_STORE = plain | nt): HD on the
+  // reference route 3-4 % faster per call at 64 and 256 MiB per rank, equal
+  // below (profiles/round5/r5u_*)
+  bool reducePlain_ = true;
   bool foldSend_ = true;         // a FOLD's result SENDs ride in the fold's pass (launchFoldSend)
   bool foldSendUsed_ = false;    // ... and some enqueue did so
   unsigned* ticket_ = nullptr;   // copy_signal_kernel tickets, one counter per (peer, slot)

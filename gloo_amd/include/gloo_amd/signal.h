@@ -165,6 +165,11 @@ inline bool stampSpan(const uint64_t* slot, uint64_t* ticks) {
   return true;
 }
 uint64_t* setLaunchStamp(uint64_t* slot);
+// The stores of the element-wise reduce kernels launched on this thread
+// (gloo_hip_reduce / reduce3): `nt` (default, the chunk-reduce of the
+// headline bench streams past the Infinity Cache) or plain (a plan's REDUCE
+// into a buffer that is re-read soon).  Returns the previous setting.
+bool setReducePlainStores(bool plain);
 int launchStampInit(uint64_t* stamps, int k, hipStream_t stream);
 
 // Registered custom reductions (gloo_hip_register_op): op codes
