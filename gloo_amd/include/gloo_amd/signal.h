@@ -107,13 +107,13 @@ hipError_t launchWaitMulti(const uint64_t* const* flags, const Seq* targets, int
 // (no grid barrier): every rank slices every message alike, so slice g of a
 // message is produced, sent, received and consumed by workgroups g alone.  The
 // executor proves per plan that each step reads exactly the ranges earlier
-// steps or peers wrote (executor.cc sliceable) before choosing it.
+// steps or peers wrote (executor_modes.cc sliceable) before choosing it.
 enum { kInterpCopy = 0, kInterpSend = 1, kInterpSignal = 2, kInterpWait = 3, kInterpFold = 4 };
 struct InterpStep {
   int32_t kind;       // kInterp*
   int32_t mode;       // FOLD: 0 left fold, 1 reverse (acc = s op acc), 2 balanced tree
   int32_t nsrc;       // FOLD: sources
-  int32_t flags;      // kInterpDefer: the next step is independent of this one (executor.cc buildInterp)
+  int32_t flags;      // kInterpDefer: the next step is independent of this one (executor_run.cc buildInterp)
   uint64_t* flag;     // SEND / SIGNAL: the flag written; WAIT: the flag polled (slice 0's)
   uint64_t base, perRun;
   char* dst;

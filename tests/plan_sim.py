@@ -188,7 +188,7 @@ def sliceable(algo, P, n, rank, k=1, nin=0, recv=None, elem_size=4, max_seg=0):
 
 
 def reduce_forward_order(steps):
-    """The executor's reduce + forward rewrite (executor.cc enqueue): a window
+    """The executor's reduce + forward rewrite (executor_run.cc enqueue): a window
     REDUCE(range R) NOTIFY WAIT_NOTIFY SEND(R, unchanged) runs as
     WAIT_NOTIFY, then ONE launch that reduces R and stores the result into
     the peer's inbox as it goes (here: REDUCE then SEND), then NOTIFY.
@@ -335,7 +335,7 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
             dst[s.dst_off + a0:s.dst_off + a1] = src[s.src_off + a0:s.src_off + a1].copy()
         elif K in (KIND["LOCAL_REDUCE"], KIND["LOCAL_BCAST"]):
             # sliced: the executor first splits whole-range local steps at the
-            # user-buffer boundaries the other steps use (executor.cc userCuts)
+            # user-buffer boundaries the other steps use (executor_modes.cc userCuts)
             pieces = cut_range(cuts[r], s.dst_off, s.length) if slices > 1 else [(s.dst_off, s.length)]
             for o, ln in pieces:
                 b0, b1 = slice_range(ln, g, slices, es)
@@ -373,7 +373,7 @@ MAX_SRCS = 8            # include/gloo_amd.h GLOO_HIP_MAX_SRCS
 
 
 def sliced_interp_steps(algo, P, n, rank, k=1, nin=0, recv=None, elem_size=4, max_seg=0):
-    """Python statement of executor.cc slicedInterpSteps: an upper bound on the
+    """Python statement of executor_modes.cc slicedInterpSteps: an upper bound on the
     device step list buildInterp() emits for `rank`'s sliced plan.  A rank
     proposes slicing only when this is <= INTERP_MAX_STEPS."""
     steps, _ = get_plan(algo, rank, P, n, k, recv, nin=nin, elem_size=elem_size, max_seg=max_seg)

@@ -583,7 +583,7 @@ for _c, _e, _f in FOLD_SEND_CASES:
 def test_processes_fold_send(torch, golden_sched, case, env, fused):
     """Fold + forward: a mesh owner's fold stores its finished range into
     every peer's inbox in the same pass and signals them from its last
-    workgroup (executor.cc enqueue, reduce.hip fold_send_kernel).  Five runs
+    workgroup (executor_run.cc enqueue, reduce.hip fold_send_kernel).  Five runs
     (eager, or enqueued / captured / replayed) must each equal the reference's
     output byte for byte; `fused` says whether the mode query must report the
     fused launch (None: not asserted)."""

@@ -1,5 +1,5 @@
 """CPU: which plan shapes the executor may fuse into fold + forward launches
-(executor.cc enqueue; reduce.hip fold_send_kernel), checked on the plan
+(executor_run.cc enqueue; reduce.hip fold_send_kernel), checked on the plan
 simulator (tests/plan_sim.py) against the reference's goldens.
 
 The executor fuses a FOLD with the SENDs of its result that follow it

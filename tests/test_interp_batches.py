@@ -1,5 +1,5 @@
 """CPU: the one-launch interpreter's batching rule (signal.h kInterpDefer,
-executor.cc markInterpBatches, exported as gloo_hip_interp_batches).
+executor_run.cc markInterpBatches, exported as gloo_hip_interp_batches).
 
 The interpreter kernel (reduce.hip plan_interp_kernel) drains memory and
 passes a workgroup barrier only at the LAST step of a batch, so every pair of

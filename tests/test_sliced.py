@@ -161,7 +161,7 @@ def test_sliced_new_style_matches_reference(golden_sched, golden_new, src, case)
 
 def test_many_segment_plans_are_not_proposed_for_slicing():
     """A sliced plan has no fallback route, so a rank proposes slicing only if
-    its device step list fits (executor.cc slicedInterpSteps).  The new-style
+    its device step list fits (executor_modes.cc slicedInterpSteps).  The new-style
     gloo::reduce on the reference route at 256 MiB with 1 MiB segments, 4 ranks
     (the 4-rank bench rehearsal that failed before the bound existed), needs
     far more than the 512 entries; the small default test plans fit."""
