@@ -326,6 +326,203 @@ void PlanExecutor::classifyPointers() {
                    "gloo::reduce: the input must live on the rank's own device");
 }
 
+// This rank's proposal for the sliced interpreter (executor.h): one
+// workgroup per sliceBytes() of its largest message, if its own plan and the
+// messages its peers write into its arena slice consistently (sliceable); 0
+// otherwise.  All ranks then take the smallest proposal, so they agree.
+int32_t PlanExecutor::proposeSlices(const std::set<int>& recvPeers) {
+  const int me = ctx_->rank, P = ctx_->size;
+  int32_t proposal = 0;
+  if (interpMode_ && mailbox_ && !anyRemote_ && !hostArena_) {
+    size_t maxMsg = 0;
+    for (const Step& s : plan_.steps) maxMsg = std::max(maxMsg, (size_t)s.length * es_);
+    const size_t want = std::min<size_t>(maxSlices(), std::max<size_t>(1, (maxMsg + sliceBytes() - 1) / sliceBytes()));
+    // above maxSlices() slices of sliceCapBytes() graph replay is as fast
+    if (maxMsg <= (size_t)maxSlices() * sliceCapBytes()) {
+      std::map<std::pair<int, int>, size_t> decl;  // (sender, slot) -> arena offset
+      for (const Step& d : plan_.steps)
+        if (d.kind == GLOO_HIP_STEP_DECL_RECV) decl[{d.peer, d.slot}] = d.dst_off;
+      std::vector<Access> remote;
+      bool ok = true;
+      for (int peer : recvPeers) {
+        const Plan theirs = planFor(planAlgo_, peer, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
+        for (const Step& t : theirs.steps)
+          if (t.kind == GLOO_HIP_STEP_SEND && t.peer == me) {
+            auto it = decl.find({peer, t.slot});
+            if (it == decl.end()) ok = false;
+            else remote.push_back({kArena, it->second + t.dst_off, t.length});
+          }
+      }
+      if (ok && slicedInterpSteps(plan_, (int)inputs_.size(), (int)ptrs_.size()) <= (size_t)kInterpMaxSteps &&
+          sliceable(plan_, (int)inputs_.size(), (int)ptrs_.size(), remote))
+        proposal = (int32_t)want;
+    }
+  }
+  return proposal;
+}
+
+// Every plan peer's record: its mailbox (a channel uses mailboxes when both
+// ends signal from the device and have one — both ends decide alike), and,
+// for a peer this rank sends to, its inbox arena and the region the peer
+// declared there for our messages (its own plan).
+void PlanExecutor::mapPeers(const std::vector<std::vector<char>>& arenas, const std::set<int>& planPeers,
+                            const std::set<int>& sendPeers) {
+  const int me = ctx_->rank, P = ctx_->size;
+  peerMailbox_.assign(P, nullptr);
+  peerMailboxIpc_.assign(P, false);
+  for (int peer : planPeers) {
+    ArenaRecord pr;
+    parseArena(arenas.at(peer), peer, &pr);
+    if (mailbox_ && pr.deviceSignal && pr.hasMailbox) {
+      if (pr.pid == ctx_->pid()) {
+        peerMailbox_[peer] = reinterpret_cast<uint64_t*>(pr.mailboxPtr);
+        if (pr.device != ctx_->device()) {
+          hipError_t e = hipDeviceEnablePeerAccess(pr.device, 0);
+          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
+          (void)hipGetLastError();
+        }
+      } else {
+        ipc::Remote rm;
+        rm.pid = pr.pid;
+        rm.incarnation = pr.incarnation;
+        rm.id = pr.mailboxSlabId;
+        void* p = ipc::import(rm, pr.mailboxBytes + 4096, ctx_->device());
+        uint64_t seen = 0;
+        GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, static_cast<char*>(p) + pr.mailboxBytes, sizeof(seen),
+                                          hipMemcpyDeviceToHost, stream_));
+        GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+        GLOO_AMD_ENFORCE(seen == pr.mailboxNonce, "rank ", me, ": the IPC mapping of rank ", peer, "'s mailbox (",
+                         (void*)pr.mailboxPtr, " in pid ", pr.pid, ", mapped at ", p, ") ", kStaleImport, ": read ",
+                         seen, ", expected ", pr.mailboxNonce);
+        peerMailbox_[peer] = static_cast<uint64_t*>(p);
+        peerMailboxIpc_[peer] = true;
+      }
+    }
+    if (!sendPeers.count(peer)) continue;
+    if (pr.host && pr.pid != ctx_->pid()) {
+      // another process's host workspace: map the same pages here
+      peerShm_.push_back(HostShm::open(std::string(pr.shm), pr.bytes));
+      peers_[peer].base = static_cast<char*>(peerShm_.back()->dev);
+    } else if (pr.host || pr.pid == ctx_->pid()) {
+      // same process: registered portable (host) or peer-accessible (device)
+      peers_[peer].base = reinterpret_cast<char*>(pr.ptr);
+      if (pr.device != ctx_->device()) {
+        hipError_t e = hipDeviceEnablePeerAccess(pr.device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
+        (void)hipGetLastError();
+      }
+    } else {
+      // Another process's pool slab (ipc.h): mapped once, kept.  The mapping
+      // must show the nonce the owner just wrote at the slab's start, and
+      // span the arena; anything else is a hard error, never a silent
+      // misdelivery.
+      GLOO_AMD_TRACE_PHASE("importing rank ", peer, "'s arena slab ", pr.slabId, " (", pr.bytes, " B)");
+      ipc::Remote rm;
+      rm.pid = pr.pid;
+      rm.incarnation = pr.incarnation;
+      rm.id = pr.slabId;
+      void* p = ipc::import(rm, pr.bytes, ctx_->device());
+      GLOO_AMD_TRACE_PHASE("imported at ", p);
+      uint64_t seen = 0;
+      GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, p, sizeof(seen), hipMemcpyDeviceToHost, stream_));
+      GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+      if (ipcDiag())
+        std::fprintf(stderr, "[ipc-diag %d r%d inst%llu] import rank %d arena %p %llu B (pid %d) -> %p: seen %llx "
+                     "want %llx%s%s\n", ctx_->pid(), me, (unsigned long long)inst_, peer, (void*)pr.ptr,
+                     (unsigned long long)pr.bytes, pr.pid, p, (unsigned long long)seen,
+                     (unsigned long long)pr.nonce, seen == pr.nonce ? "" : " MISMATCH: ",
+                     seen == pr.nonce ? "" : diagProbe(p, stream_).c_str());
+      peers_[peer].base = static_cast<char*>(p);
+      peers_[peer].ipc = true;
+      // (ipc::import maps the whole slab, at least pr.bytes, or raises)
+      GLOO_AMD_ENFORCE(seen == pr.nonce, "rank ", me, ": the mapping of rank ", peer, "'s inbox arena (",
+                       (void*)pr.ptr, ", ", pr.bytes, " B, slab ", pr.slabId, " of pid ", pr.pid, ", mapped at ", p,
+                       ") ", kStaleImport, ": read ", seen, ", expected ", pr.nonce);
+    }
+    const Plan theirs = planFor(planAlgo_, peer, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
+    for (const Step& d : theirs.steps)
+      if (d.kind == GLOO_HIP_STEP_DECL_RECV && d.peer == me) {
+        GLOO_AMD_ENFORCE((d.dst_off + d.length) * es_ <= pr.bytes, "peer region outside its arena");
+        remoteRegion_[{peer, d.slot}] = d.dst_off;
+      }
+  }
+  for (const Step& s : plan_.steps)
+    if (s.kind == GLOO_HIP_STEP_SEND)
+      GLOO_AMD_ENFORCE(remoteRegion_.count({s.peer, s.slot}), "rank ", s.peer, " declared no region for rank ",
+                       me, " slot ", s.slot);
+}
+
+// Device signalling: the copy engines, fold + forward, the completion
+// protocol, copy grids and store flavours, the ticket counters, and whether
+// runs replay a hipGraph.
+void PlanExecutor::configureDeviceLaunches() {
+  const int me = ctx_->rank, P = ctx_->size;
+  (void)me;
+  (void)ctx_->counterDevicePtr(inst_, 0, 0, 0);  // register the control block now
+  ctx_->errorWord(me).store(0);
+  // Copy engine: a lone SEND is hipMemcpyAsync + signal ("memcpy", the
+  // default) or the copy+signal kernel ("kernel"); a batch of consecutive
+  // SENDs (one per peer) is one multi-destination copy kernel (default),
+  // or with "memcpy" one hipMemcpyAsync per forked stream.
+  const char* cp = std::getenv("GLOO_AMD_COPY");
+  const std::string cmode = cp ? cp : "auto";
+  kernelCopy_ = cmode == "kernel";
+  autoCopy_ = cmode == "auto";
+  batchKernelCopy_ = cmode != "memcpy";
+  // Fold + forward (enqueue, FOLD): "0" keeps the fold and its SENDs apart.
+  const char* fs = std::getenv("GLOO_AMD_FOLD_SEND");
+  foldSend_ = !(fs && std::string(fs) == "0");
+  // Completion protocol of the signalling kernels (GLOO_AMD_FWD_RELEASE)
+  refreshFwdLean();
+  // Workgroups per copy (executor.h): a few dozen saturate an xGMI link.
+  // GLOO_AMD_COPY_BLOCKS overrides both the remote and the same-GPU size.
+  if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS")) {
+    copyBlocks_ = (unsigned)std::max(1, std::atoi(cb));
+    copyBlocksLocal_ = copyBlocks_;
+  }
+  if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS_LOCAL")) copyBlocksLocal_ = (unsigned)std::max(1, std::atoi(cb));
+  if (const char* cb = std::getenv("GLOO_AMD_COPY_OUT_BYTES")) copyOutKernelBytes_ = std::strtoull(cb, nullptr, 10);
+  if (const char* cb = std::getenv("GLOO_AMD_COPY_OUT_BLOCKS")) copyOutBlocks_ = (unsigned)std::max(1, std::atoi(cb));
+  if (const char* cs = std::getenv("GLOO_AMD_REDUCE_STORE")) reducePlain_ = std::string(cs) != "nt";
+  if (const char* cs = std::getenv("GLOO_AMD_LOCAL_COPY_STORE"))
+    localStore_ = std::string(cs) == "nt" ? kCopyStoreNT : std::string(cs) == "wt" ? kCopyStoreWT : kCopyStorePlain;
+  const size_t tickets = std::max<size_t>(256, (size_t)P * GLOO_HIP_NUM_SLOTS * sizeof(unsigned));
+  GLOO_AMD_HIP_ALLOC(hipMalloc(&ticket_, tickets));
+  // zeroed on the executor's stream and complete before any copy kernel
+  // (a plain hipMemset goes to the null stream, which a non-blocking
+  // stream does not wait for)
+  GLOO_AMD_HIP_CHECK(hipMemsetAsync(ticket_, 0, tickets, stream_));
+  // Graph replay pays off where the host is the bottleneck: a plan with
+  // steps that are not fused one-workgroup launches.  A mesh plan (a few
+  // launches per call) whose messages reach GLOO_AMD_GRAPH_BYTES (default
+  // 4 MiB) is device-bound instead: the host's eager enqueue stays ahead,
+  // and eager measured 7-13 % faster than replay (HD 16 and 64 MiB per
+  // rank, 2 and 4 ranks: DESIGN.md §4, profiles/round3/r3ah_*, r3ak_*).
+  // The reference routes keep replay: their per-hop credit handshakes make
+  // many launches per call, and eager lost there (HD 16 MiB per rank, 4
+  // ranks: 149 vs 122 us, r3ax_*).  "1" / "0" force it.
+  const char* gm = std::getenv("GLOO_AMD_GRAPH");
+  const std::string gmode = gm ? gm : "auto";
+  bool unfused = fuseBytes() == 0 || custom_;
+  size_t maxMsg = 0;
+  for (const Step& s : plan_.steps) {
+    if ((s.kind == GLOO_HIP_STEP_SEND || s.kind == GLOO_HIP_STEP_REDUCE || s.kind == GLOO_HIP_STEP_COPY ||
+         s.kind == GLOO_HIP_STEP_LOCAL_REDUCE || s.kind == GLOO_HIP_STEP_LOCAL_BCAST ||
+         s.kind == GLOO_HIP_STEP_FOLD) &&
+        s.length * es_ > fuseBytes())
+      unfused = true;
+    maxMsg = std::max(maxMsg, (size_t)s.length * es_);
+  }
+  const bool meshPlan = (planAlgo_ & GLOO_HIP_ALGO_MESH) || planAlgo_ == GLOO_HIP_ALGO_RING_CHUNKED_MESH;
+  graphMode_ = gmode == "1" || (gmode == "auto" && unfused && !(meshPlan && maxMsg >= graphBytes()));
+  if (interpMode_) GLOO_AMD_HIP_ALLOC(hipMalloc(&interpSteps_, kInterpMaxSteps * sizeof(InterpStep)));
+  if (graphMode_) {
+    GLOO_AMD_HIP_ALLOC(hipMalloc(&epoch_, sizeof(uint64_t)));
+    GLOO_AMD_HIP_CHECK(hipMemsetAsync(epoch_, 0, sizeof(uint64_t), stream_));
+  }
+  GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
 PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int dtype,
                            const std::vector<void*>& ptrs, size_t count, const std::vector<int>& recvElems,
                            hipStream_t stream, const std::vector<void*>& inputs, size_t maxSegmentBytes,
@@ -547,42 +744,14 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
   }
   // Interpreter (executor.h): the knobs every rank reads alike, and this
-  // rank's proposal for the sliced form — one workgroup per sliceBytes() of
-  // its largest message, if its own plan and the messages its peers write
-  // into its arena slice consistently (sliceable).  All ranks then take the
-  // smallest proposal, so they agree.
+  // rank's proposal for the sliced form (proposeSlices).
   {
     const char* im = std::getenv("GLOO_AMD_INTERP");
     const char* gm = std::getenv("GLOO_AMD_GRAPH");
     interpMode_ = deviceSignal_ && !(im && std::string(im) == "0") && !(gm && std::string(gm) == "1") &&
                   interpBytes() > 0 && !custom_;
   }
-  int32_t proposal = 0;
-  if (interpMode_ && mailbox_ && !anyRemote_ && !hostArena_) {
-    size_t maxMsg = 0;
-    for (const Step& s : plan_.steps) maxMsg = std::max(maxMsg, (size_t)s.length * es_);
-    const size_t want = std::min<size_t>(maxSlices(), std::max<size_t>(1, (maxMsg + sliceBytes() - 1) / sliceBytes()));
-    // above maxSlices() slices of sliceCapBytes() graph replay is as fast
-    if (maxMsg <= (size_t)maxSlices() * sliceCapBytes()) {
-      std::map<std::pair<int, int>, size_t> decl;  // (sender, slot) -> arena offset
-      for (const Step& d : plan_.steps)
-        if (d.kind == GLOO_HIP_STEP_DECL_RECV) decl[{d.peer, d.slot}] = d.dst_off;
-      std::vector<Access> remote;
-      bool ok = true;
-      for (int peer : recvPeers) {
-        const Plan theirs = planFor(planAlgo_, peer, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
-        for (const Step& t : theirs.steps)
-          if (t.kind == GLOO_HIP_STEP_SEND && t.peer == me) {
-            auto it = decl.find({peer, t.slot});
-            if (it == decl.end()) ok = false;
-            else remote.push_back({kArena, it->second + t.dst_off, t.length});
-          }
-      }
-      if (ok && slicedInterpSteps(plan_, (int)inputs_.size(), (int)ptrs_.size()) <= (size_t)kInterpMaxSteps &&
-          sliceable(plan_, (int)inputs_.size(), (int)ptrs_.size(), remote))
-        proposal = (int32_t)want;
-    }
-  }
+  const int32_t proposal = proposeSlices(recvPeers);
   ArenaRecord rec;
   std::memset(&rec, 0, sizeof(rec));
   rec.interpSlices = proposal;
@@ -642,92 +811,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   std::string setupReason;
   try {
 
-  // Every plan peer's record: its mailbox (a channel uses mailboxes when
-  // both ends signal from the device and have one — both ends decide alike),
-  // and, for a peer this rank sends to, its inbox arena and the region the
-  // peer declared there for our messages (its own plan).
-  peerMailbox_.assign(P, nullptr);
-  peerMailboxIpc_.assign(P, false);
-  for (int peer : planPeers) {
-    ArenaRecord pr;
-    parseArena(arenas.at(peer), peer, &pr);
-    if (mailbox_ && pr.deviceSignal && pr.hasMailbox) {
-      if (pr.pid == ctx_->pid()) {
-        peerMailbox_[peer] = reinterpret_cast<uint64_t*>(pr.mailboxPtr);
-        if (pr.device != ctx_->device()) {
-          hipError_t e = hipDeviceEnablePeerAccess(pr.device, 0);
-          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
-          (void)hipGetLastError();
-        }
-      } else {
-        ipc::Remote rm;
-        rm.pid = pr.pid;
-        rm.incarnation = pr.incarnation;
-        rm.id = pr.mailboxSlabId;
-        void* p = ipc::import(rm, pr.mailboxBytes + 4096, ctx_->device());
-        uint64_t seen = 0;
-        GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, static_cast<char*>(p) + pr.mailboxBytes, sizeof(seen),
-                                          hipMemcpyDeviceToHost, stream_));
-        GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
-        GLOO_AMD_ENFORCE(seen == pr.mailboxNonce, "rank ", me, ": the IPC mapping of rank ", peer, "'s mailbox (",
-                         (void*)pr.mailboxPtr, " in pid ", pr.pid, ", mapped at ", p, ") ", kStaleImport, ": read ",
-                         seen, ", expected ", pr.mailboxNonce);
-        peerMailbox_[peer] = static_cast<uint64_t*>(p);
-        peerMailboxIpc_[peer] = true;
-      }
-    }
-    if (!sendPeers.count(peer)) continue;
-    if (pr.host && pr.pid != ctx_->pid()) {
-      // another process's host workspace: map the same pages here
-      peerShm_.push_back(HostShm::open(std::string(pr.shm), pr.bytes));
-      peers_[peer].base = static_cast<char*>(peerShm_.back()->dev);
-    } else if (pr.host || pr.pid == ctx_->pid()) {
-      // same process: registered portable (host) or peer-accessible (device)
-      peers_[peer].base = reinterpret_cast<char*>(pr.ptr);
-      if (pr.device != ctx_->device()) {
-        hipError_t e = hipDeviceEnablePeerAccess(pr.device, 0);
-        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
-        (void)hipGetLastError();
-      }
-    } else {
-      // Another process's pool slab (ipc.h): mapped once, kept.  The mapping
-      // must show the nonce the owner just wrote at the slab's start, and
-      // span the arena; anything else is a hard error, never a silent
-      // misdelivery.
-      GLOO_AMD_TRACE_PHASE("importing rank ", peer, "'s arena slab ", pr.slabId, " (", pr.bytes, " B)");
-      ipc::Remote rm;
-      rm.pid = pr.pid;
-      rm.incarnation = pr.incarnation;
-      rm.id = pr.slabId;
-      void* p = ipc::import(rm, pr.bytes, ctx_->device());
-      GLOO_AMD_TRACE_PHASE("imported at ", p);
-      uint64_t seen = 0;
-      GLOO_AMD_HIP_CHECK(hipMemcpyAsync(&seen, p, sizeof(seen), hipMemcpyDeviceToHost, stream_));
-      GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
-      if (ipcDiag())
-        std::fprintf(stderr, "[ipc-diag %d r%d inst%llu] import rank %d arena %p %llu B (pid %d) -> %p: seen %llx "
-                     "want %llx%s%s\n", ctx_->pid(), me, (unsigned long long)inst_, peer, (void*)pr.ptr,
-                     (unsigned long long)pr.bytes, pr.pid, p, (unsigned long long)seen,
-                     (unsigned long long)pr.nonce, seen == pr.nonce ? "" : " MISMATCH: ",
-                     seen == pr.nonce ? "" : diagProbe(p, stream_).c_str());
-      peers_[peer].base = static_cast<char*>(p);
-      peers_[peer].ipc = true;
-      // (ipc::import maps the whole slab, at least pr.bytes, or raises)
-      GLOO_AMD_ENFORCE(seen == pr.nonce, "rank ", me, ": the mapping of rank ", peer, "'s inbox arena (",
-                       (void*)pr.ptr, ", ", pr.bytes, " B, slab ", pr.slabId, " of pid ", pr.pid, ", mapped at ", p,
-                       ") ", kStaleImport, ": read ", seen, ", expected ", pr.nonce);
-    }
-    const Plan theirs = planFor(planAlgo_, peer, P, count_, 0, 1, es_, maxSegmentBytes_, recvElems_);
-    for (const Step& d : theirs.steps)
-      if (d.kind == GLOO_HIP_STEP_DECL_RECV && d.peer == me) {
-        GLOO_AMD_ENFORCE((d.dst_off + d.length) * es_ <= pr.bytes, "peer region outside its arena");
-        remoteRegion_[{peer, d.slot}] = d.dst_off;
-      }
-  }
-  for (const Step& s : plan_.steps)
-    if (s.kind == GLOO_HIP_STEP_SEND)
-      GLOO_AMD_ENFORCE(remoteRegion_.count({s.peer, s.slot}), "rank ", s.peer, " declared no region for rank ",
-                       me, " slot ", s.slot);
+  mapPeers(arenas, planPeers, sendPeers);
   // the sliced interpreter runs on every rank or on none
   int32_t agreed = proposal;
   for (int r = 0; r < P && agreed > 1; r++) {
@@ -738,71 +822,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   }
   slices_ = agreed > 1 ? agreed : 1;
   assignSeqs();
-  if (deviceSignal_) {
-    (void)ctx_->counterDevicePtr(inst_, 0, 0, 0);  // register the control block now
-    ctx_->errorWord(me).store(0);
-    // Copy engine: a lone SEND is hipMemcpyAsync + signal ("memcpy", the
-    // default) or the copy+signal kernel ("kernel"); a batch of consecutive
-    // SENDs (one per peer) is one multi-destination copy kernel (default),
-    // or with "memcpy" one hipMemcpyAsync per forked stream.
-    const char* cp = std::getenv("GLOO_AMD_COPY");
-    const std::string cmode = cp ? cp : "auto";
-    kernelCopy_ = cmode == "kernel";
-    autoCopy_ = cmode == "auto";
-    batchKernelCopy_ = cmode != "memcpy";
-    // Fold + forward (enqueue, FOLD): "0" keeps the fold and its SENDs apart.
-    const char* fs = std::getenv("GLOO_AMD_FOLD_SEND");
-    foldSend_ = !(fs && std::string(fs) == "0");
-    // Completion protocol of the signalling kernels (GLOO_AMD_FWD_RELEASE)
-    refreshFwdLean();
-    // Workgroups per copy (executor.h): a few dozen saturate an xGMI link.
-    // GLOO_AMD_COPY_BLOCKS overrides both the remote and the same-GPU size.
-    if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS")) {
-      copyBlocks_ = (unsigned)std::max(1, std::atoi(cb));
-      copyBlocksLocal_ = copyBlocks_;
-    }
-    if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS_LOCAL")) copyBlocksLocal_ = (unsigned)std::max(1, std::atoi(cb));
-    if (const char* cb = std::getenv("GLOO_AMD_COPY_OUT_BYTES")) copyOutKernelBytes_ = std::strtoull(cb, nullptr, 10);
-    if (const char* cb = std::getenv("GLOO_AMD_COPY_OUT_BLOCKS")) copyOutBlocks_ = (unsigned)std::max(1, std::atoi(cb));
-    if (const char* cs = std::getenv("GLOO_AMD_REDUCE_STORE")) reducePlain_ = std::string(cs) != "nt";
-    if (const char* cs = std::getenv("GLOO_AMD_LOCAL_COPY_STORE"))
-      localStore_ = std::string(cs) == "nt" ? kCopyStoreNT : std::string(cs) == "wt" ? kCopyStoreWT : kCopyStorePlain;
-    const size_t tickets = std::max<size_t>(256, (size_t)P * GLOO_HIP_NUM_SLOTS * sizeof(unsigned));
-    GLOO_AMD_HIP_ALLOC(hipMalloc(&ticket_, tickets));
-    // zeroed on the executor's stream and complete before any copy kernel
-    // (a plain hipMemset goes to the null stream, which a non-blocking
-    // stream does not wait for)
-    GLOO_AMD_HIP_CHECK(hipMemsetAsync(ticket_, 0, tickets, stream_));
-    // Graph replay pays off where the host is the bottleneck: a plan with
-    // steps that are not fused one-workgroup launches.  A mesh plan (a few
-    // launches per call) whose messages reach GLOO_AMD_GRAPH_BYTES (default
-    // 4 MiB) is device-bound instead: the host's eager enqueue stays ahead,
-    // and eager measured 7-13 % faster than replay (HD 16 and 64 MiB per
-    // rank, 2 and 4 ranks: DESIGN.md §4, profiles/round3/r3ah_*, r3ak_*).
-    // The reference routes keep replay: their per-hop credit handshakes make
-    // many launches per call, and eager lost there (HD 16 MiB per rank, 4
-    // ranks: 149 vs 122 us, r3ax_*).  "1" / "0" force it.
-    const char* gm = std::getenv("GLOO_AMD_GRAPH");
-    const std::string gmode = gm ? gm : "auto";
-    bool unfused = fuseBytes() == 0 || custom_;
-    size_t maxMsg = 0;
-    for (const Step& s : plan_.steps) {
-      if ((s.kind == GLOO_HIP_STEP_SEND || s.kind == GLOO_HIP_STEP_REDUCE || s.kind == GLOO_HIP_STEP_COPY ||
-           s.kind == GLOO_HIP_STEP_LOCAL_REDUCE || s.kind == GLOO_HIP_STEP_LOCAL_BCAST ||
-           s.kind == GLOO_HIP_STEP_FOLD) &&
-          s.length * es_ > fuseBytes())
-        unfused = true;
-      maxMsg = std::max(maxMsg, (size_t)s.length * es_);
-    }
-    const bool meshPlan = (planAlgo_ & GLOO_HIP_ALGO_MESH) || planAlgo_ == GLOO_HIP_ALGO_RING_CHUNKED_MESH;
-    graphMode_ = gmode == "1" || (gmode == "auto" && unfused && !(meshPlan && maxMsg >= graphBytes()));
-    if (interpMode_) GLOO_AMD_HIP_ALLOC(hipMalloc(&interpSteps_, kInterpMaxSteps * sizeof(InterpStep)));
-    if (graphMode_) {
-      GLOO_AMD_HIP_ALLOC(hipMalloc(&epoch_, sizeof(uint64_t)));
-      GLOO_AMD_HIP_CHECK(hipMemsetAsync(epoch_, 0, sizeof(uint64_t), stream_));
-    }
-    GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
-  }
+  if (deviceSignal_) configureDeviceLaunches();
   } catch (const std::exception& e) {
     setupFailure = std::current_exception();
     setupReason = e.what();

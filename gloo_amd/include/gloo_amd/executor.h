@@ -63,6 +63,7 @@
 
 #include <cstdlib>
 #include <map>
+#include <set>
 #include <string>
 #include <memory>
 #include <utility>
@@ -197,6 +198,11 @@ class PlanExecutor {
   std::vector<char*> outStage_, inStage_;
   bool anyRemote_ = false;
   void classifyPointers();
+  // construction phases (executor.cc)
+  int32_t proposeSlices(const std::set<int>& recvPeers);
+  void mapPeers(const std::vector<std::vector<char>>& arenas, const std::set<int>& planPeers,
+                const std::set<int>& sendPeers);
+  void configureDeviceLaunches();
   Plan plan_;
   uint64_t inst_;
   char* arena_ = nullptr;       // device-visible address of this rank's inboxes
