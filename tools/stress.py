@@ -11,6 +11,7 @@ against its closed form (rank r contributes r + 1 at every position, or
 run with a non-zero exit.  One JSON line per rank at the end.
 
   python tools/stress.py <ranks> <seconds> [seed]
+STRESS_BIG=1 adds 16 MiB and 64 MiB cases (eager and graph-replayed mesh plans).
 """
 import json
 import os
@@ -33,11 +34,13 @@ ctx = gloo_amd.Context(rank, P, store, device=0, timeout_ms=60000)
 tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "i32": torch.int32}
 cases = []
 sizes = [1, 7, 1000, 4099, 65536 + 3, (1 << 20) + 5, 2 << 20]
+if os.environ.get("STRESS_BIG") == "1":  # the eager and graph launch modes of the mesh routes (>= 4 MiB messages)
+    sizes += [(4 << 20) + 3, 16 << 20]
 combos = (("sum", "f32"), ("max", "bf16"), ("min", "i32"), ("sum", "i32"))
 # a context holds at most 64 live algorithms: one op / dtype per (schedule, size), rotating
 for ai, algo in enumerate(("ring_chunked", "halving_doubling", "ring", "reduce_scatter")):
     for si, n in enumerate(sizes):
-        if algo == "ring" and n > (1 << 20):
+        if algo == "ring" and n > (1 << 20):  # (the plain ring moves the whole buffer per hop)
             continue
         op, dt = combos[(ai + si) % len(combos)]
         cases.append((algo, op, dt, n))
