@@ -2,6 +2,7 @@
 #include "gloo_amd/ipc.h"
 
 #include <errno.h>
+#include <fcntl.h>
 #include <sys/socket.h>
 #include <sys/time.h>
 #include <sys/un.h>
@@ -385,7 +386,9 @@ void* import(const Remote& r, size_t bytes, int device) {
   void* osHandle = runtimeVersion() >= 70200000 ? reinterpret_cast<void*>(static_cast<intptr_t>(fd))
                                                 : static_cast<void*>(&fdv);
   const hipError_t e = hipMemImportFromShareableHandle(&h, osHandle, hipMemHandleTypePosixFileDescriptor);
-  ::close(fd);
+  // the import does not take the descriptor over (the dma-buf stays referenced
+  // by the mapping); close it unless the runtime already did
+  if (::fcntl(fd, F_GETFD) != -1) ::close(fd);
   GLOO_AMD_HIP_ALLOC(e);
   void* va = nullptr;
   try {
