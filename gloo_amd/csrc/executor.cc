@@ -516,6 +516,15 @@ void PlanExecutor::configureDeviceLaunches() {
   const bool meshPlan = (planAlgo_ & GLOO_HIP_ALGO_MESH) || planAlgo_ == GLOO_HIP_ALGO_RING_CHUNKED_MESH;
   graphMode_ = gmode == "1" || (gmode == "auto" && unfused && !(meshPlan && maxMsg >= graphBytes()));
   if (interpMode_) GLOO_AMD_HIP_ALLOC(hipMalloc(&interpSteps_, kInterpMaxSteps * sizeof(InterpStep)));
+  const char* ds = std::getenv("GLOO_AMD_DONE_SPIN");
+  if (interpMode_ && ownStream_ && !(ds && ds[0] == '0')) {
+    GLOO_AMD_HIP_ALLOC(hipHostMalloc(reinterpret_cast<void**>(&hostDone_), 64,
+                                     hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
+    __atomic_store_n(hostDone_, 0, __ATOMIC_RELEASE);
+    GLOO_AMD_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hostDoneDev_), hostDone_, 0));
+    GLOO_AMD_HIP_ALLOC(hipMalloc(&doneTicket_, 64));
+    GLOO_AMD_HIP_CHECK(hipMemsetAsync(doneTicket_, 0, 64, stream_));
+  }
   if (graphMode_) {
     GLOO_AMD_HIP_ALLOC(hipMalloc(&epoch_, sizeof(uint64_t)));
     GLOO_AMD_HIP_CHECK(hipMemsetAsync(epoch_, 0, sizeof(uint64_t), stream_));
@@ -900,6 +909,10 @@ void PlanExecutor::release() {
     epoch_ = nullptr;
     if (interpSteps_) GLOO_AMD_HIP_RELEASE(hipFree(interpSteps_));
     interpSteps_ = nullptr;
+    if (doneTicket_) GLOO_AMD_HIP_RELEASE(hipFree(doneTicket_));
+    doneTicket_ = nullptr;
+    if (hostDone_) GLOO_AMD_HIP_RELEASE(hipHostFree(hostDone_));
+    hostDone_ = hostDoneDev_ = nullptr;
     if (ticket_) GLOO_AMD_HIP_RELEASE(hipFree(ticket_));
     ticket_ = nullptr;
     if (stamps_) GLOO_AMD_HIP_RELEASE(hipFree(stamps_));

@@ -290,6 +290,7 @@ void PlanExecutor::run() {
   // sliced plans must run sliced on every rank (their flags are per slice);
   // profiling then reports no reduce events
   const bool interp = deviceSignal_ && interpMode_ && (!(profiling_ || stamping_) || slices_ > 1);
+  bool spinDone = false;  // this run publishes its completion to hostDone_
   if (interp && interpDirty_) buildInterp();
   const bool graphable = deviceSignal_ && graphMode_ && !profiling_;
   if (interp && interpCount_ > 0) {
@@ -301,8 +302,9 @@ void PlanExecutor::run() {
       if (inRemote_[j]) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(inStage_[j], inputs_[j], bytes, hipMemcpyDeviceToDevice, stream_));
     for (size_t j = 1; anyRemote_ && j < ptrs_.size(); j++)
       if (outRemote_[j]) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(outStage_[j], ptrs_[j], bytes, hipMemcpyDeviceToDevice, stream_));
+    spinDone = hostDone_ && !anyRemote_ && !profiling_ && !stamping_;
     checkRc(launchPlanInterp(op_, dtype_, interpSteps_, interpCount_, r, timeoutTicks, ctx_->errorWordDevicePtr(me),
-                             slices_, stream_),
+                             slices_, stream_, spinDone ? hostDoneDev_ : nullptr, spinDone ? doneTicket_ : nullptr),
             "plan interpreter");
     for (size_t j = 1; anyRemote_ && j < ptrs_.size(); j++)
       if (outRemote_[j]) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(ptrs_[j], outStage_[j], bytes, hipMemcpyDeviceToDevice, stream_));
@@ -331,11 +333,24 @@ void PlanExecutor::run() {
   }
   if (ownStream_ || profiling_ || stamping_) {
     const auto t0 = std::chrono::steady_clock::now();
-    GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+    // the interpreter's own completion store, spun on for a bounded time (a
+    // timed-out wait ends the kernel without it): the stream's completion
+    // signal reaches a synchronising host about 3 µs later
+    bool seen = false;
+    for (uint32_t i = 0; spinDone && !seen; i++) {
+      seen = __atomic_load_n(hostDone_, __ATOMIC_ACQUIRE) >= r;
+      if (!seen && (i & 1023) == 1023 &&
+          std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2))
+        break;
+    }
+    if (!seen) GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
     if (deviceSignal_) waitSeconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (deviceSignal_ && ctx_->errorWord(me).exchange(0) != 0)
+    if (deviceSignal_ && ctx_->errorWord(me).exchange(0) != 0) {
+      // workgroups that timed out left without their done ticket
+      if (doneTicket_) (void)hipMemsetAsync(doneTicket_, 0, 64, stream_);
       throw IoException(strcat_("Timed out on rank ", me, " waiting for a peer (device-side wait, ",
                                 ctx_->timeout().count(), " ms)"));
+    }
   }
   if (stamping_ && !(interp && interpCount_ > 0)) readStamps();
   for (size_t i = 0; profiling_ && i + 1 < evUsed_; i += 2) {

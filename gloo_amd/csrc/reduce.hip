@@ -838,7 +838,8 @@ __device__ __forceinline__ void interp_fold(const InterpStep& st, uint64_t lo, u
 
 template <class Tr, int OP>
 __global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpStep* steps, int nsteps, uint64_t run,
-                                                                   uint64_t timeoutTicks, uint32_t* err, int lean) {
+                                                                   uint64_t timeoutTicks, uint32_t* err, int lean,
+                                                                   uint64_t* done, unsigned* doneTicket) {
   using S = typename Tr::Storage;
   constexpr uint64_t kV = 16 / sizeof(S);
   __shared__ int ok;
@@ -912,17 +913,32 @@ __global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpS
     }
     batch = k + 1;
   }
+  if (!done) return;
+  // The run's completion for a host that spins on `done` instead of
+  // synchronising the stream (signal.h): every workgroup's stores are
+  // performed and released before it takes its ticket; the workgroup taking
+  // the last ticket resets the counter and publishes the run.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    const unsigned t = __hip_atomic_fetch_add(doneTicket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == G - 1) {
+      __hip_atomic_store(doneTicket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(done, run, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 template <class Tr>
 int launch_interp(int op, const InterpStep* steps, int nsteps, uint64_t run, uint64_t tt, uint32_t* err,
-                  int G, hipStream_t s) {
+                  int G, hipStream_t s, uint64_t* done, unsigned* dt) {
   const int lean = fwdLean();
   switch (op) {
-    case GLOO_HIP_SUM: plan_interp_kernel<Tr, GLOO_HIP_SUM><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean); break;
-    case GLOO_HIP_PRODUCT: plan_interp_kernel<Tr, GLOO_HIP_PRODUCT><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean); break;
-    case GLOO_HIP_MAX: plan_interp_kernel<Tr, GLOO_HIP_MAX><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean); break;
-    case GLOO_HIP_MIN: plan_interp_kernel<Tr, GLOO_HIP_MIN><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean); break;
+    case GLOO_HIP_SUM: plan_interp_kernel<Tr, GLOO_HIP_SUM><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean, done, dt); break;
+    case GLOO_HIP_PRODUCT: plan_interp_kernel<Tr, GLOO_HIP_PRODUCT><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean, done, dt); break;
+    case GLOO_HIP_MAX: plan_interp_kernel<Tr, GLOO_HIP_MAX><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean, done, dt); break;
+    case GLOO_HIP_MIN: plan_interp_kernel<Tr, GLOO_HIP_MIN><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean, done, dt); break;
     default: return GLOO_HIP_EINVAL_OP;
   }
   return GLOO_HIP_OK;
@@ -1529,22 +1545,23 @@ int launchFusedSmall(int op, int dtype, void* dst, const void* src, size_t n, co
 }
 
 int launchPlanInterp(int op, int dtype, const InterpStep* steps, int nsteps, uint64_t run, uint64_t tt,
-                     uint32_t* err, int G, hipStream_t s) {
+                     uint32_t* err, int G, hipStream_t s, uint64_t* done, unsigned* doneTicket) {
+  if ((done == nullptr) != (doneTicket == nullptr)) return set_error(GLOO_HIP_EINVAL_ARG, "interpreter: half a done signal");
   static_assert(GLOO_HIP_MAX_SRCS <= 8, "InterpStep holds 8 sources");
   if (nsteps < 0 || nsteps > kInterpMaxSteps) return set_error(GLOO_HIP_EINVAL_ARG, "interpreter: bad step count");
   if (G < 1 || G > kMaxSlices) return set_error(GLOO_HIP_EINVAL_ARG, "interpreter: bad slice count");
   int rc;
   switch (dtype) {
-    case GLOO_HIP_I8: rc = launch_interp<TrI8>(op, steps, nsteps, run, tt, err, G, s); break;
-    case GLOO_HIP_U8: rc = launch_interp<TrU8>(op, steps, nsteps, run, tt, err, G, s); break;
-    case GLOO_HIP_I32: rc = launch_interp<TrI32>(op, steps, nsteps, run, tt, err, G, s); break;
-    case GLOO_HIP_U32: rc = launch_interp<TrU32>(op, steps, nsteps, run, tt, err, G, s); break;
-    case GLOO_HIP_I64: rc = launch_interp<TrI64>(op, steps, nsteps, run, tt, err, G, s); break;
-    case GLOO_HIP_U64: rc = launch_interp<TrU64>(op, steps, nsteps, run, tt, err, G, s); break;
-    case GLOO_HIP_F16: rc = launch_interp<TrF16>(op, steps, nsteps, run, tt, err, G, s); break;
-    case GLOO_HIP_BF16: rc = launch_interp<TrBF16>(op, steps, nsteps, run, tt, err, G, s); break;
-    case GLOO_HIP_F32: rc = launch_interp<TrF32>(op, steps, nsteps, run, tt, err, G, s); break;
-    case GLOO_HIP_F64: rc = launch_interp<TrF64>(op, steps, nsteps, run, tt, err, G, s); break;
+    case GLOO_HIP_I8: rc = launch_interp<TrI8>(op, steps, nsteps, run, tt, err, G, s, done, doneTicket); break;
+    case GLOO_HIP_U8: rc = launch_interp<TrU8>(op, steps, nsteps, run, tt, err, G, s, done, doneTicket); break;
+    case GLOO_HIP_I32: rc = launch_interp<TrI32>(op, steps, nsteps, run, tt, err, G, s, done, doneTicket); break;
+    case GLOO_HIP_U32: rc = launch_interp<TrU32>(op, steps, nsteps, run, tt, err, G, s, done, doneTicket); break;
+    case GLOO_HIP_I64: rc = launch_interp<TrI64>(op, steps, nsteps, run, tt, err, G, s, done, doneTicket); break;
+    case GLOO_HIP_U64: rc = launch_interp<TrU64>(op, steps, nsteps, run, tt, err, G, s, done, doneTicket); break;
+    case GLOO_HIP_F16: rc = launch_interp<TrF16>(op, steps, nsteps, run, tt, err, G, s, done, doneTicket); break;
+    case GLOO_HIP_BF16: rc = launch_interp<TrBF16>(op, steps, nsteps, run, tt, err, G, s, done, doneTicket); break;
+    case GLOO_HIP_F32: rc = launch_interp<TrF32>(op, steps, nsteps, run, tt, err, G, s, done, doneTicket); break;
+    case GLOO_HIP_F64: rc = launch_interp<TrF64>(op, steps, nsteps, run, tt, err, G, s, done, doneTicket); break;
     default: return set_error(GLOO_HIP_EINVAL_DTYPE, "unknown dtype");
   }
   if (rc != GLOO_HIP_OK) return set_error(rc, "interpreter: bad op");

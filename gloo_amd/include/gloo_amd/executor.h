@@ -250,6 +250,14 @@ class PlanExecutor {
   bool interpMode_ = false;            // the interpreter may run this plan
   bool interpDirty_ = true;            // interpSteps_ predates the current buffers
   InterpStep* interpSteps_ = nullptr;  // device copy of the resolved steps
+  // An interpreted run on the executor's own stream publishes its completion
+  // here (launchPlanInterp's done signal) and run() spins on it instead of
+  // synchronising the stream: a launch + stream synchronise costs 10.3 µs on
+  // MI355X, a kernel's own store seen by a spinning host 7.4 µs
+  // (tools/launch_probe, profiles/round5/r5ac_*).  GLOO_AMD_DONE_SPIN=0: off.
+  uint64_t* hostDone_ = nullptr;     // coherent pinned host memory
+  uint64_t* hostDoneDev_ = nullptr;  // ... its device address
+  unsigned* doneTicket_ = nullptr;   // device: the workgroups' ticket counter
   int interpCount_ = 0;
   int slices_ = 1;                     // workgroups of the (sliced) interpreter, agreed by all ranks
   uint64_t* mailbox_ = nullptr;           // this rank's incoming counters, (sender, slot), fine-grained HBM

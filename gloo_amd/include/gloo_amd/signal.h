@@ -136,8 +136,13 @@ constexpr int kInterpDefer = 1;
 void markInterpBatches(InterpStep* v, size_t n, size_t es);
 // Flag words per (sender, slot) in a device mailbox: one per slice.
 constexpr int kMaxSlices = 256;
+// done / doneTicket (both or neither): the workgroup that finishes last
+// stores `run` into *done (system scope, after every workgroup's release) and
+// resets *doneTicket (zero between launches), so a host that owns the stream
+// can spin on *done (coherent host memory) instead of synchronising it.
 int launchPlanInterp(int op, int dtype, const InterpStep* steps, int nsteps, uint64_t run, uint64_t timeoutTicks,
-                     uint32_t* err, int slices, hipStream_t stream);
+                     uint32_t* err, int slices, hipStream_t stream, uint64_t* done = nullptr,
+                     unsigned* doneTicket = nullptr);
 
 // Multi-source fold in one pass, k <= GLOO_HIP_MAX_SRCS.  mode 0: left fold
 // acc = acc op s_j; 1: reverse, acc = s_j op acc; 2: balanced pairwise tree

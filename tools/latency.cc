@@ -48,11 +48,17 @@ int main(int argc, char** argv) {
   (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
   const char* la = std::getenv("LATENCY_ALGO");
   const std::string algoName = la ? la : "halving_doubling";
+  // LATENCY_OWN_STREAM=1: no stream passed, so run() returns with the outputs
+  // valid (the reference's synchronous form); the extra synchronise below
+  // then finds an idle stream
+  const char* os = std::getenv("LATENCY_OWN_STREAM");
+  std::vector<hipStream_t> streams;
+  if (!(os && os[0] == '1')) streams.push_back(s);
   std::unique_ptr<gloo_amd::Algorithm> algop;
   if (algoName == "ring_chunked")
-    algop.reset(new gloo_amd::HipAllreduceRingChunked<float>(ctx, {d}, count, {s}));
+    algop.reset(new gloo_amd::HipAllreduceRingChunked<float>(ctx, {d}, count, streams));
   else
-    algop.reset(new gloo_amd::HipAllreduceHalvingDoubling<float>(ctx, {d}, count, {s}));
+    algop.reset(new gloo_amd::HipAllreduceHalvingDoubling<float>(ctx, {d}, count, streams));
   gloo_amd::Algorithm& algo = *algop;
   for (int i = 0; i < 50; i++) {
     algo.run();

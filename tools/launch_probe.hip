@@ -5,6 +5,10 @@
 //
 //   launch_sync     one-wave nop kernel + hipStreamSynchronize
 //   launch_enqueue  the host time of that launch alone
+//   launch_query    the launch, then hipStreamQuery spun until the stream is idle
+//   launch_event    the launch + hipEventRecord, then hipEventQuery spun
+//   launch_flag     a kernel that stores a flag into coherent host memory, the
+//                   host spinning on the flag (then a non-blocking stream query)
 //   write_sync      hipStreamWriteValue64 + hipStreamSynchronize
 //   wait_sync       hipStreamWaitValue64 (already met) + hipStreamSynchronize
 //   persistent_ops  a resident one-workgroup kernel on another stream polls a
@@ -23,6 +27,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CHECK(x)                                                                      \
@@ -37,6 +42,10 @@
 constexpr uint64_t kQuit = ~uint64_t(0);
 
 __global__ void nop_kernel() {}
+
+__global__ void flag_kernel(uint64_t* flag, uint64_t v) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __global__ void resident_kernel(const uint64_t* door, uint64_t* done, uint64_t maxTicks) {
   if (threadIdx.x != 0) return;
@@ -65,6 +74,8 @@ static void report(const char* what, std::vector<double>& us) {
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? std::atoi(argv[1]) : 2000;
+  // launch_probe ITERS spin: hipDeviceScheduleSpin (host waits spin instead of yielding)
+  if (argc > 2 && std::string(argv[2]) == "spin") CHECK(hipSetDeviceFlags(hipDeviceScheduleSpin));
   CHECK(hipSetDevice(0));
   int canWait = 0;
   CHECK(hipDeviceGetAttribute(&canWait, hipDeviceAttributeCanUseStreamWaitValue, 0));
@@ -98,6 +109,73 @@ int main(int argc, char** argv) {
   }
   report("launch_sync", a);
   report("launch_enqueue", b);
+
+  // the same with a second stream of this process that ran one kernel and is idle now
+  nop_kernel<<<1, 64, 0, r>>>();
+  CHECK(hipStreamSynchronize(r));
+  a.clear();
+  for (int i = 0; i < iters; i++) {
+    const auto t0 = Clock::now();
+    nop_kernel<<<1, 64, 0, s>>>();
+    CHECK(hipStreamSynchronize(s));
+    a.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+  }
+  report("launch_sync_second_stream_idle", a);
+  // ... and alternating launches between the two streams, each synchronised
+  a.clear();
+  for (int i = 0; i < iters; i++) {
+    hipStream_t x = (i & 1) ? r : s;
+    const auto t0 = Clock::now();
+    nop_kernel<<<1, 64, 0, x>>>();
+    CHECK(hipStreamSynchronize(x));
+    a.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+  }
+  report("launch_sync_alternating_streams", a);
+
+  a.clear();
+  for (int i = 0; i < iters; i++) {
+    const auto t0 = Clock::now();
+    nop_kernel<<<1, 64, 0, s>>>();
+    hipError_t q;
+    while ((q = hipStreamQuery(s)) == hipErrorNotReady) {
+    }
+    CHECK(q);
+    a.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+  }
+  report("launch_query", a);
+
+  hipEvent_t ev;
+  CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  a.clear();
+  for (int i = 0; i < iters; i++) {
+    const auto t0 = Clock::now();
+    nop_kernel<<<1, 64, 0, s>>>();
+    CHECK(hipEventRecord(ev, s));
+    hipError_t q;
+    while ((q = hipEventQuery(ev)) == hipErrorNotReady) {
+    }
+    CHECK(q);
+    a.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+  }
+  report("launch_event", a);
+
+  a.clear();
+  *done = 0;
+  for (int i = 0; i < iters; i++) {
+    const uint64_t v = (uint64_t)i + 1;
+    const auto t0 = Clock::now();
+    flag_kernel<<<1, 64, 0, s>>>(done, v);
+    const auto dl = Clock::now() + std::chrono::seconds(5);
+    while (__atomic_load_n(done, __ATOMIC_ACQUIRE) < v) {
+      if (Clock::now() > dl) {
+        std::fprintf(stderr, "flag never arrived\n");
+        return 3;
+      }
+    }
+    a.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+  }
+  CHECK(hipStreamSynchronize(s));
+  report("launch_flag", a);
 
   a.clear();
   for (int i = 0; i < iters; i++) {
