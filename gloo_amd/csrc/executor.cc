@@ -517,13 +517,15 @@ void PlanExecutor::configureDeviceLaunches() {
   graphMode_ = gmode == "1" || (gmode == "auto" && unfused && !(meshPlan && maxMsg >= graphBytes()));
   if (interpMode_) GLOO_AMD_HIP_ALLOC(hipMalloc(&interpSteps_, kInterpMaxSteps * sizeof(InterpStep)));
   const char* ds = std::getenv("GLOO_AMD_DONE_SPIN");
-  if (interpMode_ && ownStream_ && !(ds && ds[0] == '0')) {
+  if (ownStream_ && !(ds && ds[0] == '0')) {
     GLOO_AMD_HIP_ALLOC(hipHostMalloc(reinterpret_cast<void**>(&hostDone_), 64,
                                      hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
     __atomic_store_n(hostDone_, 0, __ATOMIC_RELEASE);
     GLOO_AMD_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hostDoneDev_), hostDone_, 0));
-    GLOO_AMD_HIP_ALLOC(hipMalloc(&doneTicket_, 64));
-    GLOO_AMD_HIP_CHECK(hipMemsetAsync(doneTicket_, 0, 64, stream_));
+    if (interpMode_) {
+      GLOO_AMD_HIP_ALLOC(hipMalloc(&doneTicket_, 64));
+      GLOO_AMD_HIP_CHECK(hipMemsetAsync(doneTicket_, 0, 64, stream_));
+    }
   }
   if (graphMode_) {
     GLOO_AMD_HIP_ALLOC(hipMalloc(&epoch_, sizeof(uint64_t)));

@@ -250,9 +250,9 @@ class PlanExecutor {
   bool interpMode_ = false;            // the interpreter may run this plan
   bool interpDirty_ = true;            // interpSteps_ predates the current buffers
   InterpStep* interpSteps_ = nullptr;  // device copy of the resolved steps
-  // An interpreted run on the executor's own stream publishes its completion
-  // here (launchPlanInterp's done signal) and run() spins on it instead of
-  // synchronising the stream: a launch + stream synchronise costs 10.3 µs on
+  // A run on the executor's own stream publishes its completion here (the
+  // interpreter's done signal, or a signal kernel behind an eager or replayed
+  // run) and run() spins on it instead of synchronising the stream: a launch + stream synchronise costs 10.3 µs on
   // MI355X, a kernel's own store seen by a spinning host 7.4 µs
   // (tools/launch_probe, profiles/round5/r5ac_*).  GLOO_AMD_DONE_SPIN=0: off.
   uint64_t* hostDone_ = nullptr;     // coherent pinned host memory
