@@ -441,6 +441,9 @@ DEVICE_SIGNALLING_CASES = [
     ("halving_doubling/min/f32/P5/k1/n1000", {"GLOO_AMD_COPY": "memcpy"}),
     ("reduce_scatter/product/f16/P8/n4096", {"GLOO_AMD_COPY": "memcpy"}),
     ("reduce_scatter/sum/f16/P4/n1024", {}),
+    # run() synchronising the stream instead of spinning on the device-published done word
+    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_DONE_SPIN": "0"}),
+    ("reduce_scatter/sum/f16/P4/n1024", {"GLOO_AMD_DONE_SPIN": "0"}),
 ]
 for _c, _e in DEVICE_SIGNALLING_CASES:
     sched_pool.register(_c, _e, 1)
