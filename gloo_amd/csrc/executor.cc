@@ -380,6 +380,8 @@ void PlanExecutor::mapPeers(const std::vector<std::vector<char>>& arenas, const 
           hipError_t e = hipDeviceEnablePeerAccess(pr.device, 0);
           if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
           (void)hipGetLastError();
+          // a pool slab (the peer also talks to other processes): VMM access
+          if (pr.mailboxSlabId) ipc::grantAccess(reinterpret_cast<void*>(pr.mailboxPtr), ctx_->device());
         }
       } else {
         ipc::Remote rm;
@@ -410,6 +412,8 @@ void PlanExecutor::mapPeers(const std::vector<std::vector<char>>& arenas, const 
         hipError_t e = hipDeviceEnablePeerAccess(pr.device, 0);
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) GLOO_AMD_HIP_CHECK(e);
         (void)hipGetLastError();
+        // a pool slab (the peer also talks to other processes): VMM access
+        if (!pr.host && pr.slabId) ipc::grantAccess(reinterpret_cast<void*>(pr.ptr), ctx_->device());
       }
     } else {
       // Another process's pool slab (ipc.h): mapped once, kept.  The mapping

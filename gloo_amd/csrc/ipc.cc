@@ -66,6 +66,17 @@ void* freshRange(size_t bytes) {
   return va;
 }
 
+// Read-write access to [va, va + bytes) from `device` (the mapping's other
+// devices keep theirs).
+hipError_t allowAccess(void* va, size_t bytes, int device) {
+  hipMemAccessDesc d;
+  std::memset(&d, 0, sizeof(d));
+  d.location.type = hipMemLocationTypeDevice;
+  d.location.id = device;
+  d.flags = hipMemAccessFlagsProtReadWrite;
+  return hipMemSetAccess(va, bytes, &d, 1);
+}
+
 void mapAt(void* va, size_t bytes, hipMemGenericAllocationHandle_t h, int device) {
   GLOO_AMD_HIP_CHECK(hipMemMap(va, bytes, 0, h, 0));
   hipMemAccessDesc d;
@@ -91,6 +102,7 @@ struct Pool {
     size_t bytes;
     size_t users;  // executors holding it (import / unimport)
     hipMemGenericAllocationHandle_t handle;
+    uint64_t devices;  // bit d: device d may access it
   };
   std::map<std::pair<int, uint64_t>, Mapping> imports;  // (exporter pid, slab id)
   size_t opens = 0, dropped = 0;
@@ -319,6 +331,7 @@ Slab* acquire(int device, size_t bytes, bool fine) {
     void* va = freshRange(want);
     mapAt(va, want, s->handle, device);
     s->ptr = static_cast<char*>(va);
+    s->devices = device < 64 ? uint64_t(1) << device : 0;
     GLOO_AMD_HIP_CHECK(hipMemExportToShareableHandle(&s->fd, s->handle, hipMemHandleTypePosixFileDescriptor, 0));
   } catch (...) {
     if (s->ptr) (void)hipMemUnmap(s->ptr, want);
@@ -359,6 +372,12 @@ void* import(const Remote& r, size_t bytes, int device) {
       if (it->second.incarnation == r.incarnation) {
         GLOO_AMD_ENFORCE(it->second.bytes >= bytes, "slab of pid ", r.pid, " mapped at ", it->second.bytes,
                          " B, now published at ", bytes, " B");
+        // an executor of this process on another GPU reuses the mapping
+        const uint64_t bit = device < 64 ? uint64_t(1) << device : 0;
+        if (bit && !(it->second.devices & bit)) {
+          GLOO_AMD_HIP_CHECK(allowAccess(it->second.ptr, it->second.bytes, device));
+          it->second.devices |= bit;
+        }
         it->second.users++;
         return it->second.ptr;
       }
@@ -404,12 +423,40 @@ void* import(const Remote& r, size_t bytes, int device) {
     // another thread of this process mapped it meanwhile: keep that one
     GLOO_AMD_HIP_RELEASE(hipMemUnmap(va, slabBytes));
     GLOO_AMD_HIP_RELEASE(hipMemRelease(h));
+    const uint64_t bit = device < 64 ? uint64_t(1) << device : 0;
+    if (bit && !(it->second.devices & bit)) {
+      GLOO_AMD_HIP_CHECK(allowAccess(it->second.ptr, it->second.bytes, device));
+      it->second.devices |= bit;
+    }
     it->second.users++;
     return it->second.ptr;
   }
   p.opens++;
-  p.imports[key] = {r.incarnation, va, slabBytes, 1, h};
+  p.imports[key] = {r.incarnation, va, slabBytes, 1, h, device < 64 ? uint64_t(1) << device : 0};
   return va;
+}
+
+void grantAccess(void* mapped, int device) {
+  if (!mapped) return;
+  Pool& p = Pool::get();
+  std::lock_guard<std::mutex> lk(p.m);
+  const uint64_t bit = device < 64 ? uint64_t(1) << device : 0;
+  for (auto& s : p.slabs)
+    if (s->ptr == mapped) {
+      if (bit && !(s->devices & bit)) {
+        GLOO_AMD_HIP_CHECK(allowAccess(s->ptr, s->bytes, device));
+        s->devices |= bit;
+      }
+      return;
+    }
+  for (auto& kv : p.imports)
+    if (kv.second.ptr == mapped) {
+      if (bit && !(kv.second.devices & bit)) {
+        GLOO_AMD_HIP_CHECK(allowAccess(kv.second.ptr, kv.second.bytes, device));
+        kv.second.devices |= bit;
+      }
+      return;
+    }
 }
 
 Stats stats() {

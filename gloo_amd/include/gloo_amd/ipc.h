@@ -56,6 +56,7 @@ struct Slab {
   uint64_t id = 0;       // names the slab to peers
   hipMemGenericAllocationHandle_t handle = nullptr;
   int fd = -1;           // the exported dma-buf
+  uint64_t devices = 0;  // bit d: device d of this process may access the mapping
 };
 
 // What a peer publishes about one of its slabs.
@@ -81,6 +82,12 @@ void release(Slab* s);
 void* import(const Remote& r, size_t bytes, int device);
 // Drops an executor's hold on a mapping (the mapping stays for reuse).
 void unimport(void* mapped);
+// A VMM mapping is accessible only from the devices it was granted to (a
+// peer-access enable does not cover it): lets `device` of this process read
+// and write one of the pool's slabs or imports, given its mapped address (a
+// rank of this process on another GPU sending into a slab; no-op when the
+// address is not the pool's).
+void grantAccess(void* mapped, int device);
 
 struct Stats {
   size_t slabs = 0, slabBytes = 0, free = 0, imports = 0, opens = 0;
