@@ -570,7 +570,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   if (stream) {
     stream_ = stream;
   } else {
-    GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    stream_ = ctx_->sharedStream();
     ownedStream_ = stream_;
     ownStream_ = true;
   }
@@ -929,10 +929,7 @@ void PlanExecutor::release() {
     for (char* p : inStage_)
       if (p) GLOO_AMD_HIP_RELEASE(hipFree(p));
     inStage_.clear();
-    if (ownedStream_) {
-      (void)hipStreamSynchronize(ownedStream_);
-      (void)hipStreamDestroy(ownedStream_);
-    }
+    if (ownedStream_) (void)hipStreamSynchronize(ownedStream_);  // the context's: it destroys it
     ownedStream_ = nullptr;
     for (hipEvent_t e : sideEvents_) (void)hipEventDestroy(e);
     sideEvents_.clear();

@@ -130,7 +130,7 @@ void PlanExecutor::setStreams(const std::vector<hipStream_t>& streams) {
   hipStream_t next = streams.empty() ? nullptr : streams[0];
   for (hipStream_t t : streams) GLOO_AMD_ENFORCE(t != nullptr || streams.size() == 1, "null stream in the list");
   if (!next) {
-    if (!ownedStream_) GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&ownedStream_, hipStreamNonBlocking));
+    if (!ownedStream_) ownedStream_ = ctx_->sharedStream();
     next = ownedStream_;
   }
   if (next != stream_) {

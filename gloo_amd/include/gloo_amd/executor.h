@@ -216,7 +216,7 @@ class PlanExecutor {
   std::vector<std::unique_ptr<HostShm>> peerShm_;
   hipStream_t stream_ = nullptr;
   bool ownStream_ = false;            // stream_ is the executor's own: run() returns with outputs complete
-  hipStream_t ownedStream_ = nullptr;  // the executor's own stream, if created
+  hipStream_t ownedStream_ = nullptr;  // the stream runs use when given none: the context's shared one
   std::vector<hipStream_t> sideStreams_;  // the caller's streams of pointers 1.. (setStreams)
   std::vector<hipEvent_t> sideEvents_;
   hipEvent_t doneEvent_ = nullptr;     // recorded on stream_ at the end of a run on a caller's stream
