@@ -544,6 +544,7 @@ GRAPH_REPLAY_CASES = [
 # waits make each run cost up to several ms there: the P = 8 batch took 14-61 s
 # at five runs, profiles/round5/r5*_pytest_gpu_all_*.log.)
 GRAPH_REPLAY_RUNS = 3
+INTERP_RUNS = 3  # the interpreters' cases: three back-to-back runs, the buffer reset before each
 for _c, _e, _g in GRAPH_REPLAY_CASES:
     sched_pool.register(_c, _e, GRAPH_REPLAY_RUNS)
 
@@ -632,17 +633,17 @@ INTERP_CASES = [
     ("reduce_scatter/sum/f32/P5/n100", {"GLOO_AMD_SIGNAL": "host"}, False),
 ]
 for _c, _e, _i in INTERP_CASES:
-    sched_pool.register(_c, _e, 5)
+    sched_pool.register(_c, _e, INTERP_RUNS)
 
 
 @pytest.mark.parametrize("case,env,interp", INTERP_CASES)
 def test_processes_interp(torch, golden_sched, case, env, interp):
     """One-launch plan interpreter: every run() of a small plan is ONE
     one-workgroup kernel walking the resolved step list (waits, sends,
-    signals, folds, copies).  Five runs with the buffer reset to the input
+    signals, folds, copies).  Three runs with the buffer reset to the input
     each time, every one byte for byte the reference's output; interp=False
     cases check the knobs and shapes that keep the enqueued path."""
-    runs = GRAPH_REPLAY_RUNS
+    runs = INTERP_RUNS
     res = sched_pool.result(case, env, runs)
     check_pool_golden(golden_sched, case, res, runs)
     for modes in res.modes:
@@ -697,7 +698,7 @@ SLICED_CASES = [
     ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024"}),    # refused: uneven pieces
 ]
 for _c, _e in SLICED_CASES:
-    sched_pool.register(_c, _e, 5)
+    sched_pool.register(_c, _e, INTERP_RUNS)
 
 
 @pytest.mark.parametrize("case,env", SLICED_CASES)
@@ -705,9 +706,9 @@ def test_processes_sliced_interp(torch, golden_sched, case, env):
     """Sliced interpreter: every rank runs its plan in several workgroups,
     workgroup g on slice g of every step with its own flag words.  The ranks
     must agree on the slice count the rule predicts (1 where a plan is
-    refused), and five back-to-back runs must give the reference's bytes."""
+    refused), and three back-to-back runs must give the reference's bytes."""
     want_slices = _expected_slices(case, env)
-    runs = GRAPH_REPLAY_RUNS
+    runs = INTERP_RUNS
     res = sched_pool.result(case, env, runs)
     check_pool_golden(golden_sched, case, res, runs)
     for modes in res.modes:
