@@ -346,9 +346,9 @@ void PlanExecutor::run() {
     bool seen = false;
     for (uint32_t i = 0; spinDone && !seen; i++) {
       seen = __atomic_load_n(hostDone_, __ATOMIC_ACQUIRE) >= r;
-      if (!seen && (i & 1023) == 1023 &&
-          std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2))
-        break;
+      if (seen) break;
+      __builtin_ia32_pause();
+      if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
     }
     if (!seen) GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
     if (deviceSignal_) waitSeconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
