@@ -38,3 +38,20 @@ def test_every_golden_case_has_a_gpu_test(gpu_ids, name):
     assert cs
     missing = [c for c in cs if c not in gpu_ids]
     assert not missing, f"{name}: {len(missing)} golden cases no GPU test names: {missing[:10]}"
+
+
+@pytest.mark.timeout(600)
+def test_gpu_extended_cases_leave_the_default_run():
+    """gpu_extended variants (conftest.py) are deselected from `-m gpu` unless
+    GLOO_AMD_GPU_EXTENDED=1, and nothing else is."""
+    def collect(extra):
+        env = dict(os.environ, **extra)
+        env.pop("GLOO_AMD_GPU_EXTENDED", None) if not extra else None
+        r = subprocess.run([sys.executable, "-m", "pytest", "tests", "-m", "gpu", "--collect-only", "-q",
+                            "-p", "no:cacheprovider"], cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        return {ln for ln in r.stdout.splitlines() if "::" in ln}
+    default, extended = collect({}), collect({"GLOO_AMD_GPU_EXTENDED": "1"})
+    assert default < extended
+    extra = extended - default
+    assert extra and all("test_ipc_arena_of_2gib_and_more" in t for t in extra), sorted(extra)
