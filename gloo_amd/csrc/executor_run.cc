@@ -302,7 +302,7 @@ void PlanExecutor::run() {
       if (inRemote_[j]) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(inStage_[j], inputs_[j], bytes, hipMemcpyDeviceToDevice, stream_));
     for (size_t j = 1; anyRemote_ && j < ptrs_.size(); j++)
       if (outRemote_[j]) GLOO_AMD_HIP_CHECK(hipMemcpyAsync(outStage_[j], ptrs_[j], bytes, hipMemcpyDeviceToDevice, stream_));
-    spinDone = doneTicket_ && !anyRemote_ && !profiling_ && !stamping_;
+    spinDone = ownStream_ && doneTicket_ && !anyRemote_ && !profiling_ && !stamping_;
     checkRc(launchPlanInterp(op_, dtype_, interpSteps_, interpCount_, r, timeoutTicks, ctx_->errorWordDevicePtr(me),
                              slices_, stream_, spinDone ? hostDoneDev_ : nullptr, spinDone ? doneTicket_ : nullptr),
             "plan interpreter");
@@ -325,7 +325,7 @@ void PlanExecutor::run() {
   // eager or replayed: one signal kernel behind the run stores its number
   // into hostDone_ after a system-scope release (a launch of 0.8 µs on the host
   // against the stream synchronise's 3 µs, launch_probe)
-  if (hostDone_ && !spinDone && !profiling_ && !stamping_) {
+  if (ownStream_ && hostDone_ && !spinDone && !profiling_ && !stamping_) {
     GLOO_AMD_HIP_CHECK(launchSignal(hostDoneDev_, Seq{r, 0}, nullptr, stream_));
     spinDone = true;
   }
