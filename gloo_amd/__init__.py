@@ -405,8 +405,8 @@ class Algorithm:
 
     def __init__(self, ctx, algo, op, dtype, ptrs, count, recv_elems=None, stream=0, workspace="device",
                  streams=None):
-        """stream: one stream for the plan (0: the algorithm's own, run()
-        returns with outputs complete).  streams: one stream handle per
+        """stream: one stream for the plan (0: the context's shared stream,
+        and run() returns with outputs complete).  streams: one stream handle per
         pointer instead (the reference's `streams` argument,
         gloo/cuda_allreduce_ring_chunked.cc:55-67): run() orders pointer i
         after the work queued on streams[i], and every streams[i] after the
