@@ -273,10 +273,12 @@ void PlanExecutor::run() {
   const int me = ctx_->rank;
   if (deviceSignal_ && ctx_->errorWord(me).load() != 0)
     throw IoException(strcat_("rank ", me, ": a device-side wait of a previous run timed out"));
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  GLOO_AMD_HIP_CHECK(hipStreamIsCapturing(stream_, &cs));
-  GLOO_AMD_ENFORCE(cs == hipStreamCaptureStatusNone,
-                   "run() on a stream under capture: the executor captures and replays its own graph");
+  if (!ownStream_) {  // (the context's shared stream is never the caller's to capture)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    GLOO_AMD_HIP_CHECK(hipStreamIsCapturing(stream_, &cs));
+    GLOO_AMD_ENFORCE(cs == hipStreamCaptureStatusNone,
+                     "run() on a stream under capture: the executor captures and replays its own graph");
+  }
   waitSeconds_ = 0;
   reduceSeconds_ = reduceBytes_ = 0;
   reduceCount_ = 0;
