@@ -342,9 +342,12 @@ void PlanExecutor::run() {
   }
   if (ownStream_ || profiling_ || stamping_) {
     const auto t0 = std::chrono::steady_clock::now();
-    // the interpreter's own completion store, spun on for a bounded time (a
-    // timed-out wait ends the kernel without it): the stream's completion
-    // signal reaches a synchronising host about 3 µs later
+    // the run's device-published completion word (the interpreter's last
+    // workgroup, or the signal kernel behind an eager or replayed run), spun
+    // on for up to 2 ms: the stream's completion signal reaches a
+    // synchronising host about 3 µs later.  A run that takes longer, or an
+    // interpreter whose wait timed out (it ends without the store), falls
+    // back to the stream synchronise.
     bool seen = false;
     for (uint32_t i = 0; spinDone && !seen; i++) {
       seen = __atomic_load_n(hostDone_, __ATOMIC_ACQUIRE) >= r;
