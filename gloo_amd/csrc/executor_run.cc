@@ -348,14 +348,19 @@ void PlanExecutor::run() {
     // synchronising host about 3 µs later.  A run that takes longer, or an
     // interpreter whose wait timed out (it ends without the store), falls
     // back to the stream synchronise.
+    // (Runs that outlast the window skip the spin until a run is short again,
+    // so long collectives do not burn 2 ms of a core each.)
     bool seen = false;
-    for (uint32_t i = 0; spinDone && !seen; i++) {
+    for (uint32_t i = 0; spinDone && !spinSkip_ && !seen; i++) {
       seen = __atomic_load_n(hostDone_, __ATOMIC_ACQUIRE) >= r;
       if (seen) break;
       __builtin_ia32_pause();
       if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
     }
-    if (!seen) GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (!seen) {
+      GLOO_AMD_HIP_CHECK(hipStreamSynchronize(stream_));
+      if (spinDone) spinSkip_ = std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(1);
+    }
     if (deviceSignal_) waitSeconds_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (deviceSignal_ && ctx_->errorWord(me).exchange(0) != 0) {
       // workgroups that timed out left without their done ticket

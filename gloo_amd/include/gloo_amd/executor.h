@@ -258,6 +258,7 @@ class PlanExecutor {
   uint64_t* hostDone_ = nullptr;     // coherent pinned host memory
   uint64_t* hostDoneDev_ = nullptr;  // ... its device address
   unsigned* doneTicket_ = nullptr;   // device: the workgroups' ticket counter
+  bool spinSkip_ = false;            // the last run outlasted the spin window: synchronise instead
   int interpCount_ = 0;
   int slices_ = 1;                     // workgroups of the (sliced) interpreter, agreed by all ranks
   uint64_t* mailbox_ = nullptr;           // this rank's incoming counters, (sender, slot), fine-grained HBM
