@@ -9,6 +9,8 @@
 //        -o tools/latency -Lgloo_amd -lgloo_amd -Wl,-rpath,'$ORIGIN/../gloo_amd'
 // Prints one JSON line per rank with p50 / p90 of both, in microseconds.
 // LATENCY_ALGO=ring_chunked runs HipAllreduceRingChunked<float> instead.
+// LATENCY_OWN_STREAM=1 passes no stream: run() returns with the outputs
+// complete (the synchronous form) and `total` is run() alone.
 //
 //   latency <rank> <size> <store-url> [count=256] [iters=2000]
 #include <hip/hip_runtime.h>
