@@ -665,13 +665,21 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                    "reference_route": {"GLOO_AMD_MESH": "0"},
                    "reference_route_kernel_copy": {"GLOO_AMD_MESH": "0", "GLOO_AMD_COPY": "kernel"},
                    "reference_route_eager": {"GLOO_AMD_MESH": "0", "GLOO_AMD_GRAPH": "0", "GLOO_AMD_INTERP": "0"}}
+    # With a GPU per rank, a larger sliced-interpreter cap (DESIGN.md §8
+    # "Remaining" 4): 8 MiB messages (64 MiB per rank at P = 8) run sliced
+    # instead of eager.  Only there: ranks sharing a GPU cannot all keep 128
+    # workgroups resident, and their device-side waits time out.
+    one_rank_per_gpu = world <= torch.cuda.device_count()
+    if one_rank_per_gpu and world > 1:
+        hd_variants["mesh_slices_128"] = {"GLOO_AMD_INTERP_MAX_SLICES": "128"}
     hd_summary = {}
     partial["halving_doubling"] = hd_summary
     for k, v in hd_variants.items():
         if args.quick and k not in ("mesh", "reference_route"):
             continue
         big = k in ("mesh", "reference_route") and not args.quick
-        hd_summary[k] = hd_sweep(k, v, full_sizes if big else short_sizes)
+        sizes = (16 << 20, 64 << 20) if k == "mesh_slices_128" else full_sizes if big else short_sizes
+        hd_summary[k] = hd_sweep(k, v, sizes)
     mark("config4_halving_doubling")
 
     # Config 5: reduce-scatter (HD), fp16 / bf16 buckets, every op, 16 Mi
