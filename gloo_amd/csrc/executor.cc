@@ -684,32 +684,40 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     }
   }
   peers_.resize(P);
-  bool sharesDeviceInProcess = false, crossSender = false;
+  bool sharesDeviceInProcess = false;
   for (int peer : planPeers) {
     const Where& w = where.at(peer);
     peers_[peer].pid = w.pid;
     peers_[peer].device = w.device;
     if (w.pid == ctx_->pid() && w.device == ctx_->device()) sharesDeviceInProcess = true;
-    if (recvPeers.count(peer) && (w.device != ctx_->device() || w.pid != ctx_->pid())) crossSender = true;
     if (w.pid != ctx_->pid()) crossProcess_ = true;
   }
   const char* sig = std::getenv("GLOO_AMD_SIGNAL");
   const std::string sigMode = sig ? sig : "auto";
   deviceSignal_ = sigMode == "device" || (sigMode == "auto" && !sharesDeviceInProcess);
-  // A peer GPU (over xGMI) or a peer PROCESS (through its own IPC mapping)
-  // writes this rank's inboxes: keep them in fine-grained memory, so no
-  // stale line of an L2 can be read on either side.  Measured with
-  // coarse-grained inboxes and two processes on one MI355X: after an
-  // executor of the same size had run, the importer read the previous
-  // contents through its mapping even after a device synchronise, and a
-  // ring route's messages were not seen by the receiver (bench.py
-  // config-3 variants back to back, tests/test_bench_gpu.py).
+  // Any peer that writes this rank's inboxes — another GPU (over xGMI),
+  // another process (through its own mapping), or another rank of this
+  // process on this same GPU (its own stream) — writes them in fine-grained
+  // memory, so no stale cache line can be read on the receiving side.
+  // Two measurements with coarse-grained inboxes on one MI355X:
+  //  - two processes: after an executor of the same size had run, the
+  //    importer read the previous contents through its mapping even after a
+  //    device synchronise (bench.py config-3 variants back to back);
+  //  - twelve ranks as threads (BCUBE, GPUTEST_r05): rank 8's phase-1 fold
+  //    of the SECOND run read arena element 5 as it stood at the end of the
+  //    first run (rank 10's phase-2 message, which shares that offset) and
+  //    not rank 9's new phase-1 message that the host counter had already
+  //    announced — a stale line, not a protocol gap: the model of exactly
+  //    that read reproduces the wrong value bit for bit
+  //    (tests/test_newstyle_plan.py::test_bcube_p12_stale_inbox_read_explains_r05).
+  // A plan reuses arena offsets for different messages of one run, so a
+  // line cached by one step's read is wrong for a later step's.
   const char* ar = std::getenv("GLOO_AMD_ARENA");
   const std::string arMode = ar ? ar : "auto";
   GLOO_AMD_ENFORCE(workspace == GLOO_HIP_WORKSPACE_DEVICE || workspace == GLOO_HIP_WORKSPACE_HOST,
                    "unknown workspace ", workspace);
   hostArena_ = workspace == GLOO_HIP_WORKSPACE_HOST || arMode == "host";
-  fineArena_ = !hostArena_ && (arMode == "fine" || (arMode == "auto" && crossSender));
+  fineArena_ = !hostArena_ && (arMode == "fine" || (arMode == "auto" && !recvPeers.empty()));
 
   // Phase 2: the inbox arena.  Whole 2 MiB granules.  When a peer in
   // another process maps it, it is a slab of the process-wide pool (ipc.h):

@@ -210,7 +210,7 @@ def reduce_forward_order(steps):
 
 
 def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, runs=1, slices=1,
-             reduce_forward=False):
+             reduce_forward=False, arena_init=None, stale=(), arenas_out=None):
     """inputs: [P][k][n] array of the dtype's storage type (the outputs'
     initial contents); ins: optional [P][kin][n] separate inputs (new-style
     allreduce).  runs > 1 executes the plan back to back that many times
@@ -219,7 +219,11 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
     the sliced interpreter does: every (rank, slice) is its own process
     applying each step to its slice only, with its own channel counters,
     interleaved at random with all the others.  reduce_forward: every plan
-    rewritten by reduce_forward_order first.  Returns the outputs."""
+    rewritten by reduce_forward_order first.  arena_init: each rank's arena
+    contents at the start (default zeros); stale: {(rank, step index)} of
+    FOLD_SRC steps whose arena operand is read as it stood at the start (a
+    stale cache line of the inbox, the fault model of GPUTEST_r05);
+    arenas_out: a list that receives the final arenas.  Returns the outputs."""
     P, k, n = inputs.shape
     nin = 0 if ins is None else ins.shape[1]
     es = inputs.dtype.itemsize
@@ -238,6 +242,10 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
                                           if st.kind != KIND["DECL_RECV"]], a) for steps, a in plans]
     user = [[inputs[r, j].copy() for j in range(k)] for r in range(P)]
     arena = [np.zeros(max(1, a), dtype=inputs.dtype) for _, a in plans]
+    if arena_init is not None:
+        for r in range(P):
+            arena[r][:] = arena_init[r]
+    arena0 = [a.copy() for a in arena]
     regions = {}
     for r, (steps, _) in enumerate(plans):
         for s in steps:
@@ -341,10 +349,11 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
                 b0, b1 = slice_range(ln, g, slices, es)
                 local_step(r, s, o + b0, o + b1)
         elif K == KIND["FOLD_SRC"]:
-            pending[(r, g)].append((s.flags, s.src_off))
+            pending[(r, g)].append((s.flags, s.src_off, (r, pc[(r, g)] - 1) in stale))
         elif K == KIND["FOLD"]:
-            srcs = [(ins[r, 0] if f & FROM_INPUTS else space(r, f & SRC_ARENA))[o + a0:o + a1].copy()
-                    for f, o in pending[(r, g)]]
+            srcs = [(ins[r, 0] if f & FROM_INPUTS else arena0[r] if old and f & SRC_ARENA
+                     else space(r, f & SRC_ARENA))[o + a0:o + a1].copy()
+                    for f, o, old in pending[(r, g)]]
             pending[(r, g)] = []
             if s.flags & FOLD_TREE:
                 while len(srcs) > 1:
@@ -365,6 +374,8 @@ def simulate(algo, op, dtype, inputs, recv=None, seed=0, ins=None, max_seg=0, ru
             continue
         if sent[key] != consumed.get(key, 0):
             raise ProtocolError(f"{key}: {sent[key]} sent, {consumed.get(key, 0)} consumed")
+    if arenas_out is not None:
+        arenas_out[:] = arena
     return np.array([[user[r][j] for j in range(k)] for r in range(P)])
 
 

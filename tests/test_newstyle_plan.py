@@ -14,7 +14,9 @@ import os
 import numpy as np
 import pytest
 
-from plan_sim import simulate
+from plan_sim import KIND, SRC_ARENA, get_plan, simulate
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "newstyle_golden.npz")
 
@@ -125,7 +127,7 @@ def test_reduce_repeated_runs(P, n):
         assert (got == chained).all(), seed
 
 
-@pytest.mark.parametrize("P,n", [(3, 1000), (6, 4099), (8, 100003)])
+@pytest.mark.parametrize("P,n", [(3, 1000), (6, 4099), (8, 100003), (12, 10), (12, 4099)])
 def test_bcube_repeated_runs(P, n):
     rng = np.random.default_rng(P * 3 + n)
     x = rng.integers(0, 1 << 20, size=(P, 1, n), dtype=np.uint64)
@@ -135,6 +137,31 @@ def test_bcube_repeated_runs(P, n):
     for seed in (0, 1):
         got = simulate("allreduce_bcube", "sum", "u64", x, seed=seed, runs=3)
         assert (got == chained).all(), seed
+
+
+def test_bcube_p12_stale_inbox_read_explains_r05():
+    """GPUTEST_r05's one red case (BCUBE P=12, ranks as threads on one GPU,
+    coarse-grained inboxes): every rank's element 0 came back -1.9609444
+    instead of -3.8116968 in the second call, elements 1-9 right.  The plan
+    is exact (test_bcube_repeated_runs above).  The model of ONE stale read
+    reproduces the wrong value bit for bit: rank 8's phase-1 fold (step 13,
+    its inbox [5, 10) from rank 9) reads the inbox as it stood at the end of
+    the first run, when offset 5 held rank 10's phase-2 message (rank 8's
+    region for rank 10 is [3, 6)).  Offsets 6-9 still held rank 9's equal
+    first-run data, so only element 0 is wrong.  The fix (executor.cc:
+    inboxes that any peer writes are fine-grained) removes the stale line;
+    the GPU side is test_newstyle_gpu.py::test_threads_inboxes_fine_grained."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "newstyle_golden.npz"))
+    case = "bcube/sum/f32/P12/i0/o1/n10/s0"
+    init, want = z[case + "/init"], z[case + "/out"]
+    end_of_run1 = []
+    y1 = simulate("allreduce_bcube", "sum", "f32", init, seed=1, arenas_out=end_of_run1)
+    assert (y1[:, 0] == want).all()
+    steps, _ = get_plan("allreduce_bcube", 8, 12, 10)
+    assert steps[13].kind == KIND["FOLD_SRC"] and steps[13].flags & SRC_ARENA and steps[13].src_off == 5
+    y2 = simulate("allreduce_bcube", "sum", "f32", init, seed=2, arena_init=end_of_run1, stale={(8, 13)})
+    assert [str(v) for v in y2[:, 0, 0]] == ["-1.9609444"] * 12
+    assert (y2[:, 0, 1:] == want[1:]).all()
 
 
 def test_reduce_rejects_bad_root():

@@ -19,3 +19,22 @@ def test_no_file_named_like_a_flag():
         pytest.skip("not a git checkout")
     tracked = [f for f in out.stdout.splitlines() if os.path.basename(f).startswith("-")]
     assert not tracked, tracked
+
+
+def test_gpu_run_starts_with_hot_path_parity():
+    """under `pytest -m gpu -x` the kernel's own parity suite
+    (tests/test_reduce_gpu.py, config 2's 64 MiB case first) is collected
+    before any collective file, so a collective failure cannot leave it
+    unrun."""
+    import sys
+    out = subprocess.run([sys.executable, "-m", "pytest", "--collect-only", "-q", "-m", "gpu", "tests"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=600)
+    ids = [ln for ln in out.stdout.splitlines() if "::" in ln]
+    assert ids, out.stdout[-2000:] + out.stderr[-2000:]
+    assert ids[0] == "tests/test_reduce_gpu.py::test_full_size_64mib_f32_sum_properties", ids[:3]
+    files = [i.split("::")[0] for i in ids]
+    k = files.count("tests/test_reduce_gpu.py")
+    assert k > 50 and files[:k] == ["tests/test_reduce_gpu.py"] * k, files[:k + 1]
+    for name in ("test_golden_reduce3", "test_golden_nan_payloads", "test_misaligned_offsets",
+                 "test_beyond_4gi_elements"):
+        assert any(name in i for i in ids[:k]), name
