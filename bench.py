@@ -356,8 +356,8 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     Config 3: AllreduceRingChunked fp32 sum, 256 MiB per rank.  Chunks move
     GPU->GPU into the peer's HBM inbox (xGMI) and are reduced by the HIP
     kernel on the receiving GPU.  Default: the mesh plan (the ring's bytes,
-    every link at once); variants: forked hipMemcpyAsync sends, the classic
-    ring with either copy engine, the HOST workspace.  Reported: the slowest
+    every link at once); variants: the mesh replayed as a hipGraph, the
+    reference's (pipelined) ring route replayed and eager, the HOST workspace.  Reported: the slowest
     rank's time per allreduce, bus bandwidth, and the reduction kernels' own
     GiB/s measured with HIP events while the exchange runs (per-GPU
     efficiency vs the 1-GPU figure).
@@ -430,10 +430,12 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
 
     want_sample = expected_at_sample()
 
-    def ring_once(engine, workspace="device", mesh="1", extra_env=None):
-        progress(f"config 3: ring_chunked engine={engine} workspace={workspace} mesh={mesh} {extra_env or ''}")
+    def ring_once(launch="auto", workspace="device", mesh="1"):
+        """launch: "auto" (the library's choice), "eager" (GLOO_AMD_GRAPH=0)
+        or "graph" (GLOO_AMD_GRAPH=1)."""
+        progress(f"config 3: ring_chunked launch={launch} workspace={workspace} mesh={mesh}")
 
-        url = store_url("ring_%s_%s_%s" % (engine, workspace, mesh))  # taken first: every rank, same order
+        url = store_url("ring_%s_%s_%s" % (launch, workspace, mesh))  # taken first: every rank, same order
 
         def body():
             import hashlib
@@ -451,7 +453,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
             bad_detail = [[int(sample[i]), float(got[i]), float(want_sample[i]), float(x_np[sample[i]])]
                           for i in np.nonzero(badmask)[0][:3]]
             # timed: steady state (eager enqueue for these 32 MiB messages by default,
-            # graph replay from run 3 on below GLOO_AMD_GRAPH_BYTES or with GLOO_AMD_GRAPH=1)
+            # graph replay from run 3 on below 4 MiB messages, on the ring route, or with GLOO_AMD_GRAPH=1)
             times = []
             for _ in range(args.allreduce_iters):
                 dist.barrier()
@@ -498,13 +500,16 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                     "graph": graphed, "stamp_s": st_s, "stamp_b": st_b, "stamp_graph": all(st_graph),
                     "stamp_fused": bool(st_fused)}
         try:
-            res = with_env(dict({"GLOO_AMD_COPY": engine, "GLOO_AMD_RING_MESH": mesh}, **(extra_env or {})), body)
+            env = {"GLOO_AMD_MESH": mesh}
+            if launch != "auto":
+                env["GLOO_AMD_GRAPH"] = "0" if launch == "eager" else "1"
+            res = with_env(env, body)
         except Exception as e:  # noqa: BLE001
             res = {"error": repr(e)}
         gathered = gather(res)
         errs = [g["error"] for g in gathered if "error" in g]
         if errs:
-            return {"copy_engine": engine, "error": errs[0],
+            return {"launch": launch, "error": errs[0],
                     "errors_per_rank": [g.get("error") for g in gathered]}
         ms = sorted(max(g["ms"][i] for g in gathered) for i in range(args.allreduce_iters))
         t = ms[len(ms) // 2] / 1e3
@@ -512,9 +517,8 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         fused = all(g["stamp_fused"] for g in gathered)
         busbw = 2 * (world - 1) / world * n * 4 / t
         links = link_bounds(world, n * 4, t, link["figures"])
-        return {"plan": "mesh" if mesh == "1" and world <= 8 else "ring", "copy_engine": engine,
+        return {"plan": "mesh" if mesh == "1" and world <= 8 else "ring", "launch": launch,
                 "workspace": workspace, "graph": all(g["graph"] for g in gathered),
-                **({"env": extra_env} if extra_env else {}),
                 "ms_p50": round(t * 1e3, 3), "algbw_gib_s": round(n * 4 / t / GIB, 2),
                 "busbw_gib_s": round(busbw / GIB, 2), **links,
                 "schedule": ("%s%s" % ("mesh" if mesh == "1" and world <= 8 else "ring",
@@ -527,7 +531,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
                                          (", forward stores included: the fused fold + forward launch as it ships"
                                           if fused else "",
                                           args.allreduce_iters, "graph-replayed" if all(g["stamp_graph"] for g in gathered)
-                                          else "eagerly enqueued (the default above GLOO_AMD_GRAPH_BYTES)")),
+                                          else "eagerly enqueued (the mesh default from 4 MiB messages)")),
                 "host_wait_ms_per_run_max_profiled": max(g["wait_ms_per_run"] for g in gathered),
                 "verified": bool(all(g["first_run_ok"] for g in gathered) and
                                  len({g["digest"] for g in gathered}) == 1),
@@ -543,7 +547,7 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     link = link_figures(torch, dist, rank, world, n * 4)
     partial["link"] = link
     # default: the mesh plan (batched sends = one multi-destination copy kernel)
-    ring = ring_once("auto")
+    ring = ring_once()
     partial["config"] = "allreduce_ring_chunked fp32 sum, %d ranks, %d MiB/rank" % (world, args.allreduce_mib)
     partial["data_path"] = "xGMI peer copies" if ngpu >= world else f"{world} ranks on {ngpu} GPU(s)"
     partial.update(ring)
@@ -551,24 +555,16 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
         return dict(partial)
     variants = {}
     partial["variants"] = variants
-    # SURVEY 8(e)'s efficiency on the unfused mesh (a pure fold kernel between
-    # the sends), beside the default fused schedule above
-    variants["mesh_unfused"] = ring_once("auto", extra_env={"GLOO_AMD_FOLD_SEND": "0"})
-    # the single-release completion protocol against a release in every
-    # workgroup, over the links (both bit-checked)
-    if not args.quick:
-        variants["mesh_release_each"] = ring_once("auto", extra_env={"GLOO_AMD_FWD_RELEASE": "each"})
-        # workgroups per peer copy (64 by default, sized for one link without
-        # measurement over real links): half and double, for the next tuning
-        for blocks in ("32", "128"):
-            variants["mesh_copy_blocks_" + blocks] = ring_once("auto", extra_env={"GLOO_AMD_COPY_BLOCKS": blocks})
-    specs = {"ring_memcpy": ("memcpy", "device", "0"), "ring_kernel": ("kernel", "device", "0"),
-             "mesh_memcpy_forked": ("memcpy", "device", "1"), "mesh_host_workspace": ("auto", "host", "1")}
+    # the launch modes and routes that ship (the knobs that switched copy
+    # engines, store flavours and completion protocols are gone: each lost
+    # its A/B, DESIGN.md §4 / INTEGRATION.md §4)
+    specs = {"ring_graph": ("auto", "device", "0"), "ring_eager": ("eager", "device", "0"),
+             "mesh_graph": ("graph", "device", "1"), "mesh_host_workspace": ("auto", "host", "1")}
     chosen = (args.config3_variants.split(",") if args.config3_variants
-              else ["ring_memcpy"] if args.quick else list(specs))
+              else ["ring_graph"] if args.quick else list(specs))
     for k, name in enumerate(chosen):
-        engine, workspace, mesh = specs[name]
-        variants[name if name not in variants else "%s#%d" % (name, k + 1)] = ring_once(engine, workspace, mesh)
+        launch, workspace, mesh = specs[name]
+        variants[name if name not in variants else "%s#%d" % (name, k + 1)] = ring_once(launch, workspace, mesh)
     partial["ipc_pool"] = hip.ipc_stats()
     mark("config3")
     if args.config3_only:
@@ -655,15 +651,9 @@ def xgmi_allreduce(torch, dist, hip, rank, world, dev, args, partial):
     # mesh = the derived mesh plan (default); reference_route = the
     # reference's halving/doubling exchange (GLOO_AMD_MESH=0)
     hd_variants = {"mesh": {},
-                   "mesh_memcpy_forked": {"GLOO_AMD_COPY": "memcpy"},
                    "mesh_eager": {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_INTERP": "0"},
                    "mesh_no_interp": {"GLOO_AMD_INTERP": "0"},
-                   "mesh_interp_unbatched": {"GLOO_AMD_INTERP_BATCH": "0"},
-                   "mesh_host_block_flags": {"GLOO_AMD_MAILBOX": "0"},
-                   "mesh_copy_blocks_32": {"GLOO_AMD_COPY_BLOCKS": "32"},
-                   "mesh_copy_blocks_128": {"GLOO_AMD_COPY_BLOCKS": "128"},
                    "reference_route": {"GLOO_AMD_MESH": "0"},
-                   "reference_route_kernel_copy": {"GLOO_AMD_MESH": "0", "GLOO_AMD_COPY": "kernel"},
                    "reference_route_eager": {"GLOO_AMD_MESH": "0", "GLOO_AMD_GRAPH": "0", "GLOO_AMD_INTERP": "0"}}
     # With a GPU per rank, a larger sliced-interpreter cap (DESIGN.md §8
     # "Remaining" 4): 8 MiB messages (64 MiB per rank at P = 8) run sliced
@@ -1223,8 +1213,11 @@ def main():
             fold kernel), and the default schedule as it ships (fold and
             forward in one launch, its forward stores inside the stamps)."""
             base = xr.get("data_path") or partial.get("data_path")
-            unf = (xr.get("variants") or {}).get("mesh_unfused") or {}
-            res = efficiency_of(unf, f"{base}; unfused mesh: fold kernel, then the sends (GLOO_AMD_FOLD_SEND=0)")
+            # the unfused fold: the default run's event-profiled runs (events
+            # need a pure fold kernel between them, so those runs are unfused)
+            unf = {"reduce_kernel_gib_s_per_gpu": xr.get("reduce_kernel_gib_s_per_gpu_eager_events"),
+                   "error": xr.get("error")}
+            res = efficiency_of(unf, f"{base}; unfused mesh (event-profiled runs): fold kernel, then the sends")
             fused = efficiency_of(xr, f"{base}; default schedule: {xr.get('schedule', 'mesh')}")
             if fused.get("value") and "fused" in (xr.get("schedule") or "") and "unfused" not in xr["schedule"]:
                 # the fused launch also stores each owner's range to its P - 1

@@ -359,8 +359,7 @@ def _mode_dict(out):
     err = lib.gloo_hip_last_error()
     err = err.decode() if isinstance(err, bytes) else (err or "")
     return {"device_signal": bool(out[0]), "fine_arena": out[1] == 1,
-            "host_arena": out[1] == 2, "kernel_copy": bool(out[2] & 1),
-            "fold_send": bool(out[2] & 2),
+            "host_arena": out[1] == 2, "fold_send": bool(out[2] & 2), "own_stream": bool(out[2] & 4),
             "graph": out[3] == 1, "interp": out[3] >= 2, "interp_slices": max(0, out[3] - 1),
             "graph_error": err[len("graph capture abandoned: "):]
             if err.startswith("graph capture abandoned: ") else ""}
@@ -405,7 +404,7 @@ class Algorithm:
 
     def __init__(self, ctx, algo, op, dtype, ptrs, count, recv_elems=None, stream=0, workspace="device",
                  streams=None):
-        """stream: one stream for the plan (0: the context's shared stream,
+        """stream: one stream for the plan (0: the algorithm's own stream,
         and run() returns with outputs complete).  streams: one stream handle per
         pointer instead (the reference's `streams` argument,
         gloo/cuda_allreduce_ring_chunked.cc:55-67): run() orders pointer i

@@ -285,7 +285,7 @@ namespace {
 void modeOf(const gloo_amd::PlanExecutor& e, int* mode) {
   mode[0] = e.deviceSignalling() ? 1 : 0;
   mode[1] = e.hostArena() ? 2 : e.fineGrainedArena() ? 1 : 0;
-  mode[2] = (e.kernelCopy() ? 1 : 0) | (e.foldSendUsed() ? 2 : 0);
+  mode[2] = (e.foldSendUsed() ? 2 : 0) | (e.ownStream() ? 4 : 0);
   mode[3] = e.graphed() ? 1 : e.interpreted() ? 1 + e.interpSlices() : 0;
   gloo_amd::setError(0, e.graphError().empty() ? "" : "graph capture abandoned: " + e.graphError());
 }

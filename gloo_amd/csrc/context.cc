@@ -34,25 +34,8 @@ Context::Context(int r, int s, std::chrono::milliseconds timeout)
 }
 
 Context::~Context() {
-  if (sharedStream_) {
-    (void)hipStreamSynchronize(sharedStream_);
-    (void)hipStreamDestroy(sharedStream_);
-  }
   if (shmDev_) GLOO_AMD_HIP_RELEASE(hipHostUnregister(shm_));
   if (shm_) ::munmap(shm_, shmBytes_);
-}
-
-hipStream_t Context::sharedStream() {
-  std::lock_guard<std::mutex> lk(streamMutex_);
-  if (!sharedStream_) {
-    int prev = -1;
-    GLOO_AMD_HIP_CHECK(hipGetDevice(&prev));
-    if (device_ >= 0 && device_ != prev) GLOO_AMD_HIP_CHECK(hipSetDevice(device_));
-    const hipError_t e = hipStreamCreateWithFlags(&sharedStream_, hipStreamNonBlocking);
-    if (device_ >= 0 && device_ != prev) (void)hipSetDevice(prev);
-    GLOO_AMD_HIP_CHECK(e);
-  }
-  return sharedStream_;
 }
 
 void Context::connect(std::shared_ptr<Store> store, int device) {

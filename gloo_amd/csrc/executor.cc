@@ -131,39 +131,24 @@ std::string diagProbe(const void* p, hipStream_t s) {
                  " flags=", a.allocationFlags, " range(rc ", (int)e4, ")=", rb, "+", rs);
 }
 
-bool mailboxesEnabled() {
-  const char* e = std::getenv("GLOO_AMD_MAILBOX");
-  return !(e && e[0] == '0');
-}
-
-// The environment knobs that choose which plan a collective executes
-// (INTEGRATION.md §4).  They are read here and nowhere else; every rank must
-// read them alike, and the "where" exchange carries them with a fingerprint
-// of the plan they produce, so a rank-inconsistent choice is refused on
-// every rank instead of running mismatched step lists.
+// The environment knob that chooses which plan a collective executes
+// (INTEGRATION.md §4): GLOO_AMD_MESH.  It is read here and nowhere else;
+// every rank must read it alike, and the "where" exchange carries it with a
+// fingerprint of the plan it produces, so a rank-inconsistent choice is
+// refused on every rank instead of running mismatched step lists.
 struct RouteKnobs {
-  bool mesh = true;      // GLOO_AMD_MESH: derived mesh plans (mesh.cc) where P allows
-  bool ringMesh = true;  // GLOO_AMD_RING_MESH: ring-chunked as its mesh plan
-  bool ringPipe = true;  // GLOO_AMD_RING_PIPE: ring-chunked's ring route pipelined
-  int32_t bits() const { return (mesh ? 1 : 0) | (ringMesh ? 2 : 0) | (ringPipe ? 4 : 0); }
+  bool mesh = true;  // GLOO_AMD_MESH: derived mesh plans (mesh.cc) where P allows
+  int32_t bits() const { return mesh ? 1 : 0; }
 };
 RouteKnobs routeKnobs() {
-  auto on = [](const char* name) {
-    const char* e = std::getenv(name);
-    return !(e && e[0] == '0');
-  };
+  const char* e = std::getenv("GLOO_AMD_MESH");
   RouteKnobs k;
-  k.mesh = on("GLOO_AMD_MESH");
-  k.ringMesh = on("GLOO_AMD_RING_MESH");
-  k.ringPipe = on("GLOO_AMD_RING_PIPE");
+  k.mesh = !(e && e[0] == '0');
   return k;
 }
-std::string knobText(int32_t bits) {
-  return strcat_("GLOO_AMD_MESH=", bits & 1 ? 1 : 0, " GLOO_AMD_RING_MESH=", bits & 2 ? 1 : 0,
-                 " GLOO_AMD_RING_PIPE=", bits & 4 ? 1 : 0);
-}
+std::string knobText(int32_t bits) { return strcat_("GLOO_AMD_MESH=", bits & 1 ? 1 : 0); }
 
-// The plan `algo` executes as, given the knobs.  A custom op is called as the
+// The plan `algo` executes as, given the knob.  A custom op is called as the
 // reference calls its function: two operands at a time on the reference's own
 // routes (the mesh plans fold with reverse / tree association), and its ring
 // keeps the reference's literal two-inbox order.
@@ -175,13 +160,14 @@ int selectPlanAlgo(int algo, int P, bool custom, const RouteKnobs& k) {
   // link instead of 2(P-1) hops around the ring.  Halving-doubling,
   // reduce-scatter and the new-style collectives likewise run as their
   // derived mesh plans (mesh.cc).
-  if (mesh && algo == GLOO_HIP_ALGO_RING_CHUNKED && k.ringMesh) planAlgo = GLOO_HIP_ALGO_RING_CHUNKED_MESH;
+  if (mesh && algo == GLOO_HIP_ALGO_RING_CHUNKED) planAlgo = GLOO_HIP_ALGO_RING_CHUNKED_MESH;
   if (mesh && (algo == GLOO_HIP_ALGO_HALVING_DOUBLING || algo == GLOO_HIP_ALGO_REDUCE_SCATTER || isNewStyle(algo)))
     planAlgo = algo | GLOO_HIP_ALGO_MESH;
   // Ring-chunked on its ring route (the mesh off, or P > 8): three inboxes
   // per channel, so each round reduces and forwards in one pass (plan.cc
-  // planRingChunkedPipe; the reference's bytes).
-  if (planAlgo == GLOO_HIP_ALGO_RING_CHUNKED && !custom && k.ringPipe) planAlgo = GLOO_HIP_ALGO_RING_CHUNKED_PIPE;
+  // planRingChunkedPipe; the reference's bytes; 3.4 % faster than the
+  // literal two-inbox order at 256 MiB per rank).
+  if (planAlgo == GLOO_HIP_ALGO_RING_CHUNKED && !custom) planAlgo = GLOO_HIP_ALGO_RING_CHUNKED_PIPE;
   return planAlgo;
 }
 
@@ -330,15 +316,15 @@ void PlanExecutor::classifyPointers() {
 // workgroup per sliceBytes() of its largest message, if its own plan and the
 // messages its peers write into its arena slice consistently (sliceable); 0
 // otherwise.  All ranks then take the smallest proposal, so they agree.
-int32_t PlanExecutor::proposeSlices(const std::set<int>& recvPeers) {
+int32_t PlanExecutor::proposeSlices(const std::set<int>& recvPeers, int sliceCap) {
   const int me = ctx_->rank, P = ctx_->size;
   int32_t proposal = 0;
   if (interpMode_ && mailbox_ && !anyRemote_ && !hostArena_) {
     size_t maxMsg = 0;
     for (const Step& s : plan_.steps) maxMsg = std::max(maxMsg, (size_t)s.length * es_);
-    const size_t want = std::min<size_t>(maxSlices(), std::max<size_t>(1, (maxMsg + sliceBytes() - 1) / sliceBytes()));
-    // above maxSlices() slices of sliceCapBytes() graph replay is as fast
-    if (maxMsg <= (size_t)maxSlices() * sliceCapBytes()) {
+    const size_t want = std::min<size_t>(sliceCap, std::max<size_t>(1, (maxMsg + sliceBytes() - 1) / sliceBytes()));
+    // above sliceCap slices of sliceCapBytes() graph replay is as fast
+    if (maxMsg <= (size_t)sliceCap * sliceCapBytes()) {
       std::map<std::pair<int, int>, size_t> decl;  // (sender, slot) -> arena offset
       for (const Step& d : plan_.steps)
         if (d.kind == GLOO_HIP_STEP_DECL_RECV) decl[{d.peer, d.slot}] = d.dst_off;
@@ -456,40 +442,14 @@ void PlanExecutor::mapPeers(const std::vector<std::vector<char>>& arenas, const 
                        me, " slot ", s.slot);
 }
 
-// Device signalling: the copy engines, fold + forward, the completion
-// protocol, copy grids and store flavours, the ticket counters, and whether
-// runs replay a hipGraph.
+// Device signalling: the ticket counters, the completion word, and whether
+// runs replay a hipGraph.  (The copy engines, fold + forward, copy grids and
+// store flavours are fixed: executor.h, each from a measured A/B.)
 void PlanExecutor::configureDeviceLaunches() {
   const int me = ctx_->rank, P = ctx_->size;
   (void)me;
   (void)ctx_->counterDevicePtr(inst_, 0, 0, 0);  // register the control block now
   ctx_->errorWord(me).store(0);
-  // Copy engine: a lone SEND is hipMemcpyAsync + signal ("memcpy", the
-  // default) or the copy+signal kernel ("kernel"); a batch of consecutive
-  // SENDs (one per peer) is one multi-destination copy kernel (default),
-  // or with "memcpy" one hipMemcpyAsync per forked stream.
-  const char* cp = std::getenv("GLOO_AMD_COPY");
-  const std::string cmode = cp ? cp : "auto";
-  kernelCopy_ = cmode == "kernel";
-  autoCopy_ = cmode == "auto";
-  batchKernelCopy_ = cmode != "memcpy";
-  // Fold + forward (enqueue, FOLD): "0" keeps the fold and its SENDs apart.
-  const char* fs = std::getenv("GLOO_AMD_FOLD_SEND");
-  foldSend_ = !(fs && std::string(fs) == "0");
-  // Completion protocol of the signalling kernels (GLOO_AMD_FWD_RELEASE)
-  refreshFwdLean();
-  // Workgroups per copy (executor.h): a few dozen saturate an xGMI link.
-  // GLOO_AMD_COPY_BLOCKS overrides both the remote and the same-GPU size.
-  if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS")) {
-    copyBlocks_ = (unsigned)std::max(1, std::atoi(cb));
-    copyBlocksLocal_ = copyBlocks_;
-  }
-  if (const char* cb = std::getenv("GLOO_AMD_COPY_BLOCKS_LOCAL")) copyBlocksLocal_ = (unsigned)std::max(1, std::atoi(cb));
-  if (const char* cb = std::getenv("GLOO_AMD_COPY_OUT_BYTES")) copyOutKernelBytes_ = std::strtoull(cb, nullptr, 10);
-  if (const char* cb = std::getenv("GLOO_AMD_COPY_OUT_BLOCKS")) copyOutBlocks_ = (unsigned)std::max(1, std::atoi(cb));
-  if (const char* cs = std::getenv("GLOO_AMD_REDUCE_STORE")) reducePlain_ = std::string(cs) != "nt";
-  if (const char* cs = std::getenv("GLOO_AMD_LOCAL_COPY_STORE"))
-    localStore_ = std::string(cs) == "nt" ? kCopyStoreNT : std::string(cs) == "wt" ? kCopyStoreWT : kCopyStorePlain;
   const size_t tickets = std::max<size_t>(256, (size_t)P * GLOO_HIP_NUM_SLOTS * sizeof(unsigned));
   GLOO_AMD_HIP_ALLOC(hipMalloc(&ticket_, tickets));
   // zeroed on the executor's stream and complete before any copy kernel
@@ -498,8 +458,8 @@ void PlanExecutor::configureDeviceLaunches() {
   GLOO_AMD_HIP_CHECK(hipMemsetAsync(ticket_, 0, tickets, stream_));
   // Graph replay pays off where the host is the bottleneck: a plan with
   // steps that are not fused one-workgroup launches.  A mesh plan (a few
-  // launches per call) whose messages reach GLOO_AMD_GRAPH_BYTES (default
-  // 4 MiB) is device-bound instead: the host's eager enqueue stays ahead,
+  // launches per call) whose messages reach graphBytes() (4 MiB) is
+  // device-bound instead: the host's eager enqueue stays ahead,
   // and eager measured 7-13 % faster than replay (HD 16 and 64 MiB per
   // rank, 2 and 4 ranks: DESIGN.md §4, profiles/round3/r3ah_*, r3ak_*).
   // The reference routes keep replay: their per-hop credit handshakes make
@@ -520,8 +480,7 @@ void PlanExecutor::configureDeviceLaunches() {
   const bool meshPlan = (planAlgo_ & GLOO_HIP_ALGO_MESH) || planAlgo_ == GLOO_HIP_ALGO_RING_CHUNKED_MESH;
   graphMode_ = gmode == "1" || (gmode == "auto" && unfused && !(meshPlan && maxMsg >= graphBytes()));
   if (interpMode_) GLOO_AMD_HIP_ALLOC(hipMalloc(&interpSteps_, kInterpMaxSteps * sizeof(InterpStep)));
-  const char* ds = std::getenv("GLOO_AMD_DONE_SPIN");
-  if (ownStream_ && !(ds && ds[0] == '0')) {
+  if (ownStream_) {
     GLOO_AMD_HIP_ALLOC(hipHostMalloc(reinterpret_cast<void**>(&hostDone_), 64,
                                      hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
     __atomic_store_n(hostDone_, 0, __ATOMIC_RELEASE);
@@ -570,8 +529,13 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   if (stream) {
     stream_ = stream;
   } else {
-    stream_ = ctx_->sharedStream();
-    ownedStream_ = stream_;
+    // The executor's own stream (one stream per context was shared
+    // by every algorithm given none, so two algorithms run from two threads
+    // in different orders on two ranks queued each one's device-side waits
+    // behind the other's; the reference gives each op its stream,
+    // gloo/cuda.h:102-105)
+    GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&ownedStream_, hipStreamNonBlocking));
+    stream_ = ownedStream_;
     ownStream_ = true;
   }
   // Baseline every channel before anyone can signal this instance (instance
@@ -632,6 +596,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   struct Where {
     int32_t pid, device, knobs, planAlgo;
     uint64_t call, exchange;
+    int64_t gpu;  // the GPU's PCI location: ranks of any process on one GPU share it
   };
   const uint64_t callHash = [&] {
     uint64_t h = 0xcbf29ce484222325ull;
@@ -645,7 +610,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   }();
   std::vector<Where> where(P);
   {
-    Where w{ctx_->pid(), ctx_->device(), knobs.bits(), planAlgo_, callHash, exchangeHash(plan_)};
+    Where w{ctx_->pid(), ctx_->device(), knobs.bits(), planAlgo_, callHash, exchangeHash(plan_), gpuLocation(ctx_->device())};
     std::vector<char> blob(sizeof(w));
     std::memcpy(blob.data(), &w, sizeof(w));
     const auto all = ctx_->allgather(strcat_("inst", inst_, "/where"), blob);
@@ -679,8 +644,8 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     }
     if (!why.empty()) {
       release();
-      GLOO_AMD_ENFORCE(false, "rank-inconsistent collective: ", why, ". The plan-selecting knobs (GLOO_AMD_MESH, "
-                       "GLOO_AMD_RING_MESH, GLOO_AMD_RING_PIPE) and the call's arguments must be equal on every rank");
+      GLOO_AMD_ENFORCE(false, "rank-inconsistent collective: ", why, ". The plan-selecting knob (GLOO_AMD_MESH) "
+                       "and the call's arguments must be equal on every rank");
     }
   }
   peers_.resize(P);
@@ -692,9 +657,10 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     if (w.pid == ctx_->pid() && w.device == ctx_->device()) sharesDeviceInProcess = true;
     if (w.pid != ctx_->pid()) crossProcess_ = true;
   }
-  const char* sig = std::getenv("GLOO_AMD_SIGNAL");
-  const std::string sigMode = sig ? sig : "auto";
-  deviceSignal_ = sigMode == "device" || (sigMode == "auto" && !sharesDeviceInProcess);
+  // Stream-ordered device-side signals, unless another rank of this process
+  // shares this GPU: those ranks wait on the host (their launches need not
+  // be co-resident)
+  deviceSignal_ = !sharesDeviceInProcess;
   // Any peer that writes this rank's inboxes — another GPU (over xGMI),
   // another process (through its own mapping), or another rank of this
   // process on this same GPU (its own stream) — writes them in fine-grained
@@ -712,12 +678,10 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   //    (tests/test_newstyle_plan.py::test_bcube_p12_stale_inbox_read_explains_r05).
   // A plan reuses arena offsets for different messages of one run, so a
   // line cached by one step's read is wrong for a later step's.
-  const char* ar = std::getenv("GLOO_AMD_ARENA");
-  const std::string arMode = ar ? ar : "auto";
   GLOO_AMD_ENFORCE(workspace == GLOO_HIP_WORKSPACE_DEVICE || workspace == GLOO_HIP_WORKSPACE_HOST,
                    "unknown workspace ", workspace);
-  hostArena_ = workspace == GLOO_HIP_WORKSPACE_HOST || arMode == "host";
-  fineArena_ = !hostArena_ && (arMode == "fine" || (arMode == "auto" && !recvPeers.empty()));
+  hostArena_ = workspace == GLOO_HIP_WORKSPACE_HOST;
+  fineArena_ = !hostArena_ && !recvPeers.empty();
 
   // Phase 2: the inbox arena.  Whole 2 MiB granules.  When a peer in
   // another process maps it, it is a slab of the process-wide pool (ipc.h):
@@ -750,7 +714,7 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   // lets every importer check its mapping.
   size_t mbBytes = 0;
   uint64_t mbNonce = 0;
-  if (deviceSignal_ && mailboxesEnabled()) {
+  if (deviceSignal_) {
     // one word per (sender, slot, slice): slices of the sliced interpreter
     mbBytes = ((size_t)P * GLOO_HIP_NUM_SLOTS * kMaxSlices * sizeof(uint64_t) + 4095) / 4096 * 4096;
     if (crossProcess_) {
@@ -774,7 +738,15 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
     interpMode_ = deviceSignal_ && !(im && std::string(im) == "0") && !(gm && std::string(gm) == "1") &&
                   interpBytes() > 0 && !custom_;
   }
-  const int32_t proposal = proposeSlices(recvPeers);
+  // The sliced interpreter's slices spin until their peer slices run, so
+  // every launch of the ranks on one GPU must be resident at once.  Measured
+  // on one MI355X (256 CUs): 2 ranks x 128 slices and 8 x 32 ran, 4 x 128
+  // timed out in every rank's device wait (profiles/round5/r5at_slices_p2.jsonl).
+  // So the ranks sharing this GPU split its CUs: at most CUs / ranks slices
+  // each (below GLOO_AMD_INTERP_MAX_SLICES), the same on every rank of the GPU.
+  int ranksHere = 0;
+  for (int r = 0; r < P; r++) ranksHere += where[r].gpu == where[me].gpu;
+  const int32_t proposal = proposeSlices(recvPeers, coResidentSlices(ctx_->device(), ranksHere));
   ArenaRecord rec;
   std::memset(&rec, 0, sizeof(rec));
   rec.interpSlices = proposal;
@@ -937,7 +909,10 @@ void PlanExecutor::release() {
     for (char* p : inStage_)
       if (p) GLOO_AMD_HIP_RELEASE(hipFree(p));
     inStage_.clear();
-    if (ownedStream_) (void)hipStreamSynchronize(ownedStream_);  // the context's: it destroys it
+    if (ownedStream_) {
+      (void)hipStreamSynchronize(ownedStream_);
+      (void)hipStreamDestroy(ownedStream_);
+    }
     ownedStream_ = nullptr;
     for (hipEvent_t e : sideEvents_) (void)hipEventDestroy(e);
     sideEvents_.clear();

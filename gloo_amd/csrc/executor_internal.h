@@ -5,6 +5,7 @@
 #pragma once
 
 #include <cstddef>
+#include <cstdint>
 #include <utility>
 #include <vector>
 
@@ -30,6 +31,12 @@ size_t sliceBytes();
 size_t sliceCapBytes();
 // Most workgroups of a sliced launch (<= kMaxSlices).
 int maxSlices();
+// The slice cap for `ranksHere` ranks sharing `device`: min(maxSlices(),
+// its CU count / ranksHere), at least 1.
+int coResidentSlices(int device, int ranksHere);
+// A GPU's PCI domain / bus / device as one number (the same GPU in every
+// process, whatever its device index there).
+int64_t gpuLocation(int device);
 
 // A range of one of a rank's buffers, symbolically: output j = j, input j =
 // kIn + j, the inbox arena = kArena.

@@ -31,23 +31,13 @@ size_t fuseBytes() {
 }
 
 // Largest message below which GLOO_AMD_GRAPH=auto replays a mesh plan as a
-// hipGraph (executor constructor); larger mesh plans are enqueued eagerly.
-size_t graphBytes() {
-  static const size_t v = [] {
-    const char* e = std::getenv("GLOO_AMD_GRAPH_BYTES");
-    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)(4u << 20);
-  }();
-  return v;
-}
+// hipGraph (executor constructor); larger mesh plans are enqueued eagerly
+// (7-13 % faster than replay at 16 and 64 MiB per rank).
+size_t graphBytes() { return size_t(4) << 20; }
 
-// Largest message of a plan the one-launch interpreter runs (0: never).
-size_t interpBytes() {
-  static const size_t v = [] {
-    const char* e = std::getenv("GLOO_AMD_INTERP_BYTES");
-    return e ? (size_t)std::strtoull(e, nullptr, 10) : fuseBytes();
-  }();
-  return v;
-}
+// Largest message of a plan the one-launch interpreter runs (0: never): the
+// fused-launch size.
+size_t interpBytes() { return fuseBytes(); }
 
 // Workgroups per sliced interpreter launch: about one per this many bytes of
 // the plan's largest message.
@@ -65,13 +55,7 @@ size_t sliceBytes() {
 // fp32 4 MiB per rank, 2 rank processes on one MI355X: 32 x 64 KiB slices
 // 32.8 us against graph replay 40.9 us; at 8 MiB messages 128 x 64 KiB
 // slices lose to graph replay (profiles/round3/r3y_latency_*).
-size_t sliceCapBytes() {
-  static const size_t v = [] {
-    const char* e = std::getenv("GLOO_AMD_INTERP_SLICE_MAX_BYTES");
-    return e ? std::max<size_t>(sliceBytes(), std::strtoull(e, nullptr, 10)) : 2 * sliceBytes();
-  }();
-  return v;
-}
+size_t sliceCapBytes() { return 2 * sliceBytes(); }
 
 // The sliced form splits a plan's whole-range local steps (LOCAL_REDUCE /
 // LOCAL_BCAST over [0, n)) at every boundary the other steps use in the
@@ -237,6 +221,26 @@ int maxSlices() {
     return e ? std::min(kMaxSlices, std::max(1, std::atoi(e))) : 32;
   }();
   return v;
+}
+
+int coResidentSlices(int device, int ranksHere) {
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) {
+    (void)hipGetLastError();
+    return std::min(maxSlices(), 32);
+  }
+  return std::max(1, std::min(maxSlices(), cus / std::max(1, ranksHere)));
+}
+
+int64_t gpuLocation(int device) {
+  int dom = 0, bus = 0, dev = 0;
+  if (hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device) != hipSuccess ||
+      hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+      hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1 - device;  // unknown: the device index
+  }
+  return ((int64_t)dom << 32) | ((int64_t)bus << 8) | (int64_t)dev;
 }
 
 }  // namespace exec

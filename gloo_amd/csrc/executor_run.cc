@@ -130,7 +130,7 @@ void PlanExecutor::setStreams(const std::vector<hipStream_t>& streams) {
   hipStream_t next = streams.empty() ? nullptr : streams[0];
   for (hipStream_t t : streams) GLOO_AMD_ENFORCE(t != nullptr || streams.size() == 1, "null stream in the list");
   if (!next) {
-    if (!ownedStream_) ownedStream_ = ctx_->sharedStream();
+    if (!ownedStream_) GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&ownedStream_, hipStreamNonBlocking));
     next = ownedStream_;
   }
   if (next != stream_) {
@@ -273,7 +273,7 @@ void PlanExecutor::run() {
   const int me = ctx_->rank;
   if (deviceSignal_ && ctx_->errorWord(me).load() != 0)
     throw IoException(strcat_("rank ", me, ": a device-side wait of a previous run timed out"));
-  if (!ownStream_) {  // (the context's shared stream is never the caller's to capture)
+  if (!ownStream_) {  // (the executor's own stream is never the caller's to capture)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     GLOO_AMD_HIP_CHECK(hipStreamIsCapturing(stream_, &cs));
     GLOO_AMD_ENFORCE(cs == hipStreamCaptureStatusNone,
@@ -554,10 +554,10 @@ void PlanExecutor::buildInterp() {
   // its one acquire and barrier, and a run of mutually independent data steps
   // (a mesh owner's sends to every peer, its copies out of the inboxes, the
   // credits after them) drains once and publishes its flags together — one
-  // memory round trip per run instead of per step.  GLOO_AMD_INTERP_BATCH=0
-  // keeps every step on its own.
-  const char* ib = std::getenv("GLOO_AMD_INTERP_BATCH");
-  if (!(ib && ib[0] == '0')) markInterpBatches(v.data(), v.size(), es_);
+  // memory round trip per run instead of per step.  (On one GPU it measured
+  // within 1 us of the unbatched form; the round trips
+  // it removes are the ones over xGMI.)
+  markInterpBatches(v.data(), v.size(), es_);
   // the bound the ranks agreed on (slicedInterpSteps) must cover what was
   // emitted; an under-count would have let an unrunnable plan be proposed
   GLOO_AMD_ENFORCE(slices_ == 1 || v.size() <= slicedInterpSteps(plan_, (int)inputs_.size(), (int)ptrs_.size()),
@@ -628,7 +628,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
     explicit ReduceStoreScope(bool plain) : prev(setReducePlainStores(plain)) {}
     ~ReduceStoreScope() { setReducePlainStores(prev); }
     bool prev;
-  } reduceStores(reducePlain_);
+  } reduceStores(true);
   auto slotOf = [&](size_t step) -> uint64_t* {
     if (!stamping_) return nullptr;
     auto it = stampSlotOf_.find(step);
@@ -649,7 +649,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
           GLOO_AMD_ENFORCE(chans.insert({steps[k].peer, steps[k].slot}).second, "a SEND batch repeats channel (peer ",
                            steps[k].peer, ", slot ", steps[k].slot, ")");
       }
-      if (deviceSignal_ && batchKernelCopy_) {
+      if (deviceSignal_) {
         for (size_t b = i; b < j; b += kMaxCopyEntries) {
           CopyDesc d[kMaxCopyEntries];
           int nd = 0;
@@ -714,8 +714,8 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         int nd = 0;
         for (size_t k = 0; k < ops.size(); k++)
           if (lens[k]) d[nd++] = CopyDesc{ops[k].first, ops[k].second, lens[k], nullptr, Seq{}, nullptr,
-                                          copySignalGrid(lens[k], copyOutBlocks_)};
-        if (nd) checkRc(launchCopySignalMulti(d, nd, epoch, stream_, localStore_), "copy kernel (local batch)");
+                                          copySignalGrid(lens[k], kCopyOutBlocks)};
+        if (nd) checkRc(launchCopySignalMulti(d, nd, epoch, stream_, kCopyStorePlain), "copy kernel (local batch)");
         i = j - 1;
         continue;
       }
@@ -790,19 +790,19 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
       case GLOO_HIP_STEP_SEND: {
         char* dst = peerAt(s.peer, remoteRegion_[{s.peer, s.slot}] + s.dst_off, s.length);
         const char* src = sendSrc(s);
-        // GLOO_AMD_COPY=auto: a lone SEND of >= 16 MiB to a rank on this
+        // A lone SEND of >= 16 MiB to a rank on this
         // same GPU goes to the copy kernel with 256 workgroups, which moves
         // HBM -> HBM faster than the blit engine from 16 MiB up (one MI355X:
         // 8.1 vs 9.7 us at 16 MiB, 22.0 vs 26.0 us at 64 MiB kernel time,
         // profiles/round2/r2d_rocprof_copy_engines_segments.csv); below that,
         // and over xGMI, hipMemcpyAsync + signal inside a captured graph
-        const bool bigLocal = autoCopy_ && s.length * es_ >= (16u << 20) && peers_[s.peer].device == ctx_->device();
+        const bool bigLocal = deviceSignal_ && s.length * es_ >= (16u << 20) && peers_[s.peer].device == ctx_->device();
         // eager (not captured): hipMemcpyAsync into an IPC mapping is the slow
         // path of an eager enqueue, and the copy kernel signals without a
         // write-back since round 3; graph memcpy nodes stay faster
         // (profiles/round3/r3ag_latency_ab_release_and_copy_engine.jsonl)
-        const bool eagerKernel = autoCopy_ && !graph;
-        if (kernelCopy_ || bigLocal || eagerKernel) {
+        const bool eagerKernel = deviceSignal_ && !graph;
+        if (bigLocal || eagerKernel) {
           const unsigned grid = copySignalGrid(s.length * es_, bigLocal ? 256u : copyBlocksFor(s.peer));
           checkRc(launchCopySignal(dst, src, s.length * es_, sigFlag(s.peer, s.slot),
                                    seqOf(i, r, graph), ticket_ + (size_t)s.peer * GLOO_HIP_NUM_SLOTS + s.slot, epoch,
@@ -848,9 +848,9 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         char* dst = userOrArena(s.flags & GLOO_HIP_DST_ARENA, s.dst_off, s.length);
         const char* src = userOrArena(s.flags & GLOO_HIP_SRC_ARENA, s.src_off, s.length);
         const size_t bytes = s.length * es_;
-        if (deviceSignal_ && bytes >= copyOutKernelBytes_ && bytes > 0 && (dst + bytes <= src || src + bytes <= dst)) {
-          const CopyDesc d{dst, src, bytes, nullptr, Seq{}, nullptr, copySignalGrid(bytes, copyOutBlocks_)};
-          checkRc(launchCopySignalMulti(&d, 1, epoch, stream_, localStore_), "copy kernel (local)");
+        if (deviceSignal_ && bytes > 0 && (dst + bytes <= src || src + bytes <= dst)) {
+          const CopyDesc d{dst, src, bytes, nullptr, Seq{}, nullptr, copySignalGrid(bytes, kCopyOutBlocks)};
+          checkRc(launchCopySignalMulti(&d, 1, epoch, stream_, kCopyStorePlain), "copy kernel (local)");
           break;
         }
         deviceMove(dst, src, bytes, stream_);
@@ -917,7 +917,7 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         // markers).  Device stamps time the fused launch itself, forward
         // stores included (stamp_end waits for them), so what ships is what
         // is measured; the slot's bytes stay the fold's (k + 1) * n * s.
-        if (foldSend_ && deviceSignal_ && !custom_ && !profiling_ && s.length > 0 &&
+        if (deviceSignal_ && !custom_ && !profiling_ && s.length > 0 &&
             !(s.flags & GLOO_HIP_DST_ARENA)) {
           char* fdst = userPtr(0) + s.dst_off * es_;
           FwdDesc fwd[kMaxCopyEntries];

@@ -3,7 +3,9 @@
 
 #include <errno.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/time.h>
 #include <sys/un.h>
 #include <unistd.h>
@@ -31,11 +33,6 @@ namespace {
 constexpr size_t kGranule = size_t(2) << 20;
 
 size_t sizeClass(size_t bytes) {
-  static const bool exact = [] {
-    const char* e = std::getenv("GLOO_AMD_IPC_EXACT");
-    return e && e[0] == '1';
-  }();
-  if (exact) return (bytes + kGranule - 1) / kGranule * kGranule;
   // powers of two up to 1 GiB, then multiples of 256 MiB (no upper bound:
   // VMM imports of any size map, ipc.h)
   constexpr size_t kBig = size_t(1) << 30, kStep = size_t(256) << 20;
@@ -313,12 +310,22 @@ Slab* acquire(int device, size_t bytes, bool fine) {
   registerAtExit();
   Pool& p = Pool::get();
   std::lock_guard<std::mutex> lk(p.m);
+  // Best fit: the smallest free slab of this device and kind that
+  // holds the request.  Slabs are never freed (ipc.h), so a request of a
+  // class never used before is served from a larger idle one before a new
+  // one is created; peers map the whole slab (an import accepts any slab of
+  // at least the published bytes).
+  size_t best = p.free.size();
   for (size_t i = 0; i < p.free.size(); i++) {
-    Slab* s = p.free[i];
-    if (s->device == device && s->fine == fine && s->bytes == want) {
-      p.free.erase(p.free.begin() + (long)i);
-      return s;
-    }
+    const Slab* s = p.free[i];
+    if (s->device == device && s->fine == fine && s->bytes >= bytes &&
+        (best == p.free.size() || s->bytes < p.free[best]->bytes))
+      best = i;
+  }
+  if (best < p.free.size()) {
+    Slab* s = p.free[best];
+    p.free.erase(p.free.begin() + (long)best);
+    return s;
   }
   DeviceScope ds(device);
   auto s = std::make_unique<Slab>();
@@ -326,7 +333,20 @@ Slab* acquire(int device, size_t bytes, bool fine) {
   s->device = device;
   s->fine = fine;
   const hipMemAllocationProp prop = propFor(device, fine);
-  GLOO_AMD_HIP_ALLOC(hipMemCreate(&s->handle, want, &prop, 0));
+  const hipError_t ce = hipMemCreate(&s->handle, want, &prop, 0);
+  if (ce == hipErrorOutOfMemory || ce == hipErrorMemoryAllocation) {
+    (void)hipGetLastError();
+    size_t held = 0, idle = 0, nidle = 0;
+    for (const auto& x : p.slabs)
+      if (x->device == device) held += x->bytes;
+    for (const Slab* x : p.free)
+      if (x->device == device) idle += x->bytes, nidle++;
+    throw EnforceNotMet(strcat_("out of device memory for a ", want, "-byte cross-process slab on device ", device,
+                                ": the pool holds ", held, " B there, ", idle, " B of it in ", nidle,
+                                " idle slabs too small for this request, which HIP cannot return while the "
+                                "process lives (gloo_amd/include/gloo_amd/ipc.h)"));
+  }
+  GLOO_AMD_HIP_ALLOC(ce);
   try {
     void* va = freshRange(want);
     mapAt(va, want, s->handle, device);
@@ -350,6 +370,26 @@ void release(Slab* s) {
   p.free.push_back(s);
 }
 
+namespace {
+// Unmaps the imports nobody holds whose exporter has exited (they
+// kept the dead peer's device memory alive until this process ended).  The
+// virtual range stays reserved and is never mapped again, as on the
+// pid-reuse path.  Caller holds p.m.
+void dropDeadImports(Pool& p) {
+  for (auto it = p.imports.begin(); it != p.imports.end();) {
+    const bool dead = it->second.users == 0 && ::kill(it->first.first, 0) != 0 && errno == ESRCH;
+    if (!dead) {
+      ++it;
+      continue;
+    }
+    GLOO_AMD_HIP_RELEASE(hipMemUnmap(it->second.ptr, it->second.bytes));
+    GLOO_AMD_HIP_RELEASE(hipMemRelease(it->second.handle));
+    p.dropped++;
+    it = p.imports.erase(it);
+  }
+}
+}  // namespace
+
 void unimport(void* mapped) {
   if (!mapped) return;
   Pool& p = Pool::get();
@@ -357,8 +397,9 @@ void unimport(void* mapped) {
   for (auto& kv : p.imports)
     if (kv.second.ptr == mapped) {
       if (kv.second.users) kv.second.users--;
-      return;  // kept for reuse (ipc.h)
+      break;  // kept for reuse while its exporter lives (ipc.h)
     }
+  dropDeadImports(p);
 }
 
 void* import(const Remote& r, size_t bytes, int device) {
@@ -367,6 +408,7 @@ void* import(const Remote& r, size_t bytes, int device) {
   const auto key = std::make_pair(r.pid, r.id);
   {
     std::lock_guard<std::mutex> lk(p.m);
+    dropDeadImports(p);
     auto it = p.imports.find(key);
     if (it != p.imports.end()) {
       if (it->second.incarnation == r.incarnation) {
@@ -404,10 +446,17 @@ void* import(const Remote& r, size_t bytes, int device) {
   int fdv = fd;
   void* osHandle = runtimeVersion() >= 70200000 ? reinterpret_cast<void*>(static_cast<intptr_t>(fd))
                                                 : static_cast<void*>(&fdv);
+  struct stat before;
+  const bool known = ::fstat(fd, &before) == 0;
   const hipError_t e = hipMemImportFromShareableHandle(&h, osHandle, hipMemHandleTypePosixFileDescriptor);
-  // the import does not take the descriptor over (the dma-buf stays referenced
-  // by the mapping); close it unless the runtime already did
-  if (::fcntl(fd, F_GETFD) != -1) ::close(fd);
+  // The import does not take the descriptor over (the dma-buf stays
+  // referenced by the mapping): close it unless the runtime already did.  A
+  // number the runtime closed may already name another thread's file (an fd
+  // server's accepted socket), so it is closed only while it still
+  // names this dma-buf.
+  struct stat after;
+  if (known && ::fstat(fd, &after) == 0 && after.st_dev == before.st_dev && after.st_ino == before.st_ino)
+    ::close(fd);
   GLOO_AMD_HIP_ALLOC(e);
   void* va = nullptr;
   try {

@@ -257,31 +257,15 @@ constexpr int kAuxNT = 2;               // cache policy `nt`: streamed once
 constexpr int kAuxWT = 1 | 2 | 16;      // `sc0 nt sc1`: streamed once, written through (not held in L2)
 
 // Completion protocol of the kernels that signal a peer after writing into
-// its inbox (copy_signal_kernel, fold_send_kernel, the interpreter), GLOO_AMD_FWD_RELEASE:
-// "last" (the default) = the signalled bytes are stored write-through
-// (sc0 nt sc1) and every wave waits for them (vmcnt 0) before its workgroup
-// takes a relaxed ticket; no L2 write-back is needed except by a workgroup
-// that also made plain stores (the edge elements), and the ticket holder
-// publishes the flag with a relaxed store.  The interpreter's sends work the
-// same way, and its credits (NOTIFY) publish no data, so neither releases.
-// "each" = every workgroup releases at system scope before its ticket or
-// flag (rounds 1-2).  Read when an executor is built (refreshFwdLean), so one
-// process can measure both; the value is process-wide (the latest build's
-// applies to every later launch: both protocols are correct, they differ in
-// speed), and a graph keeps the protocol it was captured with.
-std::atomic<int> g_fwdLean{-1};
-
-int readFwdLean() {
-  const char* e = std::getenv("GLOO_AMD_FWD_RELEASE");
-  const int v = e && std::string(e) == "each" ? 0 : 1;
-  g_fwdLean.store(v, std::memory_order_relaxed);
-  return v;
-}
-
-int fwdLean() {
-  const int v = g_fwdLean.load(std::memory_order_relaxed);
-  return v < 0 ? readFwdLean() : v;
-}
+// its inbox (copy_signal_kernel, fold_send_kernel, the interpreter): the
+// signalled bytes are stored write-through (sc0 nt sc1) and every wave waits
+// for them (vmcnt 0) before its workgroup takes a relaxed ticket; no L2
+// write-back is needed except by a workgroup that also made plain stores (the
+// edge elements), and the ticket holder publishes the flag with a relaxed
+// store.  The interpreter's sends work the same way, and its credits (NOTIFY)
+// publish no data, so neither releases.  (Rounds 1-2 released at system scope
+// in every workgroup: 4x slower at 16 MiB; that protocol and its
+// switch are gone.)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, kRsrcFlags);
@@ -838,7 +822,7 @@ __device__ __forceinline__ void interp_fold(const InterpStep& st, uint64_t lo, u
 
 template <class Tr, int OP>
 __global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpStep* steps, int nsteps, uint64_t run,
-                                                                   uint64_t timeoutTicks, uint32_t* err, int lean,
+                                                                   uint64_t timeoutTicks, uint32_t* err,
                                                                    uint64_t* done, unsigned* doneTicket) {
   using S = typename Tr::Storage;
   constexpr uint64_t kV = 16 / sizeof(S);
@@ -881,7 +865,7 @@ __global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpS
     const uint64_t q = ((n + G - 1) / G + kV - 1) / kV * kV;
     const uint64_t lo = g * q < n ? g * q : n;
     const uint64_t hi = lo + q < n ? lo + q : n;
-    if (kind == kInterpSend && lean) {
+    if (kind == kInterpSend) {
       interp_copy<true>(st.dst + lo * sizeof(S), st.src[0] + lo * sizeof(S), (hi - lo) * sizeof(S));
     } else if (kind == kInterpCopy || kind == kInterpSend) {
       interp_copy(st.dst + lo * sizeof(S), st.src[0] + lo * sizeof(S), (hi - lo) * sizeof(S));
@@ -895,19 +879,12 @@ __global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      // lean (fwdLean): a SEND's bytes went out write-through and a SIGNAL is
-      // a credit that publishes no data (its reads are complete), so neither
-      // needs the L2 write-back of a release; otherwise one release covers
-      // the whole batch
-      bool released = lean;
+      // a SEND's bytes went out write-through and a SIGNAL is a credit that
+      // publishes no data (its reads are complete), so neither needs the L2
+      // write-back of a release
       for (int j = batch; j <= k; j++) {
         const InterpStep& sj = steps[j];
         if (sj.kind != kInterpSend && sj.kind != kInterpSignal) continue;
-        if (!released) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          released = true;
-        }
         __hip_atomic_store(sj.flag + g, sj.base + run * sj.perRun, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
@@ -933,12 +910,11 @@ __global__ __launch_bounds__(kInterpBlock) void plan_interp_kernel(const InterpS
 template <class Tr>
 int launch_interp(int op, const InterpStep* steps, int nsteps, uint64_t run, uint64_t tt, uint32_t* err,
                   int G, hipStream_t s, uint64_t* done, unsigned* dt) {
-  const int lean = fwdLean();
   switch (op) {
-    case GLOO_HIP_SUM: plan_interp_kernel<Tr, GLOO_HIP_SUM><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean, done, dt); break;
-    case GLOO_HIP_PRODUCT: plan_interp_kernel<Tr, GLOO_HIP_PRODUCT><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean, done, dt); break;
-    case GLOO_HIP_MAX: plan_interp_kernel<Tr, GLOO_HIP_MAX><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean, done, dt); break;
-    case GLOO_HIP_MIN: plan_interp_kernel<Tr, GLOO_HIP_MIN><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, lean, done, dt); break;
+    case GLOO_HIP_SUM: plan_interp_kernel<Tr, GLOO_HIP_SUM><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, done, dt); break;
+    case GLOO_HIP_PRODUCT: plan_interp_kernel<Tr, GLOO_HIP_PRODUCT><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, done, dt); break;
+    case GLOO_HIP_MAX: plan_interp_kernel<Tr, GLOO_HIP_MAX><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, done, dt); break;
+    case GLOO_HIP_MIN: plan_interp_kernel<Tr, GLOO_HIP_MIN><<<G, kInterpBlock, 0, s>>>(steps, nsteps, run, tt, err, done, dt); break;
     default: return GLOO_HIP_EINVAL_OP;
   }
   return GLOO_HIP_OK;
@@ -971,7 +947,6 @@ struct CopyList {
   uint64_t* flag[kMaxCopies];
   Seq seq[kMaxCopies];
   unsigned* ticket[kMaxCopies];
-  int lean;  // completion protocol (fwdLean): write-through stores, one release by the ticket holder
   int plainStore;  // stores of a flag-less copy (CopyStore, signal.h)
 };
 
@@ -1002,10 +977,10 @@ __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(CopyList L, con
     u32x4 v[kCopyUnroll];
 #pragma unroll
     for (int u = 0; u < kCopyUnroll; u++) v[u] = bload<kAuxNT>(rs, lane_off + u * kCopyBlock * 16, ss.mis);
-    if ((L.lean && L.flag[j]) || (!L.flag[j] && L.plainStore == kCopyStoreWT)) {
+    if (L.flag[j] || L.plainStore == kCopyStoreWT) {
 #pragma unroll
       for (int u = 0; u < kCopyUnroll; u++) bstore<kAuxWT>(rd, lane_off + u * kCopyBlock * 16, v[u]);
-    } else if (!L.flag[j] && L.plainStore == kCopyStorePlain) {
+    } else if (L.plainStore == kCopyStorePlain) {
 #pragma unroll
       for (int u = 0; u < kCopyUnroll; u++) bstore<0>(rd, lane_off + u * kCopyBlock * 16, v[u]);
     } else {
@@ -1017,27 +992,20 @@ __global__ __launch_bounds__(kCopyBlock) void copy_signal_kernel(CopyList L, con
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    // lean: the body went out write-through and every wave has waited for
-    // it; only the entry's block 0, whose head / tail bytes are plain
-    // stores, releases before its ticket
-    if (!L.lean || (lb == 0 && (head || tail0 < bytes))) {
+    // the body went out write-through and every wave has waited for it;
+    // only the entry's block 0, whose head / tail bytes are plain stores,
+    // releases before its ticket
+    if (lb == 0 && (head || tail0 < bytes)) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     const uint64_t ep = epoch ? *epoch : 0;
-    const unsigned t = L.lean ? __hip_atomic_fetch_add(L.ticket[j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                              : __hip_atomic_fetch_add(L.ticket[j], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned t = __hip_atomic_fetch_add(L.ticket[j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == nb - 1) {
       // last workgroup of this entry: reset the counter for the next launch
       // (launches on one channel's counter are stream-ordered), publish
       __hip_atomic_store(L.ticket[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      const uint64_t v = L.seq[j].base + ep * L.seq[j].perRun;
-      if (L.lean) {
-        __hip_atomic_store(L.flag[j], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      } else {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        __hip_atomic_store(L.flag[j], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
+      __hip_atomic_store(L.flag[j], L.seq[j].base + ep * L.seq[j].perRun, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -1081,8 +1049,6 @@ struct FwdList {
   uint64_t* flag[kMaxCopyEntries];  // nullptr: no arrival flag for this entry
   Seq seq[kMaxCopyEntries];
   unsigned* ticket;                 // zero between launches; nullptr: no signals
-  int lean;                         // completion protocol (launchFoldSend)
-  int plainLocal;                   // dst stores plain (default) or `nt` (GLOO_AMD_FOLD_STORE=nt)
 };
 
 template <class Tr, int OP>
@@ -1120,13 +1086,10 @@ __global__ __launch_bounds__(kVecBlock) void fold_send_kernel(typename Tr::Stora
     else if (mode == 1) fold_tile<Tr, OP, UNROLL, BLOCK, 1>(srcs, k, head, base, bytes, acc);
     else fold_tile<Tr, OP, UNROLL, BLOCK, 0>(srcs, k, head, base, bytes, acc);
     const auto rd = make_rsrc(reinterpret_cast<const char*>(dst + head) + base, bytes);
-    if (F.plainLocal) {
+    // plain local stores: the result stays in the Infinity Cache for its
+    // next reader (`nt` measured slower per call)
 #pragma unroll
-      for (int u = 0; u < UNROLL; u++) bstore<0>(rd, lane_off + u * BLOCK * 16, acc[u]);
-    } else {
-#pragma unroll
-      for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rd, lane_off + u * BLOCK * 16, acc[u]);
-    }
+    for (int u = 0; u < UNROLL; u++) bstore<0>(rd, lane_off + u * BLOCK * 16, acc[u]);
     for (int r = 0; r < F.n; r++) {
       if (!F.dst[r]) continue;  // a credit: no data
       // a forward destination may sit at another residue mod 16 B than dst
@@ -1134,13 +1097,8 @@ __global__ __launch_bounds__(kVecBlock) void fold_send_kernel(typename Tr::Stora
       // relatively misaligned source's does
       const Src fr = src_of(F.dst[r] + head * sizeof(S));
       const auto rf = make_rsrc(fr.base + base, bytes + fr.mis);
-      if (F.lean) {
 #pragma unroll
-        for (int u = 0; u < UNROLL; u++) bstore<kAuxWT>(rf, lane_off + u * BLOCK * 16, acc[u], fr.mis);
-      } else {
-#pragma unroll
-        for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rf, lane_off + u * BLOCK * 16, acc[u], fr.mis);
-      }
+      for (int u = 0; u < UNROLL; u++) bstore<kAuxWT>(rf, lane_off + u * BLOCK * 16, acc[u], fr.mis);
     }
   }
   stamp_end(stamp);
@@ -1148,29 +1106,22 @@ __global__ __launch_bounds__(kVecBlock) void fold_send_kernel(typename Tr::Stora
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    // lean: the forwarded bytes were stored write-through (sc0 sc1) and this
+    // the forwarded bytes were stored write-through (sc0 sc1) and this
     // workgroup's waves have all seen them acknowledged, so no workgroup
     // writes its L2 back except block 0 for its plain edge stores, and the
-    // ticket holder publishes with a relaxed store; otherwise every
-    // workgroup releases before its ticket
-    if (!F.lean || (blockIdx.x == 0 && (head || tail0 < n))) {  // block 0's edge elements are plain stores
+    // ticket holder publishes with a relaxed store
+    if (blockIdx.x == 0 && (head || tail0 < n)) {  // block 0's edge elements are plain stores
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     const uint64_t ep = epoch ? *epoch : 0;
-    const unsigned t = F.lean ? __hip_atomic_fetch_add(F.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                              : __hip_atomic_fetch_add(F.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned t = __hip_atomic_fetch_add(F.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == gridDim.x - 1) {
       __hip_atomic_store(F.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (!F.lean) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       for (int r = 0; r < F.n; r++)
-        if (F.flag[r]) {
-          const uint64_t v = F.seq[r].base + ep * F.seq[r].perRun;
-          if (F.lean)
-            __hip_atomic_store(F.flag[r], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          else
-            __hip_atomic_store(F.flag[r], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        if (F.flag[r])
+          __hip_atomic_store(F.flag[r], F.seq[r].base + ep * F.seq[r].perRun, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -1344,8 +1295,6 @@ int dispatch_multi(int op, int dtype, void* d, const void* const* srcs, int k, s
 
 }  // namespace
 
-int refreshFwdLean() { return readFwdLean(); }
-
 unsigned copySignalGrid(size_t bytes, unsigned maxBlocks) {
   const size_t tiles = (bytes + (size_t)kCopyBlock * kCopyUnroll * 16 - 1) / ((size_t)kCopyBlock * kCopyUnroll * 16);
   size_t g = tiles < maxBlocks ? tiles : maxBlocks;
@@ -1370,7 +1319,6 @@ int launchCopySignalMulti(const CopyDesc* d, int n, const uint64_t* epoch, hipSt
     L.ticket[j] = d[j].ticket;
   }
   L.first[n] = total;
-  L.lean = fwdLean();
   L.plainStore = localStore;
   copy_signal_kernel<<<total, kCopyBlock, 0, s>>>(L, epoch);
   return check_launch("copy_signal_kernel");
@@ -1469,16 +1417,10 @@ int launchFoldSend(int op, int dtype, void* dst, const void* const* srcs, int k,
   memset(&F, 0, sizeof(F));
   F.n = nf;
   F.ticket = ticket;
-  F.lean = fwdLean();
-  // The result range stays in the Infinity Cache for its next reader (the
-  // copy-out's peers, the caller, the next call): plain stores measured 1-5 %
-  // faster per HD / ring call than `nt` from 16 to 64 MiB per rank, equal at
-  // 256 MiB (profiles/round5/r5p_*)
-  static const int plainLocal = [] {
-    const char* e = std::getenv("GLOO_AMD_FOLD_STORE");
-    return e && std::string(e) == "nt" ? 0 : 1;
-  }();
-  F.plainLocal = plainLocal;
+  // (the local result is stored plain: the range stays in the Infinity Cache
+  // for its next reader — the copy-out's peers, the caller, the next call —
+  // 1-5 % faster per HD / ring call than `nt` from 16 to 64 MiB per rank,
+  // equal at 256 MiB: DESIGN.md §4, profiles/round5/r5p_*)
   for (int r = 0; r < nf; r++) {
     if (!fwd[r].dst && !fwd[r].flag) return set_error(GLOO_HIP_EINVAL_ARG, "forward entry with neither data nor flag");
     if ((uintptr_t)fwd[r].dst % es)

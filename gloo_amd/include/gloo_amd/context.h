@@ -64,14 +64,6 @@ class Context : public std::enable_shared_from_this<Context> {
   std::atomic<uint32_t>& errorWord(int r);
   uint32_t* errorWordDevicePtr(int r);
 
-  // The stream of this rank's algorithms that were given none (created on
-  // first use, destroyed with the context).  Their runs return complete, so
-  // sharing one stream serialises nothing, and a process with many such
-  // algorithms keeps to one GPU queue for them: with several rank processes
-  // on one GPU, every extra queue adds to what the GPU's scheduler must
-  // time-slice.
-  hipStream_t sharedStream();
-
   // Store-based barrier among all ranks (setup / teardown only).
   void barrier(const std::string& tag);
   // Collective exchange of one small blob per rank (setup / teardown only);
@@ -93,8 +85,6 @@ class Context : public std::enable_shared_from_this<Context> {
   size_t countersBytes_ = 0;
   void ensureDeviceMapped();
   uint64_t barrierGen_ = 0;
-  std::mutex streamMutex_;
-  hipStream_t sharedStream_ = nullptr;
 };
 
 }  // namespace gloo_amd

@@ -23,12 +23,11 @@
 // Within one process, ranks that share a GPU share its hardware queues, where
 // a spinning wait could block the very signal it waits for; those ranks keep
 // the host-side waits.  Both styles write the same monotonically increasing
-// sequence numbers, so they interoperate.  GLOO_AMD_SIGNAL=host|device
-// overrides the choice.
+// sequence numbers, so they interoperate.
 //
 // hipGraph replay (device signalling; GLOO_AMD_GRAPH=auto, the default, for
-// plans with unfused steps, except mesh plans with messages of
-// GLOO_AMD_GRAPH_BYTES or more; =1 always): once a plan has run with the same buffers, the next run() captures the whole
+// plans with unfused steps, except mesh plans with messages of 4 MiB or
+// more; =1 always): once a plan has run with the same buffers, the next run() captures the whole
 // enqueue — epoch bump, waits, copies, reductions, signals — into a hipGraph
 // and every later run() is ONE hipGraphLaunch.  Sequence numbers are
 // replayable (signal.h: base + epoch * perRun with a device-side run epoch),
@@ -41,22 +40,23 @@
 // receives from a socket/NIC.  Peers write HOST inboxes over PCIe; REDUCE
 // reads them in place (zero-copy) and accumulates into the device buffer.
 //
-// Copy engine of a SEND (device signalling): hipMemcpyAsync + signal kernel
-// (default), or GLOO_AMD_COPY=kernel: copy_signal_kernel, one launch that
-// copies with GLOO_AMD_COPY_BLOCKS workgroups (default 64) and publishes the
-// arrival itself.
+// Copy engine of a SEND (device signalling): copy_signal_kernel, one launch
+// that copies and publishes the arrival itself, in an eager enqueue and for
+// batches; hipMemcpyAsync + signal kernel inside a captured graph (the
+// PlanExecutor members below say why, with the measurements).
 //
 // One-launch interpreter (device signalling, GLOO_AMD_INTERP, default on):
-// when every message of the plan is at most GLOO_AMD_INTERP_BYTES (default
-// the fuse limit, 64 KiB) and no operand lives on another GPU of this
+// when every message of the plan is at most the fuse limit
+// (GLOO_AMD_FUSE_BYTES, 64 KiB) and no operand lives on another GPU of this
 // process, the steps are resolved once into a device-resident InterpStep
 // list (signal.h) and every run() is ONE one-workgroup launch walking it —
 // a small allreduce costs its cross-rank hops, not a kernel boundary each.
 // Larger plans (messages up to GLOO_AMD_INTERP_MAX_SLICES (32) x
-// GLOO_AMD_INTERP_SLICE_MAX_BYTES (64 KiB)) run SLICED when every rank's plan
-// allows it: one workgroup per GLOO_AMD_INTERP_SLICE_BYTES (32 KiB) of the
-// largest message, at most 32, each running the whole plan on its slice of
-// every step with its own flag words (signal.h).
+// 2 x GLOO_AMD_INTERP_SLICE_BYTES) run SLICED when every rank's plan allows
+// it: one workgroup per GLOO_AMD_INTERP_SLICE_BYTES (32 KiB) of the largest
+// message, at most the cap (also at most the GPU's CUs / the ranks on it),
+// each running the whole plan on its slice of every step with its own flag
+// words (signal.h).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -122,7 +122,6 @@ class PlanExecutor {
   bool deviceSignalling() const { return deviceSignal_; }
   bool fineGrainedArena() const { return fineArena_; }
   bool hostArena() const { return hostArena_; }
-  bool kernelCopy() const { return kernelCopy_; }
   bool foldSendUsed() const { return foldSendUsed_; }
   // True when the last run() was a replay of the captured hipGraph (a run
   // with profiling events on is enqueued eagerly even while a graph exists).
@@ -131,6 +130,9 @@ class PlanExecutor {
   bool interpreted() const { return interpMode_ && interpCount_ > 0; }
   // Workgroups of that launch: > 1 when every rank runs the plan sliced.
   int interpSlices() const { return slices_; }
+  // run() on the executor's own stream: it returns with the outputs complete
+  // (through the device-published done word); otherwise on the caller's
+  bool ownStream() const { return ownStream_; }
   // Why graph capture was abandoned (empty if it was not).
   const std::string& graphError() const { return graphError_; }
   // Host time spent blocked in WAIT steps during the last run(), seconds.
@@ -199,7 +201,7 @@ class PlanExecutor {
   bool anyRemote_ = false;
   void classifyPointers();
   // construction phases (executor.cc)
-  int32_t proposeSlices(const std::set<int>& recvPeers);
+  int32_t proposeSlices(const std::set<int>& recvPeers, int sliceCap);
   void mapPeers(const std::vector<std::vector<char>>& arenas, const std::set<int>& planPeers,
                 const std::set<int>& sendPeers);
   void configureDeviceLaunches();
@@ -216,7 +218,7 @@ class PlanExecutor {
   std::vector<std::unique_ptr<HostShm>> peerShm_;
   hipStream_t stream_ = nullptr;
   bool ownStream_ = false;            // stream_ is the executor's own: run() returns with outputs complete
-  hipStream_t ownedStream_ = nullptr;  // the stream runs use when given none: the context's shared one
+  hipStream_t ownedStream_ = nullptr;  // the stream runs use when given none: the executor's own
   std::vector<hipStream_t> sideStreams_;  // the caller's streams of pointers 1.. (setStreams)
   std::vector<hipEvent_t> sideEvents_;
   hipEvent_t doneEvent_ = nullptr;     // recorded on stream_ at the end of a run on a caller's stream
@@ -254,7 +256,7 @@ class PlanExecutor {
   // interpreter's done signal, or a signal kernel behind an eager or replayed
   // run) and run() spins on it instead of synchronising the stream: a launch + stream synchronise costs 10.3 µs on
   // MI355X, a kernel's own store seen by a spinning host 7.4 µs
-  // (tools/launch_probe, profiles/round5/r5ac_*).  GLOO_AMD_DONE_SPIN=0: off.
+  // (tools/launch_probe, profiles/round5/r5ac_*).
   uint64_t* hostDone_ = nullptr;     // coherent pinned host memory
   uint64_t* hostDoneDev_ = nullptr;  // ... its device address
   unsigned* doneTicket_ = nullptr;   // device: the workgroups' ticket counter
@@ -265,36 +267,28 @@ class PlanExecutor {
   std::vector<uint64_t*> peerMailbox_;    // peers' mailboxes (nullptr: that channel uses the host block)
   std::vector<bool> peerMailboxIpc_;
   bool fineArena_ = false;     // inbox arena in fine-grained (cross-device coherent) memory
-  bool kernelCopy_ = false;    // SEND = copy_signal_kernel instead of hipMemcpyAsync + signal
-  bool autoCopy_ = false;      // GLOO_AMD_COPY=auto: the engine picked per SEND by size and peer placement
-  unsigned copyBlocks_ = 64;        // per copy to a peer on another GPU (xGMI)
-  // per copy to a peer on this GPU: 128 — ranks sharing a GPU run their
-  // copies concurrently, and whole-chip copy grids convoy behind each other
-  // (64 MiB HD over 4 ranks on one GPU: 462 us at 64 vs 1357 us at 512
-  // workgroups per copy); 128 against 64 (round 4, profiles/round4/
-  // r4j_latency_copy_blocks_local_ab.jsonl): HD 16 MiB per rank 45.4-47.1
-  // vs 47.2-48.2 us at 2 ranks, 64 MiB 226-230 vs 240-247 us at 4 ranks,
-  // even elsewhere.  GLOO_AMD_COPY_BLOCKS_LOCAL overrides.
-  unsigned copyBlocksLocal_ = 128;
+  // Fixed launch choices, each from a measured A/B (the knobs
+  // that switched them are gone):
+  //  - a SEND in an eager enqueue, a batch of SENDs to several peers, and a
+  //    lone same-GPU SEND of 16 MiB or more run on the copy+signal kernel; a
+  //    lone SEND inside a captured graph is hipMemcpyAsync + signal kernel;
+  //  - workgroups per copy: 64 to a peer on another GPU (a few dozen saturate
+  //    an xGMI link), 128 to a peer on this GPU (ranks sharing a GPU run
+  //    their copies concurrently and whole-chip grids convoy: HD 16 MiB per
+  //    rank 45.4-47.1 vs 47.2-48.2 us at 2 ranks against 64, 64 MiB
+  //    226-230 vs 240-247 us at 4 ranks, profiles/round4/r4j_*);
+  //  - a local COPY (a mesh result out of its inbox) runs on the copy kernel
+  //    with at most 256 workgroups and plain stores (up to 11 % per call
+  //    faster than the blit, and than `nt`, profiles/round5/r5o_*);
+  //  - REDUCE steps store plain (HD on the reference route 3-4 % faster per
+  //    call at 64 and 256 MiB per rank, profiles/round5/r5u_*);
+  //  - a FOLD's result SENDs ride in the fold's pass (launchFoldSend).
+  static constexpr unsigned kCopyBlocksRemote = 64;
+  static constexpr unsigned kCopyBlocksLocal = 128;
+  static constexpr unsigned kCopyOutBlocks = 256;
   unsigned copyBlocksFor(int peer) const {
-    return peers_[peer].device == ctx_->device() ? copyBlocksLocal_ : copyBlocks_;
+    return peers_[peer].device == ctx_->device() ? kCopyBlocksLocal : kCopyBlocksRemote;
   }
-  bool batchKernelCopy_ = true;  // a batch of SENDs = one multi-destination copy kernel
-  // A lone local COPY (a mesh result out of its inbox) of at least this many
-  // bytes runs on the copy kernel instead of hipMemcpyAsync
-  // (GLOO_AMD_COPY_OUT_BYTES; default every size, with device signalling);
-  // copyOutBlocks_ caps the workgroups per local copy there and in a batch
-  // of local COPYs (GLOO_AMD_COPY_OUT_BLOCKS); localStore_ is their store
-  // flavour (signal.h CopyStore; GLOO_AMD_LOCAL_COPY_STORE = plain | nt | wt)
-  size_t copyOutKernelBytes_ = 0;
-  unsigned copyOutBlocks_ = 256;
-  CopyStore localStore_ = kCopyStorePlain;
-  // REDUCE steps (the reference routes' reduce into the user buffer) store
-  // plain instead of `nt` (GLOO_AMD_REDUCE_STORE = plain | nt): HD on the
-  // reference route 3-4 % faster per call at 64 and 256 MiB per rank, equal
-  // below (profiles/round5/r5u_*)
-  bool reducePlain_ = true;
-  bool foldSend_ = true;         // a FOLD's result SENDs ride in the fold's pass (launchFoldSend)
   bool foldSendUsed_ = false;    // ... and some enqueue did so
   unsigned* ticket_ = nullptr;   // copy_signal_kernel tickets, one counter per (peer, slot)
   std::vector<hipStream_t> aux_;        // forked SEND batches (memcpy engine)

@@ -13,10 +13,14 @@
 //     range freed with hipMemAddressFree and handed out again by the next
 //     reserve (r5j_vmm_sys_freeva_uncached.jsonl).  Since HIP returns a
 //     block's memory only when its range is freed (tools/vmm_leak.py,
-//     r5i_*), slabs and imports are never released while the process lives:
-//     they are reused by size class (powers of two of 2 MiB up to 1 GiB,
-//     then multiples of 256 MiB), which bounds the pool by the classes a
-//     process uses.
+//     r5i_*), slabs are never released while the process lives: they are
+//     created in size classes (powers of two of 2 MiB up to 1 GiB, then
+//     multiples of 256 MiB) and a request is served from the smallest idle
+//     slab that holds it (best fit), so a process never holds more than
+//     one slab per class it used at once, and a class never used before is
+//     served from a larger idle slab when there is one.  When hipMemCreate
+//     runs out of memory the error names the pool's idle bytes.  An import
+//     nobody holds is unmapped once its exporter has exited.
 //   * Peers obtain a slab's fd from its owner's fd server: a thread on an
 //     abstract Unix socket named by (pid, incarnation) that answers a slab id
 //     with the fd (SCM_RIGHTS), to processes of the same user only.
@@ -29,7 +33,7 @@
 // gone (DESIGN.md "Cross-process memory").
 //
 // An executor that no longer needs a slab returns it to the pool, and the
-// next executor of that size class on that device reuses it (its peers'
+// next executor on that device whose request it holds reuses it (its peers'
 // mappings too).  Imports are kept per (exporter pid, slab id) and counted
 // per executor; the incarnation (a random word per process) tells a new
 // process that reuses a dead one's pid apart.  Callers verify each import

@@ -201,9 +201,4 @@ struct FwdDesc {
 int launchFoldSend(int op, int dtype, void* dst, const void* const* srcs, int k, size_t n, int mode,
                    const FwdDesc* fwd, int nf, unsigned* ticket, const uint64_t* epoch, hipStream_t stream);
 
-// Re-reads GLOO_AMD_FWD_RELEASE (the completion protocol of the signalling
-// copy / fold + forward / interpreter kernels; reduce.hip fwdLean); the
-// executor calls it when it is built.  Returns 1 for "last", 0 for "each".
-int refreshFwdLean();
-
 }  // namespace gloo_amd

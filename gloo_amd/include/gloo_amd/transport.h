@@ -111,7 +111,12 @@ class Device {
 
   struct Channel {
     std::atomic<uint64_t> count;  // arrivals
-    uint64_t pad[7];
+    // the arrival number of the last message sent on the channel: senders
+    // number their messages from it, so a send buffer closed and created
+    // again on the same slot continues the numbering (set to the count's
+    // value by the receive buffer that takes the channel)
+    std::atomic<uint64_t> sent;
+    uint64_t pad[6];
   };
   static_assert(sizeof(Channel) == 64, "one line per channel");
   struct MsgRecord {

@@ -402,9 +402,10 @@ int gloo_hip_algorithm_stats(gloo_hip_algorithm_t algo, double* stats4);
 
 /* How the algorithm executes (no reference counterpart; for tests and
  * tools): mode4[0] = device-side signalling, [1] = inbox arena (0 device
- * coarse-grained, 1 device fine-grained, 2 pinned host),
- * [2] = bit 0: kernel copy engine, bit 1: some run fused a fold with the
- * SENDs of its result (fold+forward), [3] = how run() launches the plan: 0 enqueued
+ * memory no peer writes, 1 device fine-grained, 2 pinned host),
+ * [2] = bit 1: some run fused a fold with the SENDs of its result
+ * (fold+forward), bit 2: runs on the algorithm's own stream (run() returns
+ * with the outputs complete), [3] = how run() launches the plan: 0 enqueued
  * step by step, 1 a captured hipGraph replayed, k >= 2 the one-launch plan
  * interpreter with k - 1 workgroups (> 1: sliced).  If graph capture was
  * abandoned, gloo_hip_last_error() says why. */

@@ -73,3 +73,18 @@ def mem_info():
 def memset(p, value, nbytes):
     check(lib().hipMemset(ctypes.c_void_p(p), ctypes.c_int(value), ctypes.c_size_t(nbytes)), "hipMemset")
     synchronize()
+
+
+def stream_create():
+    """A new (blocking) stream: the caller's stream of a test."""
+    s = ctypes.c_void_p()
+    check(lib().hipStreamCreate(ctypes.byref(s)), "hipStreamCreate")
+    return s.value
+
+
+def stream_synchronize(s):
+    check(lib().hipStreamSynchronize(ctypes.c_void_p(s)), "hipStreamSynchronize")
+
+
+def stream_destroy(s):
+    check(lib().hipStreamDestroy(ctypes.c_void_p(s)), "hipStreamDestroy")

@@ -2,7 +2,7 @@
 reference's own outputs at BASELINE sizes.
 
   * config 3: AllreduceRingChunked fp32 sum, 8 ranks x 256 MiB, on the mesh
-    route (default) and on the reference's ring route (GLOO_AMD_RING_MESH=0);
+    route (default) and on the reference's ring route (GLOO_AMD_MESH=0);
   * config 4: AllreduceHalvingDoubling fp32, 8 ranks x 16 MiB and a ragged
     5000011-element buffer (misaligned chunk offsets), both routes;
   * config 5: ReduceScatterHalvingDoubling fp16 / bf16 x sum / product /
@@ -126,10 +126,9 @@ CONFIG3 = "ring_chunked/sum/f32/P8/n67108864"
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("env", [{}, {"GLOO_AMD_RING_MESH": "0", "GLOO_AMD_GRAPH": "1"},
-                                 {"GLOO_AMD_COPY": "memcpy", "GLOO_AMD_GRAPH": "1"},
-                                 {"GLOO_AMD_RING_MESH": "0", "GLOO_AMD_COPY": "kernel"}],
-                         ids=["mesh", "ring_route_graph", "mesh_memcpy_graph", "ring_route_kernel_copy"])
+@pytest.mark.parametrize("env", [{}, {"GLOO_AMD_MESH": "0"}, {"GLOO_AMD_GRAPH": "1"},
+                                 {"GLOO_AMD_MESH": "0", "GLOO_AMD_GRAPH": "0"}],
+                         ids=["mesh", "ring_route_graph", "mesh_graph", "ring_route_eager"])
 def test_config3_full_size(torch, env):
     """BASELINE config 3 at its configured size: 8 ranks x 256 MiB fp32,
     ring-chunked, every rank's buffer byte for byte the reference's output
@@ -138,8 +137,9 @@ def test_config3_full_size(torch, env):
     check(res, [CONFIG3])
     # GLOO_AMD_GRAPH=1, or the reference route: run 2 captures the plan and
     # run 3 replays it; the mesh plan's 32 MiB messages are enqueued eagerly
-    # by default (GLOO_AMD_GRAPH_BYTES)
-    want_graph = env.get("GLOO_AMD_GRAPH") == "1" or env.get("GLOO_AMD_RING_MESH") == "0"
+    # by default (4 MiB and up), and GLOO_AMD_GRAPH=0 keeps every run eager
+    want_graph = env.get("GLOO_AMD_GRAPH") == "1" or (env.get("GLOO_AMD_MESH") == "0" and
+                                                      env.get("GLOO_AMD_GRAPH") != "0")
     assert all(r[CONFIG3][2]["mode"]["graph"] == want_graph for r in res), [r[CONFIG3][2]["mode"] for r in res]
 
 
@@ -148,8 +148,8 @@ HD = ["halving_doubling/sum/f32/P8/n4194304", "halving_doubling/sum/f32/P8/n5000
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("env", [{}, {"GLOO_AMD_MESH": "0"}, {"GLOO_AMD_MESH": "0", "GLOO_AMD_COPY": "kernel"}],
-                         ids=["mesh", "reference_route", "reference_route_kernel_copy"])
+@pytest.mark.parametrize("env", [{}, {"GLOO_AMD_MESH": "0"}, {"GLOO_AMD_MESH": "0", "GLOO_AMD_GRAPH": "0"}],
+                         ids=["mesh", "reference_route", "reference_route_eager"])
 def test_halving_doubling_bandwidth(torch, env):
     """BASELINE config 4 in its bandwidth regime (16 MiB per rank, and a
     ragged size whose chunk offsets are not 16-byte aligned)."""
@@ -350,9 +350,10 @@ print("RESULT" + json.dumps(res), flush=True)
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("P,n", [(2, 1 << 20), (2, 1 << 26), (4, 1 << 24), (3, 10000019)])
-@pytest.mark.parametrize("copy", ["kernel", "memcpy", "auto"])
-def test_ring_route_copy_engines_closed_form(torch, P, n, copy):
-    """The reference ring route (GLOO_AMD_RING_MESH=0) with each copy engine,
+@pytest.mark.parametrize("graph", ["auto", "0"])
+def test_ring_route_launch_modes_closed_form(torch, P, n, graph):
+    """The reference ring route (GLOO_AMD_MESH=0), replayed (its default: the
+    graph's SENDs are hipMemcpyAsync nodes) and eager (the copy kernel),
     every element against the closed form of gloo/test/base_test.h:184-236,
     in eleven runs: eager, capture, replay, then with HIP-event profiling,
     with device stamps (eager, capture, replays) and with profiling off."""
@@ -360,7 +361,9 @@ def test_ring_route_copy_engines_closed_form(torch, P, n, copy):
         w = os.path.join(d, "w.py")
         with open(w, "w") as f:
             f.write(CLOSED_WORKER)
-        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_RING_MESH="0", GLOO_AMD_COPY=copy)
+        e = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_MESH="0")
+        if graph != "auto":
+            e["GLOO_AMD_GRAPH"] = graph
         procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s"), str(n), "11"],
                                   env=e, stdout=subprocess.PIPE, text=True) for r in range(P)]
         try:

@@ -169,17 +169,13 @@ np.save(out, hip_rt.d2h(buf, x))
 
 
 @pytest.mark.parametrize("algo,P,env", [
-    ("ring_chunked", 8, {"GLOO_AMD_TEST_N": "4194304"}),      # mesh, 16 MiB/rank: unfused, graph replay
-    ("ring_chunked", 8, {"GLOO_AMD_TEST_N": "4194304", "GLOO_AMD_COPY": "memcpy"}),
-    ("ring_chunked", 8, {"GLOO_AMD_TEST_N": "4194304", "GLOO_AMD_RING_MESH": "0"}),
-    ("ring_chunked", 4, {}),                                  # auto: device-side signalling
+    ("ring_chunked", 8, {"GLOO_AMD_TEST_N": "4194304"}),      # mesh, 16 MiB/rank: unfused, eager (>= 4 MiB)
+    ("ring_chunked", 8, {"GLOO_AMD_TEST_N": "4194304", "GLOO_AMD_MESH": "0"}),  # pipelined ring: graph replay
+    ("ring_chunked", 4, {}),                                  # device-side signalling, fine-grained inboxes
     ("halving_doubling", 4, {}),
     ("halving_doubling", 5, {}),                              # non-power-of-2 binary blocks
-    ("ring_chunked", 3, {"GLOO_AMD_SIGNAL": "host"}),         # host waits across processes
-    ("halving_doubling", 4, {"GLOO_AMD_ARENA": "fine"}),      # fine-grained inboxes over IPC
-    ("ring_chunked", 8, {"GLOO_AMD_ARENA": "fine"}),
-    ("ring_chunked", 4, {"GLOO_AMD_MAILBOX": "0"}),            # device signals through the host control block
-    ("halving_doubling", 5, {"GLOO_AMD_MAILBOX": "0", "GLOO_AMD_MESH": "0"}),
+    ("ring_chunked", 8, {}),
+    ("halving_doubling", 5, {"GLOO_AMD_MESH": "0"}),
 ])
 def test_processes_ipc(torch, algo, P, env):
     """Ranks as processes: inbox arenas exchanged as HIP IPC handles through a
@@ -211,7 +207,7 @@ def test_profiling_stats(torch, monkeypatch, mesh):
     (ring: 2(P-1) two-operand reductions of n/2P; mesh: one P-source fold of
     n/P, i.e. P-1 reductions and (P+1) n/P elements moved)."""
     import gloo_amd
-    monkeypatch.setenv("GLOO_AMD_RING_MESH", mesh)
+    monkeypatch.setenv("GLOO_AMD_MESH", mesh)
     P, n = 4, 1 << 20
     url = "mem:" + uuid.uuid4().hex
     bufs = [torch.ones(n, device=f"cuda:{dev_of(torch, r)}") for r in range(P)]
@@ -256,19 +252,6 @@ def test_cpp_example_program(workspace):
     r = subprocess.run([exe, "4", "100003", workspace], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ok" in r.stdout
-
-
-@pytest.mark.parametrize("env", [{"GLOO_AMD_SIGNAL": "host"}, {"GLOO_AMD_ARENA": "fine"}])
-def test_threads_forced_modes(torch, golden_sched, env, monkeypatch):
-    """Thread ranks under the non-default transport settings still match the
-    reference bit for bit (fine-grained inboxes; explicit host waits)."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    case = "halving_doubling/sum/f32/P5/k1/n10007"
-    x, want = golden_sched[case + "/in"], golden_sched[case + "/out"]
-    y = run_threads(torch, "halving_doubling", "sum", "f32", x)
-    for r in range(y.shape[0]):
-        assert same_bytes(y[r, 0], want)
 
 
 def new_style_keys():
@@ -401,22 +384,60 @@ def test_processes_zero_count(torch, algo, P, env):
     assert all(f"OK {algo}\n" in o for o in outs), outs
 
 
-@pytest.mark.parametrize("mode,interp", [("device", "1"), ("device", "0"), ("host", "1")])
-def test_dead_peer_times_out(torch, mode, interp):
+@pytest.mark.parametrize("interp", ["1", "0"])
+def test_dead_peer_times_out(torch, interp):
     """Failure detection (context timeout -> IoException): a peer
     that disappears makes run() raise after the timeout instead of hanging —
-    through the interpreter's bounded spin (it ends the launch), the
-    device-side wait kernel's, or the host wait."""
+    through the interpreter's bounded spin (it ends the launch) or the
+    device-side wait kernel's.  (Host waits: test_dead_peer_times_out_host_wait.)"""
     with tempfile.TemporaryDirectory() as d:
         w = os.path.join(d, "w.py")
         open(w, "w").write(DEAD_PEER_WORKER)
-        env = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_SIGNAL=mode, GLOO_AMD_INTERP=interp)
+        env = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_INTERP=interp)
         procs = [subprocess.Popen([sys.executable, w, str(r), "2", "file:" + os.path.join(d, "s")], env=env,
                                   stdout=subprocess.PIPE, text=True) for r in range(2)]
         outs = [p.communicate(timeout=120)[0] for p in procs]
     assert "RAISED" in outs[0], outs[0]
     assert "timed out" in outs[0].lower()
-    assert ("INTERP True" in outs[0]) == (mode == "device" and interp == "1"), outs[0]
+    assert ("INTERP True" in outs[0]) == (interp == "1"), outs[0]
+
+
+def test_dead_peer_times_out_host_wait(torch):
+    """The same with host waits (ranks as threads sharing the GPU): rank 1
+    builds the algorithm and never runs it; rank 0's run() raises after the
+    3 s timeout, and both close cleanly afterwards."""
+    import gloo_amd
+    url = "mem:" + uuid.uuid4().hex
+    n = 1 << 16
+    bufs = [torch.ones(n, device="cuda:0") for _ in range(2)]
+    torch.cuda.synchronize()
+    done = threading.Event()
+    got = {}
+
+    def body(r):
+        torch.cuda.set_device(0)
+        ctx = gloo_amd.Context(r, 2, url, device=0, timeout_ms=3000)
+        a = gloo_amd.Algorithm(ctx, "ring_chunked", "sum", "f32", [bufs[r].data_ptr()], n)
+        got[("mode", r)] = a.mode()
+        if r == 0:
+            try:
+                a.run()
+                got["run"] = "NO-ERROR"
+            except gloo_amd.GlooHipError as e:
+                got["run"] = str(e)
+            done.set()
+        else:
+            done.wait(60)
+        a.close()
+        ctx.close()
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert "timed out" in got.get("run", "").lower(), got
+    assert not got[("mode", 0)]["device_signal"] and not got[("mode", 0)]["interp"], got
 
 
 DEVICE_SIGNALLING_CASES = [
@@ -425,25 +446,20 @@ DEVICE_SIGNALLING_CASES = [
     ("ring_chunked/sum/f32/P8/k1/n10007", {}),
     ("reduce_scatter/max/bf16/P8/n4096", {}),
     ("reduce_scatter/sum/f32/P5/n100", {}),
+    ("reduce_scatter/sum/f32/P8/n10007", {}),
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0"}),
     ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0"}),
-    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0", "GLOO_AMD_COPY": "kernel"}),
-    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0", "GLOO_AMD_COPY": "kernel",
-                                               "GLOO_AMD_COPY_BLOCKS": "3"}),
-    ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_COPY": "kernel"}),
-    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_FUSE_BYTES": "0", "GLOO_AMD_COPY": "kernel"}),
+    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_FUSE_BYTES": "0"}),
     # the reference routes (GLOO_AMD_MESH=0) next to the derived mesh plans
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_MESH": "0"}),
     ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_MESH": "0"}),
     ("reduce_scatter/max/bf16/P8/n4096", {"GLOO_AMD_MESH": "0"}),
-    ("reduce_scatter/sum/f32/P5/n100", {"GLOO_AMD_MESH": "0", "GLOO_AMD_COPY": "kernel"}),
+    ("reduce_scatter/sum/f32/P5/n100", {"GLOO_AMD_MESH": "0"}),
     ("halving_doubling/sum/f64/P7/k1/n3001", {}),            # binary blocks: pairwise folds via temporaries
-    ("halving_doubling/min/f32/P5/k1/n1000", {"GLOO_AMD_COPY": "memcpy"}),
-    ("reduce_scatter/product/f16/P8/n4096", {"GLOO_AMD_COPY": "memcpy"}),
+    ("halving_doubling/min/f32/P5/k1/n1000", {}),
+    ("reduce_scatter/product/f16/P8/n4096", {}),
     ("reduce_scatter/sum/f16/P4/n1024", {}),
-    # run() synchronising the stream instead of spinning on the device-published done word
-    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_DONE_SPIN": "0"}),
-    ("reduce_scatter/sum/f16/P4/n1024", {"GLOO_AMD_DONE_SPIN": "0"}),
+    ("ring_chunked/sum/f64/P4/k1/n4099", {}),
 ]
 for _c, _e in DEVICE_SIGNALLING_CASES:
     sched_pool.register(_c, _e, 1)
@@ -511,33 +527,24 @@ GRAPH_REPLAY_CASES = [
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, True),  # fused small steps in the graph
     ("halving_doubling/sum/f32/P8/k1/n1000", {"GLOO_AMD_GRAPH": "1"}, True),
     ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_FUSE_BYTES": "0"}, True),   # auto: unfused steps
-    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0", "GLOO_AMD_COPY": "kernel"}, True),
-    ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_COPY": "kernel",
-                                          "GLOO_AMD_COPY_BLOCKS": "3"}, True),
+    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0"}, True),
     ("reduce_scatter/max/bf16/P8/n4096", {"GLOO_AMD_GRAPH": "1"}, True),
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "1024"}, True),  # mixed fused/unfused
     ("halving_doubling/sum/f32/P5/k1/n10007", {}, False),  # auto: every step fused -> eager is faster
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_FUSE_BYTES": "0"}, False),
-    ("ring_chunked/sum/f32/P3/k1/n1000", {"GLOO_AMD_SIGNAL": "host", "GLOO_AMD_GRAPH": "1"}, False),
     # ring-chunked runs as the mesh plan by default: batched sends (one
-    # multi-destination copy kernel, or forked hipMemcpyAsync streams),
-    # batched waits, one P-source fold
+    # multi-destination copy kernel), batched waits, one P-source fold
     ("ring_chunked/sum/f32/P8/k1/n10007", {}, False),
-    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_COPY": "memcpy"}, False),
     ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, True),
-    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_COPY": "memcpy"}, True),
-    ("ring_chunked/max/f32/P5/k1/n999", {"GLOO_AMD_SIGNAL": "host"}, False),
-    ("ring_chunked/product/f32/P3/k1/n777", {"GLOO_AMD_COPY_BLOCKS": "1", "GLOO_AMD_FUSE_BYTES": "0"}, True),
+    ("ring_chunked/product/f32/P3/k1/n777", {"GLOO_AMD_FUSE_BYTES": "0"}, True),
     ("ring_chunked/sum/f32/P2/k1/n1000", {}, False),
-    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_RING_MESH": "0", "GLOO_AMD_GRAPH": "1"}, True),
+    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_MESH": "0", "GLOO_AMD_GRAPH": "1"}, True),
     # derived mesh plans replayed: tree fold (P8), pairwise temporaries (P7),
     # reduce-scatter with previous-run credits
     ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, True),
     ("halving_doubling/sum/f64/P7/k1/n3001", {"GLOO_AMD_GRAPH": "1"}, True),
     ("halving_doubling/sum/f64/P7/k1/n3001", {}, False),
     ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_GRAPH": "1"}, True),
-    ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_COPY": "memcpy"}, True),
-    ("reduce_scatter/sum/f32/P5/n100", {"GLOO_AMD_SIGNAL": "host"}, False),
 ]
 # three runs: run 1 eager, run 2 captures, run 3 replays.  (Eight rank
 # processes time-slice the one GPU of the test box, and their device-side
@@ -572,13 +579,9 @@ FOLD_SEND_CASES = [(c, dict(e, GLOO_AMD_INTERP="0"), f) for c, e, f in [
     ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, True),          # reverse fold
     ("ring_chunked/product/f32/P3/k1/n777", {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_FUSE_BYTES": "0"}, True),
     ("ring_chunked/max/f32/P5/k1/n999", {"GLOO_AMD_GRAPH": "1"}, True),           # ragged: misaligned forwards
-    ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_FWD_RELEASE": "each"}, True),
-    # a lone result COPY out of the inbox on the copy kernel (GLOO_AMD_COPY_OUT_BYTES)
-    ("halving_doubling/sum/f32/P2/k1/n1000", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_FUSE_BYTES": "0",
-                                             "GLOO_AMD_COPY_OUT_BYTES": "0"}, True),
-    ("ring_chunked/sum/f32/P2/k1/n1000", {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_FUSE_BYTES": "0",
-                                         "GLOO_AMD_COPY_OUT_BYTES": "0", "GLOO_AMD_COPY_OUT_BLOCKS": "1"}, True),
-    ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_FOLD_SEND": "0"}, False),
+    # a lone result COPY out of the inbox on the copy kernel
+    ("halving_doubling/sum/f32/P2/k1/n1000", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_FUSE_BYTES": "0"}, True),
+    ("ring_chunked/sum/f32/P2/k1/n1000", {"GLOO_AMD_GRAPH": "0", "GLOO_AMD_FUSE_BYTES": "0"}, True),
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "1", "GLOO_AMD_MESH": "0"}, False),  # no FOLD
     # reduce-scatter owners: a fold and its credits (NOTIFY) in one launch
     ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_GRAPH": "1"}, True),
@@ -615,22 +618,16 @@ INTERP_CASES = [
     ("halving_doubling/sum/f32/P5/k1/n10007", {}, True),
     ("halving_doubling/sum/f32/P8/k1/n1000", {}, True),             # tree fold
     ("halving_doubling/sum/f64/P7/k1/n3001", {}, True),             # pairwise temporaries
-    ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_MAILBOX": "0"}, True),  # host-block flags
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_MESH": "0"}, True),     # the reference's step list
     ("ring_chunked/sum/f32/P8/k1/n10007", {}, True),
-    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_RING_MESH": "0"}, True),    # chunked ring: many hops
+    ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_MESH": "0"}, True),    # chunked ring: many hops
     ("ring_chunked/max/f32/P5/k1/n999", {}, True),
     ("ring_chunked/product/f32/P3/k1/n777", {}, True),
     ("reduce_scatter/max/bf16/P8/n4096", {}, True),
     ("reduce_scatter/sum/f32/P8/n10007", {}, True),                 # previous-run credits
-    ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_INTERP_BYTES": "1000000000"}, True),
-    # every step on its own (no batches: signal.h kInterpDefer)
-    ("halving_doubling/sum/f32/P8/k1/n1000", {"GLOO_AMD_INTERP_BATCH": "0"}, True),
-    ("reduce_scatter/sum/f32/P8/n10007", {"GLOO_AMD_INTERP_BATCH": "0"}, True),
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_INTERP": "0"}, False),
-    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_INTERP_BYTES": "1024"}, False),
+    ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "1024"}, False),  # messages over the limit
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_GRAPH": "1"}, False),
-    ("reduce_scatter/sum/f32/P5/n100", {"GLOO_AMD_SIGNAL": "host"}, False),
 ]
 for _c, _e, _i in INTERP_CASES:
     sched_pool.register(_c, _e, INTERP_RUNS)
@@ -650,35 +647,36 @@ def test_processes_interp(torch, golden_sched, case, env, interp):
         assert [m["interp"] for m in modes] == [interp] * runs, modes
 
 
-def _expected_slices(case, env):
+def _expected_slices(case, env, cus=256):
     """The slice count the executor must agree on (executor.cc): per rank
-    min(32, ceil(largest message / GLOO_AMD_INTERP_SLICE_BYTES)) if the
-    largest message is at most 32 x GLOO_AMD_INTERP_SLICE_MAX_BYTES (default
-    twice the slice bytes) and its plan is sliceable (plan_sim.sliceable, the
-    rule restated), the minimum over ranks, 1 if that is not above 1."""
+    min(cap, ceil(largest message / GLOO_AMD_INTERP_SLICE_BYTES)) if the
+    largest message is at most cap x twice the slice bytes and its plan is
+    sliceable (plan_sim.sliceable, the rule restated), the minimum over ranks,
+    1 if that is not above 1.  cap = min(32, CUs / the P ranks sharing the one
+    GPU) (executor_modes.cc coResidentSlices)."""
     from plan_sim import get_plan, sliceable
     algo, P = case.split("/")[0], int(case.split("/")[3][1:])
     n = int(case.split("/")[-1][1:])
     es = {"f16": 2, "bf16": 2, "f32": 4, "f64": 8}[case.split("/")[2]]
-    if env.get("GLOO_AMD_MAILBOX") == "0":
-        return 1  # slices need every channel's flags in device mailboxes
     mesh = env.get("GLOO_AMD_MESH", "1") != "0"
     route = algo
-    if mesh and algo == "ring_chunked" and env.get("GLOO_AMD_RING_MESH", "1") != "0":
+    if mesh and algo == "ring_chunked":
         route = "ring_chunked_mesh"
     elif mesh and algo in ("halving_doubling", "reduce_scatter"):
         route = "mesh_" + algo
+    elif algo == "ring_chunked":
+        route = "ring_chunked_pipe"
     recv = None
     if algo == "reduce_scatter":
         recv = np.array([n // P + (1 if r < n % P else 0) for r in range(P)], np.int32)
     sb = int(env.get("GLOO_AMD_INTERP_SLICE_BYTES", 32768))
-    cap = max(sb, int(env.get("GLOO_AMD_INTERP_SLICE_MAX_BYTES", 2 * sb)))
+    slice_cap = min(32, max(1, cus // P))
     props = []
     for r in range(P):
         steps, _ = get_plan(route, r, P, n, 1, recv, elem_size=es)
         biggest = max(s.length for s in steps) * es
-        ok = biggest <= 32 * cap and sliceable(route, P, n, r, recv=recv, elem_size=es)
-        props.append(min(32, max(1, -(-biggest // sb))) if ok else 0)
+        ok = biggest <= slice_cap * 2 * sb and sliceable(route, P, n, r, recv=recv, elem_size=es)
+        props.append(min(slice_cap, max(1, -(-biggest // sb))) if ok else 0)
     g = min(props)
     return g if g > 1 else 1
 
@@ -688,7 +686,6 @@ SLICED_CASES = [
     ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024"}),
     ("halving_doubling/sum/f64/P7/k1/n3001", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024"}),
     ("halving_doubling/sum/f32/P8/k1/n1000", {"GLOO_AMD_INTERP_SLICE_BYTES": "64"}),
-    ("halving_doubling/sum/f32/P8/k1/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024", "GLOO_AMD_MAILBOX": "0"}),
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024", "GLOO_AMD_MESH": "0"}),
     ("ring_chunked/sum/f32/P8/k1/n10007", {"GLOO_AMD_INTERP_SLICE_BYTES": "1024"}),
     ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_INTERP_SLICE_BYTES": "512"}),
@@ -707,7 +704,7 @@ def test_processes_sliced_interp(torch, golden_sched, case, env):
     workgroup g on slice g of every step with its own flag words.  The ranks
     must agree on the slice count the rule predicts (1 where a plan is
     refused), and three back-to-back runs must give the reference's bytes."""
-    want_slices = _expected_slices(case, env)
+    want_slices = _expected_slices(case, env, torch.cuda.get_device_properties(0).multi_processor_count)
     runs = INTERP_RUNS
     res = sched_pool.result(case, env, runs)
     check_pool_golden(golden_sched, case, res, runs)
@@ -738,12 +735,13 @@ np.save(out, np.array(res))
 '''
 
 
-@pytest.mark.parametrize("env", [{}, {"GLOO_AMD_INTERP_BYTES": str(1 << 24)}])
+@pytest.mark.parametrize("env", [{}, {"GLOO_AMD_INTERP": "0"}])
 def test_processes_new_style_rebinding_graph(torch, env):
-    """Function-style allreduce (1.6 MB per rank: unfused steps, so the plan
-    is captured) called with alternating buffer sets: every rebinding drops
-    the captured graph, the next steady call re-captures it.  With the
-    interpreter limit raised, every rebinding re-resolves its step list.
+    """Function-style allreduce (1.6 MB per rank) called with alternating
+    buffer sets.  By default the plan runs on the sliced interpreter and every
+    rebinding re-resolves its step list; with the interpreter off its steps
+    are unfused, so every rebinding drops the captured graph and the next
+    steady call re-captures it.
     Each call sums (rank + 1) * (it + 1) over the ranks exactly."""
     P = 4
     with tempfile.TemporaryDirectory() as d:
@@ -788,9 +786,9 @@ a.close(); ctx.close()
     ("ring_chunked/max/f32/P5/k1/n999", {}),
     ("halving_doubling/sum/f32/P5/k1/n10007", {}),
     ("halving_doubling/sum/f32/P5/k1/n10007", {"GLOO_AMD_FUSE_BYTES": "0"}),
-    ("reduce_scatter/max/bf16/P8/n4096", {"GLOO_AMD_COPY": "kernel"}),
+    ("reduce_scatter/max/bf16/P8/n4096", {}),
     ("ring_chunked/sum/f64/P4/k1/n4099", {"GLOO_AMD_FUSE_BYTES": "0", "GLOO_AMD_GRAPH": "1"}),
-    ("ring_chunked/sum/f32/P3/k1/n1000", {"GLOO_AMD_SIGNAL": "host"}),
+    ("ring_chunked/sum/f32/P3/k1/n1000", {"GLOO_AMD_MESH": "0"}),
 ])
 def test_processes_host_workspace(torch, golden_sched, case, env):
     """HOST workspace (the reference's CudaHostWorkspace placement): every
@@ -856,7 +854,7 @@ def test_device_stamps_keep_graph_replay(torch):
     with tempfile.TemporaryDirectory() as d:
         w = os.path.join(d, "w.py")
         open(w, "w").write(STAMP_WORKER)
-        # 8 MiB messages run eagerly by default (GLOO_AMD_GRAPH_BYTES): force replay
+        # 8 MiB messages run eagerly by default (graphBytes, 4 MiB): force replay
         e = dict(os.environ, GLOO_AMD_ROOT=ROOT, GLOO_AMD_GRAPH="1")
         procs = [subprocess.Popen([sys.executable, w, str(r), str(P), "file:" + os.path.join(d, "s")], env=e,
                                   stdout=subprocess.PIPE, text=True) for r in range(P)]
@@ -906,14 +904,14 @@ print("RESULT" + json.dumps(out), flush=True)
 
 @pytest.mark.parametrize("algo,env,graph", [
     ("halving_doubling", {}, False),                                    # 8 MiB messages: eager enqueue
-    ("halving_doubling", {"GLOO_AMD_GRAPH_BYTES": str(1 << 30)}, True),  # threshold raised: replay
+    ("halving_doubling", {"GLOO_AMD_GRAPH": "1"}, True),                # replay forced
     ("ring_chunked", {}, False),
     ("ring_chunked", {"GLOO_AMD_GRAPH": "1"}, True),
     ("halving_doubling", {"GLOO_AMD_MESH": "0"}, True),                 # reference route: replay
 ])
 def test_processes_launch_mode_policy(torch, algo, env, graph):
     """GLOO_AMD_GRAPH=auto replays plans, except mesh plans whose messages
-    reach GLOO_AMD_GRAPH_BYTES (4 MiB), which it enqueues eagerly (executor.cc
+    reach 4 MiB, which it enqueues eagerly (executor_modes.cc
     graphBytes); the mesh owners fold and forward in one launch either way.
     16 MiB per rank, 2 rank processes, four runs, exact closed form."""
     P, n = 2, 1 << 22
@@ -1019,8 +1017,7 @@ except gloo_amd.GlooHipError as e:
     print("RAISED", round(time.time() - t0, 2), str(e)[:400], flush=True)
 # the context still runs a consistent collective afterwards (the knobs
 # made equal: the library reads them at construction, putenv reaches it)
-for k in ("GLOO_AMD_MESH", "GLOO_AMD_RING_MESH", "GLOO_AMD_RING_PIPE"):
-    os.environ.pop(k, None)
+os.environ.pop("GLOO_AMD_MESH", None)
 x = np.full(1000, rank + 1, np.float32)
 hip_rt.h2d(buf, x)
 a = gloo_amd.Algorithm(ctx, "ring_chunked", "sum", "f32", [buf], 1000)
@@ -1033,8 +1030,7 @@ ctx.close()
 
 @pytest.mark.parametrize("algo,env1,n1,what", [
     ("halving_doubling", {"GLOO_AMD_MESH": "0"}, 100003, "GLOO_AMD_MESH"),
-    ("ring_chunked", {"GLOO_AMD_RING_MESH": "0"}, 100003, "GLOO_AMD_RING_MESH"),
-    ("ring_chunked", {"GLOO_AMD_MESH": "0", "GLOO_AMD_RING_PIPE": "0"}, 100003, "GLOO_AMD_RING_PIPE"),
+    ("ring_chunked", {"GLOO_AMD_MESH": "0"}, 100003, "GLOO_AMD_MESH"),
     ("halving_doubling", {}, 100000, "count"),
 ])
 def test_rank_inconsistent_plan_is_refused(torch, algo, env1, n1, what):

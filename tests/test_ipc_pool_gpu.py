@@ -28,7 +28,8 @@ import torch, gloo_amd
 rank, store = int(sys.argv[1]), sys.argv[2]
 torch.cuda.set_device(0)
 ctx = gloo_amd.Context(rank, 2, store, device=0, timeout_ms=60000)
-sizes = [1 << k for k in range(19, 29)] + [1 << 27, 1 << 21, 1 << 24, 3 << 22]
+sizes = json.loads(os.environ.get("GLOO_AMD_TEST_SIZES", "null")) or \
+    [1 << k for k in range(19, 29)] + [1 << 27, 1 << 21, 1 << 24, 3 << 22]
 out = []
 for n in sizes:
     i7 = torch.arange(n, device="cuda:0", dtype=torch.int64) * 7
@@ -89,6 +90,26 @@ def test_ipc_pool_reuses_size_classes():
         # ten arena classes (2 MiB .. 1 GiB, an arena of n fp32 rounds up to
         # at most 2 x 4 n B) and the mailboxes' class: below 2 x the sum
         assert up["slab_bytes"] <= 2 * sum(4 * s["n"] for s in steps[:10]) + (64 << 20), up
+
+
+@pytest.mark.timeout(200)
+def test_ipc_pool_best_fit_decreasing_sizes():
+    """a request of a class never used before is served from a
+    larger idle slab (best fit) instead of a new one.  Halving-doubling
+    executors of strictly decreasing size classes, each closed before the
+    next: the first creates the arena slab (and the mailbox's), no later one
+    creates any, and every run is exact."""
+    pytest.importorskip("torch")
+    sizes = [1 << 25, 3 << 22, 1 << 23, 1 << 22, 1 << 21, 1 << 20]
+    res = run_pair(WORKER, [], {"GLOO_AMD_TEST_SIZES": json.dumps(sizes)}, 180)
+    for r in res:
+        steps = r["steps"]
+        for s in steps:
+            assert s["ok"] == [True, True], s
+        first = steps[0]["stats"]
+        for s in steps[1:]:
+            assert s["stats"]["slabs"] == first["slabs"], (first, s)
+            assert s["stats"]["slab_bytes"] == first["slab_bytes"], (first, s)
 
 
 CHURN_WORKER = r'''

@@ -220,10 +220,10 @@ np.save(out + ".slices.npy", np.array(modes))
     ("bcube", 4, {}),                                   # 2 x 2: recursive halving shape (mesh: tree fold)
     ("bcube", 6, {}),                                   # 2 x 3 (mesh: pairwise folds)
     ("bcube", 4, {"GLOO_AMD_MESH": "0"}),               # the reference's exchange route
-    ("bcube", 3, {"GLOO_AMD_SIGNAL": "host"}),
+    ("bcube", 3, {"GLOO_AMD_MESH": "0", "GLOO_AMD_INTERP": "0"}),
     ("reduce", 4, {}),
     ("reduce", 5, {"GLOO_AMD_MESH": "0"}),
-    ("reduce", 3, {"GLOO_AMD_COPY": "kernel"}),
+    ("reduce", 3, {"GLOO_AMD_MESH": "0", "GLOO_AMD_GRAPH": "0"}),
     ("ring", 4, {}),                                    # new-style RING, mesh route
     ("ring", 3, {"GLOO_AMD_MESH": "0"}),
     # the sliced interpreter (executor.h), ragged slices, local steps split

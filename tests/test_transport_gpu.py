@@ -170,6 +170,43 @@ elif case == "ring_depth":
             sb.send(4 * i, 4, 4 * i)
         sb.wait_send()
         sb.close()
+elif case == "resend":
+    # ADVICE r5: a send buffer closed and created again on the same slot
+    # while the peer's receive buffer lives continues the channel's arrival
+    # numbering (device, host and notification buffers; three lifetimes)
+    # (lifetime k writes the receive buffers' k-th 16 bytes)
+    if rank == 1:
+        d = hip_rt.malloc(48)
+        hip_rt.memset(d, 0, 48)
+        h = np.zeros(12, np.uint32)
+        rd = t.buffer(0, 1, d, 48, False)
+        rh = t.buffer(0, 2, hp(h), h.nbytes, False)
+        rn = t.buffer(0, 3, 0, 0, False)
+        for life in range(3):
+            for _ in range(2):
+                rd.wait_recv()
+                rh.wait_recv()
+            rn.wait_recv()
+        dv = hip_rt.d2h(d, np.zeros(12, np.int32))
+        out["got"] = [[dv[4 * k:4 * k + 4].tolist(), h[4 * k:4 * k + 4].tolist()] for k in range(3)]
+        for b in (rd, rh, rn):
+            b.close()
+    else:
+        ds = hip_rt.malloc(16)
+        for life in range(3):
+            hip_rt.h2d(ds, np.arange(4, dtype=np.int32) + 10 * life)
+            hs = np.arange(4, dtype=np.uint32) + 100 * life
+            sd = t.buffer(1, 1, ds, 16, True)
+            sh = t.buffer(1, 2, hp(hs), hs.nbytes, True)
+            dummy = np.zeros(1, np.int32)
+            sn = t.buffer(1, 3, hp(dummy), 4, True)
+            for half in range(2):
+                sd.send(8 * half, 8, 16 * life + 8 * half)
+                sh.send(8 * half, 8, 16 * life + 8 * half)
+            sn.send(0, 0)
+            for b in (sd, sh, sn):
+                b.wait_send()
+                b.close()
 elif case == "big_alloc":
     # VERDICT r4 missing 1: a receive buffer in an allocation of 2 GiB or more
     # (the whole 2.5 GiB allocation here), written by a peer process: its
@@ -254,6 +291,13 @@ def test_transport_host_buffer_any_length_across_processes(tmp_path):
 def test_transport_sender_waits_beyond_record_ring(tmp_path):
     res = run_transport_case(tmp_path, "ring_depth")
     assert res[1]["host"] == list(range(1000, 1040)), res
+
+
+@pytest.mark.timeout(150)
+def test_transport_send_buffer_recreated_on_live_channel(tmp_path):
+    res = run_transport_case(tmp_path, "resend")
+    assert res[1]["got"] == [[[10 * k, 10 * k + 1, 10 * k + 2, 10 * k + 3],
+                              [100 * k, 100 * k + 1, 100 * k + 2, 100 * k + 3]] for k in range(3)], res
 
 
 @pytest.mark.timeout(150)

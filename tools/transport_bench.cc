@@ -149,7 +149,7 @@ int main(int argc, char** argv) {
       auto pct = [&](double p) { return s[std::min(s.size() - 1, (size_t)(p * (double)s.size()))]; };
       std::printf("{\"kind\": \"%s\", \"publish\": \"%s\", \"bytes\": %zu, \"samples\": %zu, \"min_us\": %.2f, "
                   "\"p50_us\": %.2f, \"p99_us\": %.2f, \"max_us\": %.2f, \"GiB_s\": %.3f, \"intact\": %s}\n",
-                  kind.c_str(), std::getenv("GLOO_AMD_TRANSPORT_HOSTFN") ? "host_function" : "device", bytes,
+                  kind.c_str(), "device", bytes,
                   s.size(), s.front() * 1e6, pct(0.5) * 1e6, pct(0.99) * 1e6, s.back() * 1e6,
                   (double)bytes * (double)s.size() / sum / (1024.0 * 1024 * 1024), intact ? "true" : "false");
       std::fflush(stdout);
