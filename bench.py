@@ -209,9 +209,9 @@ def host_staged(torch, hip, n, dev, iters=20):
     """Chunks starting and ending in pinned host memory (a transport recv
     buffer on a socket/NIC).  Four ways to reduce them on the GPU:
       serial     H2D dst + H2D src + kernel + D2H dst, one stream;
-      pipelined  gloo_hip_reduce_staged: the same in 4 / 8 / 16 MiB pieces over
-                 three streams, so H2D, kernel and D2H of different pieces
-                 overlap (both PCIe directions);
+      library_staged  gloo_hip_reduce_staged with a piece size: the same
+                 one pass on the caller's stream through device scratch (the
+                 pipelined pieces of rounds 2-5 lost to it and are gone);
       zero_copy_src  the accumulator stays in HBM and the kernel reads the
                  host chunk in place (the HOST-workspace allreduce's reduce);
       zero_copy_both the kernel reads both operands from host memory and
@@ -249,9 +249,9 @@ def host_staged(torch, hip, n, dev, iters=20):
         hip.reduce_ptr("sum", "f32", d_dst.data_ptr(), d_src.data_ptr(), n, s.cuda_stream)
         h_dst.copy_(d_dst, non_blocking=True)
 
-    def pipelined(piece):
-        # gloo_hip_reduce_staged: H2D of piece k+1, kernel of piece k and
-        # D2H of piece k-1 on separate streams (both PCIe directions busy)
+    def staged(piece):
+        # gloo_hip_reduce_staged: piece > 0 stages through the device
+        # scratch; piece 0 is zero-copy on mapped buffers
         return lambda: hip.reduce_staged("sum", "f32", h_dst.data_ptr(), h_src.data_ptr(), n, d_dst.data_ptr(),
                                          d_src.data_ptr(), piece, s.cuda_stream)
 
@@ -264,24 +264,20 @@ def host_staged(torch, hip, n, dev, iters=20):
         hip.reduce_ptr("sum", "f32", hd, hs, n, s.cuda_stream)
 
     out = {}
-    for name, fn in (("serial", serial), ("pipelined_4MiB", pipelined(1 << 20)),
-                     ("pipelined_8MiB", pipelined(1 << 21)), ("pipelined_16MiB", pipelined(1 << 22)),
-                     ("pipelined_32MiB", pipelined(1 << 23)),
+    for name, fn in (("serial", serial), ("library_staged", staged(n)),
                      ("zero_copy_src", zc_src), ("zero_copy_both", zc_both),
-                     ("library_default", pipelined(0))):
+                     ("library_default", staged(0))):
         dt = timed(fn)
         out[name] = {"gib_s_alg": round(3.0 * n * 4 / dt / GIB, 2), "ms_per_chunk": round(dt * 1e3, 3)}
-    best = min((k for k in out if k.startswith("pipelined")), key=lambda k: out[k]["ms_per_chunk"])
-    out["pipelined"] = dict(out[best], piece=best.split("_")[1])
-    # the product check: the pipelined staging gives the IEEE sums on the host
+    # the product check: the staged pass gives the IEEE sums on the host
     a0 = torch.empty(n, dtype=torch.float32).uniform_(-1, 1)
     h_dst.copy_(a0)
-    pipelined(1 << 21)()
+    staged(n)()
     torch.cuda.synchronize(dev)
-    out["pipelined_verified"] = bool(torch.equal(h_dst, a0 + h_src))
+    out["library_staged_verified"] = bool(torch.equal(h_dst, a0 + h_src))
     # gloo_hip_reduce_staged with piece 0: zero-copy on these mapped buffers
     h_dst.copy_(a0)
-    pipelined(0)()
+    staged(0)()
     torch.cuda.synchronize(dev)
     out["library_default_verified"] = bool(torch.equal(h_dst, a0 + h_src))
     # the product check: the zero-copy kernel reads host memory correctly

@@ -107,13 +107,13 @@ int gloo_hip_reduce_multi(int op, int dtype, void* dst,
 /* Host-staged chunk reduction: host_dst[i] = host_dst[i] (op) host_src[i]
  * for a chunk that starts and ends in (pinned) host memory — a transport's
  * receive buffer — computed by the HIP kernel through device scratch
- * dev_dst / dev_src (n elements each, caller-owned).  The chunk moves in
- * pieces of piece_elems: the host-to-device copies of piece k+1, the kernel
- * of piece k and the device-to-host copy of piece k-1 run at once on
- * separate streams (both PCIe directions busy).  piece_elems = 0: when both
- * host buffers are pinned AND mapped (hipHostGetDevicePointer succeeds), one
- * kernel reduces them in place over PCIe (zero-copy, the scratch is unused);
- * otherwise 16 MiB pieces.  Ordered after the
+ * dev_dst / dev_src (n elements each, caller-owned).  piece_elems = 0:
+ * when both host buffers are pinned AND mapped (hipHostGetDevicePointer
+ * succeeds), one kernel reduces them in place over PCIe (zero-copy, the
+ * scratch is unused, the fastest way measured); otherwise, and for any
+ * piece_elems > 0, the chunk is staged through the scratch in one pass on
+ * `stream` (H2D, kernel, D2H; a pipeline of pieces over several streams
+ * lost to it at every piece size and is gone).  Ordered after the
  * work already on `stream`; the host result is complete once `stream` has
  * drained.  The device side of the reference's CudaLocalHostReduce
  * (gloo/cuda_collectives_host.h:22-136), with the reduction on the GPU. */

@@ -1,7 +1,7 @@
 """GPU: host-staged chunk reduction (gloo_hip_reduce_staged) — a chunk in
-pinned host memory reduced by the HIP kernel through device scratch, copies
-and kernel pipelined in pieces — bit for bit against the oracle
-restatement of gloo/math.h."""
+pinned host memory reduced by the HIP kernel, zero-copy (piece 0) or staged
+through device scratch in one pass (any piece size) — bit for bit against the
+oracle restatement of gloo/math.h."""
 import numpy as np
 import pytest
 
