@@ -304,8 +304,8 @@ class Transport:
     """The xGMI transport's bound buffers (gloo::transport::Pair /
     Buffer, gloo/transport/pair.h:33-41, buffer.h:26-34) over a Context:
     construction is collective.  Receive buffers in device memory are written
-    in place by the peer (hipIpc across processes; an allocation of 2 GiB or
-    more through a VMM landing slab); host receive buffers across processes,
+    in place by the peer (across processes: the allocation shared as a dma-buf
+    and mapped by the sender, any size); host receive buffers across processes,
     of any length, through a landing segment in node shared memory, copied
     into the buffer at wait_recv."""
 

@@ -1,6 +1,7 @@
 // ipc.cc — see gloo_amd/ipc.h.
 #include "gloo_amd/ipc.h"
 
+#include <dlfcn.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <signal.h>
@@ -102,6 +103,11 @@ struct Pool {
     uint64_t devices;  // bit d: device d may access it
   };
   std::map<std::pair<int, uint64_t>, Mapping> imports;  // (exporter pid, slab id)
+  struct Exported {
+    int fd;
+    uint64_t bytes;  // of the whole dma-buf
+  };
+  std::map<uint64_t, Exported> exports;  // exportRange: id -> dma-buf
   size_t opens = 0, dropped = 0;
   static Pool& get() {
     static Pool* p = new Pool();  // never destroyed: releaseAllAtExit unmaps
@@ -149,6 +155,12 @@ void serveConnection(int c) {
         r.ok = 1;
         r.bytes = s->bytes;
       }
+    auto e = p.exports.find(id);
+    if (e != p.exports.end()) {
+      fd = e->second.fd;
+      r.ok = 1;
+      r.bytes = e->second.bytes;
+    }
   }
   iovec iov{&r, sizeof(r)};
   msghdr h;
@@ -254,6 +266,23 @@ struct DeviceScope {
   ~DeviceScope() { (void)hipSetDevice(prev); }
   int prev = 0;
 };
+
+// The imported handle of dma-buf `fd` (hipMemImportFromShareableHandle; the
+// fd by value on HIP 7.2, by address on 7.0: runtimeVersion()); the fd is
+// closed unless the runtime already did (only while it still
+// names this dma-buf).
+hipError_t importFd(int fd, hipMemGenericAllocationHandle_t* h) {
+  int fdv = fd;
+  void* osHandle = runtimeVersion() >= 70200000 ? reinterpret_cast<void*>(static_cast<intptr_t>(fd))
+                                                : static_cast<void*>(&fdv);
+  struct stat before;
+  const bool known = ::fstat(fd, &before) == 0;
+  const hipError_t e = hipMemImportFromShareableHandle(h, osHandle, hipMemHandleTypePosixFileDescriptor);
+  struct stat after;
+  if (known && ::fstat(fd, &after) == 0 && after.st_dev == before.st_dev && after.st_ino == before.st_ino)
+    ::close(fd);
+  return e;
+}
 
 // At process exit, before the HIP runtime tears down (atexit handlers run in
 // reverse order of registration, and this one is registered after the
@@ -442,22 +471,12 @@ void* import(const Remote& r, size_t bytes, int device) {
   hipMemGenericAllocationHandle_t h = nullptr;
   // HIP 7.2 takes the fd by value (as CUDA does); HIP 7.0.51831, the runtime
   // PyTorch 2.10+rocm7.0 bundles, takes its address and crashes on the value
-  // (tools/vmm_probe, profiles/round5/r5j_vmm_torch_*)
-  int fdv = fd;
-  void* osHandle = runtimeVersion() >= 70200000 ? reinterpret_cast<void*>(static_cast<intptr_t>(fd))
-                                                : static_cast<void*>(&fdv);
-  struct stat before;
-  const bool known = ::fstat(fd, &before) == 0;
-  const hipError_t e = hipMemImportFromShareableHandle(&h, osHandle, hipMemHandleTypePosixFileDescriptor);
-  // The import does not take the descriptor over (the dma-buf stays
-  // referenced by the mapping): close it unless the runtime already did.  A
-  // number the runtime closed may already name another thread's file (an fd
-  // server's accepted socket), so it is closed only while it still
-  // names this dma-buf.
-  struct stat after;
-  if (known && ::fstat(fd, &after) == 0 && after.st_dev == before.st_dev && after.st_ino == before.st_ino)
-    ::close(fd);
-  GLOO_AMD_HIP_ALLOC(e);
+  // (tools/vmm_probe, profiles/round5/r5j_vmm_torch_*).  The import does not
+  // take the descriptor over (the dma-buf stays referenced by the mapping):
+  // importFd closes it unless the runtime already did — and a number the
+  // runtime closed may already name another thread's file (an fd server's
+  // accepted socket), so only while it still names this dma-buf.
+  GLOO_AMD_HIP_ALLOC(importFd(fd, &h));
   void* va = nullptr;
   try {
     va = freshRange(slabBytes);
@@ -506,6 +525,79 @@ void grantAccess(void* mapped, int device) {
       }
       return;
     }
+}
+
+namespace {
+// hsa_amd_portable_export_dmabuf of the HSA runtime the HIP runtime loaded
+// (the system ROCm's, or the one PyTorch bundles): found by soname, never
+// loaded by us.
+using ExportDmabufFn = int (*)(const void*, size_t, int*, uint64_t*);
+ExportDmabufFn exportDmabuf() {
+  static const ExportDmabufFn f = [] {
+    void* h = dlopen("libhsa-runtime64.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("libhsa-runtime64.so", RTLD_NOW | RTLD_NOLOAD);
+    return h ? reinterpret_cast<ExportDmabufFn>(dlsym(h, "hsa_amd_portable_export_dmabuf")) : nullptr;
+  }();
+  return f;
+}
+
+}  // namespace
+
+bool exportRange(const void* ptr, size_t bytes, RangeExport* out) {
+  ExportDmabufFn f = exportDmabuf();
+  if (!f || !ptr || !bytes) return false;
+  int fd = -1;
+  uint64_t off = 0;
+  if (f(ptr, bytes, &fd, &off) != 0 || fd < 0) return false;
+  ensureServer();
+  registerAtExit();
+  const off_t end = ::lseek(fd, 0, SEEK_END);  // a dma-buf's size
+  Pool& p = Pool::get();
+  std::lock_guard<std::mutex> lk(p.m);
+  out->id = p.nextId++;
+  out->offset = off;
+  out->bytes = bytes;
+  p.exports[out->id] = {fd, end > 0 ? (uint64_t)end : off + bytes};
+  return true;
+}
+
+void unexportRange(const RangeExport& e) {
+  if (!e.id) return;
+  Pool& p = Pool::get();
+  std::lock_guard<std::mutex> lk(p.m);
+  auto it = p.exports.find(e.id);
+  if (it == p.exports.end()) return;
+  ::close(it->second.fd);  // the peers' mappings keep the memory referenced
+  p.exports.erase(it);
+}
+
+RangeImport importRange(const Remote& r, uint64_t offset, size_t bytes, int device) {
+  size_t bufBytes = 0;
+  const int fd = fetchFd(r.pid, r.incarnation, r.id, &bufBytes);
+  GLOO_AMD_ENFORCE(offset + bytes <= bufBytes, "exported range ", r.id, " of pid ", r.pid, ": [", offset, ", +",
+                   bytes, ") beyond its ", bufBytes, "-byte buffer");
+  DeviceScope ds(device);
+  RangeImport m;
+  GLOO_AMD_HIP_ALLOC(importFd(fd, &m.handle));
+  m.vaBytes = (offset + bytes + kGranule - 1) / kGranule * kGranule;
+  if (m.vaBytes > bufBytes) m.vaBytes = (offset + bytes + 4095) / 4096 * 4096;  // a small allocation's dma-buf
+  try {
+    m.va = freshRange(m.vaBytes);
+    mapAt(m.va, m.vaBytes, m.handle, device);
+  } catch (...) {
+    (void)hipMemRelease(m.handle);
+    throw;
+  }
+  m.ptr = static_cast<char*>(m.va) + offset;
+  return m;
+}
+
+void unimportRange(RangeImport* m) {
+  if (!m || !m->va) return;
+  GLOO_AMD_HIP_RELEASE(hipMemUnmap(m->va, m->vaBytes));
+  GLOO_AMD_HIP_RELEASE(hipMemRelease(m->handle));
+  // the range stays reserved: never mapped again (ipc.h)
+  *m = RangeImport();
 }
 
 Stats stats() {

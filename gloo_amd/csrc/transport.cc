@@ -31,29 +31,29 @@ struct RecvRecord {
   int32_t device;
   uint64_t ptr;     // the buffer itself (same process)
   uint64_t size;    // bytes the peer may write
-  uint64_t offset;  // from the start of its allocation (IPC maps whole allocations)
-  int32_t ipc;      // handle valid (device memory)
+  int32_t exported; // device memory shared as a dma-buf range (ipc.h exportRange): exportId / exportOffset
   int32_t host;     // host memory: written directly within one process, through `landing` across processes
   int32_t channel;  // this buffer's channel of the transport block
   int32_t pad;
-  uint64_t alloc;   // bytes of the device allocation an import would map
+  uint64_t exportId, exportOffset, incarnation;
   uint64_t baseline;  // the channel's arrival count when the buffer was created
-  hipIpcMemHandle_t handle;
   char landing[48];   // host memory: the landing segment a peer process writes messages into
-  int32_t deviceLanding;  // device memory in an allocation of 2 GiB or more: a landing slab (ipc.h) instead
+  int32_t deviceLanding;  // device memory the runtime could not export: a landing slab (ipc.h) instead
   int32_t pad2;
-  uint64_t landingSlab, landingIncarnation;
+  uint64_t landingSlab;
 };
 
-// A hipIpc import maps the exporter's whole allocation, and importing a
-// block of 2^31 bytes or more hangs in hipIpcOpenMemHandle on ROCm 7 /
-// MI355X (profiles/round3/r3t_*, r3u_*).  A device receive buffer inside
-// such an allocation therefore gets a LANDING slab of its own size from the
-// cross-process pool (VMM, any size: ipc.h): peer processes write their
-// messages there and waitRecv copies each message's range into the buffer.
-// (A caller's hipMalloc memory cannot be exported through VMM:
-// hipMemGetHandleForAddressRange refuses it, profiles/round5/r5b_vmm_*.)
-constexpr uint64_t kMaxImportBytes = uint64_t(1) << 31;
+// A device receive buffer reached by a peer process: its allocation is
+// exported as a dma-buf (ipc.h exportRange) and the sender maps the range
+// into a virtual range of its own (VMM import) and writes in place — the
+// reference's TCP pair writes any registered buffer the same way
+// (gloo/transport/tcp/pair.cc:413-426).  Rounds 1-5 used hipIpc handles
+// here, whose imports of 2 GiB or more hung in the runtime's open call
+// (profiles/round3/r3t_*, r3u_*) and whose handles named a freed block's
+// successor at the same address stale; a dma-buf names its block.  Should
+// the runtime refuse the export, the buffer gets a LANDING slab of its own
+// size from the cross-process pool instead (peer processes write their
+// messages there and waitRecv copies each message's range into the buffer).
 
 // Most workgroups one device-to-device message's copy kernel takes: a few
 // dozen saturate an xGMI link (a link, not HBM, bounds a peer copy), a copy
@@ -125,7 +125,7 @@ class SendBuffer : public Buffer {
     if (ticket_) GLOO_AMD_HIP_RELEASE(hipFree(ticket_));
     if (landingRegistered_) GLOO_AMD_HIP_RELEASE(hipHostUnregister(landing_));
     if (landing_) ::munmap(landing_, peerSize_);
-    if (opened_) GLOO_AMD_HIP_RELEASE(hipIpcCloseMemHandle(opened_));
+    ipc::unimportRange(&imported_);
     if (landingImport_) ipc::unimport(landingImport_);
     dev_->release(true, peer_, slot_);
   }
@@ -230,38 +230,29 @@ class SendBuffer : public Buffer {
         GLOO_AMD_HIP_ALLOC(hipHostRegister(landing_, r.size, hipHostRegisterPortable));
         landingRegistered_ = true;
       }
-    } else if (r.deviceLanding) {
-      // device memory of another process in a 2 GiB+ allocation: its landing slab
+    } else if (r.exported) {
+      // device memory of another process: its dma-buf range, mapped here
+      // once per send buffer (eager copies only, never captured into a
+      // graph), unmapped when the send buffer goes
       ipc::Remote rm;
       rm.pid = r.pid;
-      rm.incarnation = r.landingIncarnation;
+      rm.incarnation = r.incarnation;
+      rm.id = r.exportId;
+      imported_ = ipc::importRange(rm, r.exportOffset, r.size, ctx.device());
+      remote_ = imported_.ptr;
+      dstDevice_ = true;
+    } else {
+      // device memory the peer's runtime could not export: its landing slab
+      GLOO_AMD_ENFORCE(r.deviceLanding, "rank ", peer_, "'s receive buffer (slot ", slot_,
+                       ") is device memory with neither an export nor a landing slab");
+      ipc::Remote rm;
+      rm.pid = r.pid;
+      rm.incarnation = r.incarnation;
       rm.id = r.landingSlab;
       landingImport_ = static_cast<char*>(ipc::import(rm, r.size, ctx.device()));
       remote_ = landingImport_;
       viaLanding_ = true;
       dstDevice_ = true;
-    } else {
-      // (an allocation of 2 GiB or more always publishes a landing slab)
-      GLOO_AMD_ENFORCE(r.alloc < kMaxImportBytes, "rank ", peer_, "'s receive buffer (slot ", slot_,
-                       ") lies in a device allocation of ", r.alloc, " B but came without a landing slab");
-      GLOO_AMD_ENFORCE(r.ipc, "rank ", peer_, "'s receive buffer is not IPC-exportable");
-      // The caller's memory cannot come from the IPC slab pool (ipc.h);
-      // this import is used by eager copies only, never captured into a
-      // graph, so closing it releases it (profiles/round3/r3g_ipc_bisect_*).
-      void* base = nullptr;
-      GLOO_AMD_HIP_ALLOC(hipIpcOpenMemHandle(&base, r.handle, hipIpcMemLazyEnablePeerAccess));
-      opened_ = base;
-      remote_ = static_cast<char*>(base) + r.offset;
-      dstDevice_ = true;
-      void* rb = nullptr;
-      size_t rs = 0;
-      if (hipMemGetAddressRange(&rb, &rs, base) == hipSuccess && rb) {
-        GLOO_AMD_ENFORCE(static_cast<char*>(rb) + rs >= remote_ + r.size, "the IPC mapping of rank ", peer_,
-                         "'s receive buffer (slot ", slot_, ") reaches ", rs, " B from ", rb, ", short of its ",
-                         r.offset + r.size, " B");
-      } else {
-        (void)hipGetLastError();
-      }
     }
     if (srcDevice_ || dstDevice_) {
       channelDev_ = dev_->channelDevicePtr(ctx.rank, peer_, r.channel);
@@ -288,7 +279,7 @@ class SendBuffer : public Buffer {
   bool landingRegistered_ = false;
   char* landingImport_ = nullptr;   // a device buffer's landing slab (imported)
   bool viaLanding_ = false;         // messages go through a landing area, with records
-  void* opened_ = nullptr;
+  ipc::RangeImport imported_;       // a device buffer of another process, mapped here
   size_t peerSize_ = 0;
   int channelIdx_ = -1;
   Device::Channel* channel_ = nullptr;
@@ -324,21 +315,18 @@ class RecvBuffer : public Buffer {
     r.channel = idx_;
     r.baseline = baseline_;
     if (ptr_ && size_) {
+      r.incarnation = ipc::incarnation();
       if (isDevice(ptr_)) {
-        void* base = nullptr;
-        size_t allocSize = 0;
-        const bool ranged = hipMemGetAddressRange(&base, &allocSize, ptr_) == hipSuccess && base;
-        (void)hipGetLastError();
-        if (ranged && allocSize >= kMaxImportBytes) {
+        ipc::RangeExport ex;
+        if (ipc::exportRange(ptr_, size_, &ex)) {
+          export_ = ex;
+          r.exported = 1;
+          r.exportId = ex.id;
+          r.exportOffset = ex.offset;
+        } else {
           deviceLanding_ = ipc::acquire(ctx.device(), size_, true);
           r.deviceLanding = 1;
           r.landingSlab = deviceLanding_->id;
-          r.landingIncarnation = ipc::incarnation();
-          r.alloc = allocSize;
-        } else if (ranged && hipIpcGetMemHandle(&r.handle, base) == hipSuccess) {
-          r.ipc = 1;
-          r.offset = (uint64_t)(ptr_ - static_cast<char*>(base));
-          r.alloc = allocSize;
         }
       } else {
         r.host = 1;
@@ -355,6 +343,7 @@ class RecvBuffer : public Buffer {
     ctx.store().set(recordKey(dev_->instance(), peer_, ctx.rank, slot_), blob);
   }
   ~RecvBuffer() override {
+    ipc::unexportRange(export_);
     if (deviceLanding_) ipc::release(deviceLanding_);
     if (landing_) {
       ::munmap(landing_, size_);
@@ -412,7 +401,8 @@ class RecvBuffer : public Buffer {
   uint64_t baseline_ = 0, received_ = 0;
   std::string landingName_;
   char* landing_ = nullptr;
-  ipc::Slab* deviceLanding_ = nullptr;  // device memory in a 2 GiB+ allocation: where peer processes write
+  ipc::Slab* deviceLanding_ = nullptr;  // device memory the runtime could not export: where peer processes write
+  ipc::RangeExport export_;             // device memory: the dma-buf range peer processes map
 };
 
 }  // namespace

@@ -93,6 +93,33 @@ void unimport(void* mapped);
 // address is not the pool's).
 void grantAccess(void* mapped, int device);
 
+// A range of a caller's device allocation (hipMalloc memory, not a pool
+// slab) shared with peer processes: exported as a dma-buf of its allocation
+// through the HSA runtime the HIP runtime loaded
+// (hsa_amd_portable_export_dmabuf), served by this process's fd server under
+// an id, and imported by a peer with hipMemImportFromShareableHandle into a
+// virtual range never mapped before (tools/dmabuf_probe.cc,
+// profiles/round6/r6d/dmabuf_probe.jsonl: reads and writes both ways, and a
+// block freed and allocated again at the same address exports as the NEW
+// block).  This replaces the hipIpc handles of rounds 1-5.
+struct RangeExport {
+  uint64_t id = 0;      // names the export to peers (fd server)
+  uint64_t offset = 0;  // of the range within its dma-buf
+  uint64_t bytes = 0;
+};
+// false: the runtime cannot export this memory (the caller falls back).
+bool exportRange(const void* ptr, size_t bytes, RangeExport* out);
+void unexportRange(const RangeExport& e);
+struct RangeImport {
+  char* ptr = nullptr;  // the peer's range, mapped here
+  void* va = nullptr;   // the mapping (reserved for good: ipc.h "never mapped twice")
+  size_t vaBytes = 0;
+  hipMemGenericAllocationHandle_t handle = nullptr;
+};
+// Maps a peer's exported range (r.id = the export's id) for `device`.
+RangeImport importRange(const Remote& r, uint64_t offset, size_t bytes, int device);
+void unimportRange(RangeImport* m);
+
 struct Stats {
   size_t slabs = 0, slabBytes = 0, free = 0, imports = 0, opens = 0;
   size_t dropped = 0;  // mappings of exited processes (their pid reused) unmapped

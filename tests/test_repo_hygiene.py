@@ -38,3 +38,17 @@ def test_gpu_run_starts_with_hot_path_parity():
     for name in ("test_golden_reduce3", "test_golden_nan_payloads", "test_misaligned_offsets",
                  "test_beyond_4gi_elements"):
         assert any(name in i for i in ids[:k]), name
+
+
+def test_no_hipipc_in_the_product():
+    """cross-process device memory goes through dma-bufs (VMM
+    slabs, exported ranges of a caller's allocation), never hipIpc handles."""
+    hits = []
+    for base in ("gloo_amd/csrc", "gloo_amd/include", "include"):
+        for dirpath, _, files in os.walk(os.path.join(ROOT, base)):
+            for f in files:
+                text = open(os.path.join(dirpath, f), errors="replace").read()
+                for name in ("hipIpcGetMemHandle", "hipIpcOpenMemHandle", "hipIpcCloseMemHandle"):
+                    if name in text:
+                        hits.append((os.path.join(dirpath, f), name))
+    assert not hits, hits
