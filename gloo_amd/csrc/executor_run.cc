@@ -969,11 +969,39 @@ void PlanExecutor::enqueue(uint64_t r, bool graph) {
         foldSrcs.clear();
         break;
       }
-      case GLOO_HIP_STEP_LOCAL_BCAST:
+      case GLOO_HIP_STEP_LOCAL_BCAST: {
+        // Output 0 to every other output in ONE pass that reads it once: a
+        // one-source fold into output 1 that forwards each tile to outputs
+        // 2.. (launchFoldSend; no flags), or the local copy kernel for a
+        // single destination.  (k - 1 copies read it k - 1 times: HD with 4
+        // pointers of 64 MiB per rank spent 65 % of its time in the local
+        // passes, profiles/round6/r6f/multi_pointer_p2.jsonl.)  Outputs on
+        // other GPUs of the process keep the peer copies.
+        const size_t off = s.dst_off * es_, bytes = s.length * es_;
+        if (bytes == 0 || ptrs_.size() < 2) break;
+        if (!anyRemote_ && !custom_) {
+          const void* src0 = userPtr(0) + off;
+          for (size_t j0 = 1; j0 < ptrs_.size(); j0 += 1 + kMaxCopyEntries) {
+            const size_t j1 = std::min(ptrs_.size(), j0 + 1 + kMaxCopyEntries);
+            if (j1 - j0 == 1) {
+              const CopyDesc d{userPtr(j0) + off, src0, bytes, nullptr, Seq{}, nullptr,
+                               copySignalGrid(bytes, kCopyOutBlocks)};
+              checkRc(launchCopySignalMulti(&d, 1, epoch, stream_, kCopyStorePlain), "copy kernel (broadcast)");
+              continue;
+            }
+            FwdDesc fwd[kMaxCopyEntries];
+            int nf = 0;
+            for (size_t j = j0 + 1; j < j1; j++) fwd[nf++] = FwdDesc{userPtr(j) + off, nullptr, Seq{}};
+            checkRc(launchFoldSend(op_, dtype_, userPtr(j0) + off, &src0, 1, s.length, 0, fwd, nf, nullptr, epoch,
+                                   stream_),
+                    "broadcast (one-source fold + forwards)");
+          }
+          break;
+        }
         for (size_t j = 1; j < ptrs_.size(); j++)
-          GLOO_AMD_HIP_CHECK(hipMemcpyAsync(userPtr(j) + s.dst_off * es_, userPtr(0) + s.dst_off * es_,
-                                            s.length * es_, hipMemcpyDeviceToDevice, stream_));
+          GLOO_AMD_HIP_CHECK(hipMemcpyAsync(userPtr(j) + off, userPtr(0) + off, bytes, hipMemcpyDeviceToDevice, stream_));
         break;
+      }
       default:
         throw EnforceNotMet(strcat_("unknown plan step ", s.kind));
     }

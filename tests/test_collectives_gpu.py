@@ -1058,3 +1058,21 @@ def test_rank_inconsistent_plan_is_refused(torch, algo, env1, n1, what):
         assert all("called with another" in o for o in outs), outs
     else:
         assert any(what + "=0" in o for o in outs), outs
+
+
+@pytest.mark.parametrize("algo,P,k", [("halving_doubling", 2, 2), ("halving_doubling", 3, 4),
+                                      ("ring_chunked", 2, 11), ("local", 1, 11), ("halving_doubling", 2, 10)])
+def test_multi_pointer_broadcast_one_pass(torch, algo, P, k):
+    """The local broadcast of a multi-pointer collective (output 0 to outputs
+    1..k-1) runs as one pass that reads output 0 once: a one-source fold into
+    output 1 forwarding to the others, in groups of 1 + kMaxCopyEntries, and
+    the copy kernel for a lone destination (k = 2, and the 11th pointer).
+    Every pointer of every rank holds the sum over all ranks and pointers
+    (exact small integers), for a ragged element count."""
+    n = 100_003
+    x = np.array([[np.full(n, 1 + r * k + j, np.float32) for j in range(k)] for r in range(P)])
+    y = run_threads(torch, algo, "sum", "f32", x, runs=1)
+    want = float(sum(1 + r * k + j for r in range(P) for j in range(k)))
+    for r in range(P):
+        for j in range(k):
+            assert (y[r, j] == want).all(), (r, j, y[r, j][:4])
