@@ -161,6 +161,10 @@ void serveConnection(int c) {
       r.ok = 1;
       r.bytes = e->second.bytes;
     }
+    // a duplicate taken under the lock: an export may be closed
+    // (unexportRange) while the reply is on its way
+    if (fd >= 0) fd = ::fcntl(fd, F_DUPFD_CLOEXEC, 0);
+    if (fd < 0) r.ok = 0;
   }
   iovec iov{&r, sizeof(r)};
   msghdr h;
@@ -178,6 +182,7 @@ void serveConnection(int c) {
     std::memcpy(CMSG_DATA(cm), &fd, sizeof(fd));
   }
   (void)::sendmsg(c, &h, MSG_NOSIGNAL);
+  if (fd >= 0) ::close(fd);
 }
 
 std::mutex& serverMutex() {
