@@ -207,6 +207,34 @@ elif case == "resend":
             for b in (sd, sh, sn):
                 b.wait_send()
                 b.close()
+elif case == "realloc":
+    # VERDICT r5 #4: a device receive buffer freed and allocated again (at the
+    # same address, as the allocator hands it back) between two buffer
+    # lifetimes on one slot: each lifetime's message lands in ITS block (a
+    # hipIpc handle of the same address and size named the old block)
+    n = 1 << 20
+    got, addrs = [], []
+    for life in range(3):
+        if rank == 1:
+            d = hip_rt.malloc(n)
+            addrs.append(d)
+            hip_rt.memset(d, 0, n)
+            rb = t.buffer(0, 10 + life, d, n, False)
+            rb.wait_recv()
+            got.append(int((hip_rt.d2h(d, np.zeros(n, np.uint8)) != (np.arange(n) * (life + 3)) % 251).sum()))
+            rb.close()
+            hip_rt.free(d)
+        else:
+            s = hip_rt.malloc(n)
+            hip_rt.h2d(s, ((np.arange(n) * (life + 3)) % 251).astype(np.uint8))
+            sb = t.buffer(1, 10 + life, s, n, True)
+            sb.send(0, n, 0)
+            sb.wait_send()
+            sb.close()
+            hip_rt.free(s)
+    if rank == 1:
+        out["bad"] = got
+        out["same_address"] = len(set(addrs)) < len(addrs)
 elif case == "big_alloc":
     # VERDICT r4 missing 1: a receive buffer in an allocation of 2 GiB or more
     # (the whole 2.5 GiB allocation here), written by a peer process: its
@@ -298,6 +326,12 @@ def test_transport_send_buffer_recreated_on_live_channel(tmp_path):
     res = run_transport_case(tmp_path, "resend")
     assert res[1]["got"] == [[[10 * k, 10 * k + 1, 10 * k + 2, 10 * k + 3],
                               [100 * k, 100 * k + 1, 100 * k + 2, 100 * k + 3]] for k in range(3)], res
+
+
+@pytest.mark.timeout(150)
+def test_transport_device_buffer_reallocated_at_same_address(tmp_path):
+    res = run_transport_case(tmp_path, "realloc")
+    assert res[1]["bad"] == [0, 0, 0], res
 
 
 @pytest.mark.timeout(150)
