@@ -572,7 +572,7 @@ __device__ __forceinline__ void fold_tile(const SrcList& srcs, int k, size_t hea
 
 template <class Tr, int OP, int UNROLL, int BLOCK, int MODE>
 __global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
-    typename Tr::Storage* dst, SrcList srcs, int k, size_t n, size_t head, uint64_t* stamp) {
+    typename Tr::Storage* dst, SrcList srcs, int k, size_t n, size_t head, uint64_t* stamp, int plain) {
   using S = typename Tr::Storage;
   constexpr int kV = 16 / sizeof(S);
   constexpr uint32_t kTileBytes = (uint32_t)BLOCK * UNROLL * 16;
@@ -594,8 +594,13 @@ __global__ __launch_bounds__(BLOCK) void reduce_multi_vec_kernel(
   u32x4 acc[UNROLL];
   fold_tile<Tr, OP, UNROLL, BLOCK, MODE>(srcs, k, head, base, bytes, acc);
   const auto rd = make_rsrc(reinterpret_cast<const char*>(dst + head) + base, bytes);
+  if (plain) {  // the executor's folds: the result's next reader is a send or the caller (setReducePlainStores)
 #pragma unroll
-  for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rd, lane_off + u * BLOCK * 16, acc[u]);
+    for (int u = 0; u < UNROLL; u++) bstore<0>(rd, lane_off + u * BLOCK * 16, acc[u]);
+  } else {
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) bstore<kAuxNT>(rd, lane_off + u * BLOCK * 16, acc[u]);
+  }
   stamp_end(stamp);
 }
 
@@ -1232,7 +1237,7 @@ int launch_multi(void* dst, const void* const* srcs, int k, size_t n, hipStream_
   size_t grid = ceil_div(nvec, (size_t)kVecBlock * kMultiUnroll);
   if (grid == 0) grid = 1;
   reduce_multi_vec_kernel<Tr, OP, kMultiUnroll, kVecBlock, MODE><<<dim3((unsigned)grid), dim3(kVecBlock), 0, s>>>(
-      static_cast<S*>(dst), list, k, n, head, t_stamp);
+      static_cast<S*>(dst), list, k, n, head, t_stamp, t_plainStores ? 1 : 0);
   return check_launch("reduce_multi_vec_kernel");
 }
 

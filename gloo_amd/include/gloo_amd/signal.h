@@ -171,9 +171,10 @@ inline bool stampSpan(const uint64_t* slot, uint64_t* ticks) {
 }
 uint64_t* setLaunchStamp(uint64_t* slot);
 // The stores of the element-wise reduce kernels launched on this thread
-// (gloo_hip_reduce / reduce3): `nt` (default, the chunk-reduce of the
-// headline bench streams past the Infinity Cache) or plain (a plan's REDUCE
-// into a buffer that is re-read soon).  Returns the previous setting.
+// (gloo_hip_reduce / reduce3) and multi-source folds (gloo_hip_reduce_multi,
+// launchFold): `nt` (default, the chunk-reduce of the headline bench streams
+// past the Infinity Cache) or plain (a plan's REDUCE, FOLD or local fold into a
+// buffer that is re-read soon).  Returns the previous setting.
 bool setReducePlainStores(bool plain);
 int launchStampInit(uint64_t* stamps, int k, hipStream_t stream);
 
