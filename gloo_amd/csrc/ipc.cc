@@ -305,6 +305,8 @@ void releaseAllAtExit() {
     (void)hipMemRelease(s->handle);
     if (s->fd >= 0) ::close(s->fd);
   }
+  for (auto& kv : p.exports) ::close(kv.second.fd);
+  p.exports.clear();
 }
 void registerAtExit() {
   static std::once_flag once;
@@ -579,8 +581,11 @@ void unexportRange(const RangeExport& e) {
 RangeImport importRange(const Remote& r, uint64_t offset, size_t bytes, int device) {
   size_t bufBytes = 0;
   const int fd = fetchFd(r.pid, r.incarnation, r.id, &bufBytes);
-  GLOO_AMD_ENFORCE(offset + bytes <= bufBytes, "exported range ", r.id, " of pid ", r.pid, ": [", offset, ", +",
-                   bytes, ") beyond its ", bufBytes, "-byte buffer");
+  if (offset + bytes > bufBytes) {
+    ::close(fd);
+    GLOO_AMD_ENFORCE(false, "exported range ", r.id, " of pid ", r.pid, ": [", offset, ", +", bytes, ") beyond its ",
+                     bufBytes, "-byte buffer");
+  }
   DeviceScope ds(device);
   RangeImport m;
   GLOO_AMD_HIP_ALLOC(importFd(fd, &m.handle));
