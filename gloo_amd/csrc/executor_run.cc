@@ -130,7 +130,15 @@ void PlanExecutor::setStreams(const std::vector<hipStream_t>& streams) {
   hipStream_t next = streams.empty() ? nullptr : streams[0];
   for (hipStream_t t : streams) GLOO_AMD_ENFORCE(t != nullptr || streams.size() == 1, "null stream in the list");
   if (!next) {
-    if (!ownedStream_) GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&ownedStream_, hipStreamNonBlocking));
+    if (!ownedStream_) {
+      // on the rank's device, whatever device the calling thread has current
+      int prev = -1;
+      GLOO_AMD_HIP_CHECK(hipGetDevice(&prev));
+      if (prev != ctx_->device()) GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
+      const hipError_t e = hipStreamCreateWithFlags(&ownedStream_, hipStreamNonBlocking);
+      if (prev != ctx_->device()) (void)hipSetDevice(prev);
+      GLOO_AMD_HIP_CHECK(e);
+    }
     next = ownedStream_;
   }
   if (next != stream_) {
