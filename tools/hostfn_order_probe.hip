@@ -9,7 +9,11 @@
 // out; a host function queued behind it on the same stream sets a flag; the
 // host thread, on the flag, overwrites x from another stream and waits for
 // that copy.  If the kernel read the NEW value the host function ran before
-// the kernel was done.  One JSON line per spin length.
+// the kernel was done.  One JSON line per spin length.  Last line: does
+// hipStreamSynchronize (and an event recorded behind the host function) return
+// only after a slow host function has returned?  (Executor release and
+// context close rely on it: a credit's host function writes the context's
+// control block.)
 //   hostfn_order_probe [trials] [spin_us...]
 #include <hip/hip_runtime.h>
 
@@ -36,6 +40,10 @@ __global__ void spin_then_read(const uint32_t* x, uint32_t* out, uint64_t ticks)
 }
 
 static void setFlag(void* p) { static_cast<std::atomic<int>*>(p)->store(1, std::memory_order_release); }
+static void slowSetFlag(void* p) {
+  std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  setFlag(p);
+}
 
 int main(int argc, char** argv) {
   const int trials = argc > 1 ? std::atoi(argv[1]) : 500;
@@ -77,5 +85,24 @@ int main(int argc, char** argv) {
                 "\"mean_wait_for_host_function_us\": %.1f}\n", spin, trials, early, waitUs / trials);
     std::fflush(stdout);
   }
+  int syncEarly = 0, eventEarly = 0;
+  const int slowTrials = 20;
+  for (int t = 0; t < slowTrials; t++) {
+    std::atomic<int> f1{0}, f2{0};
+    spin_then_read<<<1, 64, 0, R>>>(x, out, 200);
+    CHECK(hipLaunchHostFunc(R, slowSetFlag, &f1));
+    CHECK(hipStreamSynchronize(R));
+    if (!f1.load(std::memory_order_acquire)) syncEarly++;
+    hipEvent_t ev;
+    CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    CHECK(hipLaunchHostFunc(R, slowSetFlag, &f2));
+    CHECK(hipEventRecord(ev, R));
+    CHECK(hipEventSynchronize(ev));
+    if (!f2.load(std::memory_order_acquire)) eventEarly++;
+    CHECK(hipStreamSynchronize(R));
+    CHECK(hipEventDestroy(ev));
+  }
+  std::printf("{\"slow_host_function_ms\": 20, \"trials\": %d, \"stream_sync_returned_before_it\": %d, "
+              "\"event_sync_returned_before_it\": %d}\n", slowTrials, syncEarly, eventEarly);
   return 0;
 }
