@@ -21,6 +21,7 @@ Also reported (rank 0, N=1 only): the reference's own gloo::sum<float>
 pinned host memory (H2D + kernel + D2H).
 """
 import argparse
+import contextlib
 import ctypes
 import json
 import os
@@ -184,6 +185,21 @@ def cpu_baseline(args, n):
     return out
 
 
+@contextlib.contextmanager
+def stdout_fd_to_stderr():
+    """The reference's TCP context prints its connectivity line with std::cout
+    (gloo/transport/tcp/context.cc:243-246); send fd 1 to stderr meanwhile so
+    stdout carries only the bench's JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def config1(oracle, args, n=1 << 24):
     """BASELINE config 1: the reference's AllreduceRingChunked<float>, size=2,
     2 ranks (threads) over TCP loopback, n = 16 Mi fp32; 5 warmup runs, then
@@ -195,7 +211,8 @@ def config1(oracle, args, n=1 << 24):
     buf = (ctypes.c_double * cap)()
     cnt = ctypes.c_int(0)
     t0 = time.perf_counter()
-    rc = oracle.ref().ref_allreduce_samples(0, 2, n, 5, args.config1_seconds, buf, cap, ctypes.byref(cnt))
+    with stdout_fd_to_stderr():
+        rc = oracle.ref().ref_allreduce_samples(0, 2, n, 5, args.config1_seconds, buf, cap, ctypes.byref(cnt))
     if rc:
         return {"error": oracle.ref().ref_last_error().decode()}
     s = np.sort(np.array(buf[:cnt.value]))

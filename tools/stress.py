@@ -24,6 +24,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 WORKER = r'''
 import json, os, sys, time
+
+
+def emit(o):
+    # one write per line: the ranks share the parent's stdout, and print()'s
+    # separate newline write let two ranks' lines run together
+    os.write(1, (json.dumps(o) + "\n").encode())
+
+
 import numpy as np
 sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
 import torch, gloo_amd
@@ -111,7 +119,7 @@ while True:
     torch.cuda.synchronize()
     if not bool((buf[:lim] == want).all()):
         bad = int((buf[:lim] != want).sum())
-        print(json.dumps({"rank": rank, "error": "wrong result", "case": key, "bad": bad, "runs": runs}), flush=True)
+        emit({"rank": rank, "error": "wrong result", "case": key, "bad": bad, "runs": runs})
         sys.exit(2)
     runs += 1
     m = a.mode()
@@ -131,8 +139,8 @@ for a, *_ in built:
         a.close()
 stopper.close()
 ctx.close()
-print(json.dumps({"rank": rank, "runs": runs, "seconds": round(time.time() - t0, 1), "cases": len(built),
-                  "modes": modes}), flush=True)
+emit({"rank": rank, "runs": runs, "seconds": round(time.time() - t0, 1), "cases": len(built),
+                  "modes": modes})
 '''
 
 
