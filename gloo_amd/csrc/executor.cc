@@ -669,13 +669,14 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   //  - two processes: after an executor of the same size had run, the
   //    importer read the previous contents through its mapping even after a
   //    device synchronise (bench.py config-3 variants back to back);
-  //  - twelve ranks as threads (BCUBE, GPUTEST_r05): rank 8's phase-1 fold
-  //    of the SECOND run read arena element 5 as it stood at the end of the
-  //    first run (rank 10's phase-2 message, which shares that offset) and
-  //    not rank 9's new phase-1 message that the host counter had already
-  //    announced — a stale line, not a protocol gap: the model of exactly
-  //    that read reproduces the wrong value bit for bit
-  //    (tests/test_newstyle_plan.py::test_bcube_p12_stale_inbox_read_explains_r05).
+  //  - twelve ranks as threads (BCUBE, GPUTEST_r05, seen once): the wrong
+  //    value is exactly what rank 8's phase-1 fold of the SECOND run gives if
+  //    it read arena element 5 as it stood at the end of the first run (rank
+  //    10's phase-2 message, which shares that offset) instead of rank 9's
+  //    new phase-1 message the host counter had announced
+  //    (tests/test_newstyle_plan.py::test_bcube_p12_stale_inbox_read_explains_r05);
+  //    the protocol orders that read, and isolated probes of the cache and
+  //    host-function paths did not reproduce it.
   // A plan reuses arena offsets for different messages of one run, so a
   // line cached by one step's read is wrong for a later step's.
   GLOO_AMD_ENFORCE(workspace == GLOO_HIP_WORKSPACE_DEVICE || workspace == GLOO_HIP_WORKSPACE_HOST,

@@ -117,12 +117,13 @@ def test_bcube_threads_golden(torch, golden_new, case, mesh, monkeypatch):
 @pytest.mark.parametrize("algo,P,mesh", [("bcube", 12, "0"), ("bcube", 4, "1"), ("ring", 3, "0")])
 def test_threads_inboxes_fine_grained(torch, algo, P, mesh, monkeypatch):
     """GPUTEST_r05 (test_newstyle_plan.py::test_bcube_p12_stale_inbox_read_explains_r05):
-    with ranks as threads on ONE GPU the inbox arena was coarse-grained, and a
-    second run's fold read a line cached by the first run's read of a
-    different message at the same offset.  The mechanism, checked directly:
-    every executor whose inboxes another rank writes reports a fine-grained
-    arena, on the same-GPU thread route too; the results are exact over
-    repeated calls with the buffers rebound each time."""
+    with ranks as threads on ONE GPU the inbox arena was coarse-grained, and
+    the wrong value is what a second-run fold gives if it reads the first
+    run's message at a shared offset (a stale line is the one cache path; it
+    was not reproduced in isolation).  The fix, checked
+    directly: every executor whose inboxes another rank writes reports a
+    fine-grained arena, on the same-GPU thread route too; the results are
+    exact over repeated calls with the buffers rebound each time."""
     import gloo_amd
     monkeypatch.setenv("GLOO_AMD_MESH", mesh)
     n = 4099

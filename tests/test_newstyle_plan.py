@@ -141,16 +141,19 @@ def test_bcube_repeated_runs(P, n):
 
 def test_bcube_p12_stale_inbox_read_explains_r05():
     """GPUTEST_r05's one red case (BCUBE P=12, ranks as threads on one GPU,
-    coarse-grained inboxes): every rank's element 0 came back -1.9609444
-    instead of -3.8116968 in the second call, elements 1-9 right.  The plan
-    is exact (test_bcube_repeated_runs above).  The model of ONE stale read
-    reproduces the wrong value bit for bit: rank 8's phase-1 fold (step 13,
-    its inbox [5, 10) from rank 9) reads the inbox as it stood at the end of
-    the first run, when offset 5 held rank 10's phase-2 message (rank 8's
-    region for rank 10 is [3, 6)).  Offsets 6-9 still held rank 9's equal
-    first-run data, so only element 0 is wrong.  The fix (executor.cc:
-    inboxes that any peer writes are fine-grained) removes the stale line;
-    the GPU side is test_newstyle_gpu.py::test_threads_inboxes_fine_grained."""
+    coarse-grained inboxes): rank 3's element 0 (the first wrong result the
+    test met) came back -1.9609444 instead of -3.8116968 in the second call,
+    elements 1-9 right.  The plan is exact (test_bcube_repeated_runs above).
+    The model of ONE stale read reproduces the wrong value bit for bit: rank
+    8's phase-1 fold (step 13, its inbox [5, 10) from rank 9) reads the inbox
+    as it stood at the end of the first run, when offset 5 held rank 10's
+    phase-2 message (rank 8's region for rank 10 is [3, 6)).  Offsets 6-9
+    still held rank 9's equal first-run data, so only element 0 is wrong.
+    (With equal inputs in both calls, rank 10's SECOND-run message landing
+    early gives the same value; the hardware path was not reproduced in
+    isolation)  Inboxes that any peer writes are now
+    fine-grained (executor.cc), which closes the cache-line path; the GPU
+    side is test_newstyle_gpu.py::test_threads_inboxes_fine_grained."""
     z = np.load(os.path.join(ROOT, "tests", "golden", "newstyle_golden.npz"))
     case = "bcube/sum/f32/P12/i0/o1/n10/s0"
     init, want = z[case + "/init"], z[case + "/out"]
