@@ -76,3 +76,24 @@ def test_link_figures_structure_without_a_second_gpu(bench):
     assert set(link["figures"]) == set(bench.LINK_FIGURES)
     assert all(f["GBps"] is None and "no xGMI link" in f["why"] for f in link["figures"].values())
     assert link["mesh_bound_figure"] in link["figures"] and link["ring_bound_figure"] in link["figures"]
+
+
+def test_config1_keeps_the_references_stdout_chatter_off_stdout(bench):
+    """The reference's TCP context prints "[Gloo] Rank … connected" with
+    std::cout (gloo/transport/tcp/context.cc:243-246); in round 6 those lines
+    preceded the bench's JSON line on stdout.  config1 now sends fd 1 to
+    stderr for the call: a child running it prints only its own line."""
+    import subprocess
+    import sys
+    sys.path.insert(0, ROOT)
+    import oracle
+    if not oracle.ref_available():
+        pytest.skip("oracle/_ref not built")
+    code = ("import sys, types, json; sys.path.insert(0, %r); import bench, oracle; "
+            "r = bench.config1(oracle, types.SimpleNamespace(config1_seconds=0.05), n=1 << 12); "
+            "print(json.dumps(r))" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.startswith('{"elements": 4096'), r.stdout
+    assert len(r.stdout.splitlines()) == 1, r.stdout
+    assert "[Gloo] Rank" in r.stderr
