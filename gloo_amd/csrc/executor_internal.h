@@ -22,7 +22,7 @@ void checkRc(int rc, const char* what);
 // (GLOO_AMD_FUSE_BYTES).
 size_t fuseBytes();
 // Largest message below which GLOO_AMD_GRAPH=auto replays a mesh plan as a
-// hipGraph (GLOO_AMD_GRAPH_BYTES).
+// hipGraph (4 MiB, fixed since round 6).
 size_t graphBytes();
 // Largest message of a plan the one-launch interpreter runs (0: never).
 size_t interpBytes();

@@ -22,7 +22,7 @@
 // constructed from the program's existing std::shared_ptr<gloo::Context>,
 // device pointers, `int count` and (optionally) one hipStream_t per pointer,
 // exactly like the CUDA classes.  There is no second rendezvous: the
-// library's own context (inbox arenas, IPC handles, signal mailboxes) is
+// library's own context (inbox arenas, their dma-buf references, signal mailboxes) is
 // bootstrapped by gloo_hip_context_create_ex with gloo::allgather over the
 // gloo::Context's pairs (gloo/allgather.h) as its only exchange.  Like the
 // reference's algorithms, construction and destruction are collective:

@@ -1,7 +1,7 @@
 // store.h — rendezvous key/value stores (mirrors gloo::rendezvous::Store,
 // gloo/rendezvous/store.h, FileStore gloo/rendezvous/file_store.h:19 and
 // HashStore gloo/rendezvous/hash_store.h:20).  Used only at setup: to publish
-// each rank's inbox arena (IPC handle) and the control block's name.
+// each rank's inbox arena (its pool slab: pid, incarnation, slab id) and the control block's name.
 #pragma once
 
 #include <chrono>

@@ -181,8 +181,8 @@ typedef enum {
    * goes straight from every rank to the rank where the ring finishes it,
    * over all xGMI links at once, and is folded there in the ring's exact
    * association and operand order (bit-identical), then sent to every rank.
-   * 2 <= size <= GLOO_HIP_MAX_SRCS.  RING_CHUNKED executes as this plan when
-   * GLOO_AMD_RING_MESH selects it. */
+   * 2 <= size <= GLOO_HIP_MAX_SRCS.  RING_CHUNKED executes as this plan in
+   * that range unless GLOO_AMD_MESH=0. */
   GLOO_HIP_ALGO_RING_CHUNKED_MESH = 6,
   GLOO_HIP_ALGO_ALLREDUCE_BCUBE = 7,  /* new-style gloo::allreduce(opts), BCUBE
                                          (gloo/allreduce.cc:397-669)          */
@@ -192,8 +192,9 @@ typedef enum {
   /* AllreduceRingChunked's own ring route (its hops, association and bytes)
    * with three inboxes per channel, so that each round's reduce and the send
    * of its result run as one pass (plan.cc planRingChunkedPipe).  RING_CHUNKED
-   * executes as this plan where it keeps the ring route (no mesh) unless
-   * GLOO_AMD_RING_PIPE=0. */
+   * executes as this plan wherever it keeps the ring route (GLOO_AMD_MESH=0
+   * or size > GLOO_HIP_MAX_SRCS) with a built-in op; a custom op keeps the
+   * literal ring order. */
   GLOO_HIP_ALGO_RING_CHUNKED_PIPE = 9,
 } gloo_hip_algo_t;
 
