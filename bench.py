@@ -187,9 +187,11 @@ def cpu_baseline(args, n):
 
 @contextlib.contextmanager
 def stdout_fd_to_stderr():
-    """The reference's TCP context prints its connectivity line with std::cout
-    (gloo/transport/tcp/context.cc:243-246); send fd 1 to stderr meanwhile so
-    stdout carries only the bench's JSON line."""
+    """Gloo's TCP context prints its connectivity line with std::cout
+    (gloo/transport/tcp/context.cc:243-246; the reference built here for
+    config 1, and PyTorch's bundled copy behind init_process_group("gloo"));
+    send fd 1 to stderr meanwhile so stdout carries only the bench's JSON
+    line."""
     sys.stdout.flush()
     saved = os.dup(1)
     os.dup2(2, 1)
@@ -1062,7 +1064,10 @@ def main():
     import gloo_amd as hip
 
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # (PyTorch's bundled Gloo prints its "[Gloo] Rank … connected" lines
+        # with std::cout too: stdout carries only the JSON line)
+        with stdout_fd_to_stderr():
+            dist.init_process_group("gloo", rank=rank, world_size=world)
     # one GPU per rank; ranks wrap around the visible GPUs (rehearsals of the
     # multi-rank path on a 1-GPU box put every rank on cuda:0)
     dev = torch.device(f"cuda:{local_rank % max(1, torch.cuda.device_count())}")
