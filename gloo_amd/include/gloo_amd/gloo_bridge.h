@@ -291,8 +291,9 @@ class HipAllreduceHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_HAL
   // pipelineBroadcastAndReduce (gloo/cuda_allreduce_halving_doubling.h:29)
   // overlaps the reference's per-chunk local reduce / broadcast with the
   // exchange; here a rank's pointers are folded in one fused pass before the
-  // exchange, so the flag changes no byte and is accepted for source
-  // compatibility.
+  // exchange and broadcast in one pass after it, so the flag changes no
+  // result and is accepted for source compatibility (DESIGN.md §8 round 6,
+  // "Multi-pointer local passes").
   HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, const int count,
                               const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
                               bool /*pipelineBroadcastAndReduce*/ = false,

@@ -154,8 +154,9 @@ class HipAllreduceHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_HAL
   // pipelineBroadcastAndReduce overlaps the reference's per-chunk local
   // reduce / broadcast LocalOps with the exchange; here the local fold of a
   // rank's pointers is one fused pass before the exchange and the broadcast
-  // one copy after it, so the flag changes no byte and no step and is accepted
-  // for source compatibility.
+  // one pass after it (output 0 read once), so the flag changes no result
+  // and is accepted for source compatibility (what the overlap could hide:
+  // DESIGN.md §8 round 6, "Multi-pointer local passes").
   HipAllreduceHalvingDoubling(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
                               const std::vector<hipStream_t>& streams, bool /*pipelineBroadcastAndReduce*/)
       : HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING, W>(context, ptrs, count, {}, streams,
