@@ -226,11 +226,15 @@ def config1(oracle, args, n=1 << 24):
 
 def host_staged(torch, hip, n, dev, iters=20):
     """Chunks starting and ending in pinned host memory (a transport recv
-    buffer on a socket/NIC).  Four ways to reduce them on the GPU:
+    buffer on a socket/NIC).  Ways to reduce them on the GPU:
       serial     H2D dst + H2D src + kernel + D2H dst, one stream;
-      library_staged  gloo_hip_reduce_staged with a piece size: the same
-                 one pass on the caller's stream through device scratch (the
-                 pipelined pieces of rounds 2-5 lost to it and are gone);
+      library_staged  gloo_hip_reduce_staged staging through device scratch
+                 in its default 16 MiB pieces (a requested piece below
+                 16 MiB is raised to it): H2D of piece k+1, the kernel of
+                 piece k and D2H of piece k-1 overlap;
+      library_staged_32MiB  the same in 32 MiB pieces;
+      library_one_pass  the same with one piece (the chunk): serial through
+                 the library;
       zero_copy_src  the accumulator stays in HBM and the kernel reads the
                  host chunk in place (the HOST-workspace allreduce's reduce);
       zero_copy_both the kernel reads both operands from host memory and
@@ -283,17 +287,23 @@ def host_staged(torch, hip, n, dev, iters=20):
         hip.reduce_ptr("sum", "f32", hd, hs, n, s.cuda_stream)
 
     out = {}
-    for name, fn in (("serial", serial), ("library_staged", staged(n)),
+    for name, fn in (("serial", serial), ("library_staged", staged(1)),
+                     ("library_staged_32MiB", staged((32 << 20) // 4)), ("library_one_pass", staged(n)),
                      ("zero_copy_src", zc_src), ("zero_copy_both", zc_both),
                      ("library_default", staged(0))):
         dt = timed(fn)
         out[name] = {"gib_s_alg": round(3.0 * n * 4 / dt / GIB, 2), "ms_per_chunk": round(dt * 1e3, 3)}
-    # the product check: the staged pass gives the IEEE sums on the host
+    # the product check: the staged pieces and the one pass give the IEEE
+    # sums on the host
     a0 = torch.empty(n, dtype=torch.float32).uniform_(-1, 1)
+    h_dst.copy_(a0)
+    staged(1)()
+    torch.cuda.synchronize(dev)
+    out["library_staged_verified"] = bool(torch.equal(h_dst, a0 + h_src))
     h_dst.copy_(a0)
     staged(n)()
     torch.cuda.synchronize(dev)
-    out["library_staged_verified"] = bool(torch.equal(h_dst, a0 + h_src))
+    out["library_one_pass_verified"] = bool(torch.equal(h_dst, a0 + h_src))
     # gloo_hip_reduce_staged with piece 0: zero-copy on these mapped buffers
     h_dst.copy_(a0)
     staged(0)()

@@ -132,8 +132,8 @@ def reduce_multi_ptr(op, dtype, dst, srcs, n, stream=0):
 def reduce_staged(op, dtype, host_dst, host_src, n, dev_dst, dev_src, piece_elems=0, stream=0):
     """Host-staged chunk reduction (gloo_hip_reduce_staged): host_dst op=
     host_src, zero-copy over PCIe when both host buffers are pinned and
-    mapped and piece_elems is 0, else staged through the device scratch in
-    one pass on `stream` (H2D, kernel, D2H)."""
+    mapped and piece_elems is 0, else staged through the device scratch,
+    pipelined in pieces of at least 16 MiB (one pass for a smaller chunk)."""
     _check(lib.gloo_hip_reduce_staged(_as_op(op), _as_dtype(dtype), host_dst, host_src, n, dev_dst, dev_src,
                                       piece_elems, stream or None))
 

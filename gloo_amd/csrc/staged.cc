@@ -11,19 +11,62 @@
 // measured (74.2 GiB/s algorithmic on a 64 MiB fp32 chunk, BENCH_r05
 // host_staged).
 //
-// Otherwise the chunk is staged through the caller's device scratch in one
-// pass on the caller's stream: H2D dst, H2D src, the kernel, D2H dst (51.6
-// GiB/s).  Rounds 2-5 pipelined that pass in pieces over three streams so
-// that copies of different pieces overlapped; on MI355X the pipeline lost to
-// the one pass at every piece size from 4 to 32 MiB (35.4-38.1 against 51.6
-// GiB/s, BENCH_r05), so it is gone and piece_elems only chooses staging over
-// zero-copy.
+// Otherwise the chunk is staged through the caller's device scratch in
+// pieces of at least 16 MiB:
+//
+//   piece k:  H2D dst_k, H2D src_k  (copy-in stream)
+//             kernel dst_k op= src_k (the caller's stream)
+//             D2H dst_k              (copy-out stream)
+//
+// so the copy-in of piece k+1, the kernel of piece k and the copy-out of
+// piece k-1 overlap (PCIe is full duplex).  On one MI355X (BENCH_r05, 64 MiB
+// fp32): 16 MiB pieces 62.5 GiB/s and 32 MiB 58.9 against 51.6 for one
+// unpipelined pass, but 4 and 8 MiB pieces 35.4 and 38.1 (their per-piece
+// event and copy overheads outweigh the overlap).  So a piece size below
+// 16 MiB is raised to 16 MiB, and a chunk of at most one piece is staged in
+// one pass on the caller's stream.  Streams and events are per thread and
+// device, created once.
 #include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <map>
+#include <vector>
 
 #include "gloo_amd.h"
 #include "gloo_amd/common.h"
 #include "gloo_amd/errors.h"
 #include "gloo_amd/signal.h"
+
+namespace gloo_amd {
+namespace {
+
+struct StagingStreams {
+  hipStream_t in = nullptr, out = nullptr;
+  std::vector<hipEvent_t> inDone, redDone, outDone;
+  hipEvent_t event(std::vector<hipEvent_t>& v, size_t k) {
+    while (v.size() <= k) {
+      hipEvent_t e;
+      GLOO_AMD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      v.push_back(e);
+    }
+    return v[k];
+  }
+};
+
+StagingStreams& streamsFor(int device) {
+  thread_local std::map<int, StagingStreams> m;
+  StagingStreams& s = m[device];
+  if (!s.in) {
+    GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&s.in, hipStreamNonBlocking));
+    GLOO_AMD_HIP_CHECK(hipStreamCreateWithFlags(&s.out, hipStreamNonBlocking));
+  }
+  return s;
+}
+
+constexpr size_t kMinPieceBytes = size_t(16) << 20;
+
+}  // namespace
+}  // namespace gloo_amd
 
 extern "C" int gloo_hip_reduce_staged(int op, int dtype, void* host_dst, const void* host_src, size_t n,
                                       void* dev_dst, void* dev_src, size_t piece_elems,
@@ -47,12 +90,49 @@ extern "C" int gloo_hip_reduce_staged(int op, int dtype, void* host_dst, const v
       (void)hipGetLastError();  // a buffer that is not mapped is not an error here
       if (mapped) return gloo_hip_reduce(op, dtype, mdst, msrc, n, s);
     }
-    const size_t bytes = n * es;
-    GLOO_AMD_HIP_CHECK(hipMemcpyAsync(dev_dst, host_dst, bytes, hipMemcpyHostToDevice, s));
-    GLOO_AMD_HIP_CHECK(hipMemcpyAsync(dev_src, host_src, bytes, hipMemcpyHostToDevice, s));
-    const int rc = gloo_hip_reduce(op, dtype, dev_dst, dev_src, n, s);
-    if (rc != GLOO_HIP_OK) return rc;
-    GLOO_AMD_HIP_CHECK(hipMemcpyAsync(host_dst, dev_dst, bytes, hipMemcpyDeviceToHost, s));
+    const size_t minPiece = std::max<size_t>(1, kMinPieceBytes / es);
+    const size_t piece = std::max(piece_elems, minPiece);
+    char* hd = static_cast<char*>(host_dst);
+    const char* hs = static_cast<const char*>(host_src);
+    char* dd = static_cast<char*>(dev_dst);
+    char* ds = static_cast<char*>(dev_src);
+    if (n <= piece) {  // one pass on the caller's stream
+      const size_t bytes = n * es;
+      GLOO_AMD_HIP_CHECK(hipMemcpyAsync(dd, hd, bytes, hipMemcpyHostToDevice, s));
+      GLOO_AMD_HIP_CHECK(hipMemcpyAsync(ds, hs, bytes, hipMemcpyHostToDevice, s));
+      const int rc = gloo_hip_reduce(op, dtype, dd, ds, n, s);
+      if (rc != GLOO_HIP_OK) return rc;
+      GLOO_AMD_HIP_CHECK(hipMemcpyAsync(hd, dd, bytes, hipMemcpyDeviceToHost, s));
+      return GLOO_HIP_OK;
+    }
+    int device = 0;
+    GLOO_AMD_HIP_CHECK(hipGetDevice(&device));
+    StagingStreams& st = streamsFor(device);
+    // the copy-in may not overwrite device scratch an earlier call on `s`
+    // still uses, nor start before work the caller queued on `s`
+    hipEvent_t start = st.event(st.outDone, 0);
+    GLOO_AMD_HIP_CHECK(hipEventRecord(start, s));
+    GLOO_AMD_HIP_CHECK(hipStreamWaitEvent(st.in, start, 0));
+    size_t k = 0;
+    for (size_t off = 0; off < n; off += piece, k++) {
+      const size_t len = std::min(piece, n - off);
+      const size_t b = off * es, bytes = len * es;
+      GLOO_AMD_HIP_CHECK(hipMemcpyAsync(dd + b, hd + b, bytes, hipMemcpyHostToDevice, st.in));
+      GLOO_AMD_HIP_CHECK(hipMemcpyAsync(ds + b, hs + b, bytes, hipMemcpyHostToDevice, st.in));
+      hipEvent_t in = st.event(st.inDone, k);
+      GLOO_AMD_HIP_CHECK(hipEventRecord(in, st.in));
+      GLOO_AMD_HIP_CHECK(hipStreamWaitEvent(s, in, 0));
+      const int rc = gloo_hip_reduce(op, dtype, dd + b, ds + b, len, s);
+      if (rc != GLOO_HIP_OK) return rc;
+      hipEvent_t red = st.event(st.redDone, k);
+      GLOO_AMD_HIP_CHECK(hipEventRecord(red, s));
+      GLOO_AMD_HIP_CHECK(hipStreamWaitEvent(st.out, red, 0));
+      GLOO_AMD_HIP_CHECK(hipMemcpyAsync(hd + b, dd + b, bytes, hipMemcpyDeviceToHost, st.out));
+    }
+    // the caller's stream covers the whole chunk, copy-out included
+    hipEvent_t done = st.event(st.outDone, 1);
+    GLOO_AMD_HIP_CHECK(hipEventRecord(done, st.out));
+    GLOO_AMD_HIP_CHECK(hipStreamWaitEvent(s, done, 0));
     return GLOO_HIP_OK;
   } catch (const std::exception& e) {
     return setError(GLOO_HIP_EINVAL_ARG, e.what());

@@ -111,11 +111,12 @@ int gloo_hip_reduce_multi(int op, int dtype, void* dst,
  * when both host buffers are pinned AND mapped (hipHostGetDevicePointer
  * succeeds), one kernel reduces them in place over PCIe (zero-copy, the
  * scratch is unused, the fastest way measured); otherwise, and for any
- * piece_elems > 0, the chunk is staged through the scratch in one pass on
- * `stream` (H2D, kernel, D2H; a pipeline of pieces over several streams
- * lost to it at every piece size and is gone).  Ordered after the
- * work already on `stream`; the host result is complete once `stream` has
- * drained.  The device side of the reference's CudaLocalHostReduce
+ * piece_elems > 0, the chunk is staged through the scratch in pieces of
+ * max(piece_elems, 16 MiB) elements' bytes: H2D of piece k+1, the kernel of
+ * piece k and D2H of piece k-1 overlap on per-thread copy streams (smaller
+ * pieces measured slower than one pass); a chunk of at most one piece goes
+ * H2D, kernel, D2H in one pass on `stream`.  Ordered after the work already
+ * on `stream`; the host result is complete once `stream` has drained.  The device side of the reference's CudaLocalHostReduce
  * (gloo/cuda_collectives_host.h:22-136), with the reduction on the GPU. */
 int gloo_hip_reduce_staged(int op, int dtype, void* host_dst, const void* host_src, size_t n,
                            void* dev_dst, void* dev_src, size_t piece_elems, gloo_hip_stream_t stream);

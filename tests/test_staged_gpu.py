@@ -1,7 +1,8 @@
 """GPU: host-staged chunk reduction (gloo_hip_reduce_staged) — a chunk in
 pinned host memory reduced by the HIP kernel, zero-copy (piece 0) or staged
-through device scratch in one pass (any piece size) — bit for bit against the
-oracle restatement of gloo/math.h."""
+through device scratch — in one pass when the chunk fits one piece, else
+pipelined in pieces of at least 16 MiB (smaller requested pieces are raised
+to 16 MiB) — bit for bit against the oracle restatement of gloo/math.h."""
 import numpy as np
 import pytest
 
@@ -20,8 +21,11 @@ def torch():
 
 @pytest.mark.parametrize("dtype,op,n,piece", [
     ("f32", "sum", 1 << 20, 0),            # default: zero-copy (torch pins mapped memory)
-    ("f32", "sum", 1_000_003, 65_537),     # ragged pieces
+    ("f32", "sum", 1_000_003, 65_537),     # below 16 MiB: one staged pass
     ("f32", "max", 4099, 1 << 20),         # one piece
+    ("f32", "sum", 9_000_017, 1),          # raised to 16 MiB pieces: 16 + 16 + 2.3 MB, pipelined
+    ("bf16", "max", 20_000_003, 12_000_000),  # 24 MB pieces: 24 + 16 MB
+    ("i64", "product", 5_000_001, 3_000_000),  # 24 MB pieces: 24 + 16 MB
     ("bf16", "product", 300_007, 50_000),
     ("f16", "min", 123_457, 10_000),
     ("i64", "sum", 77_777, 4096),
