@@ -237,7 +237,7 @@ ReductionFunction.min = ReductionFunction(ReductionType.MIN)
 # ---- contexts and algorithms (GPU allreduce / reduce-scatter drop-ins) -----
 
 ALGORITHMS = {"ring_chunked": 0, "halving_doubling": 1, "ring": 2, "local": 3,
-              "reduce_scatter": 4}
+              "reduce_scatter": 4, "bcube": 10}  # bcube: AllreduceBcube, recv_elems = [base]
 
 
 def _bind_collectives(L):
@@ -405,14 +405,17 @@ class Algorithm:
     inboxes, the CudaHostWorkspace placement; gloo/cuda_workspace.h:20-31)."""
 
     def __init__(self, ctx, algo, op, dtype, ptrs, count, recv_elems=None, stream=0, workspace="device",
-                 streams=None):
+                 streams=None, base=None):
         """stream: one stream for the plan (0: the algorithm's own stream,
         and run() returns with outputs complete).  streams: one stream handle per
         pointer instead (the reference's `streams` argument,
         gloo/cuda_allreduce_ring_chunked.cc:55-67): run() orders pointer i
         after the work queued on streams[i], and every streams[i] after the
-        collective."""
+        collective.  base: AllreduceBcube's group size (gloo::Context::base,
+        gloo/context.h:28-33), the same as recv_elems=[base]."""
         self.ctx = ctx
+        if base is not None:
+            recv_elems = [int(base)]
         arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
         rp = None
         if recv_elems is not None:

@@ -128,6 +128,7 @@ int gloo_hip_algorithm_create_ws(gloo_hip_context_t ctx, int algo, int op, int d
       GLOO_AMD_ENFORCE(recv_elems, "reduce-scatter needs recv_elems");
       re.assign(recv_elems, recv_elems + ctx->ctx->size);
     }
+    if (algo == GLOO_HIP_ALGO_BCUBE && recv_elems) re.assign(recv_elems, recv_elems + 1);  // {base}
     auto a = std::make_unique<gloo_hip_algorithm>();
     a->exec = gloo_amd::PlanExecutor::create(ctx->ctx, algo, op, dtype,
                                                        std::vector<void*>(ptrs, ptrs + nptrs), count, re,
@@ -151,6 +152,7 @@ int gloo_hip_algorithm_create_streams(gloo_hip_context_t ctx, int algo, int op, 
       GLOO_AMD_ENFORCE(recv_elems, "reduce-scatter needs recv_elems");
       re.assign(recv_elems, recv_elems + ctx->ctx->size);
     }
+    if (algo == GLOO_HIP_ALGO_BCUBE && recv_elems) re.assign(recv_elems, recv_elems + 1);  // {base}
     std::vector<hipStream_t> ss;
     for (int i = 0; i < nstreams; i++) ss.push_back(static_cast<hipStream_t>(streams[i]));
     // Validated before the collective construction: a refusal after it would

@@ -16,6 +16,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <limits>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -553,6 +554,133 @@ Plan planLocal(int, int, uint64_t count, int nptrs) {
 }
 
 // ---------------------------------------------------------------------------
+// AllreduceBcube (gloo/allreduce_bcube.h:265-699), GPU twin CudaAllreduceBcube
+// (gloo/cuda_allreduce_bcube.cc:49-215).  Ranks form groups of `base` whose
+// members are `base^step` apart; each step reduce-scatters the group's range
+// among its members, the all-gather walks the steps back.  The geometry is
+// the reference's Node / Group bookkeeping restated (its int arithmetic, the
+// count-0 -> 1 rule and the wrap `ptrOffset %= count`), so small or uneven
+// counts take the reference's ranges too.  The reference tests P = base^k
+// only (gloo/test/allreduce_test.cc:271-299).
+// ---------------------------------------------------------------------------
+struct BcubeNode {
+  std::vector<std::vector<int>> peers;  // per step, self excluded
+  std::vector<int> numElems, ptrOffset;
+};
+
+// computeSteps (gloo/allreduce_bcube.h:528-532): float logarithms, as there.
+int bcubeSteps(int nodes, int base) {
+  const float lg2n = std::log2(nodes);
+  const float lg2p = std::log2(base);
+  return (int)std::ceil(lg2n / lg2p);
+}
+
+// setupNodes / updateGroupNodes / Group (gloo/allreduce_bcube.h:163-250,
+// 646-699).
+std::vector<BcubeNode> bcubeNodes(int nodes, int base, int count, int steps) {
+  std::vector<BcubeNode> all(nodes);
+  for (auto& n : all) {
+    n.peers.resize(steps);
+    n.numElems.assign(steps, 0);
+    n.ptrOffset.assign(steps, 0);
+  }
+  int peerDistance = 1;
+  for (int step = 0; step < steps; ++step) {
+    for (int rank = 0; rank < nodes; ++rank) {
+      const BcubeNode& first = all[rank];
+      if (!first.peers[step].empty()) continue;  // only nodes without peers start a group
+      std::vector<int> group;
+      for (int i = 0; i < base; ++i)
+        if (rank + i * peerDistance < nodes) group.push_back(rank + i * peerDistance);
+      int ptrOffset = step == 0 ? 0 : first.ptrOffset[step - 1];
+      const int groupCount = step == 0 ? count : first.numElems[step - 1];
+      const int numElems = std::max(groupCount, (int)group.size());
+      const int sz = (int)group.size();
+      int each = numElems / sz;
+      const int rem = numElems % sz;
+      if (each == 0) each = 1;
+      for (int i = 0; i < sz; ++i) {
+        BcubeNode& node = all[group[i]];
+        for (int peer : group)
+          if (peer != group[i]) node.peers[step].push_back(peer);
+        const int n = i != sz - 1 ? each : each + rem;
+        node.numElems[step] = n;
+        node.ptrOffset[step] = ptrOffset;
+        ptrOffset += n;
+        ptrOffset %= count;
+      }
+    }
+    peerDistance *= base;
+  }
+  return all;
+}
+
+// Arena: one inbox per (step, peer), sized max(mine, the peer's) as the
+// reference's recvBufs_ (:300-308); a peer meets this rank in one step only.
+// Notifications: the reference's (one per reduce-scatter receive, one per
+// step-0 all-gather receive, waited for before each all-gather send and at the
+// end) plus one per all-gather receive of the later steps, waited for at the
+// end.  A plan runs repeatedly on asynchronous streams, and nothing else
+// orders a step-s peer's next-run reduce-scatter send (s > 0) after this
+// rank's copy out of the same inbox: the reference's final wait covers the
+// step-0 peers only.  Data and order are the reference's, so the results are
+// too.
+Plan planBcube(int rank, int size, uint64_t count64, int nptrs, int base) {
+  Plan p;
+  if (count64 == 0) return p;                                          // run() :348-351
+  if (count64 > (uint64_t)std::numeric_limits<int>::max())
+    throw std::invalid_argument("AllreduceBcube counts elements in int");
+  const int count = (int)count64;
+  if (base < 2) base = 2;  // CudaAllreduceBcube: `context->base ? context->base : 2`
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, 0, 0, 0, count64));  // :352-355
+  if (size == 1) {                                                      // :357-363
+    if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count64));
+    return p;
+  }
+  const int steps = bcubeSteps(size, base);
+  const std::vector<BcubeNode> all = bcubeNodes(size, base, count, steps);
+  const BcubeNode& me = all[rank];
+  std::vector<std::vector<uint64_t>> inbox(steps);                      // ctor :296-320
+  for (int step = 0; step < steps; ++step)
+    for (int peer : me.peers[step]) {
+      const uint64_t n = (uint64_t)std::max(me.numElems[step], all[peer].numElems[step]);
+      inbox[step].push_back(p.arena);
+      p.steps.push_back(mk(GLOO_HIP_STEP_DECL_RECV, peer, GLOO_HIP_SLOT_DATA0, 0, p.arena, 0, n));
+      p.arena += n;
+    }
+  for (int step = 0; step < steps; ++step) {                           // reduce-scatter :365-391
+    for (int dest : me.peers[step])
+      p.steps.push_back(mk(GLOO_HIP_STEP_SEND, dest, GLOO_HIP_SLOT_DATA0, 0, 0,
+                           (uint64_t)all[dest].ptrOffset[step], (uint64_t)all[dest].numElems[step]));
+    for (size_t j = 0; j < me.peers[step].size(); ++j) {
+      const int src = me.peers[step][j];
+      p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, src, GLOO_HIP_SLOT_DATA0));
+      p.steps.push_back(mk(GLOO_HIP_STEP_REDUCE, -1, 0, GLOO_HIP_SRC_ARENA, (uint64_t)me.ptrOffset[step],
+                           inbox[step][j], (uint64_t)me.numElems[step]));
+      p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, src, GLOO_HIP_SLOT_NOTIFY));  // :389
+    }
+  }
+  for (int step = steps - 1; step >= 0; --step) {                      // all-gather :395-429
+    for (int dest : me.peers[step]) {
+      p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, dest, GLOO_HIP_SLOT_NOTIFY));  // :404
+      p.steps.push_back(mk(GLOO_HIP_STEP_SEND, dest, GLOO_HIP_SLOT_DATA0, 0, 0, (uint64_t)me.ptrOffset[step],
+                           (uint64_t)me.numElems[step]));
+    }
+    for (size_t j = 0; j < me.peers[step].size(); ++j) {
+      const int src = me.peers[step][j];
+      p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_RECV, src, GLOO_HIP_SLOT_DATA0));
+      p.steps.push_back(mk(GLOO_HIP_STEP_COPY, -1, 0, GLOO_HIP_SRC_ARENA, (uint64_t)all[src].ptrOffset[step],
+                           inbox[step][j], (uint64_t)all[src].numElems[step]));
+      p.steps.push_back(mk(GLOO_HIP_STEP_NOTIFY, src, GLOO_HIP_SLOT_NOTIFY));  // :419-424 (step 0 there)
+    }
+  }
+  if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count64));  // :431-434
+  for (int step = 0; step < steps; ++step)                             // :441-443 (+ the later steps)
+    for (int peer : me.peers[step]) p.steps.push_back(mk(GLOO_HIP_STEP_WAIT_NOTIFY, peer, GLOO_HIP_SLOT_NOTIFY));
+  return p;
+}
+
+// ---------------------------------------------------------------------------
 // ReduceScatterHalvingDoubling (gloo/reduce_scatter.h:112-442).
 // Arena = [recvBuf_ (chunkSize << steps) | recvBufDist_ (count)].
 // ---------------------------------------------------------------------------
@@ -1080,6 +1208,7 @@ Plan makePlan(int algo, int rank, int size, uint64_t count, int nptrs, const std
     case GLOO_HIP_ALGO_HALVING_DOUBLING: return planHalvingDoubling(rank, size, count, nptrs);
     case GLOO_HIP_ALGO_RING: return planRing(rank, size, count, nptrs);
     case GLOO_HIP_ALGO_LOCAL: return planLocal(rank, size, count, nptrs);
+    case GLOO_HIP_ALGO_BCUBE: return planBcube(rank, size, count, nptrs, recvElems.empty() ? 2 : recvElems[0]);
     case GLOO_HIP_ALGO_REDUCE_SCATTER:
       if ((int)recvElems.size() != size) throw std::invalid_argument("recvElems must have size entries");
       return planReduceScatter(rank, size, count, nptrs, recvElems);
@@ -1104,6 +1233,7 @@ extern "C" int gloo_hip_plan_ex(int algo, int rank, int size, size_t count, int 
       if (!recv_elems) return GLOO_HIP_EINVAL_ARG;
       re.assign(recv_elems, recv_elems + size);
     }
+    if (algo == GLOO_HIP_ALGO_BCUBE && recv_elems) re.assign(recv_elems, recv_elems + 1);  // {base}
     gloo_amd::Plan p;
     if (gloo_amd::isNewStyle(algo)) {
       gloo_amd::NewStyleOptions o;

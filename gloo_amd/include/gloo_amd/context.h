@@ -37,6 +37,8 @@ class Context : public std::enable_shared_from_this<Context> {
 
   const int rank;
   const int size;
+  // AllreduceBcube's group size (gloo::Context::base, gloo/context.h:28-33)
+  int base = 2;
 
   int device() const { return device_; }
   std::chrono::milliseconds timeout() const { return timeout_; }

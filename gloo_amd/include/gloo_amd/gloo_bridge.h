@@ -301,6 +301,29 @@ class HipAllreduceHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_HAL
       : HipPlanAlgorithm<T, GLOO_HIP_ALGO_HALVING_DOUBLING, W>(context, ptrs, count, {}, streams, fn) {}
 };
 
+// gloo::CudaAllreduceHalvingDoublingPipelined
+// (gloo/cuda_allreduce_halving_doubling_pipelined.h:13-28).
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipAllreduceHalvingDoublingPipelined : public HipAllreduceHalvingDoubling<T, W> {
+ public:
+  HipAllreduceHalvingDoublingPipelined(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
+                                       const int count,
+                                       const std::vector<hipStream_t>& streams = std::vector<hipStream_t>())
+      : HipAllreduceHalvingDoubling<T, W>(context, ptrs, count, streams, true) {}
+};
+
+// gloo::CudaAllreduceBcube (gloo/cuda_allreduce_bcube.h:50-58): groups of the
+// program's context->base ranks (0 = 2, gloo/cuda_allreduce_bcube.cc:57).
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipAllreduceBcube : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_BCUBE, W> {
+ public:
+  HipAllreduceBcube(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, const int count,
+                    const std::vector<hipStream_t>& streams = std::vector<hipStream_t>(),
+                    const ReductionFunction<T>* fn = ReductionFunction<T>::sum)
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_BCUBE, W>(context, ptrs, count, {context->base ? context->base : 2},
+                                                    streams, fn) {}
+};
+
 template <typename T, typename W = HipDeviceWorkspace<T>>
 class HipAllreduceRing : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_RING, W> {
  public:

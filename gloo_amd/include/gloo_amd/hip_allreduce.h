@@ -191,6 +191,29 @@ class HipReduceScatterHalvingDoubling : public HipPlanAlgorithm<T, GLOO_HIP_ALGO
       : HipPlanAlgorithm<T, GLOO_HIP_ALGO_REDUCE_SCATTER, W>(context, ptrs, count, recvElems, streams, fn) {}
 };
 
+// AllreduceBcube / CudaAllreduceBcube (gloo/allreduce_bcube.h:265-346,
+// gloo/cuda_allreduce_bcube.h:50-58): groups of context->base ranks (0 = 2,
+// gloo/cuda_allreduce_bcube.cc:57).
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipAllreduceBcube : public HipPlanAlgorithm<T, GLOO_HIP_ALGO_BCUBE, W> {
+ public:
+  HipAllreduceBcube(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs, int count,
+                    const std::vector<hipStream_t>& streams = {},
+                    const HipReductionFunction<T>* fn = HipReductionFunction<T>::sum)
+      : HipPlanAlgorithm<T, GLOO_HIP_ALGO_BCUBE, W>(context, ptrs, count, {context->base}, streams, fn) {}
+};
+
+// CudaAllreduceHalvingDoublingPipelined
+// (gloo/cuda_allreduce_halving_doubling_pipelined.h:13-28): halving-doubling
+// with pipelineBroadcastAndReduce set (see HipAllreduceHalvingDoubling).
+template <typename T, typename W = HipDeviceWorkspace<T>>
+class HipAllreduceHalvingDoublingPipelined : public HipAllreduceHalvingDoubling<T, W> {
+ public:
+  HipAllreduceHalvingDoublingPipelined(const std::shared_ptr<Context>& context, const std::vector<T*>& ptrs,
+                                       int count, const std::vector<hipStream_t>& streams = {})
+      : HipAllreduceHalvingDoubling<T, W>(context, ptrs, count, streams, true) {}
+};
+
 // New-style function API (gloo/allreduce.h:89-193): options object + free
 // function; RING algorithm.  Same setter names as gloo::AllreduceOptions.
 class AllreduceOptions {

@@ -197,6 +197,13 @@ typedef enum {
    * or size > GLOO_HIP_MAX_SRCS) with a built-in op; a custom op keeps the
    * literal ring order. */
   GLOO_HIP_ALGO_RING_CHUNKED_PIPE = 9,
+  /* AllreduceBcube (gloo/allreduce_bcube.h) and its GPU twin
+   * CudaAllreduceBcube (gloo/cuda_allreduce_bcube.{h,cc}): groups of `base`
+   * ranks, log_base(P) reduce-scatter steps and the all-gather back.  The
+   * base (gloo::Context::base, gloo/context.h:28-33; 0 or absent = 2) is
+   * recv_elems[0] in gloo_hip_plan* and gloo_hip_algorithm_create.  Always
+   * the reference's own route (no mesh plan). */
+  GLOO_HIP_ALGO_BCUBE = 10,
 } gloo_hip_algo_t;
 
 /* algo | GLOO_HIP_ALGO_MESH: the algorithm's result with mesh data movement,

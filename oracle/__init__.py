@@ -80,6 +80,8 @@ def ref():
         L.ref_allreduce_new_algo.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
                                              ctypes.c_void_p, ctypes.c_void_p]
+        L.ref_allreduce_bcube.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
         L.ref_reduce_new.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
                                      ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.ref_allreduce_timed.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,

@@ -12,6 +12,12 @@ The fixtures (not the reference) travel to the GPU box.
   sched_golden.npz     AllreduceRingChunked / AllreduceHalvingDoubling /
                        AllreduceRing / ReduceScatterHalvingDoubling outputs at
                        P ranks (threads over the reference's TCP transport).
+  bcube_golden.npz     AllreduceBcube (gloo/allreduce_bcube.h) on contexts of
+                       base 2, 3 and 4: the P = base^k grid of
+                       gloo/test/allreduce_test.cc:271-299 plus larger counts,
+                       several pointers, other dtypes and ops, and two P that
+                       are not powers of the base (the reference's ranges as
+                       they fall there); every rank's output is kept.
 
 Usage:  make -C oracle ref && python oracle/gen_golden.py
 """
@@ -231,6 +237,47 @@ def gen_sched():
     print("sched_golden.npz:", len(out), "arrays")
 
 
+def ref_allreduce_bcube(op, dtype, base, inputs):
+    code, npt = oracle.DTYPES[dtype]
+    P, k, n = inputs.shape
+    out = np.empty_like(inputs)
+    rc = oracle.ref().ref_allreduce_bcube(oracle.OPS[op], code, P, base, k, n, inputs.ctypes.data,
+                                          out.ctypes.data)
+    if rc:
+        raise RuntimeError(f"ref_allreduce_bcube({P},{base},{n}) = {rc}: {oracle.ref().ref_last_error()}")
+    return out
+
+
+def bcube_cases():
+    """(op, dtype, P, base, k, n): the reference's own grid first."""
+    cases = []
+    for base, Ps in ((2, (2, 4, 8, 16)), (3, (3, 9, 27)), (4, (4, 16))):
+        for P in Ps:
+            for n in (1, 64, 1000):
+                cases.append(("sum", "f32", P, base, 1, n))
+    cases += [("sum", "f32", 8, 2, 1, 20011), ("sum", "f32", 9, 3, 1, 4099), ("sum", "f32", 4, 2, 3, 1000),
+              ("max", "f32", 8, 2, 1, 4099), ("min", "f32", 4, 4, 1, 777), ("product", "f64", 4, 2, 2, 999),
+              ("sum", "bf16", 8, 2, 1, 2000), ("sum", "f16", 9, 3, 1, 1001), ("sum", "i32", 4, 2, 1, 3000),
+              # P not a power of the base: the reference's ranges as they fall
+              ("sum", "f32", 6, 2, 1, 1000), ("sum", "f32", 5, 3, 1, 500)]
+    return cases
+
+
+def gen_bcube():
+    rng = np.random.default_rng(SEED + 3)
+    out = {}
+    for op, dtype, P, base, k, n in bcube_cases():
+        x = _values(dtype, op, (P, k, n), rng)
+        y = ref_allreduce_bcube(op, dtype, base, np.ascontiguousarray(x))
+        key = f"bcube/{op}/{dtype}/P{P}/b{base}/k{k}/n{n}"
+        for r in range(P):  # each rank's pointers end alike (the local broadcast)
+            assert all((y[r, j].view(np.uint8) == y[r, 0].view(np.uint8)).all() for j in range(k)), key
+        out[key + "/in"] = x
+        out[key + "/out"] = y[:, 0].copy()  # [P][n]: every rank's result
+    np.savez_compressed(os.path.join(OUT, "bcube_golden.npz"), **out)
+    print("bcube_golden.npz:", len(out), "arrays")
+
+
 def _values(dtype, op, shape, rng):
     if dtype in ("u64", "i32"):
         npt = oracle.DTYPES[dtype][1]
@@ -434,3 +481,5 @@ if __name__ == "__main__":
         gen_sched()
     if "newstyle" in which:
         gen_newstyle()
+    if "bcube" in which:
+        gen_bcube()

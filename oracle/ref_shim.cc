@@ -10,6 +10,7 @@
 //   * AllreduceRingChunked<T>                        gloo/allreduce_ring_chunked.h
 //   * AllreduceHalvingDoubling<T>                    gloo/allreduce_halving_doubling.h
 //   * AllreduceRing<T>                               gloo/allreduce_ring.h
+//   * AllreduceBcube<T>                              gloo/allreduce_bcube.h
 //   * ReduceScatterHalvingDoubling<T>                gloo/reduce_scatter.h
 //   * AllreduceLocal<T>                              gloo/allreduce_local.{h,cc}
 // with P ranks as threads in one process over the reference's own TCP
@@ -34,6 +35,7 @@
 #include <c10/util/BFloat16.h>
 
 #include "gloo/allreduce.h"
+#include "gloo/allreduce_bcube.h"
 #include "gloo/allreduce_halving_doubling.h"
 #include "gloo/allreduce_local.h"
 #include "gloo/allreduce_ring.h"
@@ -122,7 +124,7 @@ class Barrier {
 };
 
 // Spawn P ranks as threads, connect a full mesh over TCP localhost, run fn.
-int spawn(int P, const std::function<void(std::shared_ptr<gloo::Context>)>& fn) {
+int spawn(int P, const std::function<void(std::shared_ptr<gloo::Context>)>& fn, int base = 2) {
   auto store = std::make_shared<gloo::rendezvous::HashStore>();
   Barrier barrier(P);
   std::vector<std::thread> threads;
@@ -131,7 +133,7 @@ int spawn(int P, const std::function<void(std::shared_ptr<gloo::Context>)>& fn) 
   for (int rank = 0; rank < P; rank++) {
     threads.emplace_back([&, rank] {
       try {
-        auto ctx = std::make_shared<gloo::rendezvous::Context>(rank, P);
+        auto ctx = std::make_shared<gloo::rendezvous::Context>(rank, P, base);
         ctx->setTimeout(std::chrono::seconds(60));
         if (P > 1) {
           gloo::transport::tcp::attr attr("localhost");
@@ -213,6 +215,25 @@ int reduce_scatter(int op, int P, size_t n, const int* recvElems, const void* in
     gloo::ReduceScatterHalvingDoubling<T> a(ctx, ptrs, (int)n, re, fn);
     a.run();
   });
+}
+
+// AllreduceBcube<T> (gloo/allreduce_bcube.h) on a context of the given base
+// (gloo/context.h:28).  in/out laid out [P][k][n].
+template <typename T>
+int allreduce_bcube(int op, int P, int base, int k, size_t n, const void* in, void* out) {
+  const auto* fn = pickFn<T>(op);
+  if (!fn) return -1;
+  T* dst = static_cast<T*>(out);
+  std::memcpy(dst, in, sizeof(T) * (size_t)P * k * n);
+  return spawn(
+      P,
+      [&](std::shared_ptr<gloo::Context> ctx) {
+        std::vector<T*> ptrs;
+        for (int j = 0; j < k; j++) ptrs.push_back(dst + ((size_t)ctx->rank * k + j) * n);
+        gloo::AllreduceBcube<T> a(ctx, ptrs, (int)n, fn);
+        a.run();
+      },
+      base);
 }
 
 // New-style gloo::allreduce(opts), RING (gloo/allreduce.cc:147-392) or BCUBE
@@ -305,6 +326,11 @@ int ref_reduce3_f16_scalar(int op, void* c, const void* a, const void* b, size_t
 int ref_allreduce(int algo, int op, int dtype, int P, int k, size_t n, const void* in,
                   void* out) {
   DISPATCH(dtype, allreduce<T>(algo, op, P, k, n, in, out));
+}
+
+// AllreduceBcube over P ranks of context base `base`, k pointers each.
+int ref_allreduce_bcube(int op, int dtype, int P, int base, int k, size_t n, const void* in, void* out) {
+  DISPATCH(dtype, allreduce_bcube<T>(op, P, base, k, n, in, out));
 }
 
 // New-style allreduce; out holds the initial outputs and receives the result.

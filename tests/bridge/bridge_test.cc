@@ -8,7 +8,7 @@
 // std::shared_ptr<gloo::Context> to gloo::HipAllreduce*<T>, which derives from
 // gloo::Algorithm.  Mirrors gloo/test/cuda_allreduce_test.cc:60-349:
 // SinglePointer / MultiPointer / MultiPointerAsync (user streams) across
-// ring, ring-chunked, halving-doubling (+ pipelined), fp16, plus the
+// ring, ring-chunked, halving-doubling (+ pipelined), bcube, fp16, plus the
 // reduce-scatter, the host workspace and the IoException on a silent peer.
 // Expected values: the closed form of gloo/test/base_test.h:184-236.
 //
@@ -66,7 +66,9 @@ class Barrier {
 };
 
 // P ranks as threads; each gets a connected gloo::Context (timeout `ms`).
-std::string spawn(int P, int ms, const std::function<void(std::shared_ptr<gloo::Context>)>& fn, bool gpu = true) {
+// base: gloo::Context::base (gloo/context.h:28), AllreduceBcube's group size.
+std::string spawn(int P, int ms, const std::function<void(std::shared_ptr<gloo::Context>)>& fn, bool gpu = true,
+                  int base = 2) {
   auto store = std::make_shared<gloo::rendezvous::HashStore>();
   Barrier barrier(P);
   std::vector<std::thread> ts;
@@ -76,7 +78,7 @@ std::string spawn(int P, int ms, const std::function<void(std::shared_ptr<gloo::
     ts.emplace_back([&, rank] {
       try {
         if (gpu) HIPOK(hipSetDevice(0));
-        auto ctx = std::make_shared<gloo::rendezvous::Context>(rank, P);
+        auto ctx = std::make_shared<gloo::rendezvous::Context>(rank, P, base);
         ctx->setTimeout(std::chrono::milliseconds(ms));
         if (P > 1) {
           gloo::transport::tcp::attr attr("localhost");
@@ -129,7 +131,8 @@ using Make = std::function<std::unique_ptr<gloo::Algorithm>(std::shared_ptr<gloo
 // (j % mod) * P * k + r * k + i (mod 0: j), so the sum is known in closed form
 // (mod keeps 16-bit sums exact).
 template <typename T>
-std::string allreduceCase(int P, int k, int count, Inputs inputs, int runs, const Make& make, int mod = 0) {
+std::string allreduceCase(int P, int k, int count, Inputs inputs, int runs, const Make& make, int mod = 0,
+                          int base = 2) {
   return spawn(P, 30000, [&](std::shared_ptr<gloo::Context> ctx) {
     const size_t stride = (size_t)P * k;
     std::vector<void*> ptrs(k);
@@ -193,7 +196,7 @@ std::string allreduceCase(int P, int k, int count, Inputs inputs, int runs, cons
     for (void* p : ptrs) HIPOK(hipFree(p));
     for (T* h : host) HIPOK(hipHostFree(h));
     for (T* h : out) HIPOK(hipHostFree(h));
-  });
+  }, true, base);
 }
 
 template <typename T>
@@ -226,6 +229,22 @@ Make halvingDoubling(bool pipelined) {
     std::vector<T*> tp;
     for (void* x : p) tp.push_back(static_cast<T*>(x));
     return std::unique_ptr<gloo::Algorithm>(new gloo::HipAllreduceHalvingDoubling<T>(c, tp, n, s, pipelined));
+  };
+}
+template <typename T>
+Make halvingDoublingPipelined() {  // gloo::CudaAllreduceHalvingDoublingPipelined's twin
+  return [](std::shared_ptr<gloo::Context>& c, std::vector<void*>& p, int n, std::vector<hipStream_t>& s) {
+    std::vector<T*> tp;
+    for (void* x : p) tp.push_back(static_cast<T*>(x));
+    return std::unique_ptr<gloo::Algorithm>(new gloo::HipAllreduceHalvingDoublingPipelined<T>(c, tp, n, s));
+  };
+}
+template <typename T>
+Make bcube() {  // gloo::CudaAllreduceBcube's twin: groups of the context's base
+  return [](std::shared_ptr<gloo::Context>& c, std::vector<void*>& p, int n, std::vector<hipStream_t>& s) {
+    std::vector<T*> tp;
+    for (void* x : p) tp.push_back(static_cast<T*>(x));
+    return std::unique_ptr<gloo::Algorithm>(new gloo::HipAllreduceBcube<T>(c, tp, n, s));
   };
 }
 
@@ -360,6 +379,19 @@ int main(int argc, char** argv) {
   }
   cases.push_back({"halving_doubling_pipelined/P4/n4099",
                    [] { return allreduceCase<float>(4, 1, 4099, Inputs::kSync, 1, halvingDoubling<float>(true)); }});
+  cases.push_back({"halving_doubling_pipelined_class/P4/k2/n4099",
+                   [] { return allreduceCase<float>(4, 2, 4099, Inputs::kSync, 2, halvingDoublingPipelined<float>()); }});
+  // CudaAllreduceBcube (gloo/test/cuda_allreduce_test.cc:311-339: P = base^k)
+  for (auto pb : {std::make_pair(2, 2), std::make_pair(4, 2), std::make_pair(8, 2), std::make_pair(3, 3),
+                  std::make_pair(9, 3), std::make_pair(4, 4), std::make_pair(16, 4)}) {
+    for (int n : {1, 64, 1000}) {
+      const int P = pb.first, base = pb.second;
+      cases.push_back({"bcube/P" + std::to_string(P) + "/b" + std::to_string(base) + "/n" + std::to_string(n),
+                       [=] { return allreduceCase<float>(P, 1, n, Inputs::kSync, 2, bcube<float>(), 0, base); }});
+    }
+  }
+  cases.push_back({"multi_pointer_async/bcube/P4/k2/n4099",
+                   [] { return allreduceCase<float>(4, 2, 4099, Inputs::kAsyncSpin, 2, bcube<float>(), 0, 2); }});
   cases.push_back({"multi_pointer/ring_chunked/P3/k2/n1000",
                    [] { return allreduceCase<float>(3, 2, 1000, Inputs::kSync, 1, ringChunked<float>()); }});
   cases.push_back({"multi_pointer_streams/ring_chunked/P2/k2/n10007",

@@ -32,7 +32,7 @@ def cases(name):
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("name", ["sched_golden.npz", "newstyle_golden.npz", "math_golden.npz",
-                                  "bw_golden.npz"])
+                                  "bw_golden.npz", "bcube_golden.npz"])
 def test_every_golden_case_has_a_gpu_test(gpu_ids, name):
     cs = cases(name)
     assert cs
