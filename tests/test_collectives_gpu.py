@@ -987,15 +987,19 @@ def test_processes_byte_sums_any_offset(torch, algo, dtype, P, n, env):
 
 
 @pytest.mark.timeout(300)
-def test_stress_mixed_collectives_short(torch):
-    """tools/stress.py for a few seconds at 3 ranks: four schedules, three
-    dtypes, sizes 1 element .. 8 MiB in a shared random order, every result
-    checked exactly (launch modes mix: interpreter, graph replay, eager)."""
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "stress.py"), "3", "8", "11"],
+@pytest.mark.parametrize("P", [3, 4])
+def test_stress_mixed_collectives_short(torch, P):
+    """tools/stress.py for a few seconds at 3 and 4 ranks: four schedules (five
+    at 4 ranks: AllreduceBcube too) and the new-style calls, three dtypes,
+    sizes 1 element .. 8 MiB in a shared random order, every result checked
+    exactly (launch modes mix: interpreter, graph replay, eager)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "stress.py"), str(P), "8", "11"],
                        capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
     lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith('{"rank"')]
-    assert len(lines) == 3 and all(x["runs"] > 100 and "error" not in x for x in lines), lines
+    assert len(lines) == P and all(x["runs"] > 100 and "error" not in x for x in lines), lines
+    if P == 4:
+        assert any(k.startswith("bcube/") for k in lines[0]["modes"]), lines[0]["modes"]
 
 
 INCONSISTENT_WORKER = r'''

@@ -61,14 +61,16 @@ def test_reduce3_and_multi(torch, xor_op):
 
 
 @pytest.mark.parametrize("algo,P", [("ring_chunked", 3), ("ring_chunked", 4), ("halving_doubling", 4),
-                                    ("halving_doubling", 5), ("ring", 3), ("local", 1)])
+                                    ("halving_doubling", 5), ("ring", 3), ("local", 1), ("bcube", 4),
+                                    ("bcube", 9)])
 def test_threads(torch, xor_op, algo, P):
     from test_collectives_gpu import run_threads
     op, _ = xor_op
     k = 3 if algo == "local" else 1
     rng = np.random.default_rng(P)
     x = rng.integers(-2**31, 2**31, (P, k, 10_007), dtype=np.int64).astype(np.int32)
-    y = run_threads(torch, algo, op, "i32", x, runs=1)
+    recv = ([3] if P == 9 else [2]) if algo == "bcube" else None  # AllreduceBcube's base
+    y = run_threads(torch, algo, op, "i32", x, recv=recv, runs=1)
     want = np.bitwise_xor.reduce(x.reshape(P * k, -1), axis=0)
     for r in range(P):
         for j in range(k):

@@ -46,7 +46,9 @@ if os.environ.get("STRESS_BIG") == "1":  # the eager and graph launch modes of t
     sizes += [(4 << 20) + 3, 16 << 20]
 combos = (("sum", "f32"), ("max", "bf16"), ("min", "i32"), ("sum", "i32"))
 # a context holds at most 64 live algorithms: one op / dtype per (schedule, size), rotating
-for ai, algo in enumerate(("ring_chunked", "halving_doubling", "ring", "reduce_scatter")):
+# (AllreduceBcube sums every rank only where P is a power of its base, 2 here)
+schedules = ("ring_chunked", "halving_doubling", "ring", "reduce_scatter") + (("bcube",) if P & (P - 1) == 0 else ())
+for ai, algo in enumerate(schedules):
     for si, n in enumerate(sizes):
         if algo == "ring" and n > (1 << 20):  # (the plain ring moves the whole buffer per hop)
             continue
@@ -62,7 +64,8 @@ for algo, op, dt, n in cases:
         for _ in range(P):
             recv.append(min(chunk, rem))
             rem = rem - chunk if rem > chunk else 0
-    a = gloo_amd.Algorithm(ctx, algo, op, dt, [buf.data_ptr()], n, recv_elems=recv)
+    a = gloo_amd.Algorithm(ctx, algo, op, dt, [buf.data_ptr()], n, recv_elems=recv,
+                           base=2 if algo == "bcube" else None)
     idx = torch.arange(n, device=dev)
     if op == "sum":
         mine = ((rank + 1) * (idx % 7 + 1)).to(tdt[dt])
