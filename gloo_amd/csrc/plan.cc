@@ -584,15 +584,16 @@ std::vector<BcubeNode> bcubeNodes(int nodes, int base, int count, int steps) {
     n.numElems.assign(steps, 0);
     n.ptrOffset.assign(steps, 0);
   }
-  int peerDistance = 1;
+  // (64-bit where the reference's int arithmetic could overflow for huge
+  // bases or counts; equal results wherever it does not)
+  int64_t peerDistance = 1;
   for (int step = 0; step < steps; ++step) {
     for (int rank = 0; rank < nodes; ++rank) {
       const BcubeNode& first = all[rank];
       if (!first.peers[step].empty()) continue;  // only nodes without peers start a group
       std::vector<int> group;
-      for (int i = 0; i < base; ++i)
-        if (rank + i * peerDistance < nodes) group.push_back(rank + i * peerDistance);
-      int ptrOffset = step == 0 ? 0 : first.ptrOffset[step - 1];
+      for (int64_t i = 0; i < base && rank + i * peerDistance < nodes; ++i) group.push_back((int)(rank + i * peerDistance));
+      int64_t ptrOffset = step == 0 ? 0 : first.ptrOffset[step - 1];
       const int groupCount = step == 0 ? count : first.numElems[step - 1];
       const int numElems = std::max(groupCount, (int)group.size());
       const int sz = (int)group.size();
@@ -605,7 +606,7 @@ std::vector<BcubeNode> bcubeNodes(int nodes, int base, int count, int steps) {
           if (peer != group[i]) node.peers[step].push_back(peer);
         const int n = i != sz - 1 ? each : each + rem;
         node.numElems[step] = n;
-        node.ptrOffset[step] = ptrOffset;
+        node.ptrOffset[step] = (int)ptrOffset;
         ptrOffset += n;
         ptrOffset %= count;
       }

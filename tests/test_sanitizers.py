@@ -22,7 +22,7 @@ sys.path.insert(0, os.path.join(os.environ["GLOO_AMD_ROOT"], "tests"))
 sys.path.insert(0, os.environ["GLOO_AMD_ROOT"])
 import numpy as np
 from plan_sim import get_plan, simulate
-algos = ["ring_chunked", "halving_doubling", "ring", "local", "allreduce_new", "allreduce_bcube",
+algos = ["ring_chunked", "halving_doubling", "ring", "local", "allreduce_new", "allreduce_bcube", "bcube",
          "mesh_ring_chunked", "mesh_halving_doubling", "mesh_allreduce_new", "mesh_allreduce_bcube"]
 n_plans = 0
 for P in (1, 2, 3, 5, 6, 8, 12):
@@ -47,6 +47,8 @@ x = np.random.default_rng(0).standard_normal((6, 1, 999)).astype(np.float32)
 for algo in ("halving_doubling", "mesh_halving_doubling", "allreduce_bcube", "mesh_allreduce_bcube"):
     simulate(algo, "sum", "f32", x, seed=1)
 simulate("mesh_reduce", "sum", "f32", x, recv=np.array([2], np.int32), seed=1)
+for base in (2, 3, 1 << 30):
+    simulate("bcube", "sum", "f32", x, recv=np.array([base], np.int32), seed=1)
 print("planned", n_plans)
 '''
 
