@@ -161,7 +161,8 @@ int selectPlanAlgo(int algo, int P, bool custom, const RouteKnobs& k) {
   // reduce-scatter and the new-style collectives likewise run as their
   // derived mesh plans (mesh.cc).
   if (mesh && algo == GLOO_HIP_ALGO_RING_CHUNKED) planAlgo = GLOO_HIP_ALGO_RING_CHUNKED_MESH;
-  if (mesh && (algo == GLOO_HIP_ALGO_HALVING_DOUBLING || algo == GLOO_HIP_ALGO_REDUCE_SCATTER || isNewStyle(algo)))
+  if (mesh && (algo == GLOO_HIP_ALGO_HALVING_DOUBLING || algo == GLOO_HIP_ALGO_REDUCE_SCATTER || isNewStyle(algo) ||
+               algo == GLOO_HIP_ALGO_BCUBE))
     planAlgo = algo | GLOO_HIP_ALGO_MESH;
   // Ring-chunked on its ring route (the mesh off, or P > 8): three inboxes
   // per channel, so each round reduces and forwards in one pass (plan.cc
@@ -519,8 +520,19 @@ PlanExecutor::PlanExecutor(std::shared_ptr<Context> ctx, int algo, int op, int d
   // on the route knobs and P, and the "where" exchange below checks it.
   const RouteKnobs knobs = routeKnobs();
   planAlgo_ = selectPlanAlgo(algo_, P, custom_, knobs);
-  plan_ = planFor(planAlgo_, me, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_, maxSegmentBytes_,
-                  recvElems_);
+  try {
+    plan_ = planFor(planAlgo_, me, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_, maxSegmentBytes_,
+                    recvElems_);
+  } catch (const std::runtime_error&) {
+    // AllreduceBcube has a mesh form only where every rank ends with the same
+    // expression trees (P a power of the base, counts of at least P or so;
+    // mesh.cc throws otherwise): the reference route then, decided alike on
+    // every rank since the derivation depends only on (P, count, base)
+    if (planAlgo_ != (GLOO_HIP_ALGO_BCUBE | GLOO_HIP_ALGO_MESH)) throw;
+    planAlgo_ = GLOO_HIP_ALGO_BCUBE;
+    plan_ = planFor(planAlgo_, me, P, count_, (int)inputs_.size(), (int)ptrs_.size(), es_, maxSegmentBytes_,
+                    recvElems_);
+  }
   GLOO_AMD_HIP_CHECK(hipSetDevice(ctx_->device()));
   classifyPointers();
   inst_ = ctx_->acquireInstance();

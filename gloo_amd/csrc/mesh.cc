@@ -132,7 +132,8 @@ struct Job {
 
 bool isAllreduce(int algo) {
   return algo == GLOO_HIP_ALGO_RING_CHUNKED || algo == GLOO_HIP_ALGO_HALVING_DOUBLING || algo == GLOO_HIP_ALGO_RING ||
-         algo == GLOO_HIP_ALGO_ALLREDUCE_RING || algo == GLOO_HIP_ALGO_ALLREDUCE_BCUBE;
+         algo == GLOO_HIP_ALGO_ALLREDUCE_RING || algo == GLOO_HIP_ALGO_ALLREDUCE_BCUBE ||
+         algo == GLOO_HIP_ALGO_BCUBE;
 }
 
 // Combine aligned piece lists of several operands position by position.

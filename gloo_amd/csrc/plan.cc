@@ -1234,7 +1234,7 @@ extern "C" int gloo_hip_plan_ex(int algo, int rank, int size, size_t count, int 
       if (!recv_elems) return GLOO_HIP_EINVAL_ARG;
       re.assign(recv_elems, recv_elems + size);
     }
-    if (algo == GLOO_HIP_ALGO_BCUBE && recv_elems) re.assign(recv_elems, recv_elems + 1);  // {base}
+    if ((algo & ~GLOO_HIP_ALGO_MESH) == GLOO_HIP_ALGO_BCUBE && recv_elems) re.assign(recv_elems, recv_elems + 1);  // {base}
     gloo_amd::Plan p;
     if (gloo_amd::isNewStyle(algo)) {
       gloo_amd::NewStyleOptions o;

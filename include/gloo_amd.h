@@ -201,8 +201,10 @@ typedef enum {
    * CudaAllreduceBcube (gloo/cuda_allreduce_bcube.{h,cc}): groups of `base`
    * ranks, log_base(P) reduce-scatter steps and the all-gather back.  The
    * base (gloo::Context::base, gloo/context.h:28-33; 0 or absent = 2) is
-   * recv_elems[0] in gloo_hip_plan* and gloo_hip_algorithm_create.  Always
-   * the reference's own route (no mesh plan). */
+   * recv_elems[0] in gloo_hip_plan* and gloo_hip_algorithm_create.  For
+   * 2 <= size <= 8 it executes as its derived mesh plan (| GLOO_HIP_ALGO_MESH)
+   * wherever every rank ends with the same expression trees (P a power of
+   * the base, counts of about P and more), else on the reference's route. */
   GLOO_HIP_ALGO_BCUBE = 10,
 } gloo_hip_algo_t;
 

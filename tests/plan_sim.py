@@ -21,7 +21,7 @@ KIND = dict(DECL_RECV=0, SEND=1, WAIT_RECV=2, REDUCE=3, COPY=4, NOTIFY=5, WAIT_N
 ALGO = dict(ring_chunked=0, halving_doubling=1, ring=2, local=3, reduce_scatter=4, allreduce_new=5,
             ring_chunked_mesh=6, allreduce_bcube=7, reduce=8, ring_chunked_pipe=9, bcube=10)
 MESH = 0x100  # algo | MESH: the derived mesh plan (gloo_amd/csrc/mesh.cc)
-ALGO.update({"mesh_" + k: v | MESH for k, v in list(ALGO.items()) if v < 5 or v in (5, 7, 8)})
+ALGO.update({"mesh_" + k: v | MESH for k, v in list(ALGO.items()) if v < 5 or v in (5, 7, 8, 10)})
 SRC_ARENA, DST_ARENA, FROM_INPUTS, FOLD_REVERSE, FOLD_TREE, PREV_RUN = 1, 2, 4, 8, 16, 32
 
 

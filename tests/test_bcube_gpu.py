@@ -3,8 +3,11 @@ gloo/cuda_allreduce_bcube.{h,cc}) through the HIP plan executor, byte for
 byte against the reference's own outputs (tests/golden/bcube_golden.npz,
 every rank's).  Ranks as threads of one process for every golden case; ranks
 as processes (tests/sched_pool.py batches) for a subset, in the default
-launch modes, with graph replay forced and with the interpreter off.  The
-base rides in recv_elems[0] (gloo::Context::base, gloo/context.h:28-33)."""
+launch modes, with graph replay forced, with the interpreter off and on the
+reference route.  For 2 <= P <= 8 the default is the derived mesh plan
+wherever it exists (gloo_amd/csrc/mesh.cc; tests/test_bcube_plan.py lists
+which cases), else the reference route.  The base rides in recv_elems[0]
+(gloo::Context::base, gloo/context.h:28-33)."""
 import os
 
 import numpy as np
@@ -51,6 +54,20 @@ def test_bcube_threads_golden(torch, golden, case):
             assert same_bytes(y[r, j], want[r]), (r, j)
 
 
+@pytest.mark.parametrize("case", ["bcube/sum/f32/P8/b2/k1/n1000", "bcube/sum/f32/P4/b4/k1/n64",
+                                  "bcube/sum/f32/P4/b2/k3/n1000", "bcube/max/f32/P8/b2/k1/n4099"])
+def test_bcube_threads_reference_route(torch, golden, case, monkeypatch):
+    """The reference's own route (GLOO_AMD_MESH=0) where the default is the
+    derived mesh plan (2 <= P <= 8 with a mesh form)."""
+    monkeypatch.setenv("GLOO_AMD_MESH", "0")
+    op, dtype = case.split("/")[1:3]
+    x, want = golden[case + "/in"], golden[case + "/out"]
+    y = run_threads(torch, "bcube", op, dtype, x, recv=[_base(case)])
+    for r in range(y.shape[0]):
+        for j in range(y.shape[1]):
+            assert same_bytes(y[r, j], want[r]), (r, j)
+
+
 @pytest.mark.parametrize("P,base", [(8, 2), (9, 3), (16, 4)])
 def test_bcube_threads_repeated_runs_and_user_stream(torch, P, base):
     """Closed form of gloo/test/base_test.h:184-236 (input j*P + rank): one run
@@ -72,6 +89,8 @@ PROCESS_CASES = [
     ("bcube/sum/f32/P4/b4/k1/n1000", {}, 1),
     ("bcube/max/f32/P8/b2/k1/n4099", {"GLOO_AMD_GRAPH": "1"}, 3),
     ("bcube/sum/f32/P4/b2/k1/n1000", {"GLOO_AMD_INTERP": "0"}, 3),
+    ("bcube/sum/f32/P8/b2/k1/n20011", {"GLOO_AMD_MESH": "0"}, 1),
+    ("bcube/sum/f32/P4/b4/k1/n1000", {"GLOO_AMD_MESH": "0"}, 1),
 ]
 for _c, _e, _n in PROCESS_CASES:
     sched_pool.register(_c, _e, _n)

@@ -121,3 +121,38 @@ def test_bcube_zero_count_and_single_rank():
     assert len(get_plan("bcube", 0, 4, 0, 1, np.array([2], np.int32))[0]) == 0
     st, arena = get_plan("bcube", 0, 1, 100, 3, np.array([2], np.int32))
     assert [s.kind for s in st] == [KIND["LOCAL_REDUCE"], KIND["LOCAL_BCAST"]] and arena == 0
+
+
+def _mesh_plans(P, base, n, k=1):
+    """Every rank's derived mesh plan (gloo_amd/csrc/mesh.cc), or None where
+    the derivation refuses (ranks ending with different expression trees,
+    partial reductions, mixed element indices): the executor then keeps the
+    reference route (executor.cc, the constructor's fallback)."""
+    try:
+        return [get_plan("mesh_bcube", r, P, n, k, np.array([base], np.int32)) for r in range(P)]
+    except RuntimeError:
+        return None
+
+
+@pytest.mark.parametrize("case", [c for c in _keys() if 2 <= _parse(c)[2] <= 8])
+def test_mesh_bcube_matches_reference_golden(golden, case):
+    """Where the mesh form exists (the executor's default for 2 <= P <= 8) it
+    gives the reference's bytes on every rank; it exists for every P = base^k
+    case with n >= 64, and not where the reference's ranks end differently
+    (P not a power of the base)."""
+    op, dtype, P, base, k, n = _parse(case)
+    plans = _mesh_plans(P, base, n, k)
+    power = base ** round(math.log(P, base)) == P
+    if power and n >= 64:
+        assert plans is not None, case
+    if not power:
+        assert plans is None, case
+    if plans is None:
+        return
+    x = golden[case + "/in"]
+    want = golden[case + "/out"]
+    for seed in (0, 1):
+        y = simulate("mesh_bcube", op, dtype, x.copy(), recv=np.array([base], np.int32), seed=seed)
+        for r in range(P):
+            for j in range(k):
+                assert same_bytes(np.asarray(y[r][j]), want[r]), (seed, r, j)
