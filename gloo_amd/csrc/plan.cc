@@ -632,7 +632,10 @@ Plan planBcube(int rank, int size, uint64_t count64, int nptrs, int base) {
   if (count64 > (uint64_t)std::numeric_limits<int>::max())
     throw std::invalid_argument("AllreduceBcube counts elements in int");
   const int count = (int)count64;
-  if (base < 2) base = 2;  // CudaAllreduceBcube: `context->base ? context->base : 2`
+  // CudaAllreduceBcube takes `context->base ? context->base : 2`
+  // (gloo/cuda_allreduce_bcube.cc:57); a base
+  // of 1 would divide by log2(1) = 0 in computeSteps, so it plans as 2 too
+  if (base < 2) base = 2;
   if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_REDUCE, -1, 0, 0, 0, 0, count64));  // :352-355
   if (size == 1) {                                                      // :357-363
     if (nptrs > 1) p.steps.push_back(mk(GLOO_HIP_STEP_LOCAL_BCAST, -1, 0, 0, 0, 0, count64));
