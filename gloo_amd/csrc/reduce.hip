@@ -353,11 +353,15 @@ thread_local bool t_plainStores = false;   // setReducePlainStores
 // round1): `nt` on both loads and stores, UNROLL 2, BLOCK 512, one tile per
 // workgroup is the fastest of 126 variants for the 64 MiB fp32 chunk.
 //
-// IL: the two operands' loads are issued interleaved, packet by packet (a0 b0
-// a1 b1) rather than stream by stream (a0 a1 b0 b1).  Round 3, in the
-// stripped harness (tools/tune/hbm_ceiling.hip, profiles/round3/r3ab_*):
-// 0.800-0.802 against 0.796-0.800 of 8 TB/s for the in-place 2R + 1W mix.
-template <class Tr, int OP, int UNROLL, int BLOCK, int LAUX, int SAUX, int IL = 1>
+// IL: the two operands' loads issued interleaved, packet by packet (a0 b0 a1
+// b1), instead of stream by stream (a0 a1 b0 b1, the default).  Round 3 made
+// IL the default on stripped-harness readings within the run-to-run spread
+// (profiles/round3/r3ab_*, r3ac_*); round 6 timed the product kernel both ways
+// in two sessions, interleaved over 3 and 10 repetitions of 500 launches at
+// 64 MiB (profiles/round6/r6ad/, r6ae/): stream by stream 0.8023 / 0.8000 of
+// 8 TB/s against 0.7986 / 0.7971 interleaved, equal at 16 MiB (0.6743 against
+// 0.6745), so the default went back to stream by stream (variant 15 keeps IL).
+template <class Tr, int OP, int UNROLL, int BLOCK, int LAUX, int SAUX, int IL = 0>
 __global__ __launch_bounds__(BLOCK) void reduce_vec_kernel(
     typename Tr::Storage* c, const typename Tr::Storage* a,
     const typename Tr::Storage* b, size_t n, size_t head, uint64_t* stamp) {
@@ -1158,14 +1162,16 @@ int by_op_fold_send(int op, void* dst, const SrcList& list, int k, int mode, siz
   }
 }
 
-template <class Tr, int OP, int UNROLL, int BLOCK, int LAUX, int SAUX, int IL = 1>
-int launch_vec(void* c, const void* a, const void* b, size_t n, size_t head, hipStream_t s) {
+// lds: a dynamic LDS allocation the kernel never touches; it only caps the
+// workgroups a CU holds (160 KiB / lds), a measurement knob (variants 16, 17).
+template <class Tr, int OP, int UNROLL, int BLOCK, int LAUX, int SAUX, int IL = 0>
+int launch_vec(void* c, const void* a, const void* b, size_t n, size_t head, hipStream_t s, unsigned lds = 0) {
   using S = typename Tr::Storage;
   constexpr int kV = 16 / sizeof(S);
   const size_t nvec = (n - head) / kV;
   size_t grid = ceil_div(nvec, (size_t)BLOCK * UNROLL);
   if (grid == 0) grid = 1;
-  reduce_vec_kernel<Tr, OP, UNROLL, BLOCK, LAUX, SAUX, IL><<<dim3((unsigned)grid), dim3(BLOCK), 0, s>>>(
+  reduce_vec_kernel<Tr, OP, UNROLL, BLOCK, LAUX, SAUX, IL><<<dim3((unsigned)grid), dim3(BLOCK), lds, s>>>(
       static_cast<S*>(c), static_cast<const S*>(a), static_cast<const S*>(b), n, head, t_stamp);
   return check_launch("reduce_vec_kernel");
 }
@@ -1208,7 +1214,11 @@ int launch3(void* c, const void* a, const void* b, size_t n, hipStream_t s) {
       case 12: return launch_vec_pipe<Tr, OP, 2, 512, kAuxNT, kAuxNT>(c, a, b, n, head, 2048, s);
       case 13: return launch_vec_pipe<Tr, OP, 1, 512, kAuxNT, kAuxNT>(c, a, b, n, head, 1024, s);
       case 14: return launch_vec_pipe<Tr, OP, 2, 256, kAuxNT, kAuxNT>(c, a, b, n, head, 2048, s);
-      case 15: return launch_vec<Tr, OP, 2, 512, kAuxNT, kAuxNT, 0>(c, a, b, n, head, s);  // rounds 1-2 load order
+      case 15: return launch_vec<Tr, OP, 2, 512, kAuxNT, kAuxNT, 1>(c, a, b, n, head, s);  // round 3-5 load order (IL)
+      // round 6: three workgroups per CU instead of four (48 KiB of unused LDS
+      // each): 64 MiB +0.1-0.2 %, 16 MiB -1.3-2 % (profiles/round6/r6ae/)
+      case 16: return launch_vec<Tr, OP, 2, 512, kAuxNT, kAuxNT, 1>(c, a, b, n, head, s, 48u << 10);
+      case 17: return launch_vec<Tr, OP, 2, 512, kAuxNT, kAuxNT, 0>(c, a, b, n, head, s, 48u << 10);
       default: break;
     }
   }

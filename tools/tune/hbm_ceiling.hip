@@ -110,6 +110,41 @@ __global__ __launch_bounds__(B) void stream_pol_k(float* c, const float* a, cons
   }
 }
 
+// Round 6, the product's shape (u2 x 512 lanes, nt loads interleaved, nt
+// stores) with three levers not measured before: MODE 0 with a dynamic LDS
+// allocation the kernel never touches, which only caps the workgroups a CU
+// holds (160 KiB / LDS); MODE 1 tiles dealt XCD-contiguously (workgroup i
+// runs on XCD i % 8, so XCD x streams one contiguous eighth of the buffer);
+// MODE 2 each wave's two packets per stream adjacent (2 KiB contiguous per
+// wave and stream instead of 2 x 1 KiB, 8 KiB apart).
+template <int MODE>
+__global__ __launch_bounds__(512) void stream_x_k(float* c, const float* a, const float* b, uint32_t*) {
+  constexpr int U = 2, B = 512;
+  constexpr uint32_t kTile = (uint32_t)B * U * 16;
+  uint32_t tile = blockIdx.x;
+  if (MODE == 1) tile = (blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u;
+  const size_t base = (size_t)tile * kTile;
+  const auto ra = rsrc(reinterpret_cast<const char*>(a) + base, kTile);
+  const auto rb = rsrc(reinterpret_cast<const char*>(b) + base, kTile);
+  const auto rc = rsrc(reinterpret_cast<const char*>(c) + base, kTile);
+  uint32_t off[U];
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    off[u] = MODE == 2 ? ((threadIdx.x / 64u) * (64u * U) + u * 64u + threadIdx.x % 64u) * 16u
+                       : threadIdx.x * 16u + u * B * 16u;
+  u32x4 x[U], y[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    x[u] = __builtin_amdgcn_raw_buffer_load_b128(ra, off[u], 0, kNT);
+    y[u] = __builtin_amdgcn_raw_buffer_load_b128(rb, off[u], 0, kNT);
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const f32x4 s = __builtin_bit_cast(f32x4, x[u]) + __builtin_bit_cast(f32x4, y[u]);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, s), rc, off[u], 0, kNT);
+  }
+}
+
 struct P {
   int r, w, u, b;
   void (*launch)(float*, const float*, const float*, uint32_t*, size_t, hipStream_t);
@@ -122,6 +157,11 @@ struct P {
 #define XL(U, B)                                                                                        \
   {2, 1 + 10 * U, U, B, [](float* c, const float* a, const float* b, uint32_t* sink, size_t bytes, hipStream_t s) { \
      stream_lds_k<U, B><<<(unsigned)(bytes / ((size_t)B * U * 16)), B, 0, s>>>(c, a, b, sink);          \
+   }},
+#define XX(MODE, LDSKIB)                                                                                \
+  {2, 1 + 1000000 * (1 + MODE) + 1000 * LDSKIB, 2, 512,                                                \
+   [](float* c, const float* a, const float* b, uint32_t* sink, size_t bytes, hipStream_t s) {          \
+     stream_x_k<MODE><<<(unsigned)(bytes / (512 * 2 * 16)), 512, LDSKIB * 1024, s>>>(c, a, b, sink);    \
    }},
 #define XP(U, B, LP, SP, IL)                                                                            \
   {2, 1 + 100 * (1 + LP + 32 * SP + 1024 * IL), U, B,                                                   \
@@ -137,10 +177,13 @@ static const P kP[] = {X(1, 0, 2, 512) X(1, 0, 4, 512) X(0, 1, 2, 512) X(0, 1, 4
                                    XP(2, 512, 2, 2, 1) XP(2, 512, 2, 18, 0) XP(2, 512, 2, 19, 0)
                                        XP(2, 512, 2, 0, 0) XP(2, 512, 0, 2, 0) XP(2, 512, 3, 2, 0)
                                            XP(2, 512, 18, 2, 0) XP(2, 1024, 2, 2, 0) XP(1, 1024, 2, 2, 0)
-                                               XP(4, 256, 2, 2, 1) XP(1, 512, 2, 2, 0)};
+                                               XP(4, 256, 2, 2, 1) XP(1, 512, 2, 2, 0)
+                                                   // 25..: round 6 (w = 1 + 1e6 (1 + mode) + 1e3 LDS KiB)
+                                                   XX(0, 0) XX(0, 48) XX(0, 64) XX(0, 96) XX(1, 0) XX(2, 0)};
 #undef X
 #undef XL
 #undef XP
+#undef XX
 
 extern "C" {
 int ceil_count() { return (int)(sizeof(kP) / sizeof(kP[0])); }

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--mib", type=int, default=64, help="MiB per stream per launch")
     ap.add_argument("--only", default="", help="comma list of pattern prefixes")
+    ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     L = ctypes.CDLL(os.path.join(HERE, args.lib))
     vp = ctypes.c_void_p
@@ -46,7 +47,11 @@ def main():
         d = (ctypes.c_int * 4)()
         L.ceil_desc(i, d)
         r, w, u, b = list(d)
-        if w >= 100:  # w = 1 + 100 * (1 + LP + 32 SP + 1024 IL): stream_pol_k
+        if w >= 1000000:  # w = 1 + 1e6 (1 + mode) + 1e3 LDS KiB: stream_x_k (round 6)
+            mode, lds = w // 1000000 - 1, (w % 1000000) // 1000
+            tag = f"R2W1_x{mode}_lds{lds}"
+            w = 1
+        elif w >= 100:  # w = 1 + 100 * (1 + LP + 32 SP + 1024 IL): stream_pol_k
             code = w // 100 - 1
             lp, sp, il = code % 32, (code // 32) % 32, code // 1024
             tag = f"R2W1_pol_lp{lp}_sp{sp}{'_il' if il else ''}"
@@ -59,8 +64,13 @@ def main():
         if r == 2 and w == 1:
             pats.append((f"{tag}_inplace_u{u}_b{b}", i, r + w, True))
     pats.append(("product_reduce_inplace", -1, 3, True))
-    # the product kernel with the round-1/2 load order (gloo_hip_set_variant 15)
+    # the product kernel with the other load order (gloo_hip_set_variant 15:
+    # interleaved, the round 3-5 default; before round 6's switch the product
+    # was interleaved and variant 15 stream by stream)
     pats.append(("product_reduce_inplace_v15", -16, 3, True))
+    # round 6: three workgroups per CU (48 KiB of unused LDS), interleaved / stream by stream
+    pats.append(("product_reduce_inplace_v16", -17, 3, True))
+    pats.append(("product_reduce_inplace_v17", -18, 3, True))
     if args.only:
         pats = [p for p in pats if p[0].startswith(tuple(args.only.split(",")))]
 
@@ -80,13 +90,13 @@ def main():
     a, b, c = sets[0]
     for p in pats:
         name, i, streams, inplace = p
-        if i >= 0 and name.startswith(("R2W1_u", "R1W1", "R2W1_ldsdma_u", "R2W1_pol")):
+        if i >= 0 and name.startswith(("R2W1_u", "R1W1", "R2W1_ldsdma_u", "R2W1_pol", "R2W1_x")):
             L.ceil_run(i, c.data_ptr(), a.data_ptr(), b.data_ptr(), sink.data_ptr(), nbytes, s)
             torch.cuda.synchronize()
             want = a + b if name.startswith("R2W1") else a
             assert torch.equal(c, want), name
 
-    for rep in range(3):
+    for rep in range(args.reps):
         for p in pats:
             for j in range(20):
                 launch(p, j)
