@@ -5,7 +5,9 @@
             (oracle/_ref, built from /root/reference) — the plumbing baseline
   config 3  ring-chunked fp32 sum, P ranks, 256 MiB per rank, chunks moved
             GPU->GPU (xGMI when ranks sit on different GPUs)
-  config 4  halving-doubling fp32 sum, P ranks, sizes 1 KiB .. 1 GiB
+  config 4  halving-doubling fp32 sum, P ranks, sizes 1 KiB .. 1 GiB (--algo4 bcube
+            --base B: AllreduceBcube instead, the reference benchmark's
+            `allreduce_bcube --base`, gloo/benchmark/options.cc:80)
   config 5  reduce-scatter HD, fp16 / bf16, sum / product / min / max
 
 Ranks are threads of this process, rank r on GPU r % device_count (on a
@@ -124,6 +126,8 @@ def main():
     p.add_argument("--configs", default="1,3,4,5")
     p.add_argument("--iters", type=int, default=5)
     p.add_argument("--max-lg", type=int, default=30, help="config 4: largest size, log2 bytes per rank")
+    p.add_argument("--algo4", default="halving_doubling", choices=["halving_doubling", "bcube"])
+    p.add_argument("--base", type=int, default=2, help="--algo4 bcube: the group size (gloo::Context::base)")
     args = p.parse_args()
     cfgs = set(args.configs.split(","))
     import torch
@@ -190,8 +194,10 @@ def main():
             n = max(1, (1 << lg) // 4)
             it = args.iters if lg < 28 else 3
             # latency: no profiling events, so the plan replays as a hipGraph
-            per, st = run_collective(torch, "halving_doubling", "sum", "f32", P, n, max(it, 3), profile=False)
-            print(json.dumps({"config": 4, "algo": "halving_doubling", "ranks": P, "gpus": ndev,
+            recv4 = [args.base] if args.algo4 == "bcube" else None
+            per, st = run_collective(torch, args.algo4, "sum", "f32", P, n, max(it, 3), profile=False, recv=recv4)
+            print(json.dumps({"config": 4, "algo": args.algo4, "ranks": P, "gpus": ndev,
+                              **({"base": args.base} if args.algo4 == "bcube" else {}),
                               "data_path": where, "bytes_per_rank": n * 4,
                               "env": {k: v for k, v in os.environ.items() if k.startswith("GLOO_AMD_")},
                               "us_p50": round(per[len(per) // 2] * 1e6, 1),
