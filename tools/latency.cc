@@ -56,9 +56,13 @@ int main(int argc, char** argv) {
   std::vector<hipStream_t> streams;
   if (!(os && os[0] == '1')) streams.push_back(s);
   std::unique_ptr<gloo_amd::Algorithm> algop;
-  if (algoName == "ring_chunked")
+  if (algoName == "ring_chunked") {
     algop.reset(new gloo_amd::HipAllreduceRingChunked<float>(ctx, {d}, count, streams));
-  else
+  } else if (algoName == "bcube") {  // LATENCY_BASE: gloo::Context::base (default 2)
+    const char* lb = std::getenv("LATENCY_BASE");
+    ctx->base = lb ? std::atoi(lb) : 2;
+    algop.reset(new gloo_amd::HipAllreduceBcube<float>(ctx, {d}, count, streams));
+  } else
     algop.reset(new gloo_amd::HipAllreduceHalvingDoubling<float>(ctx, {d}, count, streams));
   gloo_amd::Algorithm& algo = *algop;
   for (int i = 0; i < 50; i++) {
