@@ -239,12 +239,12 @@ Make halvingDoublingPipelined() {  // gloo::CudaAllreduceHalvingDoublingPipeline
     return std::unique_ptr<gloo::Algorithm>(new gloo::HipAllreduceHalvingDoublingPipelined<T>(c, tp, n, s));
   };
 }
-template <typename T>
+template <typename T, typename W = gloo::HipDeviceWorkspace<T>>
 Make bcube() {  // gloo::CudaAllreduceBcube's twin: groups of the context's base
   return [](std::shared_ptr<gloo::Context>& c, std::vector<void*>& p, int n, std::vector<hipStream_t>& s) {
     std::vector<T*> tp;
     for (void* x : p) tp.push_back(static_cast<T*>(x));
-    return std::unique_ptr<gloo::Algorithm>(new gloo::HipAllreduceBcube<T>(c, tp, n, s));
+    return std::unique_ptr<gloo::Algorithm>(new gloo::HipAllreduceBcube<T, W>(c, tp, n, s));
   };
 }
 
@@ -390,6 +390,9 @@ int main(int argc, char** argv) {
                        [=] { return allreduceCase<float>(P, 1, n, Inputs::kSync, 2, bcube<float>(), 0, base); }});
     }
   }
+  cases.push_back({"host_workspace/bcube/P4/b2/n10007",  // CudaAllreduceBcube's default workspace is the host's
+                   [] { return allreduceCase<float>(4, 1, 10007, Inputs::kSync, 2,
+                                                    bcube<float, gloo::HipHostWorkspace<float>>(), 0, 2); }});
   cases.push_back({"multi_pointer_async/bcube/P4/k2/n4099",
                    [] { return allreduceCase<float>(4, 2, 4099, Inputs::kAsyncSpin, 2, bcube<float>(), 0, 2); }});
   cases.push_back({"multi_pointer/ring_chunked/P3/k2/n1000",
