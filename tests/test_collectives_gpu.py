@@ -336,6 +336,8 @@ for i, algo in enumerate(sys.argv[4].split(",")):
     hip_rt.h2d(buf, x)
     ctx = gloo_amd.Context(rank, size, store + f"_{i}", device=0, timeout_ms=30000)
     recv = [0] * size if algo == "reduce_scatter" else None
+    if algo == "bcube":
+        recv = [size]  # base = P: one group of every rank, a full allreduce at any P
     a = gloo_amd.Algorithm(ctx, algo, "sum", "f32", [buf], 0, recv_elems=recv)
     for _ in range(4):  # eager, then enqueued / captured / replayed where graphs apply
         a.run()
@@ -347,18 +349,20 @@ for i, algo in enumerate(sys.argv[4].split(",")):
     b = hip_rt.malloc(y.nbytes)
     hip_rt.h2d(b, y)
     recv = [1000 // size + (1 if r < 1000 % size else 0) for r in range(size)] if algo == "reduce_scatter" else None
+    if algo == "bcube":
+        recv = [size]
     a = gloo_amd.Algorithm(ctx, algo, "sum", "f32", [b], 1000, recv_elems=recv)
     a.run()
     want = size * (size + 1) / 2
     got = hip_rt.d2h(b, y)
-    got = got[:recv[rank]] if recv else got
+    got = got[:recv[rank]] if algo == "reduce_scatter" else got
     assert (got == want).all(), got
     a.close(); ctx.close()
     hip_rt.free(buf); hip_rt.free(b)
     print("OK", algo, flush=True)
 '''
 
-ZERO_ALGOS = ["ring_chunked", "halving_doubling", "ring", "reduce_scatter"]
+ZERO_ALGOS = ["ring_chunked", "halving_doubling", "ring", "reduce_scatter", "bcube"]
 _zero_runs = {}
 
 
